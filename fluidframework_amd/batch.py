@@ -1,0 +1,280 @@
+"""Host-side packing of sequenced merge-tree messages into engine op batches.
+
+Mirrors what the reference does per message in ``Client.applyMsg``
+(packages/dds/merge-tree/src/client.ts:819-841): register the long client id,
+dispatch ``msg.contents`` (IMergeTreeOp, MT/ops.ts:6-110) by type, flatten GROUP
+members (client.ts:804-812, all members share the message's seq), and finish
+with ``updateSeqNumbers(msg.minimumSequenceNumber, msg.sequenceNumber)``
+(client.ts:840).  The result is the SoA layout of ``mt_op_batch``
+(include/mtgpu.h).  Property sets and client ids are interned here so the
+device only ever sees small integers.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Any
+
+import numpy as np
+
+from . import jsjson
+
+MT_OP_INSERT, MT_OP_REMOVE, MT_OP_ANNOTATE, MT_OP_NOOP = 0, 1, 2, 3
+MT_OPF_END_OF_MSG, MT_OPF_MARKER, MT_OPF_REWRITE, MT_OPF_SEG_PROPS, MT_OPF_COMBINE = 1, 2, 4, 8, 16
+
+MT_DS_NAMES = {
+    0x01: "ASSERT_SEQ", 0x02: "ASSERT_MSN", 0x04: "INSERT_FAILED", 0x08: "UNSUPPORTED",
+    0x10: "OOM_ROWS", 0x20: "OOM_BLOCKS", 0x40: "OOM_TEXT", 0x80: "OOM_PROPS",
+    0x100: "OOM_HEAP", 0x200: "OOM_WINDOW", 0x400: "PROPS_TOO_MANY",
+}
+
+
+def status_names(st: int) -> list[str]:
+    return [n for b, n in MT_DS_NAMES.items() if st & b]
+
+
+class MtOpBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_runs", ctypes.c_uint32), ("doc_ids", ctypes.c_void_p), ("op_offsets", ctypes.c_void_p),
+        ("n_ops", ctypes.c_uint32), ("type", ctypes.c_void_p), ("flags", ctypes.c_void_p),
+        ("client", ctypes.c_void_p), ("seq", ctypes.c_void_p), ("ref_seq", ctypes.c_void_p),
+        ("msn", ctypes.c_void_p), ("pos1", ctypes.c_void_p), ("pos2", ctypes.c_void_p),
+        ("payload_off", ctypes.c_void_p), ("payload_len", ctypes.c_void_p), ("prop_id", ctypes.c_void_p),
+        ("payload", ctypes.c_void_p), ("payload_units", ctypes.c_uint64),
+    ]
+
+
+class MtPropTable(ctypes.Structure):
+    _fields_ = [
+        ("n_sets", ctypes.c_uint32), ("set_off", ctypes.c_void_p), ("key", ctypes.c_void_p),
+        ("value", ctypes.c_void_p), ("n_keys", ctypes.c_uint32), ("key_json", ctypes.c_void_p),
+        ("key_index", ctypes.c_void_p), ("n_values", ctypes.c_uint32), ("value_json", ctypes.c_void_p),
+        ("value_falsy", ctypes.c_void_p), ("value_class", ctypes.c_void_p),
+    ]
+
+
+class MtGenParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64 if n == "seed" else ctypes.c_uint32) for n in (
+        "seed", "n_docs", "ops_per_doc", "clients", "lag_max", "pct_insert", "pct_remove",
+        "ins_len_max", "rem_len_max", "n_ann_sets", "pct_rewrite")]
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a is not None and a.size else 0
+
+
+def _cstr_array(strs: list[str]):
+    arr = (ctypes.c_char_p * max(1, len(strs)))()
+    keep = [s.encode("utf-8", "surrogatepass") for s in strs]
+    for i, b in enumerate(keep):
+        arr[i] = b
+    return arr, keep
+
+
+class PropTable:
+    """Interned property sets in JS ``Object.keys`` order (null = delete)."""
+
+    def __init__(self):
+        self.key_ids: dict[str, int] = {}
+        self.keys: list[str] = []
+        self.value_ids: dict[str, int] = {}
+        self.values_json: list[str] = []
+        self.values_falsy: list[int] = []
+        self.values_class: list[int] = []
+        self._class_ids: dict[Any, int] = {}
+        self.set_ids: dict[tuple, int] = {}
+        self.sets: list[tuple] = []
+        self._c = None
+
+    def key_id(self, k: str) -> int:
+        i = self.key_ids.get(k)
+        if i is None:
+            i = self.key_ids[k] = len(self.keys)
+            self.keys.append(k)
+            self._c = None
+        return i
+
+    def value_id(self, v: Any) -> int:
+        if v is None:
+            return -1
+        txt = jsjson.stringify(v)
+        i = self.value_ids.get(txt)
+        if i is None:
+            i = self.value_ids[txt] = len(self.values_json)
+            self.values_json.append(txt)
+            self.values_falsy.append(0 if jsjson.js_truthy(v) else 1)
+            ck = jsjson.match_class_key(v)
+            c = self._class_ids.setdefault(ck, len(self._class_ids))
+            self.values_class.append(c)
+            self._c = None
+        return i
+
+    def intern(self, props: dict) -> int:
+        pairs = tuple((self.key_id(k), self.value_id(props[k])) for k in jsjson.js_key_order(list(props.keys())))
+        i = self.set_ids.get(pairs)
+        if i is None:
+            i = self.set_ids[pairs] = len(self.sets)
+            self.sets.append(pairs)
+            self._c = None
+        return i
+
+    def to_c(self) -> MtPropTable:
+        if self._c is not None:
+            return self._c[0]
+        off = np.zeros(len(self.sets) + 1, np.uint32)
+        keys, vals = [], []
+        for i, s in enumerate(self.sets):
+            off[i + 1] = off[i] + len(s)
+            for k, v in s:
+                keys.append(k)
+                vals.append(v)
+        keys = np.asarray(keys, np.uint16)
+        vals = np.asarray(vals, np.int32)
+        kj, kk = _cstr_array([jsjson.quote(k) for k in self.keys])
+        kidx = np.asarray([(jsjson.array_index(k) if jsjson.array_index(k) is not None else 0xFFFFFFFF)
+                           for k in self.keys] or [0], np.uint32)
+        vj, vk = _cstr_array(self.values_json)
+        vf = np.asarray(self.values_falsy or [0], np.uint8)
+        vc = np.asarray(self.values_class or [0], np.uint32)
+        t = MtPropTable(len(self.sets), _ptr(off), _ptr(keys), _ptr(vals), len(self.keys),
+                        ctypes.cast(kj, ctypes.c_void_p).value, _ptr(kidx), len(self.values_json),
+                        ctypes.cast(vj, ctypes.c_void_p).value, _ptr(vf), _ptr(vc))
+        self._c = (t, [off, keys, vals, kj, kk, kidx, vj, vk, vf, vc])
+        return t
+
+
+class ClientNames:
+    """Long client ids (strings) <-> per-document client index."""
+
+    def __init__(self):
+        self.ids: dict[str, int] = {}
+        self.names: list[str] = []
+
+    def index(self, long_id: str) -> int:
+        i = self.ids.get(long_id)
+        if i is None:
+            i = self.ids[long_id] = len(self.names)
+            self.names.append(long_id)
+        return i
+
+    def json_literals(self) -> list[str]:
+        return [jsjson.quote(n) for n in self.names]
+
+
+_FIELDS = [("type", np.uint8), ("flags", np.uint8), ("client", np.uint16), ("seq", np.int32),
+           ("ref_seq", np.int32), ("msn", np.int32), ("pos1", np.int32), ("pos2", np.int32),
+           ("payload_off", np.uint32), ("payload_len", np.uint32), ("prop_id", np.int32)]
+
+
+@dataclass
+class OpBatch:
+    """Per-document runs of flattened op members (the mt_op_batch arrays)."""
+    doc_ids: np.ndarray
+    op_offsets: np.ndarray
+    arrays: dict
+    payload: np.ndarray
+    _c: Any = field(default=None, repr=False)
+
+    @property
+    def n_ops(self) -> int:
+        return int(self.op_offsets[-1])
+
+    def to_c(self) -> MtOpBatch:
+        if self._c is None:
+            a = self.arrays
+            self._c = MtOpBatch(len(self.doc_ids), _ptr(self.doc_ids), _ptr(self.op_offsets), self.n_ops,
+                                *(_ptr(a[n]) for n, _ in _FIELDS), _ptr(self.payload), int(self.payload.size))
+        return self._c
+
+    @staticmethod
+    def from_arrays(doc_ids, op_offsets, payload, **arrays) -> "OpBatch":
+        arrs = {n: np.ascontiguousarray(arrays[n], dtype=t) for n, t in _FIELDS}
+        return OpBatch(np.ascontiguousarray(doc_ids, np.uint32), np.ascontiguousarray(op_offsets, np.uint32),
+                       arrs, np.ascontiguousarray(payload, np.uint16))
+
+
+class BatchBuilder:
+    """Packs ISequencedDocumentMessage dicts (protocol.ts:126-166) per document."""
+
+    def __init__(self, props: PropTable, names: ClientNames):
+        self.props, self.names = props, names
+        self.cols = {n: [] for n, _ in _FIELDS}
+        self.payload: list[int] = []
+        self.doc_ids: list[int] = []
+        self.offsets: list[int] = [0]
+
+    def begin_doc(self, doc_id: int):
+        if len(self.doc_ids) and self.offsets[-1] == len(self.cols["type"]) and len(self.doc_ids) == len(self.offsets) - 1:
+            pass
+        self.doc_ids.append(doc_id)
+        self.offsets.append(self.offsets[-1])
+
+    def _emit(self, **kw):
+        for n, _ in _FIELDS:
+            self.cols[n].append(kw.get(n, 0))
+        self.offsets[-1] += 1
+
+    def _member(self, op: dict, client: int, seq: int, ref: int, msn: int, last: bool):
+        t = op["type"]
+        fl = MT_OPF_END_OF_MSG if last else 0
+        common = dict(client=client, seq=seq, ref_seq=ref, msn=msn, prop_id=-1)
+        if t == MT_OP_INSERT:
+            seg = op.get("seg")
+            if seg is None:
+                raise NotImplementedError("register-based insert (client.ts:425-440) is not on the batch path")
+            if "pos1" not in op:
+                raise NotImplementedError("relativePos1 inserts (mergeTree.ts:1949) are not on the batch path")
+            pos2 = 0
+            if isinstance(seg, str):
+                text = seg
+                props = None
+            elif "text" in seg:
+                text, props = seg["text"], seg.get("props")
+            elif "marker" in seg:
+                text, props = None, seg.get("props")
+                fl |= MT_OPF_MARKER
+                pos2 = int(seg["marker"].get("refType", 0) or 0)
+            else:
+                raise ValueError(f"Unrecognized IJSONSegment type: {seg!r}")
+            pid = -1
+            if props:
+                pid = self.props.intern(props)
+                fl |= MT_OPF_SEG_PROPS
+            units = jsjson.utf16_units(text) if text is not None else []
+            off = len(self.payload)
+            self.payload.extend(units)
+            self._emit(type=t, flags=fl, pos1=int(op["pos1"]), pos2=pos2, payload_off=off,
+                       payload_len=len(units), **{**common, "prop_id": pid})
+        elif t in (MT_OP_REMOVE, MT_OP_ANNOTATE):
+            if "pos1" not in op or "pos2" not in op:
+                raise NotImplementedError("relative positions are not on the batch path")
+            pid = -1
+            if t == MT_OP_ANNOTATE:
+                cop = op.get("combiningOp")
+                if cop is not None:
+                    fl |= MT_OPF_REWRITE if cop.get("name") == "rewrite" else MT_OPF_COMBINE
+                pid = self.props.intern(op["props"])
+            self._emit(type=t, flags=fl, pos1=int(op["pos1"]), pos2=int(op["pos2"]), **{**common, "prop_id": pid})
+        else:
+            self._emit(type=MT_OP_NOOP, flags=fl, **common)
+
+    def add_message(self, msg: dict):
+        """One sequenced message (Client.applyMsg semantics, client.ts:819-841)."""
+        client = self.names.index(msg["clientId"])
+        seq, ref, msn = int(msg["sequenceNumber"]), int(msg["referenceSequenceNumber"]), int(msg["minimumSequenceNumber"])
+        if msg.get("type", "op") != "op":
+            self._emit(type=MT_OP_NOOP, flags=MT_OPF_END_OF_MSG, client=client, seq=seq, ref_seq=ref, msn=msn, prop_id=-1)
+            return
+        op = msg["contents"]
+        members = op["ops"] if op["type"] == 3 else [op]
+        members = [m for m in members if m["type"] in (MT_OP_INSERT, MT_OP_REMOVE, MT_OP_ANNOTATE)]
+        if not members:
+            self._emit(type=MT_OP_NOOP, flags=MT_OPF_END_OF_MSG, client=client, seq=seq, ref_seq=ref, msn=msn, prop_id=-1)
+            return
+        for i, m in enumerate(members):
+            self._member(m, client, seq, ref, msn, i == len(members) - 1)
+
+    def build(self) -> OpBatch:
+        arrays = {n: np.asarray(self.cols[n], dtype=t) for n, t in _FIELDS}
+        return OpBatch(np.asarray(self.doc_ids, np.uint32), np.asarray(self.offsets, np.uint32), arrays,
+                       np.asarray(self.payload or [0], np.uint16))

@@ -1,0 +1,236 @@
+/*
+ * mtgpu.h — C ABI of the MI355X batched merge-tree replay engine.
+ *
+ * This is the drop-in boundary for the data-parallel hot path of Fluid's
+ * sequence DDS: server-side replay of sequenced SharedString op streams by a
+ * passive observer client.  Every entry point replaces a
+ * method of the reference merge-tree `Client`
+ * (/root/reference/packages/dds/merge-tree/src/client.ts, cited as MT/client.ts)
+ * applied to many independent documents at once:
+ *
+ *   mt_create / mt_destroy      one engine context per GPU (no reference analogue:
+ *                               the reference holds one JS `Client` per document)
+ *   mt_docs_open                `new Client(...)` + `startOrUpdateCollaboration(obs)`
+ *                               MT/client.ts:78-87, :1073-1093 for n documents
+ *   mt_apply_batch              `Client.applyMsg(msg)` for every message of every
+ *                               document, in sequence order per document
+ *                               MT/client.ts:819-841 (→ applyRemoteOp :790-817,
+ *                               updateSeqNumbers :843-850)
+ *   mt_update_seq               `Client.updateSeqNumbers(min, seq)` MT/client.ts:843
+ *   mt_get_length               `MergeTree.getLength(refSeq, clientId)`
+ *                               packages/dds/merge-tree/src/mergeTree.ts:1569
+ *   mt_snapshot_v1              `Client.snapshot(...)` with newMergeTreeSnapshotFormat
+ *                               (MT/client.ts:923-956 → SnapshotV1.extractSync/emit,
+ *                               MT/snapshotV1.ts:98-256): per-document header and
+ *                               body_i blob strings + a 64-bit digest
+ *   mt_get_text                 `createTextHelper().getText(currentSeq, obs)`
+ *                               MT/textSegment.ts:163-181
+ *   mt_dump_segments            walkAllSegments (mergeTree.ts:2998) row dump, parity
+ *
+ * Conventions: every function returns an int status (MT_OK == 0); no exception
+ * crosses the ABI.  Per-document errors (the reference's `assert` throws,
+ * common-utils assert.ts:12-16) are reported in a per-document status word.
+ * Plain pointers and sizes only; host pointers unless a name says `_dev`.
+ */
+#ifndef MTGPU_H
+#define MTGPU_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------- */
+#define MT_OK               0
+#define MT_E_INVALID        1  /* bad argument / shape                          */
+#define MT_E_HIP            2  /* a HIP runtime call failed                     */
+#define MT_E_OOM            3  /* a per-document pool (rows/blocks/text) is full */
+/* per-document status bits (mt_doc_status) */
+#define MT_DS_ASSERT_SEQ     0x01u /* currentSeq >= seq   (MT/client.ts:482, :846) */
+#define MT_DS_ASSERT_MSN     0x02u /* msn went backwards  (MT/client.ts:484, mergeTree.ts:1716) */
+#define MT_DS_INSERT_FAILED  0x04u /* insert fell off the tree (mergeTree.ts:2228-2233) */
+#define MT_DS_UNSUPPORTED    0x08u /* combiningOp other than none/"rewrite", >64 clients, ... */
+#define MT_DS_OOM_ROWS       0x10u
+#define MT_DS_OOM_BLOCKS     0x20u
+#define MT_DS_OOM_TEXT       0x40u
+#define MT_DS_OOM_PROPS      0x80u
+#define MT_DS_OOM_HEAP       0x100u
+#define MT_DS_OOM_WINDOW     0x200u
+#define MT_DS_PROPS_TOO_MANY 0x400u
+
+/* ---- op records (IMergeTreeOp flattened; MT/ops.ts:6-110) --------------- */
+#define MT_OP_INSERT   0   /* MergeTreeDeltaType.INSERT   */
+#define MT_OP_REMOVE   1   /* MergeTreeDeltaType.REMOVE   */
+#define MT_OP_ANNOTATE 2   /* MergeTreeDeltaType.ANNOTATE */
+#define MT_OP_NOOP     3   /* a sequenced message whose type !== "op" (or an empty
+                              GROUP): only seq/msn advance (MT/client.ts:840)  */
+
+#define MT_OPF_END_OF_MSG 0x01u /* last member of one sequenced message: the
+                                   engine runs updateSeqNumbers(msn, seq) after it.
+                                   GROUP members (MT/client.ts:804-812) share seq/
+                                   ref_seq/msn and only the last carries this flag */
+#define MT_OPF_MARKER     0x02u /* insert of a Marker; pos2 holds refType          */
+#define MT_OPF_REWRITE    0x04u /* annotate with combiningOp {name:"rewrite"}      */
+#define MT_OPF_SEG_PROPS  0x08u /* insert seg has props (prop_id)                  */
+#define MT_OPF_COMBINE    0x10u /* annotate with another combiningOp: unsupported  */
+
+/*
+ * One batch = per-document runs of ops, concatenated by document.
+ * Run d covers ops [op_offsets[d], op_offsets[d+1]) and targets engine
+ * document slot doc_ids[d].  Text payloads are UTF-16 code units
+ * (JS string semantics: lengths are .length of the JS string).
+ */
+typedef struct mt_op_batch {
+    uint32_t        n_runs;
+    const uint32_t* doc_ids;      /* [n_runs]                                  */
+    const uint32_t* op_offsets;   /* [n_runs+1]                                */
+    uint32_t        n_ops;
+    const uint8_t*  type;         /* [n_ops] MT_OP_*                           */
+    const uint8_t*  flags;        /* [n_ops] MT_OPF_*                          */
+    const uint16_t* client;       /* [n_ops] per-document client index (< 64)   */
+    const int32_t*  seq;          /* [n_ops] sequenceNumber                     */
+    const int32_t*  ref_seq;      /* [n_ops] referenceSequenceNumber            */
+    const int32_t*  msn;          /* [n_ops] minimumSequenceNumber              */
+    const int32_t*  pos1;         /* [n_ops]                                    */
+    const int32_t*  pos2;         /* [n_ops] (insert marker: refType)           */
+    const uint32_t* payload_off;  /* [n_ops] into payload                       */
+    const uint32_t* payload_len;  /* [n_ops] UTF-16 units                       */
+    const int32_t*  prop_id;      /* [n_ops] index into the prop table, -1 none */
+    const uint16_t* payload;      /* UTF-16 arena                               */
+    uint64_t        payload_units;
+} mt_op_batch;
+
+/*
+ * Host-interned property sets (the `props` of an annotate op or of an inserted
+ * segment spec), already in JS Object.keys() order.  Values are interned JS
+ * values: value -1 means `null` (delete the key, segmentPropertiesManager.ts:104).
+ */
+typedef struct mt_prop_table {
+    uint32_t        n_sets;
+    const uint32_t* set_off;      /* [n_sets+1] into key/value                  */
+    const uint16_t* key;          /* key id per pair                            */
+    const int32_t*  value;        /* value id per pair, -1 = null               */
+    uint32_t        n_keys;
+    const char* const* key_json;  /* [n_keys] JSON string literal (with quotes) */
+    const uint32_t* key_index;    /* [n_keys] array-index value or 0xFFFFFFFF   */
+    uint32_t        n_values;
+    const char* const* value_json;/* [n_values] JSON text of the value          */
+    const uint8_t*  value_falsy;  /* [n_values] JS falsiness (rewrite rule)     */
+    const uint32_t* value_class;  /* [n_values] matchProperties() equivalence   */
+} mt_prop_table;
+
+/* Engine limits per document (pool capacities, sized from the op counts). */
+typedef struct mt_limits {
+    uint32_t max_docs;
+    uint32_t rows_per_doc;      /* segment rows (append-only within a stream)     */
+    uint32_t blocks_per_doc;    /* B-tree blocks (free-listed)                    */
+    uint32_t text_per_doc;      /* UTF-16 units of the text arena                 */
+    uint32_t propsets_per_doc;  /* device property-set arena entries              */
+    uint32_t heap_per_doc;      /* zamboni heap entries                           */
+    uint32_t window_per_doc;    /* collab-window row list                         */
+} mt_limits;
+
+typedef struct mt_ctx mt_ctx;
+
+/* Counters the engine accumulates per document (algorithmic-byte accounting,
+ * B_op = 32 + 4 L_ins + 32 (R_r + R_w) + 64 D + 64 Z). */
+typedef struct mt_doc_counters {
+    uint64_t ops;          /* sequenced op members applied                      */
+    uint64_t msgs;         /* sequenced messages                                */
+    uint64_t ins_units;    /* Σ L_ins                                          */
+    uint64_t rows_rw;      /* Σ (R_r + R_w)                                    */
+    uint64_t depth;        /* Σ D (one descent per op)                         */
+    uint64_t scoured;      /* Σ Z                                              */
+} mt_doc_counters;
+
+int  mt_create(int device, const mt_limits* limits, mt_ctx** out);
+void mt_destroy(mt_ctx* ctx);
+const char* mt_last_error(mt_ctx* ctx);
+
+/* Open (reset) documents [first, first+n) as empty collaborating documents with
+ * a passive observer (startCollaboration(obs, 0, 0), mergeTree.ts:1243). */
+int  mt_docs_open(mt_ctx* ctx, uint32_t first, uint32_t n);
+
+/* Upload the property table used by subsequent batches. */
+int  mt_set_props(mt_ctx* ctx, const mt_prop_table* props);
+
+/* Apply a host-resident batch (copies to HBM, then replays). Asynchronous on the
+ * context stream; call mt_sync before reading results. */
+int  mt_apply_batch(mt_ctx* ctx, const mt_op_batch* batch);
+
+/* Upload a batch once and keep it resident; mt_replay_resident replays it on the
+ * documents it names without any host->device traffic (the bench's timed path). */
+int  mt_upload_batch(mt_ctx* ctx, const mt_op_batch* batch);
+int  mt_replay_resident(mt_ctx* ctx);
+/* Milliseconds of the last replay kernel(s), timed with HIP events on the
+ * context stream. */
+int  mt_last_replay_ms(mt_ctx* ctx, float* ms);
+
+int  mt_update_seq(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
+                   const int32_t* msn, const int32_t* seq);
+int  mt_sync(mt_ctx* ctx);
+
+int  mt_doc_status(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, uint32_t* out_status);
+int  mt_doc_counters_get(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, mt_doc_counters* out);
+
+/* Perspective length (refSeq, client) of each document (mergeTree.ts:1569). */
+int  mt_get_length(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
+                   const int32_t* ref_seq, const int32_t* client, int32_t* out_len);
+
+/* Client long-id strings (JSON literals) by per-document client index; used for
+ * the snapshot's "client"/"removedClient" fields (snapshotV1.ts:229, :237). */
+int  mt_set_client_names(mt_ctx* ctx, uint32_t n, const char* const* client_json);
+
+/*
+ * SnapshotV1 of each document: runs updateSeqNumbers(msn[i], seq[i]) first
+ * (MT/client.ts:936), then extracts and serializes.  Blobs are concatenated into
+ * a library-owned arena: document i owns blobs [blob_first[i], blob_first[i+1]);
+ * blob j is bytes [blob_off[j], blob_off[j+1]) of *arena; blob 0 of a document is
+ * "header", blob k>0 is "body_{k-1}".  digest[i] = xxh64-style digest of the
+ * document's blob bytes (each blob prefixed by its length).
+ */
+int  mt_snapshot_v1(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
+                    const int32_t* msn, const int32_t* seq,
+                    uint64_t* out_digest,
+                    const char** arena, const uint64_t** blob_off,
+                    const uint32_t** blob_first);
+/* Observer text (UTF-16) of each document into a library-owned arena. */
+int  mt_get_text(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
+                 const uint16_t** arena, const uint64_t** off);
+/* walkAllSegments order dump: per row {len, seq, client, removed_seq (INT32_MIN =
+ * undefined), removed_client, overlap_mask_lo, overlap_mask_hi, prop_set(-1 none),
+ * marker_ref_type(-1 text), text_off, parent_block, flags}. 12 int32 per row. */
+int  mt_dump_segments(mt_ctx* ctx, uint32_t doc_id, int32_t** rows, uint32_t* n_rows);
+void mt_free(void* p);
+
+/* Synthetic stream generation on the device (SURVEY.md §8(d) stream rules):
+ * the engine itself acts as sequencer + observer, so every position is valid
+ * under the author's (refSeq, client) perspective. */
+typedef struct mt_gen_params {
+    uint64_t seed;
+    uint32_t n_docs;
+    uint32_t ops_per_doc;        /* messages per document                        */
+    uint32_t clients;            /* authoring clients per document (<= 64)        */
+    uint32_t lag_max;            /* refSeq lag U[0, lag_max]                      */
+    uint32_t pct_insert;         /* op mix in percent                             */
+    uint32_t pct_remove;         /* (annotate = rest)                             */
+    uint32_t ins_len_max;        /* insert length U[1, ins_len_max]               */
+    uint32_t rem_len_max;        /* remove/annotate length U[1, rem_len_max]      */
+    uint32_t n_ann_sets;         /* annotate prop sets drawn from table [0, n)    */
+    uint32_t pct_rewrite;        /* annotate rewrite percentage                   */
+} mt_gen_params;
+int  mt_generate(mt_ctx* ctx, const mt_gen_params* params);
+/* Copy the generated stream to host memory (arrays sized n_docs*ops_per_doc,
+ * payload sized n_docs*ops_per_doc*ins_len_max). */
+int  mt_generated_download(mt_ctx* ctx, uint8_t* type, uint8_t* flags, uint16_t* client,
+                           int32_t* seq, int32_t* ref_seq, int32_t* msn, int32_t* pos1,
+                           int32_t* pos2, uint32_t* payload_off, uint32_t* payload_len,
+                           int32_t* prop_id, uint16_t* payload);
+/* Make the generated stream the resident batch (docs 0..n_docs-1). */
+int  mt_generated_to_resident(mt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTGPU_H */

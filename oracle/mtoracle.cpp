@@ -1,0 +1,1226 @@
+/*
+ * mtoracle.cpp — CPU ORACLE for the merge-tree replay path.  TEST INFRASTRUCTURE.
+ *
+ * A restatement, in C++, of the reference TypeScript merge-tree algorithm
+ * (/root/reference/packages/dds/merge-tree/src = MT/ below) for the two modes
+ * the parity tests need:
+ *   * a passive observer client applying sequenced remote ops
+ *     (Client.applyMsg MT/client.ts:819, the replay workload), and
+ *   * a detached (non-collaborating) document edited by local ops
+ *     (how packages/dds/sequence/src/test/generateSharedStrings.ts builds the
+ *     golden snapshotV1 fixtures).
+ * It keeps the reference's object model: B-tree blocks of <= 8 children
+ * (MT/mergeTree.ts:350), partial lengths (MT/partialLengths.ts, restated, not
+ * replaced), the zamboni heap (MT/collections.ts:214-268), scourNode/packParent,
+ * SegmentPropertiesManager rules and SnapshotV1 JSON emission.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+ * The product engine (fluidframework_amd/csrc) never links or calls this file.
+ */
+#include "mtoracle.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace ora {
+
+using u16s = std::u16string;
+
+/* ======================================================================== */
+/* JS values, JSON.parse / JSON.stringify semantics                          */
+/* ======================================================================== */
+
+struct JVal {
+    enum T { Undef, Null, Bool, Num, Str, Arr, Obj } t = Undef;
+    bool b = false;
+    double n = 0;
+    u16s s;
+    std::vector<JVal> arr;
+    std::vector<u16s> okeys;   // insertion order (JS order applied on enumeration)
+    std::vector<JVal> ovals;
+};
+
+// Canonical array-index key ("0".."4294967294"): JS enumerates these first,
+// ascending (OrdinaryOwnPropertyKeys).
+static bool array_index(const u16s& k, uint32_t* out) {
+    if (k.empty() || k.size() > 10) return false;
+    if (k.size() > 1 && k[0] == u'0') return false;
+    uint64_t v = 0;
+    for (char16_t c : k) {
+        if (c < u'0' || c > u'9') return false;
+        v = v * 10 + (c - u'0');
+    }
+    if (v >= 4294967295ull) return false;
+    if (out) *out = (uint32_t)v;
+    return true;
+}
+
+static std::vector<int> obj_order(const JVal& o) {
+    std::vector<std::pair<uint32_t, int>> idx;
+    std::vector<int> rest;
+    for (int i = 0; i < (int)o.okeys.size(); i++) {
+        uint32_t v;
+        if (array_index(o.okeys[i], &v)) idx.push_back({v, i});
+        else rest.push_back(i);
+    }
+    std::sort(idx.begin(), idx.end());
+    std::vector<int> out;
+    for (auto& p : idx) out.push_back(p.second);
+    out.insert(out.end(), rest.begin(), rest.end());
+    return out;
+}
+static int obj_find(const JVal& o, const u16s& k) {
+    for (int i = 0; i < (int)o.okeys.size(); i++)
+        if (o.okeys[i] == k) return i;
+    return -1;
+}
+static void obj_set(JVal& o, const u16s& k, const JVal& v) {
+    int i = obj_find(o, k);
+    if (i >= 0) o.ovals[i] = v;
+    else { o.okeys.push_back(k); o.ovals.push_back(v); }
+}
+static void obj_del(JVal& o, const u16s& k) {
+    int i = obj_find(o, k);
+    if (i >= 0) { o.okeys.erase(o.okeys.begin() + i); o.ovals.erase(o.ovals.begin() + i); }
+}
+static JVal make_obj() { JVal o; o.t = JVal::Obj; return o; }
+
+// ---- JSON.parse (UTF-8 text -> JVal) ----
+struct Parser {
+    const char* p; const char* e; bool ok = true;
+    void ws() { while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++; }
+    static void put_cp(u16s& s, uint32_t cp) {
+        if (cp >= 0x10000) { cp -= 0x10000; s.push_back((char16_t)(0xD800 + (cp >> 10))); s.push_back((char16_t)(0xDC00 + (cp & 0x3FF))); }
+        else s.push_back((char16_t)cp);
+    }
+    u16s str() {
+        u16s s; if (p >= e || *p != '"') { ok = false; return s; } p++;
+        while (p < e && *p != '"') {
+            unsigned char c = (unsigned char)*p;
+            if (c == '\\') {
+                p++; if (p >= e) { ok = false; return s; }
+                char x = *p++;
+                switch (x) {
+                case '"': s.push_back(u'"'); break; case '\\': s.push_back(u'\\'); break; case '/': s.push_back(u'/'); break;
+                case 'b': s.push_back(u'\b'); break; case 'f': s.push_back(u'\f'); break; case 'n': s.push_back(u'\n'); break;
+                case 'r': s.push_back(u'\r'); break; case 't': s.push_back(u'\t'); break;
+                case 'u': { if (e - p < 4) { ok = false; return s; } unsigned v = 0; for (int i = 0; i < 4; i++) { char h = *p++; v <<= 4;
+                            if (h >= '0' && h <= '9') v |= h - '0'; else if (h >= 'a' && h <= 'f') v |= h - 'a' + 10; else if (h >= 'A' && h <= 'F') v |= h - 'A' + 10; else ok = false; }
+                            s.push_back((char16_t)v); break; }
+                default: ok = false; return s;
+                }
+            } else {
+                uint32_t cp; int n;
+                if (c < 0x80) { cp = c; n = 1; } else if ((c >> 5) == 6) { cp = c & 0x1F; n = 2; } else if ((c >> 4) == 14) { cp = c & 0x0F; n = 3; } else { cp = c & 0x07; n = 4; }
+                p++; for (int i = 1; i < n && p < e; i++) cp = (cp << 6) | ((unsigned char)*p++ & 0x3F);
+                put_cp(s, cp);
+            }
+        }
+        if (p < e) p++; else ok = false;
+        return s;
+    }
+    JVal val() {
+        ws(); JVal v; if (p >= e) { ok = false; return v; }
+        char c = *p;
+        if (c == '{') {
+            p++; v.t = JVal::Obj; ws();
+            if (p < e && *p == '}') { p++; return v; }
+            while (ok) { ws(); u16s k = str(); ws(); if (p >= e || *p != ':') { ok = false; break; } p++; JVal x = val(); obj_set(v, k, x); ws();
+                if (p < e && *p == ',') { p++; continue; } if (p < e && *p == '}') { p++; break; } ok = false; }
+        } else if (c == '[') {
+            p++; v.t = JVal::Arr; ws();
+            if (p < e && *p == ']') { p++; return v; }
+            while (ok) { v.arr.push_back(val()); ws(); if (p < e && *p == ',') { p++; continue; } if (p < e && *p == ']') { p++; break; } ok = false; }
+        } else if (c == '"') { v.t = JVal::Str; v.s = str(); }
+        else if (!strncmp(p, "true", 4)) { v.t = JVal::Bool; v.b = true; p += 4; }
+        else if (!strncmp(p, "false", 5)) { v.t = JVal::Bool; v.b = false; p += 5; }
+        else if (!strncmp(p, "null", 4)) { v.t = JVal::Null; p += 4; }
+        else { char* end; v.t = JVal::Num; v.n = strtod(p, &end); if (end == p) ok = false; p = end; }
+        return v;
+    }
+};
+static JVal json_parse(const char* s) { Parser ps{s, s + strlen(s)}; JVal v = ps.val(); return v; }
+static u16s parse_key(const char* json_lit) { Parser ps{json_lit, json_lit + strlen(json_lit)}; return ps.str(); }
+
+// ---- JSON.stringify ----
+static void put_utf8(std::string& o, uint32_t cp) {
+    if (cp < 0x80) o.push_back((char)cp);
+    else if (cp < 0x800) { o.push_back((char)(0xC0 | (cp >> 6))); o.push_back((char)(0x80 | (cp & 0x3F))); }
+    else if (cp < 0x10000) { o.push_back((char)(0xE0 | (cp >> 12))); o.push_back((char)(0x80 | ((cp >> 6) & 0x3F))); o.push_back((char)(0x80 | (cp & 0x3F))); }
+    else { o.push_back((char)(0xF0 | (cp >> 18))); o.push_back((char)(0x80 | ((cp >> 12) & 0x3F))); o.push_back((char)(0x80 | ((cp >> 6) & 0x3F))); o.push_back((char)(0x80 | (cp & 0x3F))); }
+}
+// Well-formed JSON.stringify string quoting (V8 >= 7.2): lone surrogates -> \udxxx.
+static void quote(std::string& o, const u16s& s) {
+    static const char* hx = "0123456789abcdef";
+    o.push_back('"');
+    for (size_t i = 0; i < s.size(); i++) {
+        char16_t c = s[i];
+        switch (c) {
+        case u'"': o += "\\\""; continue; case u'\\': o += "\\\\"; continue;
+        case u'\b': o += "\\b"; continue; case u'\f': o += "\\f"; continue; case u'\n': o += "\\n"; continue;
+        case u'\r': o += "\\r"; continue; case u'\t': o += "\\t"; continue;
+        default: break;
+        }
+        if (c < 0x20) { o += "\\u00"; o.push_back(hx[c >> 4]); o.push_back(hx[c & 15]); continue; }
+        if (c >= 0xD800 && c <= 0xDBFF && i + 1 < s.size() && s[i + 1] >= 0xDC00 && s[i + 1] <= 0xDFFF) {
+            uint32_t cp = 0x10000 + (((uint32_t)c - 0xD800) << 10) + ((uint32_t)s[i + 1] - 0xDC00);
+            put_utf8(o, cp); i++; continue;
+        }
+        if (c >= 0xD800 && c <= 0xDFFF) { o += "\\u"; o.push_back(hx[(c >> 12) & 15]); o.push_back(hx[(c >> 8) & 15]); o.push_back(hx[(c >> 4) & 15]); o.push_back(hx[c & 15]); continue; }
+        put_utf8(o, c);
+    }
+    o.push_back('"');
+}
+// ECMAScript Number::toString(10).
+static void num_to_js(std::string& o, double v) {
+    if (v == 0) { o += "0"; return; }
+    if (std::isnan(v)) { o += "NaN"; return; }
+    if (std::isinf(v)) { o += v < 0 ? "-Infinity" : "Infinity"; return; }
+    if (v < 0) { o.push_back('-'); v = -v; }
+    char buf[64]; int prec;
+    for (prec = 1; prec <= 17; prec++) { snprintf(buf, sizeof buf, "%.*e", prec - 1, v); if (strtod(buf, nullptr) == v) break; }
+    std::string digits; int i = 0;
+    for (; buf[i] && buf[i] != 'e'; i++) if (buf[i] >= '0' && buf[i] <= '9') digits.push_back(buf[i]);
+    int ex = atoi(buf + i + 1);
+    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+    int k = (int)digits.size(), n = ex + 1;
+    if (k <= n && n <= 21) { o += digits; o.append(n - k, '0'); }
+    else if (0 < n && n <= 21) { o += digits.substr(0, n); o.push_back('.'); o += digits.substr(n); }
+    else if (-6 < n && n <= 0) { o += "0."; o.append(-n, '0'); o += digits; }
+    else {
+        o.push_back(digits[0]); if (k > 1) { o.push_back('.'); o += digits.substr(1); }
+        o.push_back('e'); int e1 = n - 1; o.push_back(e1 < 0 ? '-' : '+'); o += std::to_string(e1 < 0 ? -e1 : e1);
+    }
+}
+static void stringify(std::string& o, const JVal& v) {
+    switch (v.t) {
+    case JVal::Undef: case JVal::Null: o += "null"; return;
+    case JVal::Bool: o += v.b ? "true" : "false"; return;
+    case JVal::Num: if (std::isfinite(v.n)) num_to_js(o, v.n); else o += "null"; return;
+    case JVal::Str: quote(o, v.s); return;
+    case JVal::Arr: o.push_back('['); for (size_t i = 0; i < v.arr.size(); i++) { if (i) o.push_back(','); stringify(o, v.arr[i]); } o.push_back(']'); return;
+    case JVal::Obj: {
+        o.push_back('{'); bool first = true;
+        for (int i : obj_order(v)) {
+            if (v.ovals[i].t == JVal::Undef) continue;
+            if (!first) o.push_back(','); first = false;
+            quote(o, v.okeys[i]); o.push_back(':'); stringify(o, v.ovals[i]);
+        }
+        o.push_back('}'); return;
+    }
+    }
+}
+
+// ---- MT/properties.ts:64-95 matchProperties (JS semantics) ----
+static bool truthy(const JVal* v) {
+    if (!v) return false;
+    switch (v->t) {
+    case JVal::Undef: case JVal::Null: return false;
+    case JVal::Bool: return v->b;
+    case JVal::Num: return v->n != 0 && !std::isnan(v->n);
+    case JVal::Str: return !v->s.empty();
+    default: return true;
+    }
+}
+static bool is_object_type(const JVal* v) { return v && (v->t == JVal::Obj || v->t == JVal::Arr || v->t == JVal::Null); }
+static std::vector<u16s> for_in_keys(const JVal* v) {
+    std::vector<u16s> ks;
+    if (!v) return ks;
+    if (v->t == JVal::Obj) { for (int i : obj_order(*v)) ks.push_back(v->okeys[i]); }
+    else if (v->t == JVal::Arr || v->t == JVal::Str) {
+        size_t n = v->t == JVal::Arr ? v->arr.size() : v->s.size();
+        for (size_t i = 0; i < n; i++) { std::string d = std::to_string(i); ks.push_back(u16s(d.begin(), d.end())); }
+    }
+    return ks;
+}
+static const JVal* member(const JVal* v, const u16s& k, std::vector<std::unique_ptr<JVal>>& tmp) {
+    if (!v) return nullptr;
+    if (v->t == JVal::Obj) { int i = obj_find(*v, k); return i >= 0 ? &v->ovals[i] : nullptr; }
+    uint32_t ix;
+    if (v->t == JVal::Arr && array_index(k, &ix) && ix < v->arr.size()) return &v->arr[ix];
+    if (v->t == JVal::Str && array_index(k, &ix) && ix < v->s.size()) {
+        tmp.emplace_back(new JVal()); tmp.back()->t = JVal::Str; tmp.back()->s = u16s(1, v->s[ix]); return tmp.back().get();
+    }
+    return nullptr;
+}
+static bool strict_eq(const JVal* a, const JVal* b) {
+    if (!a || !b) return a == b;
+    if (a->t != b->t) return false;
+    switch (a->t) {
+    case JVal::Undef: case JVal::Null: return true;
+    case JVal::Bool: return a->b == b->b;
+    case JVal::Num: return a->n == b->n;
+    case JVal::Str: return a->s == b->s;
+    default: return a == b;   // object identity
+    }
+}
+static bool match_properties(const JVal* a, const JVal* b) {
+    std::vector<std::unique_ptr<JVal>> tmp;
+    if (truthy(a)) {
+        if (!truthy(b)) return false;
+        for (const u16s& key : for_in_keys(a)) {
+            const JVal* bk = member(b, key, tmp);
+            const JVal* ak = member(a, key, tmp);
+            if (!bk || bk->t == JVal::Undef) return false;
+            else if (is_object_type(bk)) { if (!match_properties(ak, bk)) return false; }
+            else if (!strict_eq(bk, ak)) return false;
+        }
+        for (const u16s& key : for_in_keys(b)) {
+            const JVal* ak = member(a, key, tmp);
+            if (!ak || ak->t == JVal::Undef) return false;
+        }
+    } else {
+        if (truthy(b)) return false;
+    }
+    return true;
+}
+
+/* ======================================================================== */
+/* Merge tree                                                                */
+/* ======================================================================== */
+
+constexpr int UniversalSeq = 0, UnassignedSeq = -1, TreeMaintSeq = -2;
+constexpr int LocalClientId = -1, NonCollabClient = -2;
+constexpr int MaxNodesInBlock = 8;            // MT/mergeTree.ts:350
+constexpr int TextSegmentGranularity = 256;   // MT/mergeTree.ts:1056
+constexpr int ZamboniMaxCount = 2;            // MT/mergeTree.ts:1058
+
+struct Block;
+struct Node {
+    bool leaf = false;
+    Block* parent = nullptr;
+    int index = 0;
+    int cachedLength = 0;
+};
+struct Seg : Node {
+    bool marker = false; int refType = 0;
+    u16s text;
+    int seq = UniversalSeq;              // BaseSegment defaults, MT/mergeTree.ts:449-450
+    int clientId = LocalClientId;
+    bool hasRemoved = false; int removedSeq = 0; int removedClientId = 0;
+    bool hasOverlap = false; std::vector<int> overlap;
+    bool hasProps = false; JVal props;   // props.t == Obj when hasProps
+    Seg() { leaf = true; }
+};
+struct PSL {                            // MT/partialLengths.ts:50-56
+    int seq = 0, len = 0, seglen = 0, clientId = 0;
+    bool hasOvl = false; std::map<int, int> ovl;   // RedBlackTree<clientId, {seglen}>
+};
+struct CliPSL { int seq, len, seglen; };
+struct PSLs {                           // class PartialSequenceLengths
+    int minLength = 0, segmentCount = 0;
+    std::vector<PSL> pl;
+    std::map<int, std::vector<CliPSL>> cli;
+};
+struct Block : Node {
+    int childCount = 0;
+    Node* children[MaxNodesInBlock] = {};
+    int needsScour = -1;                // undefined / false(0) / true(1)
+    std::unique_ptr<PSLs> pl;
+};
+struct LRU { Seg* seg; int maxSeq; };
+
+template <class V>
+static int latestLEQ(const V& a, int key) {     // MT/partialLengths.ts:32-48
+    int best = -1, lo = 0, hi = (int)a.size() - 1;
+    while (lo <= hi) {
+        int mid = lo + (hi - lo) / 2;
+        if (a[mid].seq <= key) { if (best < 0 || a[best].seq < a[mid].seq) best = mid; lo = mid + 1; }
+        else hi = mid - 1;
+    }
+    return best;
+}
+
+struct PropTable {                       // host-interned op property sets
+    std::vector<std::vector<std::pair<u16s, int>>> sets;   // (key, value id or -1 = null)
+    std::vector<JVal> values;
+};
+
+struct Tree {
+    // CollaborationWindow, MT/mergeTree.ts:817-834
+    int cwClientId = LocalClientId; bool collaborating = false; int minSeq = 0, currentSeq = 0;
+    Block* root = nullptr;
+    std::vector<std::unique_ptr<Block>> blocks;
+    std::vector<std::unique_ptr<Seg>> segs;
+    std::vector<LRU> heap;               // Heap<LRUSegment>, L[0] sentinel
+    uint32_t status = 0;
+
+    Tree() { root = makeBlock(0); heap.push_back({nullptr, -2}); }
+    Block* makeBlock(int n) { blocks.emplace_back(new Block()); blocks.back()->childCount = n; return blocks.back().get(); }
+    Seg* makeSeg() { segs.emplace_back(new Seg()); return segs.back().get(); }
+
+    static void assignChild(Block* b, Node* c, int i) { c->parent = b; c->index = i; b->children[i] = c; }
+
+    /* ---- lengths ---- */
+    int localNetLength(Seg* s) { return s->hasRemoved ? 0 : s->cachedLength; }           // :1151
+    int nodeTotalLength(Node* n) { return n->leaf ? localNetLength((Seg*)n) : n->cachedLength; }
+    void blockUpdate(Block* b) {                                                            // :2770
+        int len = 0; for (int i = 0; i < b->childCount; i++) len += nodeTotalLength(b->children[i]);
+        b->cachedLength = len;
+    }
+    int partialLength(Block* b, int refSeq, int clientId) {                                 // partialLengths.ts:466-496
+        PSLs& P = *b->pl;
+        int pLen = P.minLength;
+        int seqIndex = latestLEQ(P.pl, refSeq);
+        auto it = P.cli.find(clientId);
+        const std::vector<CliPSL>* cs = it == P.cli.end() ? nullptr : &it->second;
+        int cliLatestIndex = (cs && !cs->empty()) ? (int)cs->size() - 1 : -1;
+        if (seqIndex >= 0) {
+            pLen += P.pl[seqIndex].len;
+            if (cliLatestIndex >= 0) {
+                const CliPSL& cl = (*cs)[cliLatestIndex];
+                if (cl.seq > refSeq) {
+                    pLen += cl.len;
+                    int prec = latestLEQ(*cs, refSeq);
+                    if (prec >= 0) pLen -= (*cs)[prec].len;
+                }
+            }
+        } else if (cliLatestIndex >= 0) pLen += (*cs)[cliLatestIndex].len;
+        return pLen;
+    }
+    int nodeLength(Node* node, int refSeq, int clientId) {                                 // :1652-1692
+        if (!collaborating || cwClientId == clientId) return node->leaf ? localNetLength((Seg*)node) : node->cachedLength;
+        if (!node->leaf) return partialLength((Block*)node, refSeq, clientId);
+        Seg* s = (Seg*)node;
+        if (s->clientId == clientId || (s->seq != UnassignedSeq && s->seq <= refSeq)) {
+            if (s->hasRemoved) {
+                bool ovl = s->hasOverlap && std::find(s->overlap.begin(), s->overlap.end(), clientId) != s->overlap.end();
+                if (s->removedClientId == clientId || ovl || (s->removedSeq != UnassignedSeq && s->removedSeq <= refSeq)) return 0;
+                return s->cachedLength;
+            }
+            return s->cachedLength;
+        }
+        return 0;
+    }
+    int blockLength(Block* b, int refSeq, int clientId) {                                  // :1629
+        if (collaborating && clientId != cwClientId) return partialLength(b, refSeq, clientId);
+        return b->cachedLength;
+    }
+    int getLength(int refSeq, int clientId) { return blockLength(root, refSeq, clientId); }
+
+    /* ---- PartialSequenceLengths (restated) ---- */
+    static void addClientSeqNumber(PSLs& P, int clientId, int seq, int seglen) {           // :530-540
+        auto& cl = P.cli[clientId];
+        int pLen = seglen; if (!cl.empty()) pLen += cl.back().len;
+        cl.push_back({seq, pLen, seglen});
+    }
+    static void addClientSeqNumberFromPartial(PSLs& P, const PSL& p) {                    // :543-552
+        addClientSeqNumber(P, p.clientId, p.seq, p.seglen);
+        if (p.hasOvl) for (auto& kv : p.ovl) addClientSeqNumber(P, kv.first, p.seq, kv.second);
+    }
+    static void insertSegmentPL(PSLs& P, Seg* s, bool removal) {                           // :309-367
+        int seq = s->seq, segLen = s->cachedLength, clientId = s->clientId;
+        const std::vector<int>* rco = nullptr;
+        if (removal) { seq = s->removedSeq; segLen = -segLen; clientId = s->removedClientId; if (s->hasOverlap) rco = &s->overlap; }
+        auto& sp = P.pl;
+        size_t i = 0; for (; i < sp.size(); i++) if (sp[i].seq >= seq) break;
+        if (i < sp.size() && sp[i].seq == seq) {
+            sp[i].seglen += segLen;
+            if (rco) {
+                if (sp[i].hasOvl) { for (int c : *rco) { auto it = sp[i].ovl.find(c); if (it == sp[i].ovl.end()) sp[i].ovl[c] = segLen; else it->second += segLen; } }
+                else { sp[i].hasOvl = true; sp[i].ovl.clear(); for (int c : *rco) sp[i].ovl[c] = segLen; }
+            }
+        } else {
+            PSL p; p.seq = seq; p.clientId = clientId; p.len = 0; p.seglen = segLen;
+            if (rco) { p.hasOvl = true; for (int c : *rco) p.ovl[c] = segLen; }
+            sp.insert(sp.begin() + i, p);
+        }
+    }
+    void fromLeaves(PSLs& P, Block* b) {                                                    // :223-280
+        P.minLength = 0; P.segmentCount = b->childCount;
+        auto seqLTE = [&](int seq) { return seq != UnassignedSeq && seq <= minSeq; };
+        for (int i = 0; i < b->childCount; i++) {
+            Node* c = b->children[i]; if (!c->leaf) continue;
+            Seg* s = (Seg*)c;
+            if (seqLTE(s->seq)) P.minLength += s->cachedLength;
+            else if (s->seq != UnassignedSeq) insertSegmentPL(P, s, false);
+            if (s->hasRemoved && seqLTE(s->removedSeq)) P.minLength -= s->cachedLength;
+            else if (s->hasRemoved && s->removedSeq != UnassignedSeq) insertSegmentPL(P, s, true);
+        }
+        int prevLen = 0;
+        for (auto& p : P.pl) { p.len = prevLen + p.seglen; prevLen = p.len; addClientSeqNumberFromPartial(P, p); }
+    }
+    void zamboniPL(PSLs& P) {                                                                // :499-528
+        auto copyDown = [&](auto& list) {
+            int mindex = latestLEQ(list, minSeq); int ml = 0;
+            if (mindex >= 0) {
+                ml = list[mindex].len; int seqCount = (int)list.size(); int rem = seqCount - mindex - 1;
+                for (int i = 0; i < rem; i++) { list[i] = list[i + mindex + 1]; list[i].len -= ml; }
+                list.resize(rem);
+            }
+            return ml;
+        };
+        P.minLength += copyDown(P.pl);
+        for (auto& kv : P.cli) copyDown(kv.second);
+    }
+    std::unique_ptr<PSLs> combine(Block* b, bool recur) {                                  // :69-221
+        std::unique_ptr<PSLs> comb(new PSLs());
+        fromLeaves(*comb, b);
+        int prevIdx = -1;
+        std::vector<PSLs*> childPartials;
+        for (int i = 0; i < b->childCount; i++) {
+            Node* c = b->children[i];
+            if (!c->leaf) { Block* cb = (Block*)c; if (recur) cb->pl = combine(cb, true); childPartials.push_back(cb->pl.get()); }
+        }
+        std::unique_ptr<PSLs> leafComb;
+        if (!childPartials.empty()) {
+            if (!comb->pl.empty()) { leafComb = std::move(comb); childPartials.push_back(leafComb.get()); comb.reset(new PSLs()); }
+            size_t K = childPartials.size();
+            std::vector<size_t> idx(K, 0);
+            for (size_t k = 0; k < K; k++) { comb->minLength += childPartials[k]->minLength; comb->segmentCount += childPartials[k]->segmentCount; }
+            PSLs& C = *comb;
+            auto addNext = [&](const PSL& p) {
+                int pLen = 0;
+                if (prevIdx >= 0) {
+                    PSL& prev = C.pl[prevIdx];
+                    if (prev.seq == p.seq) {
+                        prev.seglen += p.seglen; prev.len += p.seglen;
+                        if (prev.hasOvl) { if (p.hasOvl) for (auto& kv : p.ovl) { auto it = prev.ovl.find(kv.first); if (it != prev.ovl.end()) it->second += kv.second; else prev.ovl[kv.first] = kv.second; } }
+                        else if (p.hasOvl) { prev.hasOvl = true; prev.ovl = p.ovl; }
+                        return;
+                    }
+                    pLen = prev.len;
+                    addClientSeqNumberFromPartial(C, prev);
+                }
+                PSL np; np.clientId = p.clientId; np.len = pLen + p.seglen; np.hasOvl = p.hasOvl; np.ovl = p.ovl; np.seglen = p.seglen; np.seq = p.seq;
+                C.pl.push_back(np); prevIdx = (int)C.pl.size() - 1;
+            };
+            for (;;) {
+                int best = -1; const PSL* earliest = nullptr;
+                for (size_t k = 0; k < K; k++) {
+                    if (idx[k] < childPartials[k]->pl.size()) {
+                        const PSL& cp = childPartials[k]->pl[idx[k]];
+                        if (best < 0 || cp.seq < earliest->seq) { best = (int)k; earliest = &cp; }
+                    }
+                }
+                if (best < 0) break;
+                addNext(*earliest); idx[best]++;
+            }
+            if (prevIdx >= 0) addClientSeqNumberFromPartial(C, C.pl[prevIdx]);
+        }
+        zamboniPL(*comb);
+        return comb;
+    }
+    static void addSeq(std::vector<PSL>& list, int seq, int seglen, int clientId) {         // :369-402
+        PSL* seqP = nullptr; PSL* penult = nullptr;
+        int leq = latestLEQ(list, seq);
+        if (leq >= 0) {
+            if (list[leq].seq == seq) { seqP = &list[leq]; int l2 = latestLEQ(list, seq - 1); if (l2 >= 0) penult = &list[l2]; }
+            else penult = &list[leq];
+        }
+        int penLen = penult ? penult->len : 0; bool hasPen = penult != nullptr;
+        if (!seqP) { PSL p; p.clientId = clientId; p.seglen = seglen; p.seq = seq; list.push_back(p); seqP = &list.back(); }
+        else seqP->seglen = seglen;
+        seqP->len = hasPen ? seqP->seglen + penLen : seqP->seglen;
+    }
+    static void addSeqCli(std::vector<CliPSL>& list, int seq, int seglen) {
+        CliPSL* seqP = nullptr; CliPSL* penult = nullptr;
+        int leq = latestLEQ(list, seq);
+        if (leq >= 0) {
+            if (list[leq].seq == seq) { seqP = &list[leq]; int l2 = latestLEQ(list, seq - 1); if (l2 >= 0) penult = &list[l2]; }
+            else penult = &list[leq];
+        }
+        int penLen = penult ? penult->len : 0; bool hasPen = penult != nullptr;
+        if (!seqP) { list.push_back({seq, 0, seglen}); seqP = &list.back(); }
+        else seqP->seglen = seglen;
+        seqP->len = hasPen ? seqP->seglen + penLen : seqP->seglen;
+    }
+    void updatePL(Block* node, int seq, int clientId) {                                      // :557-616
+        PSLs& P = *node->pl;
+        int seqSeglen = 0, segCount = 0;
+        for (int i = 0; i < node->childCount; i++) {
+            Node* c = node->children[i];
+            if (!c->leaf) {
+                PSLs& cp = *((Block*)c)->pl;
+                int si = latestLEQ(cp.pl, seq);
+                if (si >= 0 && cp.pl[si].seq == seq) seqSeglen += cp.pl[si].seglen;
+                segCount += cp.segmentCount;
+            } else {
+                Seg* s = (Seg*)c;
+                if (s->seq == seq) { if (!(s->hasRemoved && s->removedSeq == seq)) seqSeglen += s->cachedLength; }
+                else if (s->hasRemoved && s->removedSeq == seq) seqSeglen -= s->cachedLength;
+                segCount++;
+            }
+        }
+        P.segmentCount = segCount;
+        addSeq(P.pl, seq, seqSeglen, clientId);
+        addSeqCli(P.cli[clientId], seq, seqSeglen);
+        zamboniPL(P);
+    }
+    void nodeUpdateLengthNewStructure(Block* b, bool recur = false) {                       // :2741
+        blockUpdate(b);
+        if (collaborating) b->pl = combine(b, recur);
+    }
+    void blockUpdateLength(Block* b, int seq, int clientId) {                                // :2803
+        blockUpdate(b);
+        if (collaborating && seq != UnassignedSeq && seq != TreeMaintSeq) {
+            if (b->pl && clientId != NonCollabClient) updatePL(b, seq, clientId);
+            else b->pl = combine(b, false);
+        }
+    }
+    void blockUpdatePathLengths(Block* b, int seq, int clientId, bool newStructure) {       // :2791
+        while (b) { if (newStructure) nodeUpdateLengthNewStructure(b); else blockUpdateLength(b, seq, clientId); b = b->parent; }
+    }
+
+    /* ---- structure ---- */
+    Block* split(Block* node) {                                                              // :2495-2508
+        int half = MaxNodesInBlock / 2;
+        Block* nn = makeBlock(half);
+        node->childCount = half;
+        for (int i = 0; i < half; i++) { assignChild(nn, node->children[half + i], i); node->children[half + i] = nullptr; }
+        nodeUpdateLengthNewStructure(node);
+        nodeUpdateLengthNewStructure(nn);
+        return nn;
+    }
+    void updateRoot(Block* splitNode) {                                                     // :1868
+        if (!splitNode) return;
+        Block* nr = makeBlock(2);
+        assignChild(nr, root, 0); assignChild(nr, splitNode, 1);
+        root = nr;
+        nodeUpdateLengthNewStructure(root);
+    }
+    bool breakTie(int pos, Node* node, int refSeq, int clientId) {                          // :2267-2296
+        if (node->leaf) {
+            if (pos == 0) {
+                Seg* s = (Seg*)node;
+                if (s->hasRemoved && s->removedSeq != 0 && s->removedSeq <= refSeq && s->removedSeq != UnassignedSeq) return false;
+                if (clientId == cwClientId) return true;
+                if (s->seq != UnassignedSeq) return true;
+            }
+            return false;
+        }
+        return true;
+    }
+    Seg* splitAt(Seg* s, int pos) {                                                          // BaseSegment.splitAt :538-582
+        if (pos <= 0 || s->marker) return nullptr;                                          // Marker.createSplitSegmentAt -> undefined
+        Seg* l = makeSeg();
+        l->text = s->text.substr(pos); s->text = s->text.substr(0, pos);                    // textSegment.ts:103-111
+        s->cachedLength = (int)s->text.size(); l->cachedLength = (int)l->text.size();
+        if (s->hasProps) { l->hasProps = true; l->props = make_obj(); for (int i : obj_order(s->props)) obj_set(l->props, s->props.okeys[i], s->props.ovals[i]); }
+        l->parent = s->parent;
+        l->hasRemoved = s->hasRemoved; l->removedClientId = s->removedClientId; l->removedSeq = s->removedSeq;
+        l->seq = s->seq; l->clientId = s->clientId;
+        if (s->hasOverlap) { l->hasOverlap = true; l->overlap = s->overlap; }
+        return l;
+    }
+    enum LeafKind { LEAF_SPLIT, LEAF_INSERT };
+    // insertingWalk :2363-2493 (continuePredicate never fires: no unacked segments).
+    Block* insertingWalk(Block* block, int pos, int refSeq, int clientId, int seq, LeafKind kind, Seg* cand) {
+        int _pos = pos; Node* newNode = nullptr; int childIndex;
+        for (childIndex = 0; childIndex < block->childCount; childIndex++) {
+            Node* child = block->children[childIndex];
+            int len = nodeLength(child, refSeq, clientId);
+            if (_pos < len || (_pos == len && breakTie(_pos, child, refSeq, clientId))) {
+                if (!child->leaf) {
+                    Block* sn = insertingWalk((Block*)child, _pos, refSeq, clientId, seq, kind, cand);
+                    if (!sn) { blockUpdateLength(block, seq, clientId); return nullptr; }
+                    newNode = sn; childIndex++;
+                } else {
+                    Seg* s = (Seg*)child; Node* next = nullptr;
+                    if (kind == LEAF_SPLIT) next = splitAt(s, _pos);
+                    else { assignChild(block, cand, childIndex); next = s; }
+                    if (next) { newNode = next; childIndex++; }
+                    else return nullptr;
+                }
+                break;
+            } else _pos -= len;
+        }
+        if (!newNode && _pos == 0 && kind == LEAF_INSERT) newNode = cand;
+        if (!newNode) return nullptr;
+        for (int i = block->childCount; i > childIndex; i--) { block->children[i] = block->children[i - 1]; block->children[i]->index = i; }
+        assignChild(block, newNode, childIndex);
+        block->childCount++;
+        if (block->childCount < MaxNodesInBlock) { blockUpdateLength(block, seq, clientId); return nullptr; }
+        return split(block);
+    }
+    void ensureIntervalBoundary(int pos, int refSeq, int clientId) {                        // :2260
+        updateRoot(insertingWalk(root, pos, refSeq, clientId, TreeMaintSeq, LEAF_SPLIT, nullptr));
+    }
+    void addToLRUSet(Seg* s, int seq) {                                                      // :1262-1272
+        if (s->parent->needsScour != 1 && seq > currentSeq) { s->parent->needsScour = 1; heapAdd({s, seq}); }
+    }
+    void heapAdd(LRU x) {                                                                    // collections.ts:214-268
+        heap.push_back(x); size_t k = heap.size() - 1;
+        while (k > 1 && heap[k >> 1].maxSeq - heap[k].maxSeq > 0) { std::swap(heap[k >> 1], heap[k]); k >>= 1; }
+    }
+    LRU heapGet() {
+        LRU x = heap[1]; size_t cnt = heap.size() - 1;
+        heap[1] = heap[cnt]; heap.pop_back(); cnt--;
+        size_t k = 1;
+        while ((k << 1) <= cnt) {
+            size_t j = k << 1;
+            if (j < cnt && heap[j].maxSeq - heap[j + 1].maxSeq > 0) j++;
+            if (heap[k].maxSeq - heap[j].maxSeq <= 0) break;
+            std::swap(heap[k], heap[j]); k = j;
+        }
+        return x;
+    }
+    void insertSegment(int pos, Seg* seg, int refSeq, int clientId, int seq) {               // insertSegments :1974 + blockInsert :2159
+        ensureIntervalBoundary(pos, refSeq, clientId);
+        if (seg->cachedLength > 0) {
+            seg->seq = seq; seg->clientId = clientId;
+            Block* sn = insertingWalk(root, pos, refSeq, clientId, seq, LEAF_INSERT, seg);
+            if (!seg->parent) { status |= MT_DS_INSERT_FAILED; return; }
+            updateRoot(sn);
+            if (collaborating && !(seg->seq == UnassignedSeq && clientId == cwClientId) && seg->seq > minSeq) addToLRUSet(seg, seg->seq);
+        }
+        if (collaborating && seq != UnassignedSeq) zamboni();
+    }
+    template <class F>
+    bool nodeMap(Block* node, int pos, int refSeq, int clientId, int start, int end, F& leaf, Block** postList, int* nPost) {
+        for (int i = 0; i < node->childCount; i++) {                                         // :2927-2994
+            Node* child = node->children[i];
+            int len = nodeLength(child, refSeq, clientId);
+            if (end > 0 && len > 0 && start < len) {
+                if (!child->leaf) nodeMap((Block*)child, pos, refSeq, clientId, start, end, leaf, postList, nPost);
+                else leaf((Seg*)child, pos, start, end);
+            }
+            pos += len; start -= len; end -= len;
+        }
+        (void)postList; (void)nPost;
+        return true;
+    }
+    template <class F, class G>
+    void nodeMapPost(Block* node, int pos, int refSeq, int clientId, int start, int end, F& leaf, G& post) {
+        for (int i = 0; i < node->childCount; i++) {
+            Node* child = node->children[i];
+            int len = nodeLength(child, refSeq, clientId);
+            if (end > 0 && len > 0 && start < len) {
+                if (!child->leaf) nodeMapPost((Block*)child, pos, refSeq, clientId, start, end, leaf, post);
+                else leaf((Seg*)child, pos, start, end);
+            }
+            pos += len; start -= len; end -= len;
+        }
+        post(node);
+    }
+    void markRangeRemoved(int start, int end, int refSeq, int clientId, int seq) {           // :2626-2739
+        ensureIntervalBoundary(start, refSeq, clientId);
+        ensureIntervalBoundary(end, refSeq, clientId);
+        bool overwrite = false;
+        auto leaf = [&](Seg* s, int, int, int) {
+            if (s->hasRemoved) {
+                overwrite = true;
+                if (s->removedSeq == UnassignedSeq) { s->removedClientId = clientId; s->removedSeq = seq; }
+                else { if (!s->hasOverlap) { s->hasOverlap = true; s->overlap.clear(); } s->overlap.push_back(clientId); }
+            } else { s->hasRemoved = true; s->removedClientId = clientId; s->removedSeq = seq; }
+            if (collaborating) { if (!(s->removedSeq == UnassignedSeq && clientId == cwClientId)) addToLRUSet(s, seq); }
+        };
+        auto post = [&](Block* b) { if (overwrite) nodeUpdateLengthNewStructure(b); else blockUpdateLength(b, seq, clientId); };
+        nodeMapPost(root, 0, refSeq, clientId, start, end, leaf, post);
+        if (collaborating && seq != UnassignedSeq) zamboni();
+    }
+    void addProperties(Seg* s, const PropTable& pt, int set, bool rewrite, int seq, bool collab) {
+        // SegmentPropertiesManager.addProperties, MT/segmentPropertiesManager.ts:38-113 (observer: no pending keys)
+        (void)seq; (void)collab;
+        if (!s->hasProps) { s->hasProps = true; s->props = make_obj(); }
+        const auto& np = pt.sets[set];
+        auto newVal = [&](const u16s& k) -> const JVal* {
+            for (auto& kv : np) if (kv.first == k) return kv.second < 0 ? &nullv : &pt.values[kv.second];
+            return nullptr;
+        };
+        if (rewrite) {
+            std::vector<u16s> keys; for (int i : obj_order(s->props)) keys.push_back(s->props.okeys[i]);
+            for (auto& k : keys) if (!truthy(newVal(k))) obj_del(s->props, k);
+        }
+        for (auto& kv : np) {
+            if (kv.second < 0) obj_del(s->props, kv.first);
+            else obj_set(s->props, kv.first, pt.values[kv.second]);
+        }
+    }
+    JVal nullv = [] { JVal v; v.t = JVal::Null; return v; }();
+    void annotateRange(int start, int end, const PropTable& pt, int set, bool rewrite, int refSeq, int clientId, int seq) { // :2584
+        ensureIntervalBoundary(start, refSeq, clientId);
+        ensureIntervalBoundary(end, refSeq, clientId);
+        auto leaf = [&](Seg* s, int, int, int) {
+            addProperties(s, pt, set, rewrite, seq, collaborating);
+            if (collaborating && seq != UnassignedSeq) addToLRUSet(s, seq);
+        };
+        nodeMap(root, 0, refSeq, clientId, start, end, leaf, nullptr, nullptr);
+        if (collaborating && seq != UnassignedSeq) zamboni();
+    }
+    /* ---- zamboni ---- */
+    static bool canAppend(Seg* a, Seg* b) {                                                  // textSegment.ts:63-68
+        if (a->marker || b->marker) return false;
+        if (!a->text.empty() && a->text.back() == u'\n') return false;
+        return a->cachedLength <= TextSegmentGranularity || b->cachedLength <= TextSegmentGranularity;
+    }
+    void scourNode(Block* node, std::vector<Node*>& hold) {                                  // :1278-1356
+        Seg* prev = nullptr;
+        for (int k = 0; k < node->childCount; k++) {
+            Node* c = node->children[k];
+            if (c->leaf) {
+                Seg* s = (Seg*)c;
+                if (s->hasRemoved) {
+                    if (s->removedSeq > minSeq) hold.push_back(s);
+                    else s->parent = nullptr;                       // UNLINK
+                    prev = nullptr;
+                } else if (s->seq <= minSeq) {
+                    bool ca = prev && canAppend(prev, s) && match_properties(prev->hasProps ? &prev->props : nullptr, s->hasProps ? &s->props : nullptr) && localNetLength(s) > 0;
+                    if (ca) { prev->text += s->text; prev->cachedLength = (int)prev->text.size(); s->parent = nullptr; }
+                    else { hold.push_back(s); prev = localNetLength(s) > 0 ? s : nullptr; }
+                } else { hold.push_back(s); prev = nullptr; }
+            } else { hold.push_back(c); prev = nullptr; }
+        }
+    }
+    bool underflow(Block* b) { return b->childCount < MaxNodesInBlock / 2; }
+    void packParent(Block* parent) {                                                         // :1359-1410
+        std::vector<Node*> hold;
+        for (int i = 0; i < parent->childCount; i++) { Block* cb = (Block*)parent->children[i]; scourNode(cb, hold); cb->parent = nullptr; }
+        int total = (int)hold.size(), half = MaxNodesInBlock / 2;
+        int childCount = std::min(MaxNodesInBlock - 1, total / half); if (childCount < 1) childCount = 1;
+        int base = total / childCount, extra = total % childCount, rd = 0;
+        Block* packed[MaxNodesInBlock] = {};
+        for (int ni = 0; ni < childCount; ni++) {
+            int cnt = base; if (extra > 0) { cnt++; extra--; }
+            Block* pb = makeBlock(cnt);
+            for (int j = 0; j < cnt; j++) assignChild(pb, hold[rd++], j);
+            pb->parent = parent; packed[ni] = pb;
+            nodeUpdateLengthNewStructure(pb);
+        }
+        for (int j = 0; j < MaxNodesInBlock; j++) parent->children[j] = nullptr;
+        for (int j = 0; j < childCount; j++) assignChild(parent, packed[j], j);
+        parent->childCount = childCount;
+        if (underflow(parent) && parent->parent) packParent(parent->parent);
+        else blockUpdatePathLengths(parent, UnassignedSeq, -1, true);
+    }
+    void zamboni() {                                                                         // :1412-1468
+        if (!collaborating) return;
+        for (int i = 0; i < ZamboniMaxCount; i++) {
+            if (heap.size() <= 1 || heap[1].maxSeq > minSeq) break;
+            LRU e = heapGet();
+            Seg* s = e.seg;
+            if (s->parent && s->parent->needsScour != 0) {
+                Block* b = s->parent;
+                std::vector<Node*> copy;
+                scourNode(b, copy);
+                b->needsScour = 0;
+                int n = (int)copy.size();
+                if (n < b->childCount) {
+                    b->childCount = n;
+                    for (int j = 0; j < MaxNodesInBlock; j++) b->children[j] = nullptr;
+                    for (int j = 0; j < n; j++) assignChild(b, copy[j], j);
+                    if (underflow(b) && b->parent) packParent(b->parent);
+                    else blockUpdatePathLengths(b, UnassignedSeq, -1, true);
+                }
+            }
+        }
+    }
+    void setMinSeq(int ms) {                                                                 // :1712-1725
+        if (ms > currentSeq) status |= MT_DS_ASSERT_MSN;
+        if (minSeq > ms) { status |= MT_DS_ASSERT_MSN; return; }
+        if (ms > minSeq) { minSeq = ms; zamboni(); }
+    }
+    void startCollaboration(int localClientId, int ms, int cs) {                            // :1243-1260
+        cwClientId = localClientId; minSeq = ms; collaborating = true; currentSeq = cs;
+        heap.clear(); heap.push_back({nullptr, -2});
+        nodeUpdateLengthNewStructure(root, true);
+    }
+    // Debug: partial lengths vs the exact leaf sum for perspective (refSeq, clientId).
+    int exactLength(Node* n, int refSeq, int clientId) {
+        if (n->leaf) return nodeLength(n, refSeq, clientId);
+        Block* b = (Block*)n; int s = 0;
+        for (int i = 0; i < b->childCount; i++) s += exactLength(b->children[i], refSeq, clientId);
+        return s;
+    }
+    int verifyPartials(Block* b, int refSeq, int clientId) {
+        int bad = (collaborating && clientId != cwClientId && partialLength(b, refSeq, clientId) != exactLength(b, refSeq, clientId)) ? 1 : 0;
+        for (int i = 0; i < b->childCount; i++) if (!b->children[i]->leaf) bad += verifyPartials((Block*)b->children[i], refSeq, clientId);
+        return bad;
+    }
+    template <class F> void walkAll(Block* b, F& f) { for (int i = 0; i < b->childCount; i++) { Node* c = b->children[i]; if (c->leaf) f((Seg*)c); else walkAll((Block*)c, f); } }
+};
+
+/* ======================================================================== */
+/* Client (MT/client.ts) + snapshot                                          */
+/* ======================================================================== */
+
+struct Doc {
+    Tree t;
+    PropTable props;
+    std::vector<std::string> names;          // stream client index -> JSON literal of long id
+    std::map<std::string, int> nameToShort;  // clientNameToIds
+    std::vector<std::string> shortToName;    // shortClientIdMap (JSON literal)
+    std::vector<int> shortToStream;          // short id -> stream client index (-1 observer)
+    std::vector<int> streamToShort;
+
+    int shortId(int streamIdx) {             // getOrAddShortClientId, MT/client.ts:658-682
+        if (streamIdx < (int)streamToShort.size() && streamToShort[streamIdx] >= 0) return streamToShort[streamIdx];
+        std::string nm = streamIdx < (int)names.size() ? names[streamIdx] : ("\"c" + std::to_string(streamIdx) + "\"");
+        auto it = nameToShort.find(nm);
+        int id;
+        if (it != nameToShort.end()) id = it->second;
+        else { id = (int)shortToName.size(); nameToShort[nm] = id; shortToName.push_back(nm); shortToStream.push_back(streamIdx); }
+        if ((int)streamToShort.size() <= streamIdx) streamToShort.resize(streamIdx + 1, -1);
+        streamToShort[streamIdx] = id;
+        return id;
+    }
+    std::string longId(int shortId) { return shortId >= 0 ? shortToName[shortId] : std::string("\"original\""); }
+    int streamOf(int shortId) { return shortId >= 0 && shortId < (int)shortToStream.size() ? shortToStream[shortId] : -1; }
+};
+
+static Seg* specToSegment(Doc& d, const uint16_t* text, uint32_t n, int refType, bool marker, int propSet) {
+    Seg* s = d.t.makeSeg();
+    if (marker) { s->marker = true; s->refType = refType; s->cachedLength = 1; }                // Marker ctor :644-647
+    else { s->text.assign((const char16_t*)text, n); s->cachedLength = (int)n; }
+    if (propSet >= 0) {                                                                          // make(...) -> addProperties(props)
+        s->hasProps = true; s->props = make_obj();
+        for (auto& kv : d.props.sets[propSet]) { if (kv.second < 0) obj_del(s->props, kv.first); else obj_set(s->props, kv.first, d.props.values[kv.second]); }
+    }
+    return s;
+}
+
+static std::string seg_json(const Seg* s, const u16s* textOverride = nullptr) {
+    std::string o;
+    if (s->marker) {                                                                             // Marker.toJSONObject :649-653
+        o += "{\"marker\":{\"refType\":"; num_to_js(o, s->refType); o += "}";
+        if (s->hasProps) { o += ",\"props\":"; stringify(o, s->props); }
+        o += "}";
+    } else {                                                                                     // TextSegment.toJSONObject textSegment.ts:48-54
+        const u16s& tx = textOverride ? *textOverride : s->text;
+        if (s->hasProps) { o += "{\"text\":"; quote(o, tx); o += ",\"props\":"; stringify(o, s->props); o += "}"; }
+        else quote(o, tx);
+    }
+    return o;
+}
+
+static uint64_t xxh64(const uint8_t* p, size_t len, uint64_t seed) {
+    const uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL, P3 = 1609587929392839161ULL, P4 = 9650029242287828579ULL, P5 = 2870177450012600261ULL;
+    auto rotl = [](uint64_t x, int r) { return (x << r) | (x >> (64 - r)); };
+    auto rd64 = [](const uint8_t* q) { uint64_t v; memcpy(&v, q, 8); return v; };
+    auto rd32 = [](const uint8_t* q) { uint32_t v; memcpy(&v, q, 4); return (uint64_t)v; };
+    auto round = [&](uint64_t acc, uint64_t in) { acc += in * P2; acc = rotl(acc, 31); return acc * P1; };
+    auto merge = [&](uint64_t acc, uint64_t v) { v = round(0, v); acc ^= v; return acc * P1 + P4; };
+    const uint8_t* e = p + len; uint64_t h;
+    if (len >= 32) {
+        uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+        const uint8_t* lim = e - 32;
+        do { v1 = round(v1, rd64(p)); v2 = round(v2, rd64(p + 8)); v3 = round(v3, rd64(p + 16)); v4 = round(v4, rd64(p + 24)); p += 32; } while (p <= lim);
+        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+        h = merge(h, v1); h = merge(h, v2); h = merge(h, v3); h = merge(h, v4);
+    } else h = seed + P5;
+    h += (uint64_t)len;
+    while (p + 8 <= e) { h ^= round(0, rd64(p)); h = rotl(h, 27) * P1 + P4; p += 8; }
+    if (p + 4 <= e) { h ^= rd32(p) * P1; h = rotl(h, 23) * P2 + P3; p += 4; }
+    while (p < e) { h ^= (*p) * P5; h = rotl(h, 11) * P1; p++; }
+    h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+    return h;
+}
+
+// Client.snapshot -> SnapshotV1.extractSync/emit (MT/client.ts:923-956, MT/snapshotV1.ts:98-256)
+static std::vector<std::string> snapshot_v1(Doc& d, int msn, int seq) {
+    Tree& t = d.t;
+    if (t.collaborating) {                                                                        // updateSeqNumbers(minSeq, lastSeq)
+        if (t.currentSeq > seq) t.status |= MT_DS_ASSERT_SEQ;
+        t.currentSeq = seq; t.setMinSeq(msn);
+    }
+    int minSeq = t.minSeq, currentSeq = t.currentSeq;
+    std::vector<std::string> segJson; std::vector<int> segLen;
+    Seg* prev = nullptr; u16s prevText; bool prevCloned = false;
+    auto pushPrev = [&]() {
+        if (!prev) return;
+        segJson.push_back(seg_json(prev, prevCloned ? &prevText : nullptr));
+        segLen.push_back(prevCloned ? (int)prevText.size() : prev->cachedLength);
+    };
+    auto extract = [&](Seg* s) {
+        if (s->seq == UnassignedSeq || (s->hasRemoved && s->removedSeq <= minSeq)) return;
+        if (s->seq <= minSeq && (!s->hasRemoved || s->removedSeq == UnassignedSeq)) {
+            if (!prev) { prev = s; prevCloned = false; }
+            else {
+                // prev.canAppend(segment) on the (possibly coalesced) clone
+                bool ok;
+                if (prev->marker || s->marker) ok = false;
+                else {
+                    const u16s& pt = prevCloned ? prevText : prev->text;
+                    int plen = (int)pt.size();
+                    ok = !(!pt.empty() && pt.back() == u'\n') && (plen <= TextSegmentGranularity || s->cachedLength <= TextSegmentGranularity);
+                }
+                if (ok && match_properties(prev->hasProps ? &prev->props : nullptr, s->hasProps ? &s->props : nullptr)) {
+                    if (!prevCloned) { prevText = prev->text; prevCloned = true; }
+                    prevText += s->text;
+                } else { pushPrev(); prev = s; prevCloned = false; }
+            }
+        } else {
+            pushPrev(); prev = nullptr; prevCloned = false;
+            std::string raw = "{\"json\":" + seg_json(s);
+            if (s->seq > minSeq) { raw += ",\"seq\":"; num_to_js(raw, s->seq); raw += ",\"client\":" + d.longId(s->clientId); }
+            if (s->hasRemoved) { raw += ",\"removedSeq\":"; num_to_js(raw, s->removedSeq); raw += ",\"removedClient\":" + d.longId(s->removedClientId); }
+            raw += "}";
+            segJson.push_back(raw); segLen.push_back(s->cachedLength);
+        }
+    };
+    t.walkAll(t.root, extract);
+    pushPrev();
+    // emit: chunks of approx 10000 chars (snapshotV1.ts:70-92, :98-163)
+    struct Chunk { int start, count, length; };
+    std::vector<Chunk> chunks; int totalCount = 0, totalLen = 0;
+    do {
+        Chunk c{totalCount, 0, 0};
+        while (c.length < 10000 && c.start + c.count < (int)segJson.size()) { c.length += segLen[c.start + c.count]; c.count++; }
+        chunks.push_back(c); totalCount += c.count; totalLen += c.length;
+    } while (totalCount < (int)segJson.size());
+    auto chunkStr = [&](const Chunk& c, bool header) {
+        std::string o = "{\"version\":\"1\",\"segmentCount\":"; num_to_js(o, c.count);
+        o += ",\"length\":"; num_to_js(o, c.length); o += ",\"segments\":[";
+        for (int i = 0; i < c.count; i++) { if (i) o.push_back(','); o += segJson[c.start + i]; }
+        o += "],\"startIndex\":"; num_to_js(o, c.start);
+        if (header) {
+            o += ",\"headerMetadata\":{\"minSequenceNumber\":"; num_to_js(o, minSeq);
+            o += ",\"sequenceNumber\":"; num_to_js(o, currentSeq);
+            o += ",\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+            for (size_t k = 1; k < chunks.size(); k++) o += ",{\"id\":\"body_" + std::to_string(k - 1) + "\"}";
+            o += "],\"totalLength\":"; num_to_js(o, totalLen); o += ",\"totalSegmentCount\":"; num_to_js(o, totalCount); o += "}";
+        }
+        o += "}";
+        return o;
+    };
+    std::vector<std::string> blobs;
+    for (size_t k = 0; k < chunks.size(); k++) blobs.push_back(chunkStr(chunks[k], k == 0));
+    return blobs;
+}
+
+static uint64_t blobs_digest(const std::vector<std::string>& blobs) {
+    std::string buf;
+    for (auto& b : blobs) { uint64_t n = b.size(); buf.append((const char*)&n, 8); buf += b; }
+    return xxh64((const uint8_t*)buf.data(), buf.size(), 0);
+}
+
+static uint32_t fnv1a(const std::string& s) { uint32_t h = 2166136261u; for (unsigned char c : s) { h ^= c; h *= 16777619u; } return h; }
+
+static uint32_t apply_run(Doc& d, const mt_op_batch* b, uint32_t run) {
+    Tree& t = d.t;
+    uint32_t o0 = b->op_offsets[run], o1 = b->op_offsets[run + 1];
+    for (uint32_t i = o0; i < o1 && !(t.status & MT_DS_INSERT_FAILED); i++) {
+        int ty = b->type[i]; unsigned fl = b->flags[i];
+        int cl = d.shortId(b->client[i]);                                                        // applyMsg :825
+        int seq = b->seq[i], ref = b->ref_seq[i], msn = b->msn[i];
+        if (ty != MT_OP_NOOP) {
+            if (t.currentSeq >= seq) t.status |= MT_DS_ASSERT_SEQ;                              // completeAndLogOp :482
+            if (t.minSeq > msn) t.status |= MT_DS_ASSERT_MSN;                                   // :484
+            if (ty == MT_OP_INSERT) {
+                bool marker = fl & MT_OPF_MARKER;
+                int ps = (fl & MT_OPF_SEG_PROPS) ? b->prop_id[i] : -1;
+                Seg* s = specToSegment(d, b->payload + b->payload_off[i], b->payload_len[i], b->pos2[i], marker, ps);
+                t.insertSegment(b->pos1[i], s, ref, cl, seq);
+            } else if (ty == MT_OP_REMOVE) {
+                t.markRangeRemoved(b->pos1[i], b->pos2[i], ref, cl, seq);
+            } else if (ty == MT_OP_ANNOTATE) {
+                if (fl & MT_OPF_COMBINE) t.status |= MT_DS_UNSUPPORTED;
+                t.annotateRange(b->pos1[i], b->pos2[i], d.props, b->prop_id[i], fl & MT_OPF_REWRITE, ref, cl, seq);
+            }
+        }
+        if (fl & MT_OPF_END_OF_MSG) {                                                            // updateSeqNumbers :843-850
+            if (t.currentSeq > seq) t.status |= MT_DS_ASSERT_SEQ;
+            t.currentSeq = seq;
+            if (msn > seq) t.status |= MT_DS_ASSERT_MSN;
+            t.setMinSeq(msn);
+        }
+    }
+    return t.status;
+}
+
+/* ---- synthetic stream generator (same algorithm as the device generator) ---- */
+struct SplitMix { uint64_t s; uint64_t next() { uint64_t z = (s += 0x9E3779B97F4A7C15ULL); z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL; z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL; return z ^ (z >> 31); }
+                  uint32_t u(uint32_t n) { return (uint32_t)(next() % n); } };
+
+}  // namespace ora
+
+using namespace ora;
+
+struct ora_doc { Doc d; };
+static int g_verify = 0;
+static long long g_verify_bad = 0, g_verify_checks = 0;
+
+extern "C" {
+
+ora_doc* ora_new(int collaborating) {
+    ora_doc* o = new ora_doc();
+    if (collaborating) {                                                                         // startOrUpdateCollaboration("obs")
+        o->d.nameToShort["\"obs\""] = 0; o->d.shortToName.push_back("\"obs\""); o->d.shortToStream.push_back(-1);
+        o->d.t.startCollaboration(0, 0, 0);
+    }
+    return o;
+}
+void ora_free(ora_doc* d) { delete d; }
+void ora_set_verify(int on) { g_verify = on; g_verify_bad = 0; g_verify_checks = 0; }
+long long ora_verify_result(long long* checks) { if (checks) *checks = g_verify_checks; return g_verify_bad; }
+void ora_free_buf(void* p) { free(p); }
+
+static void load_props(PropTable& pt, const mt_prop_table* p) {
+    pt.sets.clear(); pt.values.clear();
+    if (!p) return;
+    std::vector<u16s> keys;
+    for (uint32_t k = 0; k < p->n_keys; k++) keys.push_back(parse_key(p->key_json[k]));
+    for (uint32_t v = 0; v < p->n_values; v++) pt.values.push_back(json_parse(p->value_json[v]));
+    for (uint32_t s = 0; s < p->n_sets; s++) {
+        std::vector<std::pair<u16s, int>> set;
+        for (uint32_t j = p->set_off[s]; j < p->set_off[s + 1]; j++) set.push_back({keys[p->key[j]], p->value[j]});
+        pt.sets.push_back(set);
+    }
+}
+int ora_set_props(ora_doc* d, const mt_prop_table* p) { load_props(d->d.props, p); return 0; }
+int ora_set_client_names(ora_doc* d, uint32_t n, const char* const* cj) { d->d.names.clear(); for (uint32_t i = 0; i < n; i++) d->d.names.push_back(cj[i]); return 0; }
+uint32_t ora_apply_run(ora_doc* d, const mt_op_batch* b, uint32_t run) { return apply_run(d->d, b, run); }
+
+int ora_local_insert(ora_doc* o, int32_t pos, const uint16_t* text, uint32_t n, int32_t refType, int32_t ps) {
+    Tree& t = o->d.t;
+    Seg* s = specToSegment(o->d, text, n, refType, refType >= 0, ps);
+    int cl = t.cwClientId, seq = t.collaborating ? UnassignedSeq : UniversalSeq;
+    t.insertSegment(pos, s, t.currentSeq, cl, seq);
+    return (int)t.status;
+}
+int ora_local_remove(ora_doc* o, int32_t start, int32_t end) {
+    Tree& t = o->d.t; t.markRangeRemoved(start, end, t.currentSeq, t.cwClientId, t.collaborating ? UnassignedSeq : UniversalSeq); return (int)t.status;
+}
+int ora_local_annotate(ora_doc* o, int32_t start, int32_t end, int32_t ps, int32_t rewrite) {
+    Tree& t = o->d.t; t.annotateRange(start, end, o->d.props, ps, rewrite != 0, t.currentSeq, t.cwClientId, t.collaborating ? UnassignedSeq : UniversalSeq); return (int)t.status;
+}
+int32_t ora_get_length(ora_doc* o, int32_t ref, int32_t client) {
+    // A client that has not sent a message yet owns no segment: any unused id gives its view.
+    int cl;
+    if (client < 0) cl = o->d.t.cwClientId;
+    else if (client < (int)o->d.streamToShort.size() && o->d.streamToShort[client] >= 0) cl = o->d.streamToShort[client];
+    else cl = -1000 - client;
+    return o->d.t.getLength(ref, cl);
+}
+uint8_t* ora_snapshot_v1(ora_doc* o, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total) {
+    std::vector<std::string> blobs = snapshot_v1(o->d, msn, seq);
+    size_t n = 4; for (auto& b : blobs) n += 8 + b.size();
+    uint8_t* buf = (uint8_t*)malloc(n); uint32_t nb = (uint32_t)blobs.size(); memcpy(buf, &nb, 4); size_t off = 4;
+    for (auto& b : blobs) { uint64_t l = b.size(); memcpy(buf + off, &l, 8); off += 8; memcpy(buf + off, b.data(), l); off += l; }
+    if (digest) *digest = blobs_digest(blobs);
+    if (total) *total = n;
+    return buf;
+}
+uint16_t* ora_get_text(ora_doc* o, uint64_t* n) {
+    // getText(currentSeq, observer) = mapRange(gatherText) over [0, getLength) — observer sees non-removed text
+    u16s out; Tree& t = o->d.t;
+    auto f = [&](Seg* s) { if (!s->marker && t.localNetLength(s) > 0) out += s->text; };
+    t.walkAll(t.root, f);
+    uint16_t* buf = (uint16_t*)malloc((out.size() + 1) * 2); memcpy(buf, out.data(), out.size() * 2); *n = out.size();
+    return buf;
+}
+int32_t* ora_dump_segments(ora_doc* o, uint32_t* n_rows) {
+    std::vector<int32_t> rows; Doc& d = o->d;
+    auto f = [&](Seg* s) {
+        int32_t r[12];
+        r[0] = s->cachedLength; r[1] = s->seq; r[2] = d.t.collaborating ? d.streamOf(s->clientId) : s->clientId;
+        r[3] = s->hasRemoved ? s->removedSeq : INT32_MIN; r[4] = s->hasRemoved ? (d.t.collaborating ? d.streamOf(s->removedClientId) : s->removedClientId) : -1;
+        uint64_t m = 0; if (s->hasOverlap) for (int c : s->overlap) { int sc = d.streamOf(c); if (sc >= 0 && sc < 64) m |= 1ull << sc; }
+        r[5] = (int32_t)(m & 0xFFFFFFFFu); r[6] = (int32_t)(m >> 32);
+        if (s->hasProps) { std::string js; stringify(js, s->props); r[7] = (int32_t)(fnv1a(js) & 0x7FFFFFFF); } else r[7] = -1;
+        r[8] = s->marker ? s->refType : -1;
+        // tree path: child index at each level, root first (3 bits each)
+        int depth = 0; uint64_t path = 0; std::vector<int> ix;
+        for (Node* x = s; x->parent; x = x->parent) ix.push_back(x->index);
+        depth = (int)ix.size();
+        for (int k = depth - 1; k >= 0; k--) path = (path << 3) | (uint64_t)(ix[k] & 7);
+        r[9] = depth; r[10] = (int32_t)(path & 0xFFFFFFFFu); r[11] = (int32_t)(path >> 32);
+        rows.insert(rows.end(), r, r + 12);
+    };
+    d.t.walkAll(d.t.root, f);
+    *n_rows = (uint32_t)(rows.size() / 12);
+    int32_t* buf = (int32_t*)malloc(rows.size() * 4 + 4); memcpy(buf, rows.data(), rows.size() * 4);
+    return buf;
+}
+void ora_stats(ora_doc* o, int32_t* out) {
+    int h = 0; for (Node* x = o->d.t.root; x && !x->leaf; x = ((Block*)x)->childCount ? ((Block*)x)->children[0] : nullptr) h++;
+    int nseg = 0; auto f = [&](Seg*) { nseg++; }; o->d.t.walkAll(o->d.t.root, f);
+    out[0] = h; out[1] = 0; out[2] = nseg; out[3] = (int)o->d.t.blocks.size();
+}
+
+uint32_t ora_generate_doc(const mt_gen_params* p, uint32_t doc, const mt_prop_table* props,
+                          uint8_t* type, uint8_t* flags, uint16_t* client, int32_t* seq,
+                          int32_t* ref_seq, int32_t* msn, int32_t* pos1, int32_t* pos2,
+                          uint32_t* payload_off, uint32_t* payload_len, int32_t* prop_id,
+                          uint16_t* payload, uint32_t payload_base, ora_doc** keep) {
+    ora_doc* o = ora_new(1);
+    load_props(o->d.props, props);
+    SplitMix rng{p->seed ^ (0x9E3779B97F4A7C15ULL * (uint64_t)(doc + 1))};
+    std::vector<int> lastRef(p->clients, 0);
+    int cur = 0, curMsn = 0; uint32_t pw = 0;
+    uint32_t offs[2] = {0, 1};
+    for (uint32_t k = 0; k < p->ops_per_doc; k++) {
+        uint32_t a = rng.u(p->clients);
+        uint32_t lag = rng.u(p->lag_max + 1);
+        int r = cur - (int)lag; if (r < lastRef[a]) r = lastRef[a]; if (r < curMsn) r = curMsn;
+        lastRef[a] = r;
+        int L = ora_get_length(o, r, (int)a);
+        if (g_verify) {
+            int cl = (a < o->d.streamToShort.size() && o->d.streamToShort[a] >= 0) ? o->d.streamToShort[a] : -1000 - (int)a;
+            g_verify_bad += o->d.t.verifyPartials(o->d.t.root, r, cl);
+            g_verify_checks++;
+        }
+        uint32_t tsel = rng.u(100);
+        int ty = tsel < p->pct_insert ? MT_OP_INSERT : (tsel < p->pct_insert + p->pct_remove ? MT_OP_REMOVE : MT_OP_ANNOTATE);
+        if (L == 0) ty = MT_OP_INSERT;
+        int s1, s2 = 0; uint32_t plen = 0; int pid = -1; uint8_t fl = MT_OPF_END_OF_MSG;
+        if (ty == MT_OP_INSERT) {
+            s1 = (int)rng.u((uint32_t)L + 1); plen = 1 + rng.u(p->ins_len_max);
+            for (uint32_t c = 0; c < plen; c++) payload[pw + c] = (uint16_t)(u'a' + rng.u(26));
+        } else {
+            s1 = (int)rng.u((uint32_t)L); uint32_t n = 1 + rng.u(p->rem_len_max); s2 = std::min(L, s1 + (int)n);
+            if (ty == MT_OP_ANNOTATE) { pid = (int)rng.u(p->n_ann_sets); if (rng.u(100) < p->pct_rewrite) fl |= MT_OPF_REWRITE; }
+        }
+        int mn = lastRef[0]; for (uint32_t c = 1; c < p->clients; c++) mn = std::min(mn, lastRef[c]);
+        type[k] = (uint8_t)ty; flags[k] = fl; client[k] = (uint16_t)a; seq[k] = cur + 1; ref_seq[k] = r; msn[k] = mn;
+        pos1[k] = s1; pos2[k] = s2; payload_off[k] = payload_base + pw; payload_len[k] = plen; prop_id[k] = pid;
+        // apply through the observer (a one-op batch over the caller's arrays)
+        mt_op_batch b{}; b.n_runs = 1; b.op_offsets = offs; b.n_ops = 1;
+        b.type = type + k; b.flags = flags + k; b.client = client + k; b.seq = seq + k; b.ref_seq = ref_seq + k; b.msn = msn + k;
+        b.pos1 = pos1 + k; b.pos2 = pos2 + k; uint32_t lo = pw; b.payload_off = &lo; b.payload_len = payload_len + k; b.prop_id = prop_id + k;
+        b.payload = payload; b.payload_units = pw + plen;
+        apply_run(o->d, &b, 0);
+        pw += plen; cur = cur + 1; curMsn = mn;
+        if (o->d.t.status) break;
+    }
+    uint32_t st = o->d.t.status;
+    if (keep) *keep = o; else ora_free(o);
+    return st;
+}
+
+double ora_replay_batch(const mt_op_batch* b, const mt_prop_table* props, int threads, uint64_t* digests, uint32_t* status) {
+    uint32_t R = b->n_runs;
+    std::vector<std::pair<uint64_t, uint32_t>> order;
+    for (uint32_t r = 0; r < R; r++) order.push_back({(uint64_t)(b->op_offsets[r + 1] - b->op_offsets[r]), r});
+    std::sort(order.begin(), order.end(), [](auto& x, auto& y) { return x.first > y.first; });
+    if (threads < 1) threads = 1;
+    std::vector<std::vector<uint32_t>> bins(threads); std::vector<uint64_t> load(threads, 0);
+    for (auto& pr : order) { int m = (int)(std::min_element(load.begin(), load.end()) - load.begin()); bins[m].push_back(pr.second); load[m] += pr.first; }
+    PropTable pt; load_props(pt, props);
+    std::vector<double> secs(threads, 0);
+    std::vector<std::thread> th;
+    for (int w = 0; w < threads; w++) th.emplace_back([&, w] {
+        auto t0 = std::chrono::steady_clock::now();
+        std::vector<ora_doc*> docs;
+        for (uint32_t r : bins[w]) {
+            ora_doc* o = ora_new(1); o->d.props = pt;
+            uint32_t st = apply_run(o->d, b, r);
+            if (status) status[r] = st;
+            docs.push_back(o);
+        }
+        secs[w] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        for (size_t i = 0; i < docs.size(); i++) {
+            uint32_t r = bins[w][i];
+            if (digests) {
+                uint32_t last = b->op_offsets[r + 1] - 1;
+                bool empty = b->op_offsets[r + 1] == b->op_offsets[r];
+                auto blobs = snapshot_v1(docs[i]->d, empty ? 0 : b->msn[last], empty ? 0 : b->seq[last]);
+                digests[r] = blobs_digest(blobs);
+            }
+            ora_free(docs[i]);
+        }
+    });
+    for (auto& x : th) x.join();
+    return *std::max_element(secs.begin(), secs.end());
+}
+
+}  // extern "C"

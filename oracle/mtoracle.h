@@ -1,0 +1,65 @@
+/*
+ * mtoracle.h — C API of the CPU ORACLE (test infrastructure only).
+ *
+ * The oracle is a restatement of the reference merge-tree algorithm
+ * (/root/reference/packages/dds/merge-tree/src) used ONLY by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker.
+ * The product (fluidframework_amd/, libmtgpu.so) never links or calls it.
+ */
+#ifndef MTORACLE_H
+#define MTORACLE_H
+#include <stdint.h>
+#include "../include/mtgpu.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ora_doc ora_doc;
+
+/* collaborating=1: passive observer "obs" (startOrUpdateCollaboration, MT/client.ts:1073);
+ * collaborating=0: detached local document (SharedString before attach). */
+ora_doc* ora_new(int collaborating);
+void     ora_free(ora_doc* d);
+int      ora_set_props(ora_doc* d, const mt_prop_table* props);
+int      ora_set_client_names(ora_doc* d, uint32_t n, const char* const* client_json);
+/* Apply run `run` of the batch (Client.applyMsg per message). Returns 0 or an
+ * MT_DS_* status bitmask (the reference would have thrown). */
+uint32_t ora_apply_run(ora_doc* d, const mt_op_batch* b, uint32_t run);
+/* Local (non-collaborating) ops, as SharedString.insertText/insertMarker/
+ * annotateRange/removeText on a detached string (seq = UniversalSequenceNumber). */
+int      ora_local_insert(ora_doc* d, int32_t pos, const uint16_t* text, uint32_t n,
+                          int32_t marker_ref_type, int32_t prop_set);
+int      ora_local_remove(ora_doc* d, int32_t start, int32_t end);
+int      ora_local_annotate(ora_doc* d, int32_t start, int32_t end, int32_t prop_set, int32_t rewrite);
+int32_t  ora_get_length(ora_doc* d, int32_t ref_seq, int32_t client); /* client -1: observer */
+/* Snapshot: returns a malloc'd buffer: u32 n_blobs, then per blob u64 len + bytes. */
+uint8_t* ora_snapshot_v1(ora_doc* d, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total_bytes);
+uint16_t* ora_get_text(ora_doc* d, uint64_t* n_units);
+int32_t* ora_dump_segments(ora_doc* d, uint32_t* n_rows);  /* 12 int32 per row */
+void     ora_free_buf(void* p);
+/* Tree statistics: height, leaf blocks, segments, blocks. */
+void     ora_stats(ora_doc* d, int32_t* out4);
+
+/* Stream generation (SURVEY.md §8(d) rules, same algorithm as mt_generate):
+ * generates and applies ops_per_doc messages for document `doc`; writes the op
+ * arrays (length ops_per_doc) and the payload (<= ops_per_doc*ins_len_max). */
+uint32_t ora_generate_doc(const mt_gen_params* p, uint32_t doc, const mt_prop_table* props,
+                          uint8_t* type, uint8_t* flags, uint16_t* client, int32_t* seq,
+                          int32_t* ref_seq, int32_t* msn, int32_t* pos1, int32_t* pos2,
+                          uint32_t* payload_off, uint32_t* payload_len, int32_t* prop_id,
+                          uint16_t* payload, uint32_t payload_base, ora_doc** keep_doc);
+
+/* Debug: verify partial lengths == exact leaf sums at every generated op. */
+void ora_set_verify(int on);
+long long ora_verify_result(long long* checks);
+
+/* CPU baseline: replay every run of the batch on fresh documents with
+ * `threads` std::threads (LPT-partitioned by op count); returns wall seconds of
+ * the apply loop and optionally per-run snapshot digests (msn/seq = last op's). */
+double   ora_replay_batch(const mt_op_batch* b, const mt_prop_table* props, int threads,
+                          uint64_t* out_digests, uint32_t* out_status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

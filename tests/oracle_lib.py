@@ -1,0 +1,212 @@
+"""ctypes binding of the CPU oracle (oracle/mtoracle.cpp).  TEST INFRASTRUCTURE.
+
+Used only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+from fluidframework_amd.batch import MtGenParams, MtOpBatch, MtPropTable, OpBatch, PropTable
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "oracle", "mtoracle.cpp")
+LIB = os.path.join(ROOT, "oracle", "_build", "libmtoracle.so")
+
+
+def build_oracle(force: bool = False) -> str:
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+        os.makedirs(os.path.dirname(LIB), exist_ok=True)
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", LIB, SRC])
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = ctypes.CDLL(build_oracle())
+        P, I32, U32, U64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+        L.ora_new.restype = P
+        L.ora_new.argtypes = [ctypes.c_int]
+        L.ora_free.argtypes = [P]
+        L.ora_free_buf.argtypes = [P]
+        L.ora_set_props.argtypes = [P, ctypes.POINTER(MtPropTable)]
+        L.ora_set_client_names.argtypes = [P, U32, P]
+        L.ora_apply_run.restype = U32
+        L.ora_apply_run.argtypes = [P, ctypes.POINTER(MtOpBatch), U32]
+        L.ora_local_insert.argtypes = [P, I32, P, U32, I32, I32]
+        L.ora_local_remove.argtypes = [P, I32, I32]
+        L.ora_local_annotate.argtypes = [P, I32, I32, I32, I32]
+        L.ora_get_length.restype = I32
+        L.ora_get_length.argtypes = [P, I32, I32]
+        L.ora_snapshot_v1.restype = P
+        L.ora_snapshot_v1.argtypes = [P, I32, I32, ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.ora_get_text.restype = P
+        L.ora_get_text.argtypes = [P, ctypes.POINTER(U64)]
+        L.ora_dump_segments.restype = P
+        L.ora_dump_segments.argtypes = [P, ctypes.POINTER(U32)]
+        L.ora_stats.argtypes = [P, P]
+        L.ora_generate_doc.restype = U32
+        L.ora_generate_doc.argtypes = [ctypes.POINTER(MtGenParams), U32, ctypes.POINTER(MtPropTable)] + [P] * 12 + [U32, P]
+        L.ora_set_verify.argtypes = [ctypes.c_int]
+        L.ora_verify_result.restype = ctypes.c_longlong
+        L.ora_verify_result.argtypes = [ctypes.POINTER(ctypes.c_longlong)]
+        L.ora_replay_batch.restype = ctypes.c_double
+        L.ora_replay_batch.argtypes = [ctypes.POINTER(MtOpBatch), ctypes.POINTER(MtPropTable), ctypes.c_int, P, P]
+        _lib = L
+    return _lib
+
+
+def parse_blobs(buf: int, total: int) -> list[bytes]:
+    raw = ctypes.string_at(buf, total)
+    n = struct.unpack_from("<I", raw, 0)[0]
+    off, out = 4, []
+    for _ in range(n):
+        ln = struct.unpack_from("<Q", raw, off)[0]
+        off += 8
+        out.append(raw[off:off + ln])
+        off += ln
+    return out
+
+
+class OracleDoc:
+    """One reference-semantics document (passive observer or detached local)."""
+
+    def __init__(self, collaborating: bool = True, props: PropTable | None = None, names: list[str] | None = None):
+        self.L = lib()
+        self.h = self.L.ora_new(1 if collaborating else 0)
+        self.props = props
+        if props is not None:
+            self.set_props(props)
+        if names is not None:
+            self.set_names(names)
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.L.ora_free(self.h)
+        except Exception:
+            pass
+
+    def set_props(self, props: PropTable):
+        self.props = props
+        self.L.ora_set_props(self.h, ctypes.byref(props.to_c()))
+
+    def set_names(self, json_literals: list[str]):
+        arr = (ctypes.c_char_p * max(1, len(json_literals)))(*[s.encode() for s in json_literals])
+        self._names = arr
+        self.L.ora_set_client_names(self.h, len(json_literals), ctypes.cast(arr, ctypes.c_void_p))
+
+    def apply_run(self, batch: OpBatch, run: int) -> int:
+        return int(self.L.ora_apply_run(self.h, ctypes.byref(batch.to_c()), run))
+
+    # detached-string local edits (SharedString before attach)
+    def insert_text(self, pos: int, text: str, props: dict | None = None):
+        from fluidframework_amd.jsjson import utf16_units
+        u = np.asarray(utf16_units(text) or [0], np.uint16)
+        pid = self.props.intern(props) if props else -1
+        if pid >= 0:
+            self.set_props(self.props)
+        return self.L.ora_local_insert(self.h, pos, u.ctypes.data, len(text.encode("utf-16-le", "surrogatepass")) // 2, -1, pid)
+
+    def insert_marker(self, pos: int, ref_type: int, props: dict | None = None):
+        pid = self.props.intern(props) if props else -1
+        if pid >= 0:
+            self.set_props(self.props)
+        return self.L.ora_local_insert(self.h, pos, None, 0, ref_type, pid)
+
+    def annotate_range(self, start: int, end: int, props: dict, rewrite: bool = False):
+        pid = self.props.intern(props)
+        self.set_props(self.props)
+        return self.L.ora_local_annotate(self.h, start, end, pid, 1 if rewrite else 0)
+
+    def remove_range(self, start: int, end: int):
+        return self.L.ora_local_remove(self.h, start, end)
+
+    def get_length(self, ref_seq: int = 0, client: int = -1) -> int:
+        return int(self.L.ora_get_length(self.h, ref_seq, client))
+
+    def snapshot(self, msn: int = 0, seq: int = 0):
+        dig, tot = ctypes.c_uint64(), ctypes.c_uint64()
+        buf = self.L.ora_snapshot_v1(self.h, msn, seq, ctypes.byref(dig), ctypes.byref(tot))
+        blobs = parse_blobs(buf, tot.value)
+        self.L.ora_free_buf(buf)
+        return blobs, dig.value
+
+    def get_text(self) -> str:
+        n = ctypes.c_uint64()
+        buf = self.L.ora_get_text(self.h, ctypes.byref(n))
+        raw = ctypes.string_at(buf, n.value * 2)
+        self.L.ora_free_buf(buf)
+        return raw.decode("utf-16-le", "surrogatepass")
+
+    def dump(self) -> np.ndarray:
+        n = ctypes.c_uint32()
+        buf = self.L.ora_dump_segments(self.h, ctypes.byref(n))
+        a = np.frombuffer(ctypes.string_at(buf, n.value * 48), np.int32).reshape(-1, 12).copy()
+        self.L.ora_free_buf(buf)
+        return a
+
+    def stats(self):
+        out = np.zeros(4, np.int32)
+        self.L.ora_stats(self.h, out.ctypes.data)
+        return out
+
+
+def gen_params(seed=1, n_docs=1, ops=1000, clients=2, lag=8, ins=55, rem=45, ins_len=8, rem_len=16,
+               ann_sets=1, rewrite=0) -> MtGenParams:
+    return MtGenParams(seed, n_docs, ops, clients, lag, ins, rem, ins_len, rem_len, ann_sets, rewrite)
+
+
+def generate(params: MtGenParams, props: PropTable, docs=None, keep=False):
+    """Generate streams with the oracle as sequencer+observer; returns (OpBatch, [status], [OracleDoc])."""
+    L = lib()
+    docs = list(range(params.n_docs)) if docs is None else list(docs)
+    n = params.ops_per_doc
+    cols = {k: [] for k in ("type", "flags", "client", "seq", "ref_seq", "msn", "pos1", "pos2",
+                            "payload_off", "payload_len", "prop_id")}
+    payloads, offs, stats, kept = [], [0], [], []
+    base = 0
+    for d in docs:
+        a = dict(type=np.zeros(n, np.uint8), flags=np.zeros(n, np.uint8), client=np.zeros(n, np.uint16),
+                 seq=np.zeros(n, np.int32), ref_seq=np.zeros(n, np.int32), msn=np.zeros(n, np.int32),
+                 pos1=np.zeros(n, np.int32), pos2=np.zeros(n, np.int32), payload_off=np.zeros(n, np.uint32),
+                 payload_len=np.zeros(n, np.uint32), prop_id=np.zeros(n, np.int32))
+        pay = np.zeros(max(1, n * params.ins_len_max), np.uint16)
+        kp = ctypes.c_void_p()
+        st = L.ora_generate_doc(ctypes.byref(params), d, ctypes.byref(props.to_c()),
+                                *(a[k].ctypes.data for k in ("type", "flags", "client", "seq", "ref_seq", "msn",
+                                                             "pos1", "pos2", "payload_off", "payload_len", "prop_id")),
+                                pay.ctypes.data, base, ctypes.byref(kp) if keep else None)
+        used = int(a["payload_len"].sum())
+        payloads.append(pay[:used])
+        base += used
+        for k in cols:
+            cols[k].append(a[k])
+        offs.append(offs[-1] + n)
+        stats.append(int(st))
+        if keep:
+            od = OracleDoc.__new__(OracleDoc)
+            od.L, od.h, od.props = L, kp.value, props
+            kept.append(od)
+    batch = OpBatch.from_arrays(np.asarray(docs, np.uint32), np.asarray(offs, np.uint32),
+                                np.concatenate(payloads) if payloads else np.zeros(1, np.uint16),
+                                **{k: np.concatenate(v) for k, v in cols.items()})
+    return batch, stats, kept
+
+
+def replay(batch: OpBatch, props: PropTable, names: list[str] | None = None):
+    """Apply every run on a fresh passive-observer document; returns docs."""
+    docs = []
+    for r in range(len(batch.doc_ids)):
+        d = OracleDoc(True, props, names)
+        st = d.apply_run(batch, r)
+        docs.append((d, st))
+    return docs
