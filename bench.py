@@ -1,0 +1,219 @@
+#!/usr/bin/env python
+"""bench.py — sequenced merge-tree ops applied/sec on MI355X (BASELINE.json metric).
+
+A "step" is one replay of the whole synthetic batch on freshly opened documents:
+every document's sequenced messages are applied through the HIP engine
+(Client.applyMsg semantics, packages/dds/merge-tree/src/client.ts:819) with the
+op arrays already resident in HBM.  Streams are produced on the device by the
+engine acting as sequencer + observer (SURVEY.md §8(d) rules), before timing.
+
+Default workload (N=1): BASELINE.json configs[1] — 4,096 documents x 8 clients x
+10,000 messages, refSeq lag U[0,32], 60/40 insert/remove (insert length U[1,8],
+remove length U[1,8]).  Multi-GPU (torchrun): documents shard across ranks with
+no data-path collective (weak scaling); timing = max over ranks.
+
+JSON fields beyond the driver contract:
+  roofline      algorithmic HBM bytes per launch (SURVEY.md §8(d) B_op formula,
+                from the engine's per-document counters) / average replay-kernel
+                time measured with HIP events on the engine's stream;
+  cpu_baseline  the oracle (C++ restatement of the reference algorithm, "port")
+                replaying a bounded sample of the same streams on host threads.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+CONFIGS = {
+    # name: (docs, ops, clients, lag, ins%, rem%, ins_len, rem_len, ann_sets, rewrite%)
+    "config2": dict(docs=4096, ops=10000, clients=8, lag=32, ins=60, rem=40, ins_len=8, rem_len=8, ann_sets=1, rewrite=0,
+                    desc="4096 docs x 8 clients x 10k msgs, lag U[0,32], 60/40 ins/rem"),
+    "config3": dict(docs=16384, ops=4000, clients=8, lag=4, ins=30, rem=30, ins_len=8, rem_len=16, ann_sets=24, rewrite=5,
+                    desc="16384 docs x 8 clients x 4k msgs, lag U[0,4], 30/30/40 ins/rem/annotate, zamboni-heavy"),
+    "config1": dict(docs=1, ops=10000, clients=2, lag=8, ins=55, rem=45, ins_len=8, rem_len=16, ann_sets=1, rewrite=0,
+                    desc="1 doc x 2 clients x 10k msgs (reference plumbing case)"),
+}
+
+
+def ann_props():
+    from fluidframework_amd.batch import PropTable
+    pt = PropTable()
+    vals = ["s0", "s1", "s2", "s3", 1, 2, None]
+    rng = np.random.RandomState(5)
+    for _ in range(24):
+        keys = rng.choice(8, size=rng.randint(1, 4), replace=False)
+        pt.intern({f"k{k}": vals[rng.randint(0, len(vals))] for k in sorted(keys)})
+    return pt
+
+
+def algorithmic_bytes(cnt):
+    # B_op = 32 + 4 L_ins + 32 (R_r + R_w) + 64 D + 64 Z, summed over messages
+    return int(32 * cnt["msgs"].sum() + 4 * cnt["ins_units"].sum() + 32 * cnt["rows_rw"].sum()
+               + 64 * cnt["depth"].sum() + 64 * cnt["scoured"].sum())
+
+
+def caps_for(c):
+    ops = c["ops"]
+    return dict(rows_per_doc=3 * ops + 64, blocks_per_doc=ops + 64, heap_per_doc=2 * ops + 64,
+                window_per_doc=max(2048, 64 * c["lag"] + 1024), text_per_doc=ops * c["ins_len"] + 4096,
+                propsets_per_doc=(2 * ops + 64) if c["ins"] + c["rem"] < 100 else 64)
+
+
+def cpu_baseline(eng, c, params_cls, seed, target_s, threads):
+    """Oracle ('port' of the reference algorithm) on a bounded sample of the same streams."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes
+    from oracle_lib import lib as oracle
+    L = oracle()
+    props = eng.props
+
+    def run(n_docs):
+        p = params_cls(seed, n_docs, c["ops"], c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"],
+                       c["rem_len"], c["ann_sets"], c["rewrite"])
+        eng.generate(p)
+        eng.sync()
+        b = eng.generated_download()
+        st = np.zeros(n_docs, np.uint32)
+        secs = L.ora_replay_batch(ctypes.byref(b.to_c()), ctypes.byref(props.to_c()), threads, None,
+                                  st.ctypes.data)
+        return secs, int(b.op_offsets[-1])
+
+    pilot_docs = min(c["docs"], max(threads, 16))
+    t, n = run(pilot_docs)
+    docs = pilot_docs
+    if t < target_s * 0.5:
+        docs = int(min(c["docs"], max(pilot_docs, pilot_docs * target_s / max(t, 1e-3))))
+        if docs > pilot_docs:
+            t, n = run(docs)
+    return {"value": n / t, "unit": "ops/s", "cores": threads, "kind": "port",
+            "sample": f"{docs} docs x {c['ops']} msgs of the same workload, oracle (C++ restatement of "
+                      f"MT/mergeTree.ts + partialLengths.ts) on {threads} host threads, {t:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
+    ap.add_argument("--docs", type=int, default=0, help="override documents per GPU")
+    ap.add_argument("--ops", type=int, default=0, help="override messages per document")
+    ap.add_argument("--seed", type=int, default=20241015)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo")  # rank coordination only: no data-path collective (weak scaling)
+        dist = (torch, tdist)
+
+    from fluidframework_amd.batch import MtGenParams
+    from fluidframework_amd.engine import Engine
+
+    c = dict(CONFIGS[args.config])
+    if args.docs:
+        c["docs"] = args.docs
+    if args.ops:
+        c["ops"] = args.ops
+    eng = Engine(c["docs"], device=local, **caps_for(c))
+    eng.upload_props(ann_props())
+    eng.upload_names(['"c%d"' % i for i in range(64)])
+    seed = args.seed ^ (rank * 0x9E3779B1)
+    params = MtGenParams(seed, c["docs"], c["ops"], c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"],
+                         c["rem_len"], c["ann_sets"], c["rewrite"])
+    t0 = time.time()
+    eng.generate(params)
+    eng.sync()
+    gen_s = time.time() - t0
+    st = eng.status(range(c["docs"]))
+    if st.any():
+        raise SystemExit(f"rank {rank}: generation failed, status {np.unique(st)}")
+    cnt = eng.counters(range(c["docs"]))
+    msgs = int(cnt["msgs"].sum())
+    bytes_per_launch = algorithmic_bytes(cnt)
+    eng.generated_to_resident()
+
+    def step():
+        eng.open_docs(0, c["docs"])
+        eng.replay_resident()
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+
+    def barrier():
+        if dist:
+            dist[1].barrier()
+
+    barrier()
+    eng.sync()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        step()
+        eng.sync()
+        kms.append(eng.last_replay_ms())
+    eng.sync()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        torch, tdist = dist
+        t = torch.tensor([dt], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    st = eng.status(range(c["docs"]))
+    cnt2 = eng.counters(range(c["docs"]))
+    ok = (not st.any()) and int(cnt2["msgs"].sum()) == msgs
+    total_msgs = msgs * world * args.steps
+    value = total_msgs / dt
+    kern_s = float(np.mean(kms)) / 1e3
+    achieved = bytes_per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
+    if rank != 0:
+        return
+    out = {
+        "metric": "sequenced merge-tree ops applied/sec (whole node) + achieved HBM GB/s",
+        "value": value,
+        "unit": "ops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (device-generated sequenced op streams, SURVEY.md §8(d) rules)",
+        "config": {"workload": f"{args.config}: {c['desc']}", "docs_per_gpu": c["docs"], "msgs_per_doc": c["ops"],
+                   "clients": c["clients"], "lag_max": c["lag"], "mix_ins_rem_ann": [c["ins"], c["rem"],
+                                                                                   100 - c["ins"] - c["rem"]],
+                   "parallelism": f"doc-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "kernel": "mt_replay_kernel", "kernel_ms": kern_s * 1e3,
+                     "bytes_per_launch": bytes_per_launch},
+        "hbm_gbps_algorithmic": achieved,
+        "parity": "status words clean" if ok else "STATUS ERROR",
+        "gen_seconds": gen_s,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(eng, c, MtGenParams, seed, args.cpu_seconds, threads)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

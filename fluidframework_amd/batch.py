@@ -220,8 +220,13 @@ class BatchBuilder:
         common = dict(client=client, seq=seq, ref_seq=ref, msn=msn, prop_id=-1)
         if t == MT_OP_INSERT:
             seg = op.get("seg")
-            if seg is None:
+            if seg is None and op.get("register") is not None:
                 raise NotImplementedError("register-based insert (client.ts:425-440) is not on the batch path")
+            if not seg:
+                # `if (op.seg)` is falsy for "" / missing: applyInsertOp returns without
+                # touching the tree (client.ts:423-444); only seq/msn advance.
+                self._emit(type=MT_OP_NOOP, flags=fl, **common)
+                return
             if "pos1" not in op:
                 raise NotImplementedError("relativePos1 inserts (mergeTree.ts:1949) are not on the batch path")
             pos2 = 0

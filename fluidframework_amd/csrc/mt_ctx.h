@@ -1,0 +1,32 @@
+// mt_ctx.h — engine context (one per GPU) shared by the backends and the ABI.
+#pragma once
+#include <string>
+#include <vector>
+#include "mt_replay.h"
+#include "mt_snapshot.h"
+
+struct mt_ctx {
+    int device = 0;
+    mt_limits lim{};
+    MtState S{};
+    MtNames names;
+    std::string err;
+    // device op batch (resident)
+    struct DevBuf { void* p = nullptr; size_t cap = 0; };
+    DevBuf b_doc, b_off, b_type, b_flags, b_client, b_seq, b_ref, b_msn, b_pos1, b_pos2, b_poff, b_plen, b_pid, b_pay,
+        b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3;
+    MtOps ops{};
+    uint32_t n_runs = 0;
+    MtGen gen{};
+    uint32_t gen_docs = 0;
+    float last_ms = 0.f;
+    void* stream = nullptr;
+    void* ev0 = nullptr;
+    void* ev1 = nullptr;
+    // host-side output arenas
+    std::string snap_arena;
+    std::vector<uint64_t> blob_off;
+    std::vector<uint32_t> blob_first;
+    std::vector<uint16_t> text_arena;
+    std::vector<uint64_t> text_off;
+};

@@ -1,0 +1,102 @@
+// mt_engine.hip — MI355X (gfx950) backend of the batched merge-tree engine.
+//
+// One 64-lane wavefront (one workgroup) per document run: documents are
+// independent, the ops inside a document are sequential.
+// All per-document state lives in HBM pools (mt_core.h MtState); per-wave
+// scratch (descent path, range-walk frames, scour hold list) lives in LDS.
+// This is the product: there is no CPU path behind any of these entry points.
+#include <hip/hip_runtime.h>
+#include "mt_ctx.h"
+
+// ------------------------------------------------------------- kernels ----
+__global__ __launch_bounds__(64) void mt_replay_kernel(MtState S, MtOps ops, MtGen gen) {
+    __shared__ MtScratch sc;
+    __shared__ int lastRef[64];
+    const uint32_t run = blockIdx.x;
+    const uint32_t doc = ops.doc_ids[run];
+    MtEng e;
+    e.bind(S, doc, &sc);
+    mt_replay_run(e, ops, run, doc, gen.enabled ? &gen : nullptr, lastRef);
+    e.store(doc);
+}
+__global__ __launch_bounds__(64) void mt_open_kernel(MtState S, uint32_t first) {
+    __shared__ MtScratch sc;
+    const uint32_t doc = first + blockIdx.x;
+    MtEng e;
+    e.bind(S, doc, &sc);
+    e.open();
+    e.store(doc);
+}
+__global__ __launch_bounds__(64) void mt_update_seq_kernel(MtState S, const uint32_t* docs, const int32_t* msn, const int32_t* seq) {
+    __shared__ MtScratch sc;
+    const uint32_t doc = docs[blockIdx.x];
+    MtEng e;
+    e.bind(S, doc, &sc);
+    if (e.curSeq > seq[blockIdx.x]) e.status |= MT_DS_ASSERT_SEQ;
+    else { e.curSeq = seq[blockIdx.x]; e.setMinSeq(msn[blockIdx.x]); }
+    e.store(doc);
+}
+__global__ __launch_bounds__(64) void mt_get_length_kernel(MtState S, const uint32_t* docs, const int32_t* ref, const int32_t* cli, int32_t* out) {
+    __shared__ MtScratch sc;
+    const uint32_t doc = docs[blockIdx.x];
+    MtEng e;
+    e.bind(S, doc, &sc);
+    const int l = e.perspectiveLength(ref[blockIdx.x], cli[blockIdx.x] < 0 ? 255 : cli[blockIdx.x]);
+    if (__lane_id() == 0) out[blockIdx.x] = l;
+}
+
+// ----------------------------------------------------- backend plumbing ----
+static int mtb_init(mt_ctx* c) {
+    if (hipSetDevice(c->device) != hipSuccess) { c->err = "hipSetDevice failed"; return 1; }
+    hipStream_t s; hipEvent_t a, b;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { c->err = "hipStreamCreate failed"; return 1; }
+    (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+    c->stream = s; c->ev0 = a; c->ev1 = b;
+    return 0;
+}
+static void mtb_fini(mt_ctx* c) {
+    if (c->stream) { (void)hipStreamSynchronize((hipStream_t)c->stream); (void)hipStreamDestroy((hipStream_t)c->stream); }
+    if (c->ev0) (void)hipEventDestroy((hipEvent_t)c->ev0);
+    if (c->ev1) (void)hipEventDestroy((hipEvent_t)c->ev1);
+}
+static int mtb_malloc(void** p, size_t n) { return hipMalloc(p, n) == hipSuccess ? 0 : 1; }
+static void mtb_free(void* p) { (void)hipFree(p); }
+static void mtb_memset(void* p, int v, size_t n) { (void)hipMemset(p, v, n); }
+static void mtb_h2d(mt_ctx* c, void* d, const void* s, size_t n) { (void)hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, (hipStream_t)c->stream); (void)hipStreamSynchronize((hipStream_t)c->stream); }
+static void mtb_d2h(mt_ctx* c, void* d, const void* s, size_t n) { (void)hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, (hipStream_t)c->stream); (void)hipStreamSynchronize((hipStream_t)c->stream); }
+static int mtb_sync(mt_ctx* c) {
+    hipError_t e = hipStreamSynchronize((hipStream_t)c->stream);
+    if (e != hipSuccess) { c->err = hipGetErrorString(e); return MT_E_HIP; }
+    if (c->ev1) { float ms = 0; if (hipEventElapsedTime(&ms, (hipEvent_t)c->ev0, (hipEvent_t)c->ev1) == hipSuccess) c->last_ms = ms; }
+    return MT_OK;
+}
+static int mtb_check(mt_ctx* c) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { c->err = hipGetErrorString(e); return MT_E_HIP; }
+    return MT_OK;
+}
+static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
+    if (n_runs == 0) return MT_OK;
+    hipStream_t s = (hipStream_t)c->stream;
+    (void)hipEventRecord((hipEvent_t)c->ev0, s);
+    hipLaunchKernelGGL(mt_replay_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, g);
+    (void)hipEventRecord((hipEvent_t)c->ev1, s);
+    return mtb_check(c);
+}
+static int mtb_launch_open(mt_ctx* c, uint32_t first, uint32_t n) {
+    hipLaunchKernelGGL(mt_open_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, first);
+    return mtb_check(c);
+}
+static int mtb_launch_update_seq(mt_ctx* c, const uint32_t* docs, const int32_t* msn, const int32_t* seq, uint32_t n) {
+    if (!n) return MT_OK;
+    hipLaunchKernelGGL(mt_update_seq_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, msn, seq);
+    return mtb_check(c);
+}
+static int mtb_launch_get_length(mt_ctx* c, const uint32_t* docs, const int32_t* ref, const int32_t* cli, int32_t* out, uint32_t n) {
+    if (!n) return MT_OK;
+    hipLaunchKernelGGL(mt_get_length_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, ref, cli, out);
+    return mtb_check(c);
+}
+
+#define MT_FN(name) mt_##name
+#include "mt_api_impl.h"

@@ -1,0 +1,260 @@
+// mt_snapshot.h — SnapshotV1 extraction + JSON emission from one document's
+// engine state (host side of mt_snapshot_v1 / mt_get_text / mt_dump_segments).
+//
+// Restates Client.snapshot -> SnapshotV1.extractSync/emit
+// (MT/client.ts:923-956, MT/snapshotV1.ts:70-256, MT/snapshotChunks.ts:125-149)
+// for the passive-observer path: walk segments in tree order
+// (walkAllSegments, mergeTree.ts:2998), elide rows removed at or below the MSN,
+// greedily coalesce rows at or below the MSN (TextSegment.canAppend +
+// matchProperties on clones), keep merge info for the rest, chunk at 10,000
+// characters, and serialize exactly as JSON.stringify does.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+#include <algorithm>
+#include <string>
+#include <vector>
+#include "mt_core.h"
+
+struct MtSnapView {                  // host copy of one document's state
+    MtDocHdr hdr;
+    const int *len, *seq, *rseq, *toff, *props, *parent;
+    const uint32_t* meta; const unsigned long long* ovl;
+    const MtBlk* blk; const uint16_t* text; const MtPSet* pset;
+};
+struct MtNames {                     // host-interned strings
+    std::vector<std::string> key_json;
+    std::vector<uint32_t> key_index;
+    std::vector<std::string> value_json;
+    std::vector<uint32_t> value_class;
+    std::vector<std::string> client_json;
+};
+
+namespace mtsnap {
+
+inline void put_utf8(std::string& o, uint32_t cp) {
+    if (cp < 0x80) o.push_back((char)cp);
+    else if (cp < 0x800) { o.push_back((char)(0xC0 | (cp >> 6))); o.push_back((char)(0x80 | (cp & 0x3F))); }
+    else if (cp < 0x10000) { o.push_back((char)(0xE0 | (cp >> 12))); o.push_back((char)(0x80 | ((cp >> 6) & 0x3F))); o.push_back((char)(0x80 | (cp & 0x3F))); }
+    else { o.push_back((char)(0xF0 | (cp >> 18))); o.push_back((char)(0x80 | ((cp >> 12) & 0x3F))); o.push_back((char)(0x80 | ((cp >> 6) & 0x3F))); o.push_back((char)(0x80 | (cp & 0x3F))); }
+}
+// JSON.stringify string quoting over UTF-16 code units (well-formed stringify).
+inline void quote16(std::string& o, const uint16_t* s, size_t n) {
+    static const char hx[] = "0123456789abcdef";
+    o.push_back('"');
+    for (size_t i = 0; i < n; i++) {
+        const uint16_t c = s[i];
+        if (c == '"') { o += "\\\""; continue; }
+        if (c == '\\') { o += "\\\\"; continue; }
+        if (c < 0x20) {
+            if (c == '\b') o += "\\b"; else if (c == '\f') o += "\\f"; else if (c == '\n') o += "\\n";
+            else if (c == '\r') o += "\\r"; else if (c == '\t') o += "\\t";
+            else { o += "\\u00"; o.push_back(hx[c >> 4]); o.push_back(hx[c & 15]); }
+            continue;
+        }
+        if (c >= 0xD800 && c <= 0xDBFF && i + 1 < n && s[i + 1] >= 0xDC00 && s[i + 1] <= 0xDFFF) {
+            put_utf8(o, 0x10000u + (((uint32_t)c - 0xD800u) << 10) + ((uint32_t)s[i + 1] - 0xDC00u));
+            i++; continue;
+        }
+        if (c >= 0xD800 && c <= 0xDFFF) {
+            o += "\\u"; o.push_back(hx[c >> 12]); o.push_back(hx[(c >> 8) & 15]); o.push_back(hx[(c >> 4) & 15]); o.push_back(hx[c & 15]);
+            continue;
+        }
+        put_utf8(o, c);
+    }
+    o.push_back('"');
+}
+inline void put_int(std::string& o, long long v) { o += std::to_string(v); }
+
+// A property map as JSON: array-index keys ascending, then insertion order.
+inline void props_json(std::string& o, const MtPSet& p, const MtNames& nm) {
+    int order[MT_PSK]; int m = 0;
+    int idx[MT_PSK]; int ni = 0;
+    for (int i = 0; i < p.n; i++) if (nm.key_index[p.key[i]] != 0xFFFFFFFFu) idx[ni++] = i;
+    std::sort(idx, idx + ni, [&](int a, int b) { return nm.key_index[p.key[a]] < nm.key_index[p.key[b]]; });
+    for (int i = 0; i < ni; i++) order[m++] = idx[i];
+    for (int i = 0; i < p.n; i++) if (nm.key_index[p.key[i]] == 0xFFFFFFFFu) order[m++] = i;
+    o.push_back('{');
+    for (int q = 0; q < m; q++) {
+        if (q) o.push_back(',');
+        const int i = order[q];
+        o += nm.key_json[p.key[i]]; o.push_back(':'); o += nm.value_json[p.val[i]];
+    }
+    o.push_back('}');
+}
+
+template <class F> void walk_all(const MtSnapView& v, int B, F& f) {
+    const MtBlk& b = v.blk[B];
+    for (int i = 0; i < b.n; i++) {
+        if (b.height == 0) f(b.c[i]);
+        else walk_all(v, b.c[i], f);
+    }
+}
+
+// TextSegment/Marker toJSONObject (textSegment.ts:48-54, mergeTree.ts:649-653)
+inline void seg_json(std::string& o, const MtSnapView& v, const MtNames& nm, int s, const uint16_t* txt, size_t tn) {
+    const bool marker = (v.meta[s] & MT_M_MARKER) != 0;
+    const int ps = v.props[s];
+    if (marker) {
+        o += "{\"marker\":{\"refType\":"; put_int(o, v.toff[s]); o += "}";
+        if (ps >= 0) { o += ",\"props\":"; props_json(o, v.pset[ps], nm); }
+        o += "}";
+    } else if (ps >= 0) {
+        o += "{\"text\":"; quote16(o, txt, tn); o += ",\"props\":"; props_json(o, v.pset[ps], nm); o += "}";
+    } else {
+        quote16(o, txt, tn);
+    }
+}
+
+inline bool props_match(const MtSnapView& v, const MtNames& nm, int a, int b) {
+    if (a == b) return true;
+    if (a < 0 || b < 0) return false;
+    const MtPSet& pa = v.pset[a]; const MtPSet& pb = v.pset[b];
+    if (pa.n != pb.n) return false;
+    for (int i = 0; i < pa.n; i++) {
+        bool f = false;
+        for (int j = 0; j < pb.n; j++) if (pb.key[j] == pa.key[i] && nm.value_class[pb.val[j]] == nm.value_class[pa.val[i]]) f = true;
+        if (!f) return false;
+    }
+    return true;
+}
+
+inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtNames& nm) {
+    const int minSeq = v.hdr.minSeq, curSeq = v.hdr.curSeq;
+    std::vector<std::string> segs; std::vector<long long> lens;
+    int prev = -1; std::vector<uint16_t> ptext; bool pcloned = false;
+    auto client = [&](int c) -> const std::string& {
+        static const std::string orig = "\"original\"";
+        return (c >= 0 && c < (int)nm.client_json.size()) ? nm.client_json[c] : orig;
+    };
+    auto pushPrev = [&]() {
+        if (prev < 0) return;
+        std::string o;
+        if (pcloned) { seg_json(o, v, nm, prev, ptext.data(), ptext.size()); lens.push_back((long long)ptext.size()); }
+        else { seg_json(o, v, nm, prev, v.text + v.toff[prev], (size_t)v.len[prev]); lens.push_back(v.len[prev]); }
+        segs.push_back(std::move(o));
+    };
+    auto extract = [&](int s) {
+        const bool removed = (v.meta[s] & MT_M_REMOVED) != 0;
+        if (removed && v.rseq[s] <= minSeq) return;                  // removed at/below the MSN: elided
+        if (v.seq[s] <= minSeq && !removed) {                         // coalesce candidates
+            if (prev < 0) { prev = s; pcloned = false; return; }
+            const bool pm = (v.meta[prev] & MT_M_MARKER) != 0, sm = (v.meta[s] & MT_M_MARKER) != 0;
+            bool ok = !pm && !sm;
+            if (ok) {
+                const uint16_t* pt = pcloned ? ptext.data() : v.text + v.toff[prev];
+                const size_t pl = pcloned ? ptext.size() : (size_t)v.len[prev];
+                ok = !(pl > 0 && pt[pl - 1] == '\n') && ((long long)pl <= MT_GRAN || v.len[s] <= MT_GRAN);
+            }
+            if (ok && props_match(v, nm, v.props[prev], v.props[s])) {
+                if (!pcloned) { ptext.assign(v.text + v.toff[prev], v.text + v.toff[prev] + v.len[prev]); pcloned = true; }
+                ptext.insert(ptext.end(), v.text + v.toff[s], v.text + v.toff[s] + v.len[s]);
+            } else { pushPrev(); prev = s; pcloned = false; }
+            return;
+        }
+        pushPrev(); prev = -1; pcloned = false;
+        std::string o = "{\"json\":";
+        const bool marker = (v.meta[s] & MT_M_MARKER) != 0;
+        seg_json(o, v, nm, s, marker ? nullptr : v.text + v.toff[s], marker ? 0 : (size_t)v.len[s]);
+        if (v.seq[s] > minSeq) { o += ",\"seq\":"; put_int(o, v.seq[s]); o += ",\"client\":"; o += client((int)(v.meta[s] & MT_M_CLIENT)); }
+        if (removed) { o += ",\"removedSeq\":"; put_int(o, v.rseq[s]); o += ",\"removedClient\":"; o += client((int)((v.meta[s] & MT_M_RCLIENT) >> 8)); }
+        o += "}";
+        segs.push_back(std::move(o)); lens.push_back(v.len[s]);
+    };
+    walk_all(v, v.hdr.root, extract);
+    pushPrev();
+    struct Chunk { size_t start, count; long long length; };
+    std::vector<Chunk> chunks; size_t total = 0; long long totalLen = 0;
+    do {
+        Chunk c{total, 0, 0};
+        while (c.length < 10000 && c.start + c.count < segs.size()) { c.length += lens[c.start + c.count]; c.count++; }
+        chunks.push_back(c); total += c.count; totalLen += c.length;
+    } while (total < segs.size());
+    std::vector<std::string> blobs;
+    for (size_t k = 0; k < chunks.size(); k++) {
+        const Chunk& c = chunks[k];
+        std::string o = "{\"version\":\"1\",\"segmentCount\":"; put_int(o, (long long)c.count);
+        o += ",\"length\":"; put_int(o, c.length); o += ",\"segments\":[";
+        for (size_t i = 0; i < c.count; i++) { if (i) o.push_back(','); o += segs[c.start + i]; }
+        o += "],\"startIndex\":"; put_int(o, (long long)c.start);
+        if (k == 0) {
+            o += ",\"headerMetadata\":{\"minSequenceNumber\":"; put_int(o, minSeq);
+            o += ",\"sequenceNumber\":"; put_int(o, curSeq);
+            o += ",\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+            for (size_t q = 1; q < chunks.size(); q++) { o += ",{\"id\":\"body_"; put_int(o, (long long)(q - 1)); o += "\"}"; }
+            o += "],\"totalLength\":"; put_int(o, totalLen); o += ",\"totalSegmentCount\":"; put_int(o, (long long)total); o += "}";
+        }
+        o += "}";
+        blobs.push_back(std::move(o));
+    }
+    return blobs;
+}
+
+inline uint64_t xxh64(const uint8_t* p, size_t len, uint64_t seed) {
+    const uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL, P3 = 1609587929392839161ULL,
+                   P4 = 9650029242287828579ULL, P5 = 2870177450012600261ULL;
+    auto rotl = [](uint64_t x, int r) { return (x << r) | (x >> (64 - r)); };
+    auto rd64 = [](const uint8_t* q) { uint64_t x; memcpy(&x, q, 8); return x; };
+    auto rd32 = [](const uint8_t* q) { uint32_t x; memcpy(&x, q, 4); return (uint64_t)x; };
+    auto rnd = [&](uint64_t acc, uint64_t in) { acc += in * P2; acc = rotl(acc, 31); return acc * P1; };
+    const uint8_t* e = p + len; uint64_t h;
+    if (len >= 32) {
+        uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+        do { v1 = rnd(v1, rd64(p)); v2 = rnd(v2, rd64(p + 8)); v3 = rnd(v3, rd64(p + 16)); v4 = rnd(v4, rd64(p + 24)); p += 32; } while (p + 32 <= e);
+        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+        for (uint64_t vv : {v1, v2, v3, v4}) { h ^= rnd(0, vv); h = h * P1 + P4; }
+    } else h = seed + P5;
+    h += (uint64_t)len;
+    while (p + 8 <= e) { h ^= rnd(0, rd64(p)); h = rotl(h, 27) * P1 + P4; p += 8; }
+    if (p + 4 <= e) { h ^= rd32(p) * P1; h = rotl(h, 23) * P2 + P3; p += 4; }
+    while (p < e) { h ^= (*p) * P5; h = rotl(h, 11) * P1; p++; }
+    h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+    return h;
+}
+inline uint64_t blobs_digest(const std::vector<std::string>& blobs) {
+    std::string buf;
+    for (const auto& b : blobs) { uint64_t n = b.size(); buf.append((const char*)&n, 8); buf += b; }
+    return xxh64((const uint8_t*)buf.data(), buf.size(), 0);
+}
+
+inline void observer_text(const MtSnapView& v, std::vector<uint16_t>& out) {
+    auto f = [&](int s) {
+        if (v.meta[s] & (MT_M_REMOVED | MT_M_MARKER)) return;
+        out.insert(out.end(), v.text + v.toff[s], v.text + v.toff[s] + v.len[s]);
+    };
+    walk_all(v, v.hdr.root, f);
+}
+
+inline uint32_t fnv1a(const std::string& s) { uint32_t h = 2166136261u; for (unsigned char c : s) { h ^= c; h *= 16777619u; } return h; }
+
+// 12 int32 per row, same layout as the oracle's ora_dump_segments.
+inline void dump_rows(const MtSnapView& v, const MtNames& nm, std::vector<int32_t>& rows) {
+    auto f = [&](int s) {
+        int32_t r[12];
+        const uint32_t mt = v.meta[s];
+        r[0] = v.len[s]; r[1] = v.seq[s]; r[2] = (int32_t)(mt & MT_M_CLIENT);
+        const bool removed = (mt & MT_M_REMOVED) != 0;
+        r[3] = removed ? v.rseq[s] : INT32_MIN; r[4] = removed ? (int32_t)((mt & MT_M_RCLIENT) >> 8) : -1;
+        r[5] = (int32_t)(v.ovl[s] & 0xFFFFFFFFull); r[6] = (int32_t)(v.ovl[s] >> 32);
+        if (v.props[s] >= 0) { std::string js; props_json(js, v.pset[v.props[s]], nm); r[7] = (int32_t)(fnv1a(js) & 0x7FFFFFFF); }
+        else r[7] = -1;
+        r[8] = (mt & MT_M_MARKER) ? v.toff[s] : -1;
+        int ix[MT_MAXH + 2]; int depth = 0;
+        int child = s; int p = v.parent[s]; bool leafLevel = true;
+        while (p >= 0) {
+            const MtBlk& b = v.blk[p];
+            int at = -1;
+            for (int i = 0; i < b.n; i++) if (b.c[i] == child) at = i;
+            ix[depth++] = at;
+            child = p; p = b.parent; leafLevel = false;
+        }
+        (void)leafLevel;
+        uint64_t path = 0;
+        for (int k = depth - 1; k >= 0; k--) path = (path << 3) | (uint64_t)(ix[k] & 7);
+        r[9] = depth; r[10] = (int32_t)(path & 0xFFFFFFFFull); r[11] = (int32_t)(path >> 32);
+        rows.insert(rows.end(), r, r + 12);
+    };
+    walk_all(v, v.hdr.root, f);
+}
+
+}  // namespace mtsnap

@@ -1,0 +1,128 @@
+// wave.h — the wave-collective vocabulary the merge-tree engine is written in.
+//
+// The engine runs one 64-lane wavefront per document.  Control flow is
+// wave-uniform ("scalar" code that every lane executes identically, so every
+// lane holds the same value and may store it), and data-parallel sections are
+// expressed with wave_map() over at most 64 items followed by collectives
+// (ballot, first, exclusive scan, sum, broadcast).  On gfx950 a LaneArr<T> is
+// the lane's own register and the collectives lower to ballot/DPP/ds_swizzle;
+// the same source also compiles for the host (MT_WAVE_EMULATION, tests only),
+// where a LaneArr<T> is a 64-element array.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define MT_HD __host__ __device__
+#define MT_INLINE __host__ __device__ __forceinline__
+#else
+#define MT_HD
+#define MT_INLINE inline
+#endif
+
+#define MT_WAVE 64
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// ---------------------------------------------------------------- device ----
+template <class T> using LaneArr = T;
+
+__device__ __forceinline__ int wave_lane() { return __lane_id(); }
+
+template <class F>
+__device__ __forceinline__ auto wave_map(int n, F f) -> decltype(f(0)) {
+    using T = decltype(f(0));
+    T v{};
+    const int k = __lane_id();
+    if (k < n) v = f(k);
+    return v;
+}
+template <class F>
+__device__ __forceinline__ void wave_for(int n, F f) {
+    const int k = __lane_id();
+    if (k < n) f(k);
+}
+template <class T> __device__ __forceinline__ T own(const T& a, int) { return a; }
+__device__ __forceinline__ int wave_at(int a, int j) { return __shfl(a, j); }
+__device__ __forceinline__ uint32_t wave_at(uint32_t a, int j) { return (uint32_t)__shfl((int)a, j); }
+__device__ __forceinline__ bool wave_at(bool a, int j) { return __shfl((int)a, j) != 0; }
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int wave_first(bool p) {
+    uint64_t b = __ballot(p);
+    return b ? __ffsll((unsigned long long)b) - 1 : -1;
+}
+__device__ __forceinline__ int wave_count(bool p) { return __popcll(__ballot(p)); }
+// exclusive prefix count of p over lanes below this one
+__device__ __forceinline__ int wave_rank(bool p) {
+    uint64_t b = __ballot(p);
+    return __popcll(b & ((1ull << __lane_id()) - 1ull));
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ int wave_excl_scan(int v) {
+    const int lane = __lane_id();
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    return x - v;
+}
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+#else
+// ------------------------------------------------------ host emulation ----
+#include <string.h>
+template <class T> struct LaneArr {
+    T v[MT_WAVE];
+};
+inline int wave_lane() { return 0; }
+
+template <class F>
+inline auto wave_map(int n, F f) -> LaneArr<decltype(f(0))> {
+    LaneArr<decltype(f(0))> a;
+    for (int k = 0; k < MT_WAVE; k++) a.v[k] = decltype(f(0)){};
+    for (int k = 0; k < n && k < MT_WAVE; k++) a.v[k] = f(k);
+    return a;
+}
+template <class F> inline void wave_for(int n, F f) {
+    for (int k = 0; k < n && k < MT_WAVE; k++) f(k);
+}
+template <class T> inline T own(const LaneArr<T>& a, int k) { return a.v[k]; }
+template <class T> inline T wave_at(const LaneArr<T>& a, int j) { return a.v[j]; }
+inline uint64_t wave_ballot(const LaneArr<bool>& p) {
+    uint64_t b = 0;
+    for (int k = 0; k < MT_WAVE; k++) if (p.v[k]) b |= 1ull << k;
+    return b;
+}
+inline int wave_first(const LaneArr<bool>& p) {
+    for (int k = 0; k < MT_WAVE; k++) if (p.v[k]) return k;
+    return -1;
+}
+inline int wave_count(const LaneArr<bool>& p) {
+    int c = 0;
+    for (int k = 0; k < MT_WAVE; k++) c += p.v[k] ? 1 : 0;
+    return c;
+}
+inline LaneArr<int> wave_rank(const LaneArr<bool>& p) {
+    LaneArr<int> r; int c = 0;
+    for (int k = 0; k < MT_WAVE; k++) { r.v[k] = c; c += p.v[k] ? 1 : 0; }
+    return r;
+}
+inline int wave_sum(const LaneArr<int>& a) {
+    int s = 0;
+    for (int k = 0; k < MT_WAVE; k++) s += a.v[k];
+    return s;
+}
+inline LaneArr<int> wave_excl_scan(const LaneArr<int>& a) {
+    LaneArr<int> r; int s = 0;
+    for (int k = 0; k < MT_WAVE; k++) { r.v[k] = s; s += a.v[k]; }
+    return r;
+}
+inline void wave_sync() {}
+#endif

@@ -1,0 +1,344 @@
+"""Python host of the MI355X merge-tree engine (ctypes over include/mtgpu.h).
+
+``Engine`` owns one engine context (one GPU).  ``MergeTreeClient`` mirrors the
+reference ``Client`` API for the passive-observer replay path
+(packages/dds/merge-tree/src/client.ts): ``applyMsg``, ``updateSeqNumbers``,
+``getLength``, ``getText``, ``snapshot``, ``getCurrentSeq`` — with the
+difference that messages are queued and applied in batches on the device
+(``flush``), many documents at a time.  Protocol violations that the reference
+reports by throwing (common-utils assert.ts:12-16) raise ``MergeTreeError``
+when the document's status is read.
+
+The product path has no CPU fallback: if ``libmtgpu.so`` (built by
+``__graft_entry__.build()``) is missing or no GPU is visible, constructing an
+``Engine`` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import jsjson
+from .batch import (BatchBuilder, ClientNames, MtGenParams, MtOpBatch, MtPropTable, OpBatch, PropTable,
+                    status_names)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmtgpu.so")
+
+
+class MergeTreeError(RuntimeError):
+    pass
+
+
+class MtLimits(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("max_docs", "rows_per_doc", "blocks_per_doc", "text_per_doc",
+                                               "propsets_per_doc", "heap_per_doc", "window_per_doc")]
+
+
+class MtDocCounters(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("ops", "msgs", "ins_units", "rows_rw", "depth", "scoured")]
+
+
+def _bind(lib, prefix: str):
+    P, U32, I32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32
+
+    def f(name, res, args):
+        fn = getattr(lib, prefix + name)
+        fn.restype, fn.argtypes = res, args
+        return fn
+
+    return dict(
+        create=f("create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(MtLimits), ctypes.POINTER(P)]),
+        destroy=f("destroy", None, [P]),
+        last_error=f("last_error", ctypes.c_char_p, [P]),
+        docs_open=f("docs_open", ctypes.c_int, [P, U32, U32]),
+        set_props=f("set_props", ctypes.c_int, [P, ctypes.POINTER(MtPropTable)]),
+        set_client_names=f("set_client_names", ctypes.c_int, [P, U32, P]),
+        apply_batch=f("apply_batch", ctypes.c_int, [P, ctypes.POINTER(MtOpBatch)]),
+        upload_batch=f("upload_batch", ctypes.c_int, [P, ctypes.POINTER(MtOpBatch)]),
+        replay_resident=f("replay_resident", ctypes.c_int, [P]),
+        last_replay_ms=f("last_replay_ms", ctypes.c_int, [P, ctypes.POINTER(ctypes.c_float)]),
+        update_seq=f("update_seq", ctypes.c_int, [P, U32, P, P, P]),
+        sync=f("sync", ctypes.c_int, [P]),
+        doc_status=f("doc_status", ctypes.c_int, [P, U32, P, P]),
+        doc_counters_get=f("doc_counters_get", ctypes.c_int, [P, U32, P, P]),
+        get_length=f("get_length", ctypes.c_int, [P, U32, P, P, P, P]),
+        snapshot_v1=f("snapshot_v1", ctypes.c_int, [P, U32, P, P, P, P, ctypes.POINTER(P), ctypes.POINTER(P),
+                                                    ctypes.POINTER(P)]),
+        get_text=f("get_text", ctypes.c_int, [P, U32, P, ctypes.POINTER(P), ctypes.POINTER(P)]),
+        dump_segments=f("dump_segments", ctypes.c_int, [P, U32, ctypes.POINTER(P), ctypes.POINTER(U32)]),
+        free=f("free", None, [P]),
+        generate=f("generate", ctypes.c_int, [P, ctypes.POINTER(MtGenParams)]),
+        generated_download=f("generated_download", ctypes.c_int, [P] + [P] * 12),
+        generated_to_resident=f("generated_to_resident", ctypes.c_int, [P]),
+    )
+
+
+def _u32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+def _i32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+class Engine:
+    """One engine context on one GPU (or, for tests, the host emulation lib)."""
+
+    def __init__(self, max_docs: int, rows_per_doc: int = 4096, blocks_per_doc: int = 0, text_per_doc: int = 0,
+                 propsets_per_doc: int = 0, heap_per_doc: int = 0, window_per_doc: int = 0, device: int = 0,
+                 lib_path: str | None = None, prefix: str = "mt_"):
+        path = lib_path or LIB_PATH
+        if not os.path.exists(path):
+            raise MergeTreeError(f"{path} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+        self.lib = ctypes.CDLL(path)
+        self.fn = _bind(self.lib, prefix)
+        self.max_docs = max_docs
+        lim = MtLimits(max_docs, rows_per_doc, blocks_per_doc, text_per_doc, propsets_per_doc, heap_per_doc,
+                       window_per_doc)
+        h = ctypes.c_void_p()
+        rc = self.fn["create"](device, ctypes.byref(lim), ctypes.byref(h))
+        self.h = h
+        if rc != 0:
+            err = self.fn["last_error"](h).decode() if h.value else "create failed"
+            raise MergeTreeError(f"mt_create failed ({rc}): {err}")
+        self.props = PropTable()
+        self.names = ClientNames()
+        self._props_uploaded = -1
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.fn["destroy"](self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise MergeTreeError(f"{what} failed ({rc}): {self.fn['last_error'](self.h).decode()}")
+
+    # ---- configuration ----
+    def open_docs(self, first: int, n: int):
+        self._check(self.fn["docs_open"](self.h, first, n), "mt_docs_open")
+
+    def upload_props(self, props: PropTable | None = None):
+        if props is not None:
+            self.props = props
+        self._props_c = self.props.to_c()
+        self._check(self.fn["set_props"](self.h, ctypes.byref(self._props_c)), "mt_set_props")
+        self._props_uploaded = len(self.props.sets)
+
+    def upload_names(self, literals: list[str] | None = None):
+        lits = literals if literals is not None else self.names.json_literals()
+        arr = (ctypes.c_char_p * max(1, len(lits)))(*[s.encode() for s in lits])
+        self._names_c = arr
+        self._check(self.fn["set_client_names"](self.h, len(lits), ctypes.cast(arr, ctypes.c_void_p)),
+                    "mt_set_client_names")
+
+    # ---- replay ----
+    def apply(self, batch: OpBatch):
+        if self._props_uploaded != len(self.props.sets):
+            self.upload_props()
+        self._batch = batch  # keep host arrays alive until sync
+        self._check(self.fn["apply_batch"](self.h, ctypes.byref(batch.to_c())), "mt_apply_batch")
+
+    def upload(self, batch: OpBatch):
+        if self._props_uploaded != len(self.props.sets):
+            self.upload_props()
+        self._batch = batch
+        self._check(self.fn["upload_batch"](self.h, ctypes.byref(batch.to_c())), "mt_upload_batch")
+
+    def replay_resident(self):
+        self._check(self.fn["replay_resident"](self.h), "mt_replay_resident")
+
+    def sync(self):
+        self._check(self.fn["sync"](self.h), "mt_sync")
+
+    def last_replay_ms(self) -> float:
+        v = ctypes.c_float()
+        self.fn["last_replay_ms"](self.h, ctypes.byref(v))
+        return float(v.value)
+
+    def generate(self, params: MtGenParams):
+        self._gen = params
+        self._check(self.fn["generate"](self.h, ctypes.byref(params)), "mt_generate")
+
+    def generated_download(self) -> OpBatch:
+        p = self._gen
+        n = p.n_docs * p.ops_per_doc
+        a = dict(type=np.zeros(n, np.uint8), flags=np.zeros(n, np.uint8), client=np.zeros(n, np.uint16),
+                 seq=np.zeros(n, np.int32), ref_seq=np.zeros(n, np.int32), msn=np.zeros(n, np.int32),
+                 pos1=np.zeros(n, np.int32), pos2=np.zeros(n, np.int32), payload_off=np.zeros(n, np.uint32),
+                 payload_len=np.zeros(n, np.uint32), prop_id=np.zeros(n, np.int32))
+        pay = np.zeros(max(1, n * p.ins_len_max), np.uint16)
+        self._check(self.fn["generated_download"](self.h, *(a[k].ctypes.data for k in (
+            "type", "flags", "client", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_off", "payload_len",
+            "prop_id")), pay.ctypes.data), "mt_generated_download")
+        offs = np.arange(p.n_docs + 1, dtype=np.uint32) * p.ops_per_doc
+        return OpBatch.from_arrays(np.arange(p.n_docs, dtype=np.uint32), offs, pay, **a)
+
+    def generated_to_resident(self):
+        self._check(self.fn["generated_to_resident"](self.h), "mt_generated_to_resident")
+
+    # ---- queries ----
+    def status(self, docs) -> np.ndarray:
+        d = _u32(docs)
+        out = np.zeros(len(d), np.uint32)
+        self._check(self.fn["doc_status"](self.h, len(d), d.ctypes.data, out.ctypes.data), "mt_doc_status")
+        return out
+
+    def counters(self, docs) -> dict:
+        d = _u32(docs)
+        out = (MtDocCounters * len(d))()
+        self._check(self.fn["doc_counters_get"](self.h, len(d), d.ctypes.data, ctypes.addressof(out)),
+                    "mt_doc_counters_get")
+        return {f: np.array([getattr(x, f) for x in out], np.uint64) for f, _ in MtDocCounters._fields_}
+
+    def update_seq(self, docs, msn, seq):
+        d, m, s = _u32(docs), _i32(msn), _i32(seq)
+        self._check(self.fn["update_seq"](self.h, len(d), d.ctypes.data, m.ctypes.data, s.ctypes.data),
+                    "mt_update_seq")
+
+    def get_length(self, docs, ref_seq, client) -> np.ndarray:
+        d, r, c = _u32(docs), _i32(ref_seq), _i32(client)
+        out = np.zeros(len(d), np.int32)
+        self._check(self.fn["get_length"](self.h, len(d), d.ctypes.data, r.ctypes.data, c.ctypes.data,
+                                          out.ctypes.data), "mt_get_length")
+        return out
+
+    def snapshot(self, docs, msn, seq):
+        """SnapshotV1 blobs per document: list of (list[bytes], digest)."""
+        d, m, s = _u32(docs), _i32(msn), _i32(seq)
+        dig = np.zeros(len(d), np.uint64)
+        arena, boff, bfirst = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        self._check(self.fn["snapshot_v1"](self.h, len(d), d.ctypes.data, m.ctypes.data, s.ctypes.data,
+                                           dig.ctypes.data, ctypes.byref(arena), ctypes.byref(boff),
+                                           ctypes.byref(bfirst)), "mt_snapshot_v1")
+        first = np.ctypeslib.as_array(ctypes.cast(bfirst, ctypes.POINTER(ctypes.c_uint32)), (len(d) + 1,)).copy()
+        nb = int(first[-1])
+        offs = np.ctypeslib.as_array(ctypes.cast(boff, ctypes.POINTER(ctypes.c_uint64)), (nb + 1,)).copy()
+        raw = ctypes.string_at(arena, int(offs[-1])) if offs[-1] else b""
+        out = []
+        for i in range(len(d)):
+            blobs = [raw[offs[j]:offs[j + 1]] for j in range(first[i], first[i + 1])]
+            out.append((blobs, int(dig[i])))
+        return out
+
+    def get_text(self, docs) -> list[str]:
+        d = _u32(docs)
+        arena, off = ctypes.c_void_p(), ctypes.c_void_p()
+        self._check(self.fn["get_text"](self.h, len(d), d.ctypes.data, ctypes.byref(arena), ctypes.byref(off)),
+                    "mt_get_text")
+        offs = np.ctypeslib.as_array(ctypes.cast(off, ctypes.POINTER(ctypes.c_uint64)), (len(d) + 1,)).copy()
+        raw = ctypes.string_at(arena, int(offs[-1]) * 2) if offs[-1] else b""
+        return [raw[2 * offs[i]:2 * offs[i + 1]].decode("utf-16-le", "surrogatepass") for i in range(len(d))]
+
+    def dump(self, doc: int) -> np.ndarray:
+        rows, n = ctypes.c_void_p(), ctypes.c_uint32()
+        self._check(self.fn["dump_segments"](self.h, doc, ctypes.byref(rows), ctypes.byref(n)), "mt_dump_segments")
+        a = np.frombuffer(ctypes.string_at(rows, n.value * 48), np.int32).reshape(-1, 12).copy()
+        self.fn["free"](rows)
+        return a
+
+
+@dataclass
+class _Pending:
+    msgs: list
+
+
+class MergeTreeClient:
+    """Drop-in subset of merge-tree ``Client`` (MT/client.ts:44) for a passive observer.
+
+    ``applyMsg`` queues; reads (``getLength``, ``getText``, ``snapshot``) flush the
+    queue of every client of the engine in one device batch.
+    """
+
+    def __init__(self, engine: Engine, doc_id: int, group: "ClientGroup"):
+        self.engine, self.doc_id, self.group = engine, doc_id, group
+        self.pending: list = []
+        self.current_seq = 0
+        self.min_seq = 0
+        self.longClientId = None
+
+    def startOrUpdateCollaboration(self, longClientId, minSeq=0, currentSeq=0, branchId=0):
+        self.longClientId = longClientId
+
+    def applyMsg(self, msg: dict):
+        self.pending.append(msg)
+
+    def updateSeqNumbers(self, min_seq: int, seq: int):
+        self.group.flush()
+        self.engine.update_seq([self.doc_id], [min_seq], [seq])
+        self._raise_status()
+
+    def _raise_status(self):
+        st = int(self.engine.status([self.doc_id])[0])
+        if st:
+            raise MergeTreeError(f"document {self.doc_id}: {', '.join(status_names(st))}")
+
+    def getLength(self) -> int:
+        self.group.flush()
+        self._raise_status()
+        return int(self.engine.get_length([self.doc_id], [0x7FFFFFFF], [-1])[0])
+
+    def getText(self) -> str:
+        self.group.flush()
+        self._raise_status()
+        return self.engine.get_text([self.doc_id])[0]
+
+    def snapshot(self, min_seq: int | None = None, seq: int | None = None) -> dict:
+        """ITree of the SnapshotV1 blobs (MT/snapshotV1.ts:98-163)."""
+        self.group.flush()
+        self._raise_status()
+        m = self.min_seq if min_seq is None else min_seq
+        s = self.current_seq if seq is None else seq
+        blobs, _ = self.engine.snapshot([self.doc_id], [m], [s])[0]
+        entries = []
+        for i, b in enumerate(blobs):
+            entries.append({"mode": "100644", "path": "header" if i == 0 else f"body_{i - 1}", "type": "Blob",
+                            "value": {"contents": b.decode("utf-8"), "encoding": "utf-8"}})
+        return {"entries": entries}
+
+    def getCurrentSeq(self) -> int:
+        return self.current_seq
+
+
+class ClientGroup:
+    """Many MergeTreeClients sharing one engine; flush() packs all queues into one batch."""
+
+    def __init__(self, engine: Engine):
+        self.engine = engine
+        self.clients: list[MergeTreeClient] = []
+
+    def new_client(self) -> MergeTreeClient:
+        d = len(self.clients)
+        if d >= self.engine.max_docs:
+            raise MergeTreeError("engine document capacity exhausted")
+        self.engine.open_docs(d, 1)
+        c = MergeTreeClient(self.engine, d, self)
+        self.clients.append(c)
+        return c
+
+    def flush(self):
+        busy = [c for c in self.clients if c.pending]
+        if not busy:
+            return
+        bb = BatchBuilder(self.engine.props, self.engine.names)
+        for c in busy:
+            bb.begin_doc(c.doc_id)
+            for m in c.pending:
+                bb.add_message(m)
+                c.current_seq = int(m["sequenceNumber"])
+                c.min_seq = max(c.min_seq, int(m["minimumSequenceNumber"]))
+            c.pending = []
+        batch = bb.build()
+        self.engine.upload_names()
+        self.engine.apply(batch)
+        self.engine.sync()

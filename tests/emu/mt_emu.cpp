@@ -1,0 +1,51 @@
+// mt_emu.cpp — TEST-ONLY host emulation of the engine (not shipped, not the product).
+//
+// Compiles the product's engine logic (fluidframework_amd/csrc/mt_core.h,
+// mt_replay.h, mt_api_impl.h) with g++, running each document's "wavefront" as a
+// host loop over emulated lanes (wave.h host branch).  CPU tests use it to check
+// the exact kernel logic against the oracle without a GPU; the GPU tests then
+// check the real gfx950 build (libmtgpu.so) the same way.  Exports emu_* symbols
+// only, so it can never be mistaken for the product library.
+#include <stdlib.h>
+#include <string.h>
+#include "../../fluidframework_amd/csrc/mt_ctx.h"
+
+static int mtb_init(mt_ctx*) { return 0; }
+static void mtb_fini(mt_ctx*) {}
+static int mtb_malloc(void** p, size_t n) { *p = calloc(1, n ? n : 16); return *p ? 0 : 1; }
+static void mtb_free(void* p) { free(p); }
+static void mtb_memset(void* p, int v, size_t n) { memset(p, v, n); }
+static void mtb_h2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
+static void mtb_d2h(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
+static int mtb_sync(mt_ctx*) { return MT_OK; }
+static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
+    for (uint32_t run = 0; run < n_runs; run++) {
+        MtScratch sc; int lastRef[64];
+        const uint32_t doc = c->ops.doc_ids[run];
+        MtEng e; e.bind(c->S, doc, &sc);
+        mt_replay_run(e, c->ops, run, doc, g.enabled ? &g : nullptr, lastRef);
+        e.store(doc);
+    }
+    return MT_OK;
+}
+static int mtb_launch_open(mt_ctx* c, uint32_t first, uint32_t n) {
+    for (uint32_t d = first; d < first + n; d++) { MtScratch sc; MtEng e; e.bind(c->S, d, &sc); e.open(); e.store(d); }
+    return MT_OK;
+}
+static int mtb_launch_update_seq(mt_ctx* c, const uint32_t* docs, const int32_t* msn, const int32_t* seq, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) {
+        MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc);
+        if (e.curSeq > seq[i]) e.status |= MT_DS_ASSERT_SEQ; else { e.curSeq = seq[i]; e.setMinSeq(msn[i]); }
+        e.store(docs[i]);
+    }
+    return MT_OK;
+}
+static int mtb_launch_get_length(mt_ctx* c, const uint32_t* docs, const int32_t* ref, const int32_t* cli, int32_t* out, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) {
+        MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc);
+        out[i] = e.perspectiveLength(ref[i], cli[i] < 0 ? 255 : cli[i]);
+    }
+    return MT_OK;
+}
+#define MT_FN(name) emu_##name
+#include "../../fluidframework_amd/csrc/mt_api_impl.h"
