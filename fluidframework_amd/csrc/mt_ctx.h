@@ -23,6 +23,7 @@ struct mt_ctx {
     void* stream = nullptr;
     void* ev0 = nullptr;
     void* ev1 = nullptr;
+    bool ev_pending = false;
     // host-side output arenas
     std::string snap_arena;
     std::vector<uint64_t> blob_off;

@@ -67,7 +67,12 @@ static void mtb_d2h(mt_ctx* c, void* d, const void* s, size_t n) { (void)hipMemc
 static int mtb_sync(mt_ctx* c) {
     hipError_t e = hipStreamSynchronize((hipStream_t)c->stream);
     if (e != hipSuccess) { c->err = hipGetErrorString(e); return MT_E_HIP; }
-    if (c->ev1) { float ms = 0; if (hipEventElapsedTime(&ms, (hipEvent_t)c->ev0, (hipEvent_t)c->ev1) == hipSuccess) c->last_ms = ms; }
+    if (c->ev_pending) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, (hipEvent_t)c->ev0, (hipEvent_t)c->ev1) == hipSuccess) c->last_ms = ms;
+        c->ev_pending = false;
+    }
+    (void)hipGetLastError();
     return MT_OK;
 }
 static int mtb_check(mt_ctx* c) {
@@ -78,22 +83,27 @@ static int mtb_check(mt_ctx* c) {
 static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     if (n_runs == 0) return MT_OK;
     hipStream_t s = (hipStream_t)c->stream;
+    (void)hipGetLastError();
     (void)hipEventRecord((hipEvent_t)c->ev0, s);
     hipLaunchKernelGGL(mt_replay_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, g);
     (void)hipEventRecord((hipEvent_t)c->ev1, s);
+    c->ev_pending = true;
     return mtb_check(c);
 }
 static int mtb_launch_open(mt_ctx* c, uint32_t first, uint32_t n) {
+    (void)hipGetLastError();
     hipLaunchKernelGGL(mt_open_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, first);
     return mtb_check(c);
 }
 static int mtb_launch_update_seq(mt_ctx* c, const uint32_t* docs, const int32_t* msn, const int32_t* seq, uint32_t n) {
     if (!n) return MT_OK;
+    (void)hipGetLastError();
     hipLaunchKernelGGL(mt_update_seq_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, msn, seq);
     return mtb_check(c);
 }
 static int mtb_launch_get_length(mt_ctx* c, const uint32_t* docs, const int32_t* ref, const int32_t* cli, int32_t* out, uint32_t n) {
     if (!n) return MT_OK;
+    (void)hipGetLastError();
     hipLaunchKernelGGL(mt_get_length_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, ref, cli, out);
     return mtb_check(c);
 }
