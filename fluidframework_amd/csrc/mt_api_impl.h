@@ -55,8 +55,7 @@ int MT_FN(create)(int device, const mt_limits* L, mt_ctx** out) {
 #define MT_ALLOC(field, T, count) \
     if (mtb_malloc(&p, sizeof(T) * (size_t)(count)) != 0) { c->err = "pool allocation failed: " #field; *out = c; return MT_E_OOM; } \
     S.field = (T*)p;
-    MT_ALLOC(seg_len, int, R) MT_ALLOC(seg_seq, int, R) MT_ALLOC(seg_rseq, int, R) MT_ALLOC(seg_meta, uint32_t, R)
-    MT_ALLOC(seg_ovl, unsigned long long, R) MT_ALLOC(seg_toff, int, R) MT_ALLOC(seg_props, int, R) MT_ALLOC(seg_parent, int, R) MT_ALLOC(seg_tcap, int, R)
+    MT_ALLOC(rows, MtRow, R)
     MT_ALLOC(blk, MtBlk, D * S.blkCap) MT_ALLOC(heap, MtHeapE, D * (S.heapCap + 1)) MT_ALLOC(win, int, D * S.winCap)
     MT_ALLOC(uid, int, D * S.winCap) MT_ALLOC(udelta, int, D * S.winCap) MT_ALLOC(uanc, int, D * S.winCap * MT_MAXH)
     MT_ALLOC(text, uint16_t, D * 2 * S.textCap) MT_ALLOC(pset, MtPSet, D * S.psetCap) MT_ALLOC(hdr, MtDocHdr, D)
@@ -70,11 +69,9 @@ int MT_FN(create)(int device, const mt_limits* L, mt_ctx** out) {
 void MT_FN(destroy)(mt_ctx* c) {
     if (!c) return;
     MtState& S = c->S;
-    void* ps[] = {S.seg_len, S.seg_seq, S.seg_rseq, S.seg_meta, S.seg_ovl, S.seg_toff, S.seg_props, S.seg_parent, S.seg_tcap,
-                  S.blk, S.heap, S.win, S.uid, S.udelta, S.uanc, S.text, S.pset, S.hdr, S.hold};
+    void* ps[] = {S.rows, S.blk, S.heap, S.win, S.uid, S.udelta, S.uanc, S.text, S.pset, S.hdr, S.hold};
     for (void* p : ps) if (p) mtb_free(p);
-    mt_ctx::DevBuf* bs[] = {&c->b_doc, &c->b_off, &c->b_type, &c->b_flags, &c->b_client, &c->b_seq, &c->b_ref, &c->b_msn,
-                            &c->b_pos1, &c->b_pos2, &c->b_poff, &c->b_plen, &c->b_pid, &c->b_pay, &c->b_pset_off,
+    mt_ctx::DevBuf* bs[] = {&c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_pset_off,
                             &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3};
     for (auto* b : bs) if (b->p) mtb_free(b->p);
     mtb_fini(c);
@@ -119,18 +116,20 @@ int MT_FN(set_client_names)(mt_ctx* c, uint32_t n, const char* const* cj) {
 static int mt_upload_ops(mt_ctx* c, const mt_op_batch* B) {
     const size_t N = B->n_ops, R = B->n_runs;
     int rc;
+    std::vector<MtOpRec> rec(N ? N : 1);
+    for (size_t i = 0; i < N; i++) {
+        MtOpRec& o = rec[i];
+        o.type = B->type[i]; o.flags = B->flags[i]; o.client = B->client[i]; o.seq = B->seq[i]; o.ref_seq = B->ref_seq[i];
+        o.msn = B->msn[i]; o.pos1 = B->pos1[i]; o.pos2 = B->pos2[i]; o.payload_off = B->payload_off[i];
+        o.payload_len = (uint16_t)B->payload_len[i]; o.prop_id = (int16_t)B->prop_id[i];
+    }
 #define UP(buf, src, bytes) if ((rc = mtb_ensure(c, c->buf, (bytes)))) return rc; if ((bytes) && (src)) mtb_h2d(c, c->buf.p, (src), (bytes));
-    UP(b_doc, B->doc_ids, 4 * R) UP(b_off, B->op_offsets, 4 * (R + 1)) UP(b_type, B->type, N) UP(b_flags, B->flags, N)
-    UP(b_client, B->client, 2 * N) UP(b_seq, B->seq, 4 * N) UP(b_ref, B->ref_seq, 4 * N) UP(b_msn, B->msn, 4 * N)
-    UP(b_pos1, B->pos1, 4 * N) UP(b_pos2, B->pos2, 4 * N) UP(b_poff, B->payload_off, 4 * N) UP(b_plen, B->payload_len, 4 * N)
-    UP(b_pid, B->prop_id, 4 * N) UP(b_pay, B->payload, 2 * B->payload_units)
+    UP(b_doc, B->doc_ids, 4 * R) UP(b_off, B->op_offsets, 4 * (R + 1)) UP(b_rec, rec.data(), sizeof(MtOpRec) * N)
+    UP(b_pay, B->payload, 2 * B->payload_units)
 #undef UP
     MtOps& o = c->ops;
-    o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.type = (uint8_t*)c->b_type.p;
-    o.flags = (uint8_t*)c->b_flags.p; o.client = (uint16_t*)c->b_client.p; o.seq = (int32_t*)c->b_seq.p;
-    o.ref_seq = (int32_t*)c->b_ref.p; o.msn = (int32_t*)c->b_msn.p; o.pos1 = (int32_t*)c->b_pos1.p;
-    o.pos2 = (int32_t*)c->b_pos2.p; o.payload_off = (uint32_t*)c->b_poff.p; o.payload_len = (uint32_t*)c->b_plen.p;
-    o.prop_id = (int32_t*)c->b_pid.p; o.payload = (uint16_t*)c->b_pay.p; o.n_runs = B->n_runs;
+    o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
+    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = B->n_runs;
     c->n_runs = B->n_runs;
     return MT_OK;
 }
@@ -146,6 +145,8 @@ static int mt_check_batch(mt_ctx* c, const mt_op_batch* B) {
         if (B->type[i] == MT_OP_INSERT && !(B->flags[i] & MT_OPF_MARKER) &&
             (uint64_t)B->payload_off[i] + B->payload_len[i] > B->payload_units) { c->err = "payload out of range"; return MT_E_INVALID; }
         if (B->prop_id[i] >= 0 && (uint32_t)B->prop_id[i] >= c->S.p_nsets) { c->err = "prop_id out of range (mt_set_props first)"; return MT_E_INVALID; }
+        if (B->prop_id[i] > 32767) { c->err = "more than 32767 property sets"; return MT_E_INVALID; }
+        if (B->payload_len[i] > 65535) { c->err = "insert longer than 65535 UTF-16 units"; return MT_E_INVALID; }
     }
     return MT_OK;
 }
@@ -227,13 +228,10 @@ int MT_FN(get_length)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t
 // Host copy of one document's state (for serialization).
 struct MtHostDoc {
     MtDocHdr hdr;
-    std::vector<int> len, seq, rseq, toff, props, parent;
-    std::vector<uint32_t> meta; std::vector<unsigned long long> ovl;
+    std::vector<MtRow> rows;
     std::vector<MtBlk> blk; std::vector<uint16_t> text; std::vector<MtPSet> pset;
     MtSnapView view() const {
-        MtSnapView v; v.hdr = hdr; v.len = len.data(); v.seq = seq.data(); v.rseq = rseq.data(); v.toff = toff.data();
-        v.props = props.data(); v.parent = parent.data(); v.meta = meta.data(); v.ovl = ovl.data();
-        v.blk = blk.data(); v.text = text.data(); v.pset = pset.data();
+        MtSnapView v; v.hdr = hdr; v.R = rows.data(); v.blk = blk.data(); v.text = text.data(); v.pset = pset.data();
         return v;
     }
 };
@@ -241,14 +239,8 @@ static int mt_download_doc(mt_ctx* c, uint32_t d, MtHostDoc& h) {
     const MtState& S = c->S;
     mtb_d2h(c, &h.hdr, S.hdr + d, sizeof(MtDocHdr));
     const size_t R = (size_t)h.hdr.rowTop, r0 = (size_t)d * S.rowCap;
-    h.len.resize(R + 1); h.seq.resize(R + 1); h.rseq.resize(R + 1); h.toff.resize(R + 1); h.props.resize(R + 1);
-    h.parent.resize(R + 1); h.meta.resize(R + 1); h.ovl.resize(R + 1);
-    if (R) {
-        mtb_d2h(c, h.len.data(), S.seg_len + r0, 4 * R); mtb_d2h(c, h.seq.data(), S.seg_seq + r0, 4 * R);
-        mtb_d2h(c, h.rseq.data(), S.seg_rseq + r0, 4 * R); mtb_d2h(c, h.toff.data(), S.seg_toff + r0, 4 * R);
-        mtb_d2h(c, h.props.data(), S.seg_props + r0, 4 * R); mtb_d2h(c, h.parent.data(), S.seg_parent + r0, 4 * R);
-        mtb_d2h(c, h.meta.data(), S.seg_meta + r0, 4 * R); mtb_d2h(c, h.ovl.data(), S.seg_ovl + r0, 8 * R);
-    }
+    h.rows.resize(R + 1);
+    if (R) mtb_d2h(c, h.rows.data(), S.rows + r0, sizeof(MtRow) * R);
     h.blk.resize((size_t)h.hdr.blkTop + 1);
     mtb_d2h(c, h.blk.data(), S.blk + (size_t)d * S.blkCap, sizeof(MtBlk) * (size_t)h.hdr.blkTop);
     h.text.resize((size_t)h.hdr.textTop + 1);
@@ -308,6 +300,16 @@ int MT_FN(dump_segments)(mt_ctx* c, uint32_t d, int32_t** rows, uint32_t* n_rows
 }
 void MT_FN(free)(void* p) { free(p); }
 
+// Diagnostic (MT_PROFILE builds fill it; product builds return zeros): phase cycles per doc.
+int MT_FN(prof_get)(mt_ctx* c, uint32_t n, unsigned long long* out) {
+    if (!c || n > c->S.maxDocs) return MT_E_INVALID;
+    mtb_sync(c);
+    std::vector<MtDocHdr> h(n);
+    mtb_d2h(c, h.data(), c->S.hdr, sizeof(MtDocHdr) * n);
+    for (uint32_t i = 0; i < n; i++) for (int k = 0; k < 8; k++) out[i * 8 + k] = h[i].prof[k];
+    return MT_OK;
+}
+
 int MT_FN(generate)(mt_ctx* c, const mt_gen_params* P) {
     if (!c || !P || P->n_docs == 0 || P->n_docs > c->S.maxDocs || P->clients == 0 || P->clients > 64 ||
         P->ins_len_max == 0 || P->rem_len_max == 0 || P->n_ann_sets == 0) return MT_E_INVALID;
@@ -316,9 +318,7 @@ int MT_FN(generate)(mt_ctx* c, const mt_gen_params* P) {
     const size_t PU = N * P->ins_len_max + 1;
     int rc;
 #define AL(buf, bytes) if ((rc = mtb_ensure(c, c->buf, (bytes)))) return rc;
-    AL(b_doc, 4ull * P->n_docs) AL(b_off, 4ull * (P->n_docs + 1)) AL(b_type, N) AL(b_flags, N) AL(b_client, 2 * N)
-    AL(b_seq, 4 * N) AL(b_ref, 4 * N) AL(b_msn, 4 * N) AL(b_pos1, 4 * N) AL(b_pos2, 4 * N) AL(b_poff, 4 * N)
-    AL(b_plen, 4 * N) AL(b_pid, 4 * N) AL(b_pay, 2 * PU)
+    AL(b_doc, 4ull * P->n_docs) AL(b_off, 4ull * (P->n_docs + 1)) AL(b_rec, sizeof(MtOpRec) * N) AL(b_pay, 2 * PU)
 #undef AL
     std::vector<uint32_t> docs(P->n_docs), off(P->n_docs + 1);
     for (uint32_t i = 0; i < P->n_docs; i++) { docs[i] = i; off[i] = (uint32_t)((size_t)i * P->ops_per_doc); }
@@ -326,11 +326,8 @@ int MT_FN(generate)(mt_ctx* c, const mt_gen_params* P) {
     mtb_h2d(c, c->b_doc.p, docs.data(), 4ull * P->n_docs);
     mtb_h2d(c, c->b_off.p, off.data(), 4ull * (P->n_docs + 1));
     MtOps& o = c->ops;
-    o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.type = (uint8_t*)c->b_type.p;
-    o.flags = (uint8_t*)c->b_flags.p; o.client = (uint16_t*)c->b_client.p; o.seq = (int32_t*)c->b_seq.p;
-    o.ref_seq = (int32_t*)c->b_ref.p; o.msn = (int32_t*)c->b_msn.p; o.pos1 = (int32_t*)c->b_pos1.p;
-    o.pos2 = (int32_t*)c->b_pos2.p; o.payload_off = (uint32_t*)c->b_poff.p; o.payload_len = (uint32_t*)c->b_plen.p;
-    o.prop_id = (int32_t*)c->b_pid.p; o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs;
+    o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
+    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs;
     c->n_runs = P->n_docs;
     rc = MT_FN(docs_open)(c, 0, P->n_docs);
     if (rc) return rc;
@@ -348,10 +345,13 @@ int MT_FN(generated_download)(mt_ctx* c, uint8_t* type, uint8_t* flags, uint16_t
     if (!c || !c->gen_docs) return MT_E_INVALID;
     mtb_sync(c);
     const size_t N = (size_t)c->gen_docs * c->gen.ops;
-    mtb_d2h(c, type, c->ops.type, N); mtb_d2h(c, flags, c->ops.flags, N); mtb_d2h(c, client, c->ops.client, 2 * N);
-    mtb_d2h(c, seq, c->ops.seq, 4 * N); mtb_d2h(c, ref, c->ops.ref_seq, 4 * N); mtb_d2h(c, msn, c->ops.msn, 4 * N);
-    mtb_d2h(c, pos1, c->ops.pos1, 4 * N); mtb_d2h(c, pos2, c->ops.pos2, 4 * N); mtb_d2h(c, poff, c->ops.payload_off, 4 * N);
-    mtb_d2h(c, plen, c->ops.payload_len, 4 * N); mtb_d2h(c, pid, c->ops.prop_id, 4 * N);
+    std::vector<MtOpRec> rec(N ? N : 1);
+    mtb_d2h(c, rec.data(), c->ops.rec, sizeof(MtOpRec) * N);
+    for (size_t i = 0; i < N; i++) {
+        const MtOpRec& o = rec[i];
+        type[i] = o.type; flags[i] = o.flags; client[i] = o.client; seq[i] = o.seq; ref[i] = o.ref_seq; msn[i] = o.msn;
+        pos1[i] = o.pos1; pos2[i] = o.pos2; poff[i] = o.payload_off; plen[i] = o.payload_len; pid[i] = o.prop_id;
+    }
     mtb_d2h(c, payload, c->ops.payload, 2 * (N * c->gen.ins_len_max));
     return MT_OK;
 }

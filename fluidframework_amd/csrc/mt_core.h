@@ -35,12 +35,35 @@
 #define MT_ZMAX 2                     // zamboniSegmentsMaxCount, MT/mergeTree.ts:1058
 #define MT_NOREM 0x7FFFFFFF           // removedSeq "undefined"
 
+// Phase profiling (diagnostic builds only, -DMT_PROFILE): shader-clock cycles
+// accumulated per phase into MtDocHdr.prof; never compiled into the product.
+#if defined(MT_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+#define MT_PB(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define MT_PE(i, v) prof[i] += __builtin_amdgcn_s_memtime() - (v)
+#else
+#define MT_PB(v)
+#define MT_PE(i, v)
+#endif
+enum { MT_PH_U = 0, MT_PH_SPLIT, MT_PH_INSERT, MT_PH_RANGE, MT_PH_ZAMBONI, MT_PH_OP, MT_PH_GEN, MT_PH_TEXT };
+
 #define MT_M_CLIENT 0x000000FFu
 #define MT_M_RCLIENT 0x0000FF00u
 #define MT_M_REMOVED 0x00010000u
 #define MT_M_MARKER 0x00020000u
 #define MT_M_INWIN 0x00040000u
 
+struct __attribute__((aligned(16))) MtRow {   // one 48-byte record per segment row
+    int len;         // cachedLength (UTF-16 units; 1 for a marker)
+    int seq;         // insertion seq
+    int rseq;        // removedSeq (MT_NOREM = undefined)
+    uint32_t meta;   // client | removedClient<<8 | REMOVED | MARKER | INWIN
+    int toff;        // text arena offset (marker: refType)
+    int props;       // property-set id, -1 = properties undefined
+    int parent;      // leaf block, -1 = unlinked
+    int tcap;        // owned text capacity at toff
+    unsigned long long ovl;  // removedClientOverlap bitmask
+    int pad[2];
+};
 struct __attribute__((aligned(16))) MtBlk {   // one 64-byte record per B-tree block
     int c[8];        // children: segment rows (height 0) or blocks
     int len;         // observer length (cachedLength, MT/mergeTree.ts:2770-2789)
@@ -63,11 +86,11 @@ struct __attribute__((aligned(16))) MtDocHdr {
     unsigned long long cnt[6];               // mt_doc_counters order
     int textHalf;                            // which half of the doc's text arena is live
     int pad[7];
+    unsigned long long prof[8];              // MT_PROFILE builds: s_memtime cycles per phase
 };
 
 struct MtState {                              // device pools, doc-major
-    int* seg_len; int* seg_seq; int* seg_rseq; uint32_t* seg_meta; unsigned long long* seg_ovl;
-    int* seg_toff; int* seg_props; int* seg_parent; int* seg_tcap;
+    MtRow* rows;
     MtBlk* blk; MtHeapE* heap; int* win; int* uid; int* udelta; int* uanc;
     uint16_t* text; MtPSet* pset; MtDocHdr* hdr; int* hold;   // text: 2 halves of textCap per doc
     uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap, holdCap, maxDocs;
@@ -76,10 +99,15 @@ struct MtState {                              // device pools, doc-major
     const uint8_t* p_falsy; const uint32_t* p_class; uint32_t p_nsets;
 };
 
+struct __attribute__((aligned(16))) MtOpRec {  // one 32-byte op record (mt_op_batch member, packed)
+    uint8_t type, flags; uint16_t client;
+    int32_t seq, ref_seq, msn, pos1, pos2;
+    uint32_t payload_off;
+    uint16_t payload_len; int16_t prop_id;
+};
 struct MtOps {                                // device copy of an mt_op_batch
     const uint32_t* doc_ids; const uint32_t* op_off;
-    uint8_t* type; uint8_t* flags; uint16_t* client; int32_t* seq; int32_t* ref_seq; int32_t* msn;
-    int32_t* pos1; int32_t* pos2; uint32_t* payload_off; uint32_t* payload_len; int32_t* prop_id;
+    MtOpRec* rec;
     uint16_t* payload;
     uint32_t n_runs;
 };
@@ -95,6 +123,7 @@ struct MtScratch {
     int pathB[MT_MAXH + 2], pathJ[MT_MAXH + 2];
     int fB[MT_MAXH + 2], fJ[MT_MAXH + 2], fS[MT_MAXH + 2], fE[MT_MAXH + 2], fL[MT_MAXH + 2], fD[MT_MAXH + 2];
     int hold[64];
+    int pk[MT_PSK], pv[MT_PSK];
     int lastOld, lastNew;
 };
 
@@ -114,7 +143,7 @@ MT_INLINE bool vis_rc(int seq, uint32_t meta, int rseq, unsigned long long ovl, 
     return true;
 }
 
-struct SegF { int id, len, seq, rseq, toff, props; uint32_t meta; };
+struct BlkH { int len, parent, n, height, scour; };
 struct ChildL { int len; bool tie; };
 struct WinI { int id; int delta; bool live; };
 
@@ -122,55 +151,74 @@ enum { MT_WALK_SPLIT = 0, MT_WALK_INSERT = 1 };
 enum { MT_W_OK = 0, MT_W_NOCHANGE = 1, MT_W_FAIL = 2 };
 enum { MT_MAP_REMOVE = 0, MT_MAP_ANNOTATE = 1 };
 
+// The wave's view of one document: doc-local pool pointers and the few global
+// parameters it needs (kept small: every field is wave-uniform and lives in SGPRs).
+struct MtEngParams {
+    uint32_t rowCap, heapCap, winCap, textCap, psetCap, p_nsets;
+    uint16_t* textBase;
+    const uint32_t* p_off; const uint16_t* p_key; const int32_t* p_val;
+    const uint8_t* p_falsy; const uint32_t* p_class;
+};
 struct MtEng {
-    MtState S;
+    MtEngParams S;
+    MtDocHdr* hdrp;
     // doc-local views
-    int *len, *seq, *rseq, *toff, *props, *parent, *tcap, *win, *uid, *udelta, *uanc;
-    uint32_t* meta; unsigned long long* ovl; MtBlk* blk; MtHeapE* heap; uint16_t* text; MtPSet* pset;
+    MtRow* R;
+    int *win, *uid, *udelta, *uanc;
+    MtBlk* blk; MtHeapE* heap; uint16_t* text; MtPSet* pset;
     MtScratch* sc;
     // uniform document state (MtDocHdr)
     int root, height, minSeq, curSeq, rowTop, blkTop, blkFree, heapN, winN, textTop, psetTop;
     uint32_t status;
-    unsigned long long cnt[6];
-    int textHalf; size_t docIdx;
+    unsigned long long c_ops, c_msgs, c_ins, c_rows, c_depth, c_scour;
+    unsigned long long prof[8];
+    int textHalf; uint32_t blkCap;
     int nU; bool uValid; int uRef, uCli;
+    int heapTop;                        // heap[1].maxSeq cached (INT_MAX when empty)
+    int gcEpoch;                        // bumped by every text compaction
+    int lastL, lastIdx; bool lastSplit; // landing spot of the last walk; did it split a block
 
     MT_HD void bind(const MtState& st, uint32_t d, MtScratch* scratch) {
-        S = st;
+        S.rowCap = st.rowCap; S.heapCap = st.heapCap; S.winCap = st.winCap; S.textCap = st.textCap;
+        S.psetCap = st.psetCap; S.p_nsets = st.p_nsets; S.p_off = st.p_off; S.p_key = st.p_key; S.p_val = st.p_val;
+        S.p_falsy = st.p_falsy; S.p_class = st.p_class; S.textBase = st.text + (size_t)d * 2 * st.textCap;
+        blkCap = st.blkCap; hdrp = st.hdr + d;
         const size_t r = (size_t)d * st.rowCap;
-        len = st.seg_len + r; seq = st.seg_seq + r; rseq = st.seg_rseq + r; meta = st.seg_meta + r;
-        ovl = st.seg_ovl + r; toff = st.seg_toff + r; props = st.seg_props + r; parent = st.seg_parent + r;
-        tcap = st.seg_tcap + r;
+        R = st.rows + r;
         blk = st.blk + (size_t)d * st.blkCap; heap = st.heap + (size_t)d * (st.heapCap + 1);
         win = st.win + (size_t)d * st.winCap; uid = st.uid + (size_t)d * st.winCap;
         udelta = st.udelta + (size_t)d * st.winCap; uanc = st.uanc + (size_t)d * st.winCap * MT_MAXH;
-        pset = st.pset + (size_t)d * st.psetCap; docIdx = d;
+        pset = st.pset + (size_t)d * st.psetCap;
         sc = scratch;
-        const MtDocHdr& h = st.hdr[d];
-        root = h.root; height = h.height; minSeq = h.minSeq; curSeq = h.curSeq; rowTop = h.rowTop;
-        blkTop = h.blkTop; blkFree = h.blkFree; heapN = h.heapN; winN = h.winN; textTop = h.textTop;
-        psetTop = h.psetTop; status = h.status; textHalf = h.textHalf;
-        text = st.text + ((size_t)d * 2 + (size_t)textHalf) * st.textCap;
-        for (int i = 0; i < 6; i++) cnt[i] = h.cnt[i];
+        const MtDocHdr& h = *hdrp;
+        root = uni(h.root); height = uni(h.height); minSeq = uni(h.minSeq); curSeq = uni(h.curSeq); rowTop = uni(h.rowTop);
+        blkTop = uni(h.blkTop); blkFree = uni(h.blkFree); heapN = uni(h.heapN); winN = uni(h.winN); textTop = uni(h.textTop);
+        psetTop = uni(h.psetTop); status = uni(h.status); textHalf = uni(h.textHalf);
+        text = S.textBase + (size_t)textHalf * st.textCap;
+        for (int i = 0; i < 8; i++) prof[i] = h.prof[i];
+        c_ops = h.cnt[0]; c_msgs = h.cnt[1]; c_ins = h.cnt[2]; c_rows = h.cnt[3]; c_depth = h.cnt[4]; c_scour = h.cnt[5];
         nU = 0; uValid = false; uRef = -1; uCli = -1;
+        heapTop = heapN > 0 ? uni(heap[1].maxSeq) : 0x7FFFFFFF;
+        lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0;
     }
-    MT_HD void store(uint32_t d) {
-        MtDocHdr& h = S.hdr[d];
+    MT_HD void store(uint32_t) {
+        MtDocHdr& h = *hdrp;
         h.root = root; h.height = height; h.minSeq = minSeq; h.curSeq = curSeq; h.rowTop = rowTop;
         h.blkTop = blkTop; h.blkFree = blkFree; h.heapN = heapN; h.winN = winN; h.textTop = textTop;
         h.psetTop = psetTop; h.status = status; h.textHalf = textHalf;
-        for (int i = 0; i < 6; i++) h.cnt[i] = cnt[i];
+        for (int i = 0; i < 8; i++) h.prof[i] = prof[i];
+        h.cnt[0] = c_ops; h.cnt[1] = c_msgs; h.cnt[2] = c_ins; h.cnt[3] = c_rows; h.cnt[4] = c_depth; h.cnt[5] = c_scour;
     }
     // Fresh empty collaborating document: root = empty block (MergeTree ctor :1105-1108,
     // startCollaboration :1243).
     MT_HD void open() {
         root = 0; height = 0; minSeq = 0; curSeq = 0; rowTop = 0; blkTop = 1; blkFree = -1;
-        heapN = 0; winN = 0; textTop = 0; psetTop = 0; status = 0; textHalf = 0;
-        text = S.text + docIdx * 2 * S.textCap;
-        for (int i = 0; i < 6; i++) cnt[i] = 0;
-        MtBlk b{}; b.len = 0; b.parent = -1; b.n = 0; b.height = 0; b.scour = -1;
-        for (int i = 0; i < 8; i++) b.c[i] = -1;
-        blk[0] = b;
+        heapN = 0; winN = 0; textTop = 0; psetTop = 0; status = 0; textHalf = 0; heapTop = 0x7FFFFFFF;
+        text = S.textBase;
+        c_ops = c_msgs = c_ins = c_rows = c_depth = c_scour = 0;
+        for (int i = 0; i < 8; i++) prof[i] = 0;
+        wave_for(8, [&](int i) MT_LAM { blk[0].c[i] = -1; });
+        blk[0].len = 0; blk[0].parent = -1; blk[0].n = 0; blk[0].height = 0; blk[0].scour = -1;
     }
 
     /* ---------------------------------------------------------- pools -- */
@@ -179,68 +227,82 @@ struct MtEng {
         return rowTop++;
     }
     MT_HD int allocBlock() {
-        if (blkFree >= 0) { int id = blkFree; blkFree = blk[id].parent; return id; }
-        if (blkTop >= (int)S.blkCap) { status |= MT_DS_OOM_BLOCKS; return -1; }
+        if (blkFree >= 0) { const int id = blkFree; blkFree = uni(blk[id].parent); return id; }
+        if (blkTop >= (int)blkCap) { status |= MT_DS_OOM_BLOCKS; return -1; }
         return blkTop++;
     }
     MT_HD void freeBlock(int id) { blk[id].parent = blkFree; blk[id].n = -1; blkFree = id; }
     MT_HD void winAdd(int s) {
-        if (meta[s] & MT_M_INWIN) return;
+        const uint32_t mt = uni(R[s].meta);
+        if (mt & MT_M_INWIN) return;
         if (winN >= (int)S.winCap) { status |= MT_DS_OOM_WINDOW; return; }
         win[winN++] = s;
-        meta[s] = meta[s] | MT_M_INWIN;
+        R[s].meta = mt | MT_M_INWIN;
     }
-    MT_HD SegF loadSeg(int s) const {
-        SegF f; f.id = s; f.len = len[s]; f.seq = seq[s]; f.rseq = rseq[s]; f.toff = toff[s]; f.props = props[s]; f.meta = meta[s];
-        return f;
+    // Scalar fields of a block (SGPRs) and its children (one per lane).
+    MT_HD BlkH head(int B) const {
+        BlkH h;
+        h.len = uni(blk[B].len); h.parent = uni(blk[B].parent); h.n = uni(blk[B].n);
+        h.height = uni(blk[B].height); h.scour = uni(blk[B].scour);
+        return h;
+    }
+    MT_HD LaneArr<int> kids(int B, int n) const { return wave_map(n, [&](int j) MT_LAM { return blk[B].c[j]; }); }
+    // Whole 64-byte block record in one transaction: lane i loads dword i;
+    // children stay in lanes 0..n-1, scalar fields are broadcast to SGPRs.
+    MT_HD LaneArr<int> blkLoad(int B, BlkH& h) const {
+        auto w = wave_map(16, [&](int i) MT_LAM { return ((const int*)&blk[B])[i]; });
+        h.len = wave_at(w, 8); h.parent = wave_at(w, 9); h.n = wave_at(w, 10); h.height = wave_at(w, 11); h.scour = wave_at(w, 12);
+        const int n = h.n;
+        return wave_map(8, [&](int j) MT_LAM { return j < n ? own(w, j) : -1; });
     }
     MT_HD int childObsLen(int h, int id) const {
-        if (h == 0) return (meta[id] & MT_M_REMOVED) ? 0 : len[id];
+        if (h == 0) return (R[id].meta & MT_M_REMOVED) ? 0 : R[id].len;
         return blk[id].len;
     }
-    MT_HD int sumObs(const MtBlk& b) const {
-        auto v = wave_map(b.n, [&](int j) { return childObsLen(b.height, pick8(b.c, j)); });
+    MT_HD int sumObs(int B, int n, int h) const {
+        auto v = wave_map(n, [&](int j) MT_LAM { return childObsLen(h, blk[B].c[j]); });
         return wave_sum(v);
     }
     MT_HD void setChildParent(int h, int id, int p) {
-        if (h == 0) parent[id] = p; else blk[id].parent = p;
+        if (h == 0) R[id].parent = p; else blk[id].parent = p;
     }
 
     /* ------------------------------------- perspective window (U set) -- */
     // Scan the window list: prune settled/unlinked rows (if prune) and collect
     // U = rows whose visibility differs between the observer and (r, c).
     MT_HD void computeU(int r, int c, bool prune) {
+        MT_PB(t0);
         int newWin = 0; nU = 0;
         for (int base = 0; base < winN; base += MT_WAVE) {
             const int m = (winN - base) < MT_WAVE ? (winN - base) : MT_WAVE;
-            auto wi = wave_map(m, [&](int k) {
+            auto wi = wave_map(m, [&](int k) MT_LAM {
                 WinI w; w.id = win[base + k];
                 const int s = w.id;
-                const uint32_t mt = meta[s];
+                const uint32_t mt = R[s].meta;
                 const bool removed = (mt & MT_M_REMOVED) != 0;
-                const int sq = seq[s], rs = rseq[s];
-                w.live = parent[s] >= 0 && (sq > minSeq || (removed && rs > minSeq));
-                const bool vr = vis_rc(sq, mt, rs, ovl[s], r, c);
+                const int sq = R[s].seq, rs = R[s].rseq;
+                w.live = R[s].parent >= 0 && (sq > minSeq || (removed && rs > minSeq));
+                const bool vr = vis_rc(sq, mt, rs, R[s].ovl, r, c);
                 const bool vo = !removed;
-                w.delta = w.live ? ((vr ? len[s] : 0) - (vo ? len[s] : 0)) : 0;
+                w.delta = w.live ? ((vr ? R[s].len : 0) - (vo ? R[s].len : 0)) : 0;
                 return w;
             });
-            auto live = wave_map(m, [&](int k) { return own(wi, k).live; });
+            auto live = wave_map(m, [&](int k) MT_LAM { return own(wi, k).live; });
             if (prune) {
                 auto rk = wave_rank(live);
                 const int cntLive = wave_count(live);
-                wave_for(m, [&](int k) {
+                wave_for(m, [&](int k) MT_LAM {
                     const WinI w = own(wi, k);
                     if (w.live) win[newWin + own(rk, k)] = w.id;
-                    else meta[w.id] = meta[w.id] & ~MT_M_INWIN;
+                    else R[w.id].meta = R[w.id].meta & ~MT_M_INWIN;
                 });
                 newWin += cntLive;
             }
-            auto du = wave_map(m, [&](int k) { return own(wi, k).delta != 0; });
+            auto du = wave_map(m, [&](int k) MT_LAM { return own(wi, k).delta != 0; });
             auto rk2 = wave_rank(du);
             const int cntU = wave_count(du);
             const int nu0 = nU;
-            wave_for(m, [&](int k) {
+            wave_for(m, [&](int k) MT_LAM {
                 if (own(du, k)) { uid[nu0 + own(rk2, k)] = own(wi, k).id; udelta[nu0 + own(rk2, k)] = own(wi, k).delta; }
             });
             nU += cntU;
@@ -251,8 +313,8 @@ struct MtEng {
         for (int base = 0; base < nU; base += MT_WAVE) {
             const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
             const int H = height;
-            wave_for(m, [&](int k) {
-                int a = parent[uid[base + k]];
+            wave_for(m, [&](int k) MT_LAM {
+                int a = R[uid[base + k]].parent;
                 for (int h = 0; h <= H; h++) {
                     uanc[(size_t)(base + k) * MT_MAXH + h] = a;
                     a = (a >= 0) ? blk[a].parent : -1;
@@ -261,25 +323,26 @@ struct MtEng {
         }
         wave_sync();
         uValid = true; uRef = r; uCli = c;
+        MT_PE(MT_PH_U, t0);
     }
     MT_HD int perspectiveLength(int r, int c) {
         if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
         int s = 0;
         for (int base = 0; base < nU; base += MT_WAVE) {
             const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
-            s += wave_sum(wave_map(m, [&](int k) { return udelta[base + k]; }));
+            s += wave_sum(wave_map(m, [&](int k) MT_LAM { return udelta[base + k]; }));
         }
-        return blk[root].len + s;
+        return uni(blk[root].len) + s;
     }
-    // Perspective lengths of block b's children (nodeLength, MT/mergeTree.ts:1652-1692).
-    MT_HD LaneArr<ChildL> childLens(const MtBlk& b, int r, int c) {
-        if (b.height == 0) {
-            return wave_map(b.n, [&](int j) {
-                const int s = pick8(b.c, j);
-                const uint32_t mt = meta[s];
-                const int rs = rseq[s];
+    // Perspective lengths of block B's children (nodeLength, MT/mergeTree.ts:1652-1692).
+    MT_HD LaneArr<ChildL> childLens(int B, const BlkH& h, const LaneArr<int>& ch, int r, int c) {
+        if (h.height == 0) {
+            return wave_map(h.n, [&](int j) MT_LAM {
+                const int s = own(ch, j);
+                const uint32_t mt = R[s].meta;
+                const int rs = R[s].rseq;
                 ChildL o;
-                o.len = vis_rc(seq[s], mt, rs, ovl[s], r, c) ? len[s] : 0;
+                o.len = vis_rc(R[s].seq, mt, rs, R[s].ovl, r, c) ? R[s].len : 0;
                 // breakTie for a leaf at pos 0 (MT/mergeTree.ts:2270-2292): false if a
                 // removal the author has seen (removedSeq <= refSeq); true otherwise
                 // (every row has an assigned seq on the replay path).
@@ -287,27 +350,20 @@ struct MtEng {
                 return o;
             });
         }
-        int corr[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) corr[j] = 0;
-        const int hc = b.height - 1;
+        auto corr = wave_map(h.n, [&](int j) MT_LAM { return 0; });
+        const int hc = h.height - 1;
         for (int base = 0; base < nU; base += MT_WAVE) {
             const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
-            auto mk = wave_map(m, [&](int k) {
-                const int a = uanc[(size_t)(base + k) * MT_MAXH + hc];
-                int idx = -1;
-#pragma unroll
-                for (int j = 0; j < 8; j++) if (j < b.n && a == b.c[j]) idx = j;
-                return idx;
-            });
-            auto dk = wave_map(m, [&](int k) { return udelta[base + k]; });
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                if (j < b.n) corr[j] += wave_sum(wave_map(m, [&](int k) { return own(mk, k) == j ? own(dk, k) : 0; }));
+            auto an = wave_map(m, [&](int k) MT_LAM { return uanc[(size_t)(base + k) * MT_MAXH + hc]; });
+            auto dk = wave_map(m, [&](int k) MT_LAM { return udelta[base + k]; });
+            for (int j = 0; j < h.n; j++) {
+                const int cj = wave_at(ch, j);
+                const int sj = wave_sum(wave_map(m, [&](int k) MT_LAM { return own(an, k) == cj ? own(dk, k) : 0; }));
+                if (sj) corr = wave_map(h.n, [&](int jj) MT_LAM { return own(corr, jj) + (jj == j ? sj : 0); });
             }
         }
-        return wave_map(b.n, [&](int j) {
-            ChildL o; o.len = blk[pick8(b.c, j)].len + pick8(corr, j); o.tie = true; return o;
+        return wave_map(h.n, [&](int j) MT_LAM {
+            ChildL o; o.len = blk[own(ch, j)].len + own(corr, j); o.tie = true; return o;
         });
     }
 
@@ -318,11 +374,13 @@ struct MtEng {
     MT_HD int splitRow(int s, int pos) {
         const int n = allocRow();
         if (n < 0) return -1;
-        len[n] = len[s] - pos; len[s] = pos;
-        seq[n] = seq[s]; rseq[n] = rseq[s]; meta[n] = meta[s] & ~MT_M_INWIN; ovl[n] = ovl[s];
-        toff[n] = toff[s] + pos; props[n] = props[s]; parent[n] = parent[s];
-        tcap[n] = tcap[s] - pos; tcap[s] = pos;   // each row owns [toff, toff+tcap) of the arena
-        if (meta[s] & MT_M_INWIN) winAdd(n);
+        const int ls = uni(R[s].len);
+        const uint32_t mt = uni(R[s].meta);
+        R[n].len = ls - pos; R[s].len = pos;
+        R[n].seq = R[s].seq; R[n].rseq = R[s].rseq; R[n].meta = mt & ~MT_M_INWIN; R[n].ovl = R[s].ovl;
+        R[n].toff = R[s].toff + pos; R[n].props = R[s].props; R[n].parent = R[s].parent;
+        R[n].tcap = R[s].tcap - pos; R[s].tcap = pos;   // each row owns [toff, toff+tcap) of the arena
+        if (mt & MT_M_INWIN) winAdd(n);
         return n;
     }
     // Insert `node` at child index idx of path level L, splitting full blocks
@@ -330,47 +388,43 @@ struct MtEng {
     // `delta` = observer length added under the path (0 for a row split).
     MT_HD void insertAtPath(int L, int idx, int node, int delta) {
         for (;;) {
-            const int B = sc->pathB[L];
-            MtBlk b = blk[B];
-            int nc[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) nc[i] = (i < idx) ? b.c[i] : ((i == idx) ? node : (i >= 1 ? b.c[i - 1] : -1));
-            const int n1 = b.n + 1;
-            setChildParent(b.height, node, B);
+            const int B = uni(sc->pathB[L]);
+            BlkH h;
+            auto cur = blkLoad(B, h);
+            auto prv = wave_from(cur, -1);
+            auto nc = wave_map(8, [&](int i) MT_LAM { return i < idx ? own(cur, i) : (i == idx ? node : own(prv, i)); });
+            const int n1 = h.n + 1;
+            setChildParent(h.height, node, B);
             if (n1 < MT_MAXN) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) b.c[i] = (i < n1) ? nc[i] : -1;
-                b.n = n1; b.len += delta;
-                blk[B] = b;
-                for (int l = L - 1; l >= 0; l--) blk[sc->pathB[l]].len += delta;
+                wave_for(8, [&](int i) MT_LAM { blk[B].c[i] = i < n1 ? own(nc, i) : -1; });
+                blk[B].n = n1; blk[B].len = h.len + delta;
+                for (int l = L - 1; l >= 0; l--) { const int pb = uni(sc->pathB[l]); blk[pb].len = uni(blk[pb].len) + delta; }
                 return;
             }
+            lastSplit = true;
             const int NB = allocBlock();
             if (NB < 0) return;
-            MtBlk nb{};
-#pragma unroll
-            for (int i = 0; i < 8; i++) { nb.c[i] = (i < 4) ? nc[i + 4] : -1; b.c[i] = (i < 4) ? nc[i] : -1; }
-            nb.n = 4; nb.height = b.height; nb.scour = -1; nb.parent = b.parent;
-            b.n = 4;
-            for (int i = 0; i < 4; i++) setChildParent(b.height, nb.c[i], NB);
+            auto hi = wave_from(nc, 4);
+            wave_for(8, [&](int i) MT_LAM {
+                blk[NB].c[i] = i < 4 ? own(hi, i) : -1;
+                blk[B].c[i] = i < 4 ? own(nc, i) : -1;
+            });
+            blk[NB].n = 4; blk[NB].height = h.height; blk[NB].scour = -1; blk[NB].parent = h.parent;
+            blk[B].n = 4;
+            wave_for(4, [&](int i) MT_LAM { setChildParent(h.height, own(hi, i), NB); });
             wave_sync();
-            nb.len = sumObs(nb);
-            b.len = sumObs(b);
-            blk[NB] = nb;
+            const int nbLen = sumObs(NB, 4, h.height), bLen = sumObs(B, 4, h.height);
+            blk[NB].len = nbLen; blk[B].len = bLen;
             if (L == 0) {
                 const int R = allocBlock();
-                if (R < 0) { blk[B] = b; return; }
-                MtBlk rb{};
-                rb.c[0] = B; rb.c[1] = NB;
-                for (int i = 2; i < 8; i++) rb.c[i] = -1;
-                rb.n = 2; rb.height = b.height + 1; rb.parent = -1; rb.scour = -1; rb.len = b.len + nb.len;
-                b.parent = R; blk[NB].parent = R;
-                blk[B] = b; blk[R] = rb;
-                root = R; height = rb.height;
+                if (R < 0) return;
+                wave_for(8, [&](int i) MT_LAM { blk[R].c[i] = i == 0 ? B : (i == 1 ? NB : -1); });
+                blk[R].n = 2; blk[R].height = h.height + 1; blk[R].parent = -1; blk[R].scour = -1; blk[R].len = bLen + nbLen;
+                blk[B].parent = R; blk[NB].parent = R;
+                root = R; height = h.height + 1;
                 return;
             }
-            blk[B] = b;
-            node = NB; idx = sc->pathJ[L - 1] + 1; L = L - 1;
+            node = NB; idx = uni(sc->pathJ[L - 1]) + 1; L = L - 1;
         }
     }
     // insertingWalk (MT/mergeTree.ts:2363-2493) for one remote op perspective.
@@ -378,31 +432,35 @@ struct MtEng {
         if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
         int B = root, L = 0, p = pos;
         for (;;) {
-            const MtBlk b = blk[B];
+            BlkH h;
+            auto ch = blkLoad(B, h);
             sc->pathB[L] = B;
-            auto ch = childLens(b, r, c);
-            auto lens = wave_map(b.n, [&](int j) { return own(ch, j).len; });
+            auto cl = childLens(B, h, ch, r, c);
+            auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
             auto pre = wave_excl_scan(lens);
             const int total = wave_sum(lens);
-            const bool interior = b.height > 0;
-            auto cond = wave_map(b.n, [&](int j) {
-                const int pj = p - own(pre, j), lj = own(ch, j).len;
+            const bool interior = h.height > 0;
+            auto cond = wave_map(h.n, [&](int j) MT_LAM {
+                const int pj = p - own(pre, j), lj = own(cl, j).len;
                 if (interior) return pj <= lj;                       // breakTie: blocks always
-                return pj < lj || (pj == lj && pj == 0 && own(ch, j).tie);
+                return pj < lj || (pj == lj && pj == 0 && own(cl, j).tie);
             });
             const int j = wave_first(cond);
             if (j >= 0) {
                 const int pj = p - wave_at(pre, j);
-                if (interior) { sc->pathJ[L] = j; L++; B = pick8(b.c, j); p = pj; continue; }
-                const int s = pick8(b.c, j);
+                if (interior) { sc->pathJ[L] = j; L++; B = wave_at(ch, j); p = pj; continue; }
+                const int s = wave_at(ch, j);
+                lastL = L; lastSplit = false;
                 if (kind == MT_WALK_SPLIT) {
-                    if (pj > 0 && !(meta[s] & MT_M_MARKER)) {
+                    if (pj > 0 && !(uni(R[s].meta) & MT_M_MARKER)) {
                         const int n = splitRow(s, pj);
                         if (n < 0) return MT_W_FAIL;
                         insertAtPath(L, j + 1, n, 0);
+                        lastIdx = j + 1;                      // an insert at pos lands before the new right half
                         uValid = false;
                         return MT_W_OK;
                     }
+                    lastIdx = j;
                     return MT_W_NOCHANGE;
                 }
                 insertAtPath(L, j, cand, candLen);           // onLeaf: candidate goes before the found row
@@ -410,8 +468,9 @@ struct MtEng {
                 return MT_W_OK;
             }
             if (p - total == 0) {
+                lastL = L; lastIdx = h.n; lastSplit = false;
                 if (kind == MT_WALK_SPLIT) return MT_W_NOCHANGE;
-                insertAtPath(L, b.n, cand, candLen);          // position used up at a block end: append
+                insertAtPath(L, h.n, cand, candLen);          // position used up at a block end: append
                 uValid = false;
                 return MT_W_OK;
             }
@@ -424,39 +483,46 @@ struct MtEng {
         if (heapN + 1 > (int)S.heapCap) { status |= MT_DS_OOM_HEAP; return; }
         int k = ++heapN;
         while (k > 1) {
-            const MtHeapE pe = heap[k >> 1];
-            if (pe.maxSeq > ms) { heap[k] = pe; k >>= 1; } else break;
+            const int pm = uni(heap[k >> 1].maxSeq);
+            if (pm > ms) { heap[k].seg = heap[k >> 1].seg; heap[k].maxSeq = pm; k >>= 1; } else break;
         }
-        MtHeapE e; e.seg = s; e.maxSeq = ms; heap[k] = e;
+        heap[k].seg = s; heap[k].maxSeq = ms;
+        if (k == 1) heapTop = ms;
     }
     MT_HD MtHeapE heapGet() {                                 // Heap.get + fixdown, collections.ts:230-268
-        const MtHeapE x = heap[1];
-        const MtHeapE last = heap[heapN];
+        MtHeapE x; x.seg = uni(heap[1].seg); x.maxSeq = uni(heap[1].maxSeq);
+        const int lseg = uni(heap[heapN].seg), lms = uni(heap[heapN].maxSeq);
         heapN--;
+        heapTop = 0x7FFFFFFF;
         if (heapN >= 1) {
             int k = 1;
+            heapTop = lms;
             while ((k << 1) <= heapN) {
                 int j = k << 1;
-                MtHeapE hj = heap[j];
-                if (j < heapN) { const MtHeapE hj1 = heap[j + 1]; if (hj.maxSeq > hj1.maxSeq) { j++; hj = hj1; } }
-                if (last.maxSeq <= hj.maxSeq) break;
-                heap[k] = hj; k = j;
+                int hs = uni(heap[j].seg), hm = uni(heap[j].maxSeq);
+                if (j < heapN) {
+                    const int hm1 = uni(heap[j + 1].maxSeq);
+                    if (hm > hm1) { j++; hs = uni(heap[j].seg); hm = hm1; }
+                }
+                if (lms <= hm) break;
+                if (k == 1) heapTop = hm;
+                heap[k].seg = hs; heap[k].maxSeq = hm; k = j;
             }
-            heap[k] = last;
+            heap[k].seg = lseg; heap[k].maxSeq = lms;
         }
         return x;
     }
     MT_HD void addToLRUSet(int s, int sq) {                   // MT/mergeTree.ts:1262-1272
-        const int p = parent[s];
-        if (blk[p].scour != 1 && sq > curSeq) { blk[p].scour = 1; heapAdd(s, sq); }
+        const int p = uni(R[s].parent);
+        if (uni(blk[p].scour) != 1 && sq > curSeq) { blk[p].scour = 1; heapAdd(s, sq); }
     }
     MT_HD bool propsMatch(int a, int b) {                      // matchProperties, MT/properties.ts:64-95
         if (a == b) return true;
         if (a < 0 || b < 0) return false;
-        const int na = pset[a].n, nb = pset[b].n;
+        const int na = uni(pset[a].n), nb = uni(pset[b].n);
         if (na != nb) return false;
-        auto ok = wave_map(na, [&](int k) {
-            const uint16_t key = pset[a].key[k];
+        auto ok = wave_map(na, [&](int k) MT_LAM {
+            const int key = pset[a].key[k];
             const uint32_t ca = S.p_class[pset[a].val[k]];
             bool f = false;
             for (int i = 0; i < nb; i++) if (pset[b].key[i] == key && S.p_class[pset[b].val[i]] == ca) f = true;
@@ -467,9 +533,9 @@ struct MtEng {
     MT_HD void copyText(int dst, int src, int n) {
         for (int base = 0; base < n; base += MT_WAVE) {
             const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
-            auto v = wave_map(m, [&](int k) { return (int)text[src + base + k]; });
+            auto v = wave_map(m, [&](int k) MT_LAM { return (int)text[src + base + k]; });
             wave_sync();
-            wave_for(m, [&](int k) { text[dst + base + k] = (uint16_t)own(v, k); });
+            wave_for(m, [&](int k) MT_LAM { text[dst + base + k] = (uint16_t)own(v, k); });
         }
         wave_sync();
     }
@@ -477,28 +543,30 @@ struct MtEng {
     // half of the document's arena (rows are immutable slices, so garbage from
     // relocated or unlinked rows accumulates until the half is full).
     MT_HD void textGC() {
+        MT_PB(t0);
         const int other = textHalf ^ 1;
-        uint16_t* dst = S.text + (docIdx * 2 + (size_t)other) * S.textCap;
+        uint16_t* dst = S.textBase + (size_t)other * S.textCap;
         int w = 0;
         for (int base = 0; base < rowTop; base += MT_WAVE) {
             const int m = (rowTop - base) < MT_WAVE ? (rowTop - base) : MT_WAVE;
-            auto ln = wave_map(m, [&](int k) {
+            auto ln = wave_map(m, [&](int k) MT_LAM {
                 const int s = base + k;
-                return (parent[s] >= 0 && !(meta[s] & MT_M_MARKER)) ? len[s] : 0;
+                return (R[s].parent >= 0 && !(R[s].meta & MT_M_MARKER)) ? R[s].len : 0;
             });
             auto pre = wave_excl_scan(ln);
             const int tot = wave_sum(ln);
-            wave_for(m, [&](int k) {
+            wave_for(m, [&](int k) MT_LAM {
                 const int s = base + k, l = own(ln, k);
                 if (l <= 0) return;
-                const int o = w + own(pre, k), t0 = toff[s];
+                const int o = w + own(pre, k), t0 = R[s].toff;
                 for (int q = 0; q < l; q++) dst[o + q] = text[t0 + q];
-                toff[s] = o; tcap[s] = l;
+                R[s].toff = o; R[s].tcap = l;
             });
             w += tot;
         }
         wave_sync();
-        textHalf = other; text = dst; textTop = w;
+        textHalf = other; text = dst; textTop = w; gcEpoch++;
+        MT_PE(MT_PH_TEXT, t0);
     }
     // Reserve n units at the top of the live half (compacting first if needed).
     MT_HD int textAlloc(int n) {
@@ -509,116 +577,143 @@ struct MtEng {
     // TextSegment.append (textSegment.ts:74-85) on the arena.  A row owns
     // [toff, toff + tcap); appends fill owned space, else the row moves to a new
     // region of twice the size (amortized O(appended chars)).
-    MT_HD void appendText(int pv, int s) {
-        const int lp = len[pv], ls = len[s];
-        if (toff[s] == toff[pv] + lp && tcap[pv] == lp) { len[pv] = lp + ls; tcap[pv] = lp + tcap[s]; return; }
-        if (lp + ls <= tcap[pv]) { copyText(toff[pv] + lp, toff[s], ls); len[pv] = lp + ls; return; }
+    // Returns the new (toff, tcap) of pv through references; lengths known by the caller.
+    MT_HD void appendText(int pv, int lp, int& tp, int& cp, int s, int ls, int ts, int cs) {
+        if (ts == tp + lp && cp == lp) { R[pv].len = lp + ls; cp = lp + cs; R[pv].tcap = cp; return; }
+        if (lp + ls <= cp) { copyText(tp + lp, ts, ls); R[pv].len = lp + ls; return; }
         int nc = 2 * (lp + ls); if (nc < 16) nc = 16;
-        if (textTop + nc > (int)S.textCap) { textGC(); nc = lp + ls; }
+        if (textTop + nc > (int)S.textCap) { textGC(); nc = lp + ls; tp = uni(R[pv].toff); ts = uni(R[s].toff); }
         const int o = textAlloc(nc);
         if (o < 0) return;
-        copyText(o, toff[pv], lp); copyText(o + lp, toff[s], ls);
-        toff[pv] = o; tcap[pv] = nc; len[pv] = lp + ls;
+        copyText(o, tp, lp); copyText(o + lp, ts, ls);
+        R[pv].toff = o; R[pv].tcap = nc; R[pv].len = lp + ls;
+        tp = o; cp = nc;
     }
     // scourNode for a block of rows (MT/mergeTree.ts:1278-1356); kept children
-    // are appended to sc->hold[*nh].
-    MT_HD void scourLeaf(const MtBlk& b, int* nh) {
-        auto f = wave_map(b.n, [&](int j) { return pick8(b.c, j); });
-        int prev = -1, prevLen = 0, prevToff = 0, prevProps = -1; bool prevMarker = false;
-        for (int k = 0; k < b.n; k++) {
+    // are appended to sc->hold starting at nh; returns the new hold count.
+    MT_HD int scourLeaf(int B, int n, int nh) {
+        // Prefetch every child's fields (and the last text unit) in parallel, then
+        // run the sequential merge chain on registers.
+        auto f = kids(B, n);
+        auto fm = wave_map(n, [&](int j) MT_LAM { return (int)R[own(f, j)].meta; });
+        auto fs = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].seq; });
+        auto fr = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].rseq; });
+        auto fl = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].len; });
+        auto fp = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].props; });
+        auto ft = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].toff; });
+        auto fc = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].tcap; });
+        auto fe = wave_map(n, [&](int j) MT_LAM {
+            const int l = own(fl, j);
+            return (!(own(fm, j) & MT_M_MARKER) && l > 0) ? (int)text[own(ft, j) + l - 1] : 0;
+        });
+        int prev = -1, prevLen = 0, prevToff = 0, prevCap = 0, prevProps = -1, prevLast = 0; bool prevMarker = false;
+        int epoch = gcEpoch;
+        for (int k = 0; k < n; k++) {
+            if (epoch != gcEpoch) {                                // text moved: refresh prefetched offsets
+                ft = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].toff; });
+                fc = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].tcap; });
+                if (prev >= 0) { prevToff = uni(R[prev].toff); prevCap = uni(R[prev].tcap); }
+                epoch = gcEpoch;
+            }
             const int s = wave_at(f, k);
-            const uint32_t mt = meta[s];
-            cnt[5]++;
+            const uint32_t mt = (uint32_t)wave_at(fm, k);
+            c_scour++;
             if (mt & MT_M_REMOVED) {
-                if (rseq[s] > minSeq) sc->hold[(*nh)++] = s;
-                else parent[s] = -1;                               // UNLINK
+                if (wave_at(fr, k) > minSeq) sc->hold[nh++] = s;
+                else R[s].parent = -1;                             // UNLINK
                 prev = -1;
-            } else if (seq[s] <= minSeq) {
-                const int ls = len[s];
-                bool can = prev >= 0 && !prevMarker && !(mt & MT_M_MARKER) &&
-                           text[prevToff + prevLen - 1] != (uint16_t)'\n' &&
+            } else if (wave_at(fs, k) <= minSeq) {
+                const int ls = wave_at(fl, k), ps = wave_at(fp, k);
+                bool can = prev >= 0 && !prevMarker && !(mt & MT_M_MARKER) && prevLast != (int)'\n' &&
                            (prevLen <= MT_GRAN || ls <= MT_GRAN) && ls > 0;
-                if (can) can = propsMatch(prevProps, props[s]);
+                if (can) can = propsMatch(prevProps, ps);
                 if (can) {
-                    appendText(prev, s);
-                    parent[s] = -1;
-                    prevLen = len[prev]; prevToff = toff[prev];
+                    appendText(prev, prevLen, prevToff, prevCap, s, ls, wave_at(ft, k), wave_at(fc, k));
+                    R[s].parent = -1;
+                    prevLen += ls; prevLast = wave_at(fe, k);
                 } else {
-                    sc->hold[(*nh)++] = s;
+                    sc->hold[nh++] = s;
                     prev = (ls > 0) ? s : -1;
-                    prevLen = ls; prevToff = toff[s]; prevProps = props[s]; prevMarker = (mt & MT_M_MARKER) != 0;
+                    prevLen = ls; prevToff = wave_at(ft, k); prevCap = wave_at(fc, k); prevProps = ps;
+                    prevMarker = (mt & MT_M_MARKER) != 0; prevLast = wave_at(fe, k);
                 }
             } else {
-                sc->hold[(*nh)++] = s;
+                sc->hold[nh++] = s;
                 prev = -1;
             }
         }
         wave_sync();
+        return nh;
     }
     MT_HD void updatePathLens(int B) {                        // blockUpdatePathLengths(..., newStructure)
         while (B >= 0) {
-            MtBlk b = blk[B];
-            const int l = sumObs(b);
-            blk[B].len = l;
-            B = b.parent;
+            const BlkH h = head(B);
+            blk[B].len = sumObs(B, h.n, h.height);
+            B = h.parent;
         }
     }
     MT_HD void packParent(int P) {                            // MT/mergeTree.ts:1359-1410
         for (;;) {
-            MtBlk pb = blk[P];
-            int nh = 0; int ch = 0;
-            for (int i = 0; i < pb.n; i++) {
-                const int cb = pick8(pb.c, i);
-                const MtBlk cbk = blk[cb];
-                ch = cbk.height;
-                if (cbk.height == 0) scourLeaf(cbk, &nh);
-                else for (int k = 0; k < cbk.n; k++) sc->hold[nh++] = pick8(cbk.c, k);
+            BlkH ph;
+            auto pch = blkLoad(P, ph);
+            int nh = 0, chh = 0;
+            for (int i = 0; i < ph.n; i++) {
+                const int cb = wave_at(pch, i);
+                const BlkH bh = head(cb);
+                chh = bh.height;
+                if (bh.height == 0) nh = scourLeaf(cb, bh.n, nh);
+                else {
+                    const int base = nh;
+                    wave_for(bh.n, [&](int k) MT_LAM { sc->hold[base + k] = blk[cb].c[k]; });
+                    nh += bh.n;
+                }
                 freeBlock(cb);
             }
+            wave_sync();
             int cc = nh / (MT_MAXN / 2); if (cc > MT_MAXN - 1) cc = MT_MAXN - 1; if (cc < 1) cc = 1;
             const int base = nh / cc; int extra = nh % cc; int rd = 0;
-            int packed[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) packed[i] = -1;
+            auto packed = wave_map(8, [&](int i) MT_LAM { return -1; });
             for (int ni = 0; ni < cc; ni++) {
                 int cntc = base; if (extra > 0) { cntc++; extra--; }
                 const int NB = allocBlock();
                 if (NB < 0) return;
-                MtBlk nb{};
-                for (int i = 0; i < 8; i++) nb.c[i] = -1;
-                for (int i = 0; i < cntc; i++) { nb.c[i] = sc->hold[rd + i]; setChildParent(ch, sc->hold[rd + i], NB); }
+                const int r0 = rd;
+                wave_for(8, [&](int i) MT_LAM { blk[NB].c[i] = i < cntc ? sc->hold[r0 + i] : -1; });
+                wave_for(cntc, [&](int i) MT_LAM { setChildParent(chh, sc->hold[r0 + i], NB); });
                 rd += cntc;
-                nb.n = cntc; nb.height = ch; nb.parent = P; nb.scour = -1;
+                blk[NB].n = cntc; blk[NB].height = chh; blk[NB].parent = P; blk[NB].scour = -1;
                 wave_sync();
-                nb.len = sumObs(nb);
-                blk[NB] = nb;
-                for (int i = 0; i < 8; i++) if (i == ni) packed[i] = NB;
+                blk[NB].len = sumObs(NB, cntc, chh);
+                packed = wave_map(8, [&](int i) MT_LAM { return i == ni ? NB : own(packed, i); });
             }
-#pragma unroll
-            for (int i = 0; i < 8; i++) pb.c[i] = packed[i];
-            pb.n = cc;
-            blk[P] = pb;
-            if (cc < MT_MAXN / 2 && pb.parent >= 0) { P = pb.parent; continue; }
+            wave_for(8, [&](int i) MT_LAM { blk[P].c[i] = own(packed, i); });
+            blk[P].n = cc;
+            wave_sync();
+            if (cc < MT_MAXN / 2 && ph.parent >= 0) { P = ph.parent; continue; }
             updatePathLens(P);
             return;
         }
     }
     MT_HD void zamboni() {                                    // MT/mergeTree.ts:1412-1468
+        MT_PB(t0);
+        zamboniInner();
+        MT_PE(MT_PH_ZAMBONI, t0);
+    }
+    MT_HD void zamboniInner() {
         uValid = false;
         for (int i = 0; i < MT_ZMAX; i++) {
-            if (heapN == 0 || heap[1].maxSeq > minSeq) break;
+            if (heapN == 0 || heapTop > minSeq) break;
             const MtHeapE e = heapGet();
-            const int p = parent[e.seg];
-            if (p >= 0 && blk[p].scour != 0) {
-                MtBlk b = blk[p];
-                int nh = 0;
-                scourLeaf(b, &nh);
+            const int p = uni(R[e.seg].parent);
+            if (p >= 0 && uni(blk[p].scour) != 0) {
+                const BlkH h = head(p);
+                const int nh = scourLeaf(p, h.n, 0);
                 blk[p].scour = 0;
-                if (nh < b.n) {
-                    for (int j = 0; j < 8; j++) b.c[j] = (j < nh) ? sc->hold[j] : -1;
-                    b.n = nh; b.scour = 0;
-                    blk[p] = b;
-                    if (nh < MT_MAXN / 2 && b.parent >= 0) packParent(b.parent);
+                if (nh < h.n) {
+                    wave_for(8, [&](int j) MT_LAM { blk[p].c[j] = j < nh ? sc->hold[j] : -1; });
+                    blk[p].n = nh;
+                    wave_sync();
+                    if (nh < MT_MAXN / 2 && h.parent >= 0) packParent(h.parent);
                     else updatePathLens(p);
                 }
             }
@@ -635,44 +730,57 @@ struct MtEng {
     // remote addProperties rules (segmentPropertiesManager.ts:43-110): rewrite
     // first deletes keys whose new value is falsy or absent; then each key in
     // Object.keys order is deleted (null) or set (existing keys keep position).
+    // Keys live one per lane (insertion order).
     MT_HD int applyPropSet(int old, int opset, bool rewrite) {
         if (opset < 0 || opset >= (int)S.p_nsets) { status |= MT_DS_UNSUPPORTED; return old; }
         if (psetTop >= (int)S.psetCap) { status |= MT_DS_OOM_PROPS; return old; }
         const int id = psetTop++;
-        int n = 0;
-        uint16_t k[MT_PSK]; int32_t v[MT_PSK];
-        for (int i = 0; i < MT_PSK; i++) { k[i] = 0; v[i] = 0; }
-        if (old >= 0) {
-            n = pset[old].n;
-            for (int i = 0; i < MT_PSK; i++) { k[i] = pset[old].key[i]; v[i] = pset[old].val[i]; }
+        int n = old >= 0 ? uni(pset[old].n) : 0;
+        auto kk = wave_map(n, [&](int i) MT_LAM { return (int)pset[old].key[i]; });
+        auto vv = wave_map(n, [&](int i) MT_LAM { return (int)pset[old].val[i]; });
+        const int o0 = uni((int)S.p_off[opset]), o1 = uni((int)S.p_off[opset + 1]);
+        if (rewrite && n > 0) {
+            auto keep = wave_map(n, [&](int i) MT_LAM {
+                const int key = own(kk, i);
+                bool kp = false;
+                for (int q = o0; q < o1; q++) if ((int)S.p_key[q] == key) { const int nv = S.p_val[q]; kp = nv >= 0 && !S.p_falsy[nv]; }
+                return kp;
+            });
+            auto rk = wave_rank(keep);
+            const int cntk = wave_count(keep);
+            wave_for(n, [&](int i) MT_LAM { if (own(keep, i)) { sc->pk[own(rk, i)] = own(kk, i); sc->pv[own(rk, i)] = own(vv, i); } });
+            wave_sync();
+            n = cntk;
+            kk = wave_map(n, [&](int i) MT_LAM { return sc->pk[i]; });
+            vv = wave_map(n, [&](int i) MT_LAM { return sc->pv[i]; });
+            wave_sync();
         }
-        const uint32_t o0 = S.p_off[opset], o1 = S.p_off[opset + 1];
-        if (rewrite) {
-            int w = 0;
-            for (int i = 0; i < MT_PSK; i++) {
-                if (i >= n) break;
-                bool keep = false;
-                for (uint32_t q = o0; q < o1; q++) if (S.p_key[q] == k[i]) { const int32_t nv = S.p_val[q]; keep = nv >= 0 && !S.p_falsy[nv]; }
-                if (keep) { k[w] = k[i]; v[w] = v[i]; w++; }
-            }
-            n = w;
-        }
-        for (uint32_t q = o0; q < o1; q++) {
-            const uint16_t key = S.p_key[q]; const int32_t nv = S.p_val[q];
-            int at = -1;
-            for (int i = 0; i < MT_PSK; i++) if (i < n && k[i] == key) at = i;
+        for (int q = o0; q < o1; q++) {
+            const int key = uni((int)S.p_key[q]), nv = uni((int)S.p_val[q]);
+            const int at = wave_first(wave_map(n, [&](int i) MT_LAM { return own(kk, i) == key; }));
             if (nv < 0) {
-                if (at >= 0) { for (int i = at; i + 1 < MT_PSK; i++) if (i + 1 < n) { k[i] = k[i + 1]; v[i] = v[i + 1]; } n--; }
-            } else if (at >= 0) v[at] = nv;
-            else {
+                if (at >= 0) {
+                    auto k1 = wave_from(kk, 1), v1 = wave_from(vv, 1);
+                    kk = wave_map(8, [&](int i) MT_LAM { return i < at ? own(kk, i) : own(k1, i); });
+                    vv = wave_map(8, [&](int i) MT_LAM { return i < at ? own(vv, i) : own(v1, i); });
+                    n--;
+                }
+            } else if (at >= 0) {
+                vv = wave_map(8, [&](int i) MT_LAM { return i == at ? nv : own(vv, i); });
+            } else {
                 if (n >= MT_PSK) { status |= MT_DS_PROPS_TOO_MANY; psetTop--; return old; }
-                k[n] = key; v[n] = nv; n++;
+                const int at2 = n;
+                kk = wave_map(8, [&](int i) MT_LAM { return i == at2 ? key : own(kk, i); });
+                vv = wave_map(8, [&](int i) MT_LAM { return i == at2 ? nv : own(vv, i); });
+                n++;
             }
         }
-        MtPSet ps;
-        for (int i = 0; i < MT_PSK; i++) { ps.key[i] = k[i]; ps.val[i] = v[i]; }
-        ps.n = n; ps.pad[0] = ps.pad[1] = ps.pad[2] = 0;
-        pset[id] = ps;
+        const int nn = n;
+        wave_for(MT_PSK, [&](int i) MT_LAM {
+            pset[id].key[i] = (uint16_t)(i < nn ? own(kk, i) : 0);
+            pset[id].val[i] = i < nn ? own(vv, i) : 0;
+        });
+        pset[id].n = nn;
         return id;
     }
 
@@ -687,122 +795,134 @@ struct MtEng {
         sc->fB[0] = root; sc->fJ[0] = 0; sc->fS[0] = start; sc->fE[0] = end; sc->fD[0] = 0;
         sc->lastOld = -2; sc->lastNew = -1;
         while (L >= 0) {
-            const int B = sc->fB[L];
-            const MtBlk b = blk[B];
-            auto ch = childLens(b, r, c);
-            auto lens = wave_map(b.n, [&](int j) { return own(ch, j).len; });
-            const int j0 = sc->fJ[L];
-            auto lensFrom = wave_map(b.n, [&](int j) { return j >= j0 ? own(lens, j) : 0; });
+            const int B = uni(sc->fB[L]);
+            BlkH h;
+            auto ch = blkLoad(B, h);
+            auto cl = childLens(B, h, ch, r, c);
+            auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
+            const int j0 = uni(sc->fJ[L]);
+            auto lensFrom = wave_map(h.n, [&](int j) MT_LAM { return j >= j0 ? own(lens, j) : 0; });
             auto pre = wave_excl_scan(lensFrom);
-            const int st = sc->fS[L], en = sc->fE[L];
-            auto cond = wave_map(b.n, [&](int j) {
+            const int st = uni(sc->fS[L]), en = uni(sc->fE[L]);
+            auto cond = wave_map(h.n, [&](int j) MT_LAM {
                 const int lj = own(lens, j), pj = own(pre, j);
                 return j >= j0 && (en - pj) > 0 && lj > 0 && (st - pj) < lj;
             });
-            if (b.height == 0) {
+            if (h.height == 0) {
                 const int first = wave_first(cond);
                 int obsDelta = 0;
                 if (first >= 0) {
+                    const int nact = wave_count(cond);
+                    c_rows += 2ull * (uint64_t)nact;
                     if (mode == MT_MAP_REMOVE) {
-                        auto nd = wave_map(b.n, [&](int j) {
+                        auto nd = wave_map(h.n, [&](int j) MT_LAM {
                             if (!own(cond, j)) return 0;
-                            const int s = pick8(b.c, j);
-                            const uint32_t mt = meta[s];
+                            const int s = own(ch, j);
+                            const uint32_t mt = R[s].meta;
                             if (mt & MT_M_REMOVED) {                   // overlapping remove: keep first remover
-                                ovl[s] = ovl[s] | (1ull << c);
+                                R[s].ovl = R[s].ovl | (1ull << c);
                                 return 0;
                             }
-                            meta[s] = (mt & ~MT_M_RCLIENT) | MT_M_REMOVED | ((uint32_t)c << 8);
-                            rseq[s] = sq;
-                            return len[s];
+                            R[s].meta = (mt & ~MT_M_RCLIENT) | MT_M_REMOVED | ((uint32_t)c << 8);
+                            R[s].rseq = sq;
+                            return R[s].len;
                         });
                         obsDelta = -wave_sum(nd);
-                        cnt[3] += 2ull * (uint64_t)wave_count(cond);
                         wave_sync();
-                        for (int j = 0; j < b.n; j++) if (wave_at(cond, j)) winAdd(pick8(b.c, j));
+                        for (int j = 0; j < h.n; j++) if (wave_at(cond, j)) winAdd(wave_at(ch, j));
                     } else {
-                        cnt[3] += 2ull * (uint64_t)wave_count(cond);
-                        for (int j = 0; j < b.n; j++) {
+                        for (int j = 0; j < h.n; j++) {
                             if (!wave_at(cond, j)) continue;
-                            const int s = pick8(b.c, j);
-                            const int old = props[s];
+                            const int s = wave_at(ch, j);
+                            const int old = uni(R[s].props);
                             int nw;
-                            if (old == sc->lastOld) nw = sc->lastNew;
+                            if (old == uni(sc->lastOld)) nw = uni(sc->lastNew);
                             else { nw = applyPropSet(old, opset, rewrite); sc->lastOld = old; sc->lastNew = nw; }
-                            props[s] = nw;
+                            R[s].props = nw;
                         }
                     }
-                    addToLRUSet(pick8(b.c, first), sq);
+                    addToLRUSet(wave_at(ch, first), sq);
                 }
-                if (mode == MT_MAP_REMOVE) blk[B].len = b.len + obsDelta;
-                sc->fD[L] += obsDelta;
-                // pop
-                const int d = sc->fD[L];
+                if (mode == MT_MAP_REMOVE) blk[B].len = h.len + obsDelta;
+                const int d = uni(sc->fD[L]) + obsDelta;
                 L--;
-                if (L >= 0) { sc->fD[L] += d; sc->fS[L] -= sc->fL[L]; sc->fE[L] -= sc->fL[L]; sc->fJ[L] += 1; }
+                if (L >= 0) {
+                    sc->fD[L] = uni(sc->fD[L]) + d; sc->fS[L] = uni(sc->fS[L]) - uni(sc->fL[L]);
+                    sc->fE[L] = uni(sc->fE[L]) - uni(sc->fL[L]); sc->fJ[L] = uni(sc->fJ[L]) + 1;
+                }
                 continue;
             }
             const int jj = wave_first(cond);
             if (jj >= 0) {
                 const int pj = wave_at(pre, jj);
                 sc->fS[L] = st - pj; sc->fE[L] = en - pj; sc->fJ[L] = jj; sc->fL[L] = wave_at(lens, jj);
-                const int child = pick8(b.c, jj);
+                const int child = wave_at(ch, jj);
                 L++;
-                sc->fB[L] = child; sc->fJ[L] = 0; sc->fS[L] = sc->fS[L - 1]; sc->fE[L] = sc->fE[L - 1]; sc->fD[L] = 0;
+                sc->fB[L] = child; sc->fJ[L] = 0; sc->fS[L] = st - pj; sc->fE[L] = en - pj; sc->fD[L] = 0;
                 continue;
             }
-            const int d = sc->fD[L];
-            if (d != 0) blk[B].len = b.len + d;
+            const int d = uni(sc->fD[L]);
+            if (d != 0) blk[B].len = h.len + d;
             L--;
-            if (L >= 0) { sc->fD[L] += d; sc->fS[L] -= sc->fL[L]; sc->fE[L] -= sc->fL[L]; sc->fJ[L] += 1; }
+            if (L >= 0) {
+                sc->fD[L] = uni(sc->fD[L]) + d; sc->fS[L] = uni(sc->fS[L]) - uni(sc->fL[L]);
+                sc->fE[L] = uni(sc->fE[L]) - uni(sc->fL[L]); sc->fJ[L] = uni(sc->fJ[L]) + 1;
+            }
         }
         uValid = false;
     }
-
     /* -------------------------------------------------------- op apply -- */
     MT_HD void opInsert(int pos, int r, int c, int sq, const uint16_t* src, int plen, bool marker, int refType, int segProps) {
         // MergeTree.insertSegments (MT/mergeTree.ts:1974-2011)
+        MT_PB(t0);
         int w = walk(MT_WALK_SPLIT, pos, r, c, -1, 0);
-        if (w == MT_W_OK) cnt[3] += 2;
+        MT_PE(MT_PH_SPLIT, t0);
+        if (w == MT_W_OK) c_rows += 2;
         if (status) return;
         const int L = marker ? 1 : plen;
         if (L > 0) {
             const int n = allocRow();
             if (n < 0) return;
-            len[n] = L; seq[n] = sq; rseq[n] = MT_NOREM;
-            meta[n] = (uint32_t)c | (marker ? MT_M_MARKER : 0u);
-            ovl[n] = 0ull; parent[n] = -1;
-            props[n] = segProps >= 0 ? applyPropSet(-1, segProps, false) : -1;
-            tcap[n] = marker ? 0 : plen;
-            if (marker) toff[n] = refType;
+            R[n].len = L; R[n].seq = sq; R[n].rseq = MT_NOREM;
+            R[n].meta = (uint32_t)c | (marker ? MT_M_MARKER : 0u);
+            R[n].ovl = 0ull; R[n].parent = -1;
+            R[n].props = segProps >= 0 ? applyPropSet(-1, segProps, false) : -1;
+            R[n].tcap = marker ? 0 : plen;
+            if (marker) R[n].toff = refType;
             else {
-                parent[n] = -1;                                  // not yet linked: excluded from compaction
+                R[n].parent = -1;                                  // not yet linked: excluded from compaction
                 const int t0 = textAlloc(plen);
                 if (t0 < 0) return;
-                toff[n] = t0;
+                R[n].toff = t0;
                 for (int base = 0; base < plen; base += MT_WAVE) {
                     const int m = (plen - base) < MT_WAVE ? (plen - base) : MT_WAVE;
-                    wave_for(m, [&](int k) { text[t0 + base + k] = src[base + k]; });
+                    wave_for(m, [&](int k) MT_LAM { text[t0 + base + k] = src[base + k]; });
                 }
-                cnt[2] += (uint64_t)plen;
+                c_ins += (uint64_t)plen;
             }
             wave_sync();
+            MT_PB(t1);
             w = walk(MT_WALK_INSERT, pos, r, c, n, L);
-            if (w != MT_W_OK || parent[n] < 0) { status |= MT_DS_INSERT_FAILED; return; }
-            cnt[3] += 2;
+            MT_PE(MT_PH_INSERT, t1);
+            if (w != MT_W_OK || R[n].parent < 0) { status |= MT_DS_INSERT_FAILED; return; }
+            c_rows += 2;
             winAdd(n);
             if (sq > minSeq) addToLRUSet(n, sq);
         }
         zamboni();
     }
     MT_HD void opRange(int mode, int start, int end, int r, int c, int sq, int opset, bool rewrite) {
+        MT_PB(t0);
         int w = walk(MT_WALK_SPLIT, start, r, c, -1, 0);
-        if (w == MT_W_OK) cnt[3] += 2;
+        if (w == MT_W_OK) c_rows += 2;
         if (status) return;
         w = walk(MT_WALK_SPLIT, end, r, c, -1, 0);
-        if (w == MT_W_OK) cnt[3] += 2;
+        if (w == MT_W_OK) c_rows += 2;
         if (status) return;
+        MT_PE(MT_PH_SPLIT, t0);
+        MT_PB(t1);
         rangeMap(mode, start, end, r, c, sq, opset, rewrite);
+        MT_PE(MT_PH_RANGE, t1);
         if (status) return;
         zamboni();
     }

@@ -13,8 +13,7 @@ struct mt_ctx {
     std::string err;
     // device op batch (resident)
     struct DevBuf { void* p = nullptr; size_t cap = 0; };
-    DevBuf b_doc, b_off, b_type, b_flags, b_client, b_seq, b_ref, b_msn, b_pos1, b_pos2, b_poff, b_plen, b_pid, b_pay,
-        b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3;
+    DevBuf b_doc, b_off, b_rec, b_pay, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3;
     MtOps ops{};
     uint32_t n_runs = 0;
     MtGen gen{};

@@ -9,7 +9,10 @@
 #include "mt_ctx.h"
 
 // ------------------------------------------------------------- kernels ----
-__global__ __launch_bounds__(64) void mt_replay_kernel(MtState S, MtOps ops, MtGen gen) {
+#ifndef MT_WAVES_PER_SIMD
+#define MT_WAVES_PER_SIMD 4
+#endif
+__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_kernel(MtState S, MtOps ops, MtGen gen) {
     __shared__ MtScratch sc;
     __shared__ int lastRef[64];
     const uint32_t run = blockIdx.x;

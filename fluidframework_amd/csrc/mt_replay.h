@@ -18,7 +18,7 @@ struct MtRng {                                     // splitmix64
 // Synthesize message i of document `doc` from the engine's own state (the
 // engine acts as sequencer + observer, so positions are valid under the
 // author's perspective), writing the op record into the batch arrays.
-MT_HD inline void mt_gen_op(MtEng& e, const MtOps& ops, uint32_t i, uint32_t k, uint32_t doc,
+MT_HD void mt_gen_op(MtEng& e, const MtOps& ops, uint32_t i, uint32_t k, uint32_t doc,
                             const MtGen& g, MtRng& rng, int* lastRef) {
     const uint32_t a = rng.u(g.clients);
     const uint32_t lag = rng.u(g.lag_max + 1);
@@ -33,6 +33,7 @@ MT_HD inline void mt_gen_op(MtEng& e, const MtOps& ops, uint32_t i, uint32_t k, 
     if (L == 0) ty = MT_OP_INSERT;
     int s1 = 0, s2 = 0, pid = -1; uint32_t plen = 0; uint8_t fl = MT_OPF_END_OF_MSG;
     const uint32_t poff = (uint32_t)((size_t)doc * g.ops * g.ins_len_max + (size_t)k * g.ins_len_max);
+    MtOpRec& o = ops.rec[i];
     if (ty == MT_OP_INSERT) {
         s1 = (int)rng.u((uint32_t)L + 1);
         plen = 1 + rng.u(g.ins_len_max);
@@ -51,13 +52,13 @@ MT_HD inline void mt_gen_op(MtEng& e, const MtOps& ops, uint32_t i, uint32_t k, 
     }
     int mn = lastRef[0];
     for (uint32_t c = 1; c < g.clients; c++) mn = lastRef[c] < mn ? lastRef[c] : mn;
-    ops.type[i] = (uint8_t)ty; ops.flags[i] = fl; ops.client[i] = (uint16_t)a;
-    ops.seq[i] = e.curSeq + 1; ops.ref_seq[i] = r; ops.msn[i] = mn;
-    ops.pos1[i] = s1; ops.pos2[i] = s2; ops.payload_off[i] = poff; ops.payload_len[i] = plen; ops.prop_id[i] = pid;
+    o.type = (uint8_t)ty; o.flags = fl; o.client = (uint16_t)a;
+    o.seq = e.curSeq + 1; o.ref_seq = r; o.msn = mn;
+    o.pos1 = s1; o.pos2 = s2; o.payload_off = poff; o.payload_len = (uint16_t)plen; o.prop_id = (int16_t)pid;
     wave_sync();
 }
 
-MT_HD inline void mt_replay_run(MtEng& e, const MtOps& ops, uint32_t run, uint32_t doc,
+MT_HD void mt_replay_run(MtEng& e, const MtOps& ops, uint32_t run, uint32_t doc,
                                 const MtGen* g, int* lastRef) {
     const uint32_t o0 = ops.op_off[run], o1 = ops.op_off[run + 1];
     MtRng rng; rng.s = 0;
@@ -66,11 +67,25 @@ MT_HD inline void mt_replay_run(MtEng& e, const MtOps& ops, uint32_t run, uint32
         for (int c = 0; c < 64; c++) lastRef[c] = 0;
     }
     for (uint32_t i = o0; i < o1; i++) {
+#if defined(MT_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+        const unsigned long long tg = __builtin_amdgcn_s_memtime();
         if (g) mt_gen_op(e, ops, i, i - o0, doc, *g, rng, lastRef);
-        const int ty = ops.type[i];
-        const uint32_t fl = ops.flags[i];
-        const int c = ops.client[i];
-        const int sq = ops.seq[i], r = ops.ref_seq[i], ms = ops.msn[i];
+        e.prof[MT_PH_GEN] += __builtin_amdgcn_s_memtime() - tg;
+        const unsigned long long top = __builtin_amdgcn_s_memtime();
+#else
+        if (g) mt_gen_op(e, ops, i, i - o0, doc, *g, rng, lastRef);
+#endif
+        // one 32-byte record: lanes 0..7 load a dword each, then broadcast
+        auto w = wave_map(8, [&](int q) MT_LAM { return ((const int*)&ops.rec[i])[q]; });
+        const uint32_t w0 = (uint32_t)wave_at(w, 0);
+        const int ty = (int)(w0 & 0xFF);
+        const uint32_t fl = (w0 >> 8) & 0xFF;
+        const int c = (int)(w0 >> 16);
+        const int sq = wave_at(w, 1), r = wave_at(w, 2), ms = wave_at(w, 3);
+        const int p1 = wave_at(w, 4), p2 = wave_at(w, 5);
+        const uint32_t poff = (uint32_t)wave_at(w, 6);
+        const uint32_t w7 = (uint32_t)wave_at(w, 7);
+        const int plen = (int)(w7 & 0xFFFF), pid = (int)(int16_t)(w7 >> 16);
         if (ty != MT_OP_NOOP) {
             if (c >= 64) e.status |= MT_DS_UNSUPPORTED;
             if (e.curSeq >= sq) e.status |= MT_DS_ASSERT_SEQ;       // completeAndLogOp, MT/client.ts:482
@@ -79,20 +94,22 @@ MT_HD inline void mt_replay_run(MtEng& e, const MtOps& ops, uint32_t run, uint32
             if (!(e.uValid && e.uRef == r && e.uCli == c)) e.computeU(r, c, true);
             if (ty == MT_OP_INSERT) {
                 const bool marker = (fl & MT_OPF_MARKER) != 0;
-                e.opInsert(ops.pos1[i], r, c, sq, ops.payload + ops.payload_off[i], (int)ops.payload_len[i],
-                           marker, ops.pos2[i], (fl & MT_OPF_SEG_PROPS) ? ops.prop_id[i] : -1);
+                e.opInsert(p1, r, c, sq, ops.payload + poff, plen, marker, p2, (fl & MT_OPF_SEG_PROPS) ? pid : -1);
             } else if (ty == MT_OP_REMOVE) {
-                e.opRange(MT_MAP_REMOVE, ops.pos1[i], ops.pos2[i], r, c, sq, -1, false);
+                e.opRange(MT_MAP_REMOVE, p1, p2, r, c, sq, -1, false);
             } else if (ty == MT_OP_ANNOTATE) {
                 if (fl & MT_OPF_COMBINE) { e.status |= MT_DS_UNSUPPORTED; break; }
-                e.opRange(MT_MAP_ANNOTATE, ops.pos1[i], ops.pos2[i], r, c, sq, ops.prop_id[i], (fl & MT_OPF_REWRITE) != 0);
+                e.opRange(MT_MAP_ANNOTATE, p1, p2, r, c, sq, pid, (fl & MT_OPF_REWRITE) != 0);
             }
             e.uValid = false;
-            e.cnt[0] += 1;
-            e.cnt[4] += (unsigned long long)(e.height + 1);
+#if defined(MT_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+            e.prof[MT_PH_OP] += __builtin_amdgcn_s_memtime() - top;
+#endif
+            e.c_ops += 1;
+            e.c_depth += (unsigned long long)(e.height + 1);
         }
         if (fl & MT_OPF_END_OF_MSG) {                               // updateSeqNumbers, MT/client.ts:843-850
-            e.cnt[1] += 1;
+            e.c_msgs += 1;
             if (e.curSeq > sq) { e.status |= MT_DS_ASSERT_SEQ; break; }
             e.curSeq = sq;
             e.setMinSeq(ms);

@@ -18,8 +18,7 @@
 
 struct MtSnapView {                  // host copy of one document's state
     MtDocHdr hdr;
-    const int *len, *seq, *rseq, *toff, *props, *parent;
-    const uint32_t* meta; const unsigned long long* ovl;
+    const MtRow* R;
     const MtBlk* blk; const uint16_t* text; const MtPSet* pset;
 };
 struct MtNames {                     // host-interned strings
@@ -93,10 +92,10 @@ template <class F> void walk_all(const MtSnapView& v, int B, F& f) {
 
 // TextSegment/Marker toJSONObject (textSegment.ts:48-54, mergeTree.ts:649-653)
 inline void seg_json(std::string& o, const MtSnapView& v, const MtNames& nm, int s, const uint16_t* txt, size_t tn) {
-    const bool marker = (v.meta[s] & MT_M_MARKER) != 0;
-    const int ps = v.props[s];
+    const bool marker = (v.R[s].meta & MT_M_MARKER) != 0;
+    const int ps = v.R[s].props;
     if (marker) {
-        o += "{\"marker\":{\"refType\":"; put_int(o, v.toff[s]); o += "}";
+        o += "{\"marker\":{\"refType\":"; put_int(o, v.R[s].toff); o += "}";
         if (ps >= 0) { o += ",\"props\":"; props_json(o, v.pset[ps], nm); }
         o += "}";
     } else if (ps >= 0) {
@@ -131,35 +130,35 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
         if (prev < 0) return;
         std::string o;
         if (pcloned) { seg_json(o, v, nm, prev, ptext.data(), ptext.size()); lens.push_back((long long)ptext.size()); }
-        else { seg_json(o, v, nm, prev, v.text + v.toff[prev], (size_t)v.len[prev]); lens.push_back(v.len[prev]); }
+        else { seg_json(o, v, nm, prev, v.text + v.R[prev].toff, (size_t)v.R[prev].len); lens.push_back(v.R[prev].len); }
         segs.push_back(std::move(o));
     };
     auto extract = [&](int s) {
-        const bool removed = (v.meta[s] & MT_M_REMOVED) != 0;
-        if (removed && v.rseq[s] <= minSeq) return;                  // removed at/below the MSN: elided
-        if (v.seq[s] <= minSeq && !removed) {                         // coalesce candidates
+        const bool removed = (v.R[s].meta & MT_M_REMOVED) != 0;
+        if (removed && v.R[s].rseq <= minSeq) return;                  // removed at/below the MSN: elided
+        if (v.R[s].seq <= minSeq && !removed) {                         // coalesce candidates
             if (prev < 0) { prev = s; pcloned = false; return; }
-            const bool pm = (v.meta[prev] & MT_M_MARKER) != 0, sm = (v.meta[s] & MT_M_MARKER) != 0;
+            const bool pm = (v.R[prev].meta & MT_M_MARKER) != 0, sm = (v.R[s].meta & MT_M_MARKER) != 0;
             bool ok = !pm && !sm;
             if (ok) {
-                const uint16_t* pt = pcloned ? ptext.data() : v.text + v.toff[prev];
-                const size_t pl = pcloned ? ptext.size() : (size_t)v.len[prev];
-                ok = !(pl > 0 && pt[pl - 1] == '\n') && ((long long)pl <= MT_GRAN || v.len[s] <= MT_GRAN);
+                const uint16_t* pt = pcloned ? ptext.data() : v.text + v.R[prev].toff;
+                const size_t pl = pcloned ? ptext.size() : (size_t)v.R[prev].len;
+                ok = !(pl > 0 && pt[pl - 1] == '\n') && ((long long)pl <= MT_GRAN || v.R[s].len <= MT_GRAN);
             }
-            if (ok && props_match(v, nm, v.props[prev], v.props[s])) {
-                if (!pcloned) { ptext.assign(v.text + v.toff[prev], v.text + v.toff[prev] + v.len[prev]); pcloned = true; }
-                ptext.insert(ptext.end(), v.text + v.toff[s], v.text + v.toff[s] + v.len[s]);
+            if (ok && props_match(v, nm, v.R[prev].props, v.R[s].props)) {
+                if (!pcloned) { ptext.assign(v.text + v.R[prev].toff, v.text + v.R[prev].toff + v.R[prev].len); pcloned = true; }
+                ptext.insert(ptext.end(), v.text + v.R[s].toff, v.text + v.R[s].toff + v.R[s].len);
             } else { pushPrev(); prev = s; pcloned = false; }
             return;
         }
         pushPrev(); prev = -1; pcloned = false;
         std::string o = "{\"json\":";
-        const bool marker = (v.meta[s] & MT_M_MARKER) != 0;
-        seg_json(o, v, nm, s, marker ? nullptr : v.text + v.toff[s], marker ? 0 : (size_t)v.len[s]);
-        if (v.seq[s] > minSeq) { o += ",\"seq\":"; put_int(o, v.seq[s]); o += ",\"client\":"; o += client((int)(v.meta[s] & MT_M_CLIENT)); }
-        if (removed) { o += ",\"removedSeq\":"; put_int(o, v.rseq[s]); o += ",\"removedClient\":"; o += client((int)((v.meta[s] & MT_M_RCLIENT) >> 8)); }
+        const bool marker = (v.R[s].meta & MT_M_MARKER) != 0;
+        seg_json(o, v, nm, s, marker ? nullptr : v.text + v.R[s].toff, marker ? 0 : (size_t)v.R[s].len);
+        if (v.R[s].seq > minSeq) { o += ",\"seq\":"; put_int(o, v.R[s].seq); o += ",\"client\":"; o += client((int)(v.R[s].meta & MT_M_CLIENT)); }
+        if (removed) { o += ",\"removedSeq\":"; put_int(o, v.R[s].rseq); o += ",\"removedClient\":"; o += client((int)((v.R[s].meta & MT_M_RCLIENT) >> 8)); }
         o += "}";
-        segs.push_back(std::move(o)); lens.push_back(v.len[s]);
+        segs.push_back(std::move(o)); lens.push_back(v.R[s].len);
     };
     walk_all(v, v.hdr.root, extract);
     pushPrev();
@@ -219,8 +218,8 @@ inline uint64_t blobs_digest(const std::vector<std::string>& blobs) {
 
 inline void observer_text(const MtSnapView& v, std::vector<uint16_t>& out) {
     auto f = [&](int s) {
-        if (v.meta[s] & (MT_M_REMOVED | MT_M_MARKER)) return;
-        out.insert(out.end(), v.text + v.toff[s], v.text + v.toff[s] + v.len[s]);
+        if (v.R[s].meta & (MT_M_REMOVED | MT_M_MARKER)) return;
+        out.insert(out.end(), v.text + v.R[s].toff, v.text + v.R[s].toff + v.R[s].len);
     };
     walk_all(v, v.hdr.root, f);
 }
@@ -231,16 +230,16 @@ inline uint32_t fnv1a(const std::string& s) { uint32_t h = 2166136261u; for (uns
 inline void dump_rows(const MtSnapView& v, const MtNames& nm, std::vector<int32_t>& rows) {
     auto f = [&](int s) {
         int32_t r[12];
-        const uint32_t mt = v.meta[s];
-        r[0] = v.len[s]; r[1] = v.seq[s]; r[2] = (int32_t)(mt & MT_M_CLIENT);
+        const uint32_t mt = v.R[s].meta;
+        r[0] = v.R[s].len; r[1] = v.R[s].seq; r[2] = (int32_t)(mt & MT_M_CLIENT);
         const bool removed = (mt & MT_M_REMOVED) != 0;
-        r[3] = removed ? v.rseq[s] : INT32_MIN; r[4] = removed ? (int32_t)((mt & MT_M_RCLIENT) >> 8) : -1;
-        r[5] = (int32_t)(v.ovl[s] & 0xFFFFFFFFull); r[6] = (int32_t)(v.ovl[s] >> 32);
-        if (v.props[s] >= 0) { std::string js; props_json(js, v.pset[v.props[s]], nm); r[7] = (int32_t)(fnv1a(js) & 0x7FFFFFFF); }
+        r[3] = removed ? v.R[s].rseq : INT32_MIN; r[4] = removed ? (int32_t)((mt & MT_M_RCLIENT) >> 8) : -1;
+        r[5] = (int32_t)(v.R[s].ovl & 0xFFFFFFFFull); r[6] = (int32_t)(v.R[s].ovl >> 32);
+        if (v.R[s].props >= 0) { std::string js; props_json(js, v.pset[v.R[s].props], nm); r[7] = (int32_t)(fnv1a(js) & 0x7FFFFFFF); }
         else r[7] = -1;
-        r[8] = (mt & MT_M_MARKER) ? v.toff[s] : -1;
+        r[8] = (mt & MT_M_MARKER) ? v.R[s].toff : -1;
         int ix[MT_MAXH + 2]; int depth = 0;
-        int child = s; int p = v.parent[s]; bool leafLevel = true;
+        int child = s; int p = v.R[s].parent; bool leafLevel = true;
         while (p >= 0) {
             const MtBlk& b = v.blk[p];
             int at = -1;

@@ -13,10 +13,12 @@
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
-#define MT_HD __host__ __device__
+#define MT_HD __host__ __device__ __attribute__((always_inline))
+#define MT_LAM __attribute__((always_inline))
 #define MT_INLINE __host__ __device__ __forceinline__
 #else
-#define MT_HD
+#define MT_HD inline
+#define MT_LAM
 #define MT_INLINE inline
 #endif
 
@@ -25,6 +27,9 @@
 #if defined(__HIP_DEVICE_COMPILE__)
 // ---------------------------------------------------------------- device ----
 template <class T> using LaneArr = T;
+// Mark a wave-uniform 32-bit value as such (moves it to an SGPR).
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
 __device__ __forceinline__ int wave_lane() { return __lane_id(); }
 
@@ -42,9 +47,9 @@ __device__ __forceinline__ void wave_for(int n, F f) {
     if (k < n) f(k);
 }
 template <class T> __device__ __forceinline__ T own(const T& a, int) { return a; }
-__device__ __forceinline__ int wave_at(int a, int j) { return __shfl(a, j); }
-__device__ __forceinline__ uint32_t wave_at(uint32_t a, int j) { return (uint32_t)__shfl((int)a, j); }
-__device__ __forceinline__ bool wave_at(bool a, int j) { return __shfl((int)a, j) != 0; }
+__device__ __forceinline__ int wave_at(int a, int j) { return __builtin_amdgcn_readlane(a, j); }
+__device__ __forceinline__ uint32_t wave_at(uint32_t a, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)a, j); }
+__device__ __forceinline__ bool wave_at(bool a, int j) { return __builtin_amdgcn_readlane((int)a, j) != 0; }
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int wave_first(bool p) {
     uint64_t b = __ballot(p);
@@ -71,6 +76,12 @@ __device__ __forceinline__ int wave_excl_scan(int v) {
     }
     return x - v;
 }
+// lane i receives a[i + off] (0 outside [0, 64)); call from uniform control flow
+__device__ __forceinline__ int wave_from(int a, int off) {
+    const int src = __lane_id() + off;
+    const int v = __shfl(a, src & 63);
+    return (src >= 0 && src < 64) ? v : 0;
+}
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -82,6 +93,8 @@ template <class T> struct LaneArr {
     T v[MT_WAVE];
 };
 inline int wave_lane() { return 0; }
+inline int uni(int x) { return x; }
+inline uint32_t uni(uint32_t x) { return x; }
 
 template <class F>
 inline auto wave_map(int n, F f) -> LaneArr<decltype(f(0))> {
@@ -122,6 +135,11 @@ inline int wave_sum(const LaneArr<int>& a) {
 inline LaneArr<int> wave_excl_scan(const LaneArr<int>& a) {
     LaneArr<int> r; int s = 0;
     for (int k = 0; k < MT_WAVE; k++) { r.v[k] = s; s += a.v[k]; }
+    return r;
+}
+inline LaneArr<int> wave_from(const LaneArr<int>& a, int off) {
+    LaneArr<int> r;
+    for (int k = 0; k < MT_WAVE; k++) { const int s = k + off; r.v[k] = (s >= 0 && s < MT_WAVE) ? a.v[s] : 0; }
     return r;
 }
 inline void wave_sync() {}

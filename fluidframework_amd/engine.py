@@ -91,7 +91,8 @@ class Engine:
     def __init__(self, max_docs: int, rows_per_doc: int = 4096, blocks_per_doc: int = 0, text_per_doc: int = 0,
                  propsets_per_doc: int = 0, heap_per_doc: int = 0, window_per_doc: int = 0, device: int = 0,
                  lib_path: str | None = None, prefix: str = "mt_"):
-        path = lib_path or LIB_PATH
+        # MTGPU_LIB: an alternate build of the same HIP engine (e.g. another occupancy target)
+        path = lib_path or os.environ.get("MTGPU_LIB") or LIB_PATH
         if not os.path.exists(path):
             raise MergeTreeError(f"{path} is missing: run __graft_entry__.build() (no CPU fallback exists)")
         self.lib = ctypes.CDLL(path)

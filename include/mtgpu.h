@@ -204,6 +204,10 @@ int  mt_get_text(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
 int  mt_dump_segments(mt_ctx* ctx, uint32_t doc_id, int32_t** rows, uint32_t* n_rows);
 void mt_free(void* p);
 
+/* Diagnostic: per-document phase cycle counters (8 u64 each); zeros unless the
+ * library was built with -DMT_PROFILE (tools/phase_profile.py). */
+int  mt_prof_get(mt_ctx* ctx, uint32_t n_docs_from_0, unsigned long long* out);
+
 /* Synthetic stream generation on the device (SURVEY.md §8(d) stream rules):
  * the engine itself acts as sequencer + observer, so every position is valid
  * under the author's (refSeq, client) perspective. */

@@ -93,3 +93,14 @@ def test_device_generator_matches_oracle_generator(cfg):
         a = gb.payload[gb.arrays["payload_off"][i]:][:n]
         b = ob.payload[ob.arrays["payload_off"][i]:][:n]
         assert np.array_equal(a, b)
+
+
+def test_emu_matches_oracle_under_text_compaction_pressure():
+    # A text arena barely larger than the live text forces compaction inside
+    # zamboni merges (prefetched offsets must be refreshed).
+    props = ann_props()
+    cfg = dict(clients=4, lag=6, ins=70, rem=20, ins_len=8, rem_len=6, ops=4000, ann_sets=24, rewrite=5)
+    p = gen_params(seed=17, n_docs=3, **cfg)
+    batch, st, kept = generate(p, props, keep=True)
+    live = max(k.get_length() for k in kept)
+    compare(batch, props, 3, text=live + 600)
