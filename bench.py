@@ -109,6 +109,7 @@ def main():
     ap.add_argument("--seed", type=int, default=20241015)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--caps", default="", help="override pool caps, e.g. rows_per_doc=400,text_per_doc=16384")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,7 +130,11 @@ def main():
         c["docs"] = args.docs
     if args.ops:
         c["ops"] = args.ops
-    eng = Engine(c["docs"], device=local, **caps_for(c))
+    caps = caps_for(c)
+    for kv in filter(None, args.caps.split(",")):
+        k, v = kv.split("=")
+        caps[k] = int(v)
+    eng = Engine(c["docs"], device=local, **caps)
     eng.upload_props(ann_props())
     eng.upload_names(['"c%d"' % i for i in range(64)])
     seed = args.seed ^ (rank * 0x9E3779B1)

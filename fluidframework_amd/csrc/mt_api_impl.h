@@ -49,7 +49,7 @@ int MT_FN(create)(int device, const mt_limits* L, mt_ctx** out) {
     S.winCap = L->window_per_doc ? L->window_per_doc : 4096;
     S.textCap = L->text_per_doc ? L->text_per_doc : S.rowCap * 8;
     S.psetCap = L->propsets_per_doc ? L->propsets_per_doc : 1024;
-    S.holdCap = 64;
+    S.holdCap = MT_RFL;
     const size_t D = S.maxDocs, R = (size_t)D * S.rowCap;
     void* p;
 #define MT_ALLOC(field, T, count) \
@@ -59,7 +59,7 @@ int MT_FN(create)(int device, const mt_limits* L, mt_ctx** out) {
     MT_ALLOC(blk, MtBlk, D * S.blkCap) MT_ALLOC(heap, MtHeapE, D * (S.heapCap + 1)) MT_ALLOC(win, int, D * S.winCap)
     MT_ALLOC(uid, int, D * S.winCap) MT_ALLOC(udelta, int, D * S.winCap) MT_ALLOC(uanc, int, D * S.winCap * MT_MAXH)
     MT_ALLOC(text, uint16_t, D * 2 * S.textCap) MT_ALLOC(pset, MtPSet, D * S.psetCap) MT_ALLOC(hdr, MtDocHdr, D)
-    MT_ALLOC(hold, int, 64)
+    MT_ALLOC(hold, int, D * MT_RFL)
 #undef MT_ALLOC
     mtb_memset(S.hdr, 0, sizeof(MtDocHdr) * D);
     *out = c;

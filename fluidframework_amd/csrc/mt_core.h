@@ -34,6 +34,7 @@
 #define MT_GRAN 256                   // TextSegmentGranularity, MT/mergeTree.ts:1056
 #define MT_ZMAX 2                     // zamboniSegmentsMaxCount, MT/mergeTree.ts:1058
 #define MT_NOREM 0x7FFFFFFF           // removedSeq "undefined"
+#define MT_RFL 128                    // recycled-row stack per document (LDS while a run executes)
 
 // Phase profiling (diagnostic builds only, -DMT_PROFILE): shader-clock cycles
 // accumulated per phase into MtDocHdr.prof; never compiled into the product.
@@ -44,6 +45,24 @@
 #define MT_PB(v)
 #define MT_PE(i, v)
 #endif
+// Event counters (host-emulation diagnostic builds only, -DMT_EVCOUNT): reuse prof[].
+#if defined(MT_EVCOUNT)
+#define MT_EV(i, v) prof[i] += (unsigned long long)(v)
+#else
+#define MT_EV(i, v)
+#endif
+// Fine-grained latency probes (device diagnostic builds only, -DMT_PROFILE2):
+// 0 walk blkLoad cyc, 1 walk childLens cyc, 2 walk levels, 3 computeU cyc,
+// 4 computeU calls, 5 heapGet cyc, 6 heapGet calls, 7 scourLeaf cyc.
+#if defined(MT_PROFILE2) && defined(__HIP_DEVICE_COMPILE__)
+#define MT_QB(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define MT_QE(i, v) prof[i] += __builtin_amdgcn_s_memtime() - (v)
+#define MT_QC(i) prof[i] += 1
+#else
+#define MT_QB(v)
+#define MT_QE(i, v)
+#define MT_QC(i)
+#endif
 enum { MT_PH_U = 0, MT_PH_SPLIT, MT_PH_INSERT, MT_PH_RANGE, MT_PH_ZAMBONI, MT_PH_OP, MT_PH_GEN, MT_PH_TEXT };
 
 #define MT_M_CLIENT 0x000000FFu
@@ -51,6 +70,8 @@ enum { MT_PH_U = 0, MT_PH_SPLIT, MT_PH_INSERT, MT_PH_RANGE, MT_PH_ZAMBONI, MT_PH
 #define MT_M_REMOVED 0x00010000u
 #define MT_M_MARKER 0x00020000u
 #define MT_M_INWIN 0x00040000u
+#define MT_M_HREF1 0x01000000u        // heap-entry reference count, bits 24..31 (saturating)
+#define MT_M_HREF 0xFF000000u
 
 struct __attribute__((aligned(16))) MtRow {   // one 48-byte record per segment row
     int len;         // cachedLength (UTF-16 units; 1 for a marker)
@@ -85,14 +106,15 @@ struct __attribute__((aligned(16))) MtDocHdr {
     uint32_t status;
     unsigned long long cnt[6];               // mt_doc_counters order
     int textHalf;                            // which half of the doc's text arena is live
-    int pad[7];
+    int rfN;                                 // recycled rows on the document's stack (hold pool)
+    int pad[6];
     unsigned long long prof[8];              // MT_PROFILE builds: s_memtime cycles per phase
 };
 
 struct MtState {                              // device pools, doc-major
     MtRow* rows;
     MtBlk* blk; MtHeapE* heap; int* win; int* uid; int* udelta; int* uanc;
-    uint16_t* text; MtPSet* pset; MtDocHdr* hdr; int* hold;   // text: 2 halves of textCap per doc
+    uint16_t* text; MtPSet* pset; MtDocHdr* hdr; int* hold;   // text: 2 halves of textCap per doc; hold: recycled-row stacks
     uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap, holdCap, maxDocs;
     // interned op property sets (mt_prop_table)
     const uint32_t* p_off; const uint16_t* p_key; const int32_t* p_val;
@@ -125,6 +147,8 @@ struct MtScratch {
     int hold[64];
     int pk[MT_PSK], pv[MT_PSK];
     int lastOld, lastNew;
+    int rfree[MT_RFL];                // recycled rows (unlinked, out of the window, no heap entry)
+    int corr[MT_MAXN];                // per-child perspective corrections (childLens)
 };
 
 MT_INLINE int pick8(const int* c, int j) {
@@ -145,7 +169,7 @@ MT_INLINE bool vis_rc(int seq, uint32_t meta, int rseq, unsigned long long ovl, 
 
 struct BlkH { int len, parent, n, height, scour; };
 struct ChildL { int len; bool tie; };
-struct WinI { int id; int delta; bool live; };
+struct WinI { int id; int delta; bool live; bool recycle; };
 
 enum { MT_WALK_SPLIT = 0, MT_WALK_INSERT = 1 };
 enum { MT_W_OK = 0, MT_W_NOCHANGE = 1, MT_W_FAIL = 2 };
@@ -177,6 +201,7 @@ struct MtEng {
     int heapTop;                        // heap[1].maxSeq cached (INT_MAX when empty)
     int gcEpoch;                        // bumped by every text compaction
     int lastL, lastIdx; bool lastSplit; // landing spot of the last walk; did it split a block
+    int rfN; int* rfHbm;                // recycled-row stack: depth, HBM home between runs
 
     MT_HD void bind(const MtState& st, uint32_t d, MtScratch* scratch) {
         S.rowCap = st.rowCap; S.heapCap = st.heapCap; S.winCap = st.winCap; S.textCap = st.textCap;
@@ -200,12 +225,25 @@ struct MtEng {
         nU = 0; uValid = false; uRef = -1; uCli = -1;
         heapTop = heapN > 0 ? uni(heap[1].maxSeq) : 0x7FFFFFFF;
         lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0;
+        rfHbm = st.hold + (size_t)d * MT_RFL; rfN = uni(h.rfN);
+        if (rfN < 0 || rfN > MT_RFL) rfN = 0;
+        { const int n = rfN; const int* src = rfHbm;
+          for (int base = 0; base < n; base += MT_WAVE) {
+              const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
+              wave_for(m, [&](int k) MT_LAM { sc->rfree[base + k] = src[base + k]; });
+          } }
+        wave_sync();
     }
     MT_HD void store(uint32_t) {
         MtDocHdr& h = *hdrp;
         h.root = root; h.height = height; h.minSeq = minSeq; h.curSeq = curSeq; h.rowTop = rowTop;
         h.blkTop = blkTop; h.blkFree = blkFree; h.heapN = heapN; h.winN = winN; h.textTop = textTop;
-        h.psetTop = psetTop; h.status = status; h.textHalf = textHalf;
+        h.psetTop = psetTop; h.status = status; h.textHalf = textHalf; h.rfN = rfN;
+        { const int n = rfN; int* dst = rfHbm;
+          for (int base = 0; base < n; base += MT_WAVE) {
+              const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
+              wave_for(m, [&](int k) MT_LAM { dst[base + k] = sc->rfree[base + k]; });
+          } }
         for (int i = 0; i < 8; i++) h.prof[i] = prof[i];
         h.cnt[0] = c_ops; h.cnt[1] = c_msgs; h.cnt[2] = c_ins; h.cnt[3] = c_rows; h.cnt[4] = c_depth; h.cnt[5] = c_scour;
     }
@@ -213,7 +251,7 @@ struct MtEng {
     // startCollaboration :1243).
     MT_HD void open() {
         root = 0; height = 0; minSeq = 0; curSeq = 0; rowTop = 0; blkTop = 1; blkFree = -1;
-        heapN = 0; winN = 0; textTop = 0; psetTop = 0; status = 0; textHalf = 0; heapTop = 0x7FFFFFFF;
+        heapN = 0; winN = 0; textTop = 0; psetTop = 0; status = 0; textHalf = 0; heapTop = 0x7FFFFFFF; rfN = 0;
         text = S.textBase;
         c_ops = c_msgs = c_ins = c_rows = c_depth = c_scour = 0;
         for (int i = 0; i < 8; i++) prof[i] = 0;
@@ -222,10 +260,14 @@ struct MtEng {
     }
 
     /* ---------------------------------------------------------- pools -- */
+    // Rows are recycled once unlinked, out of the window and referenced by no
+    // heap entry (nothing can reach them); the stack is LIFO so reuse stays cache-hot.
     MT_HD int allocRow() {
+        if (rfN > 0) { rfN--; return uni(sc->rfree[rfN]); }
         if (rowTop >= (int)S.rowCap) { status |= MT_DS_OOM_ROWS; return -1; }
         return rowTop++;
     }
+    MT_HD void freeRow(int s) { if (rfN < MT_RFL) { sc->rfree[rfN] = s; rfN++; } }
     MT_HD int allocBlock() {
         if (blkFree >= 0) { const int id = blkFree; blkFree = uni(blk[id].parent); return id; }
         if (blkTop >= (int)blkCap) { status |= MT_DS_OOM_BLOCKS; return -1; }
@@ -261,7 +303,7 @@ struct MtEng {
     }
     MT_HD int sumObs(int B, int n, int h) const {
         auto v = wave_map(n, [&](int j) MT_LAM { return childObsLen(h, blk[B].c[j]); });
-        return wave_sum(v);
+        return wave_sum8(v);
     }
     MT_HD void setChildParent(int h, int id, int p) {
         if (h == 0) R[id].parent = p; else blk[id].parent = p;
@@ -272,6 +314,8 @@ struct MtEng {
     // U = rows whose visibility differs between the observer and (r, c).
     MT_HD void computeU(int r, int c, bool prune) {
         MT_PB(t0);
+        MT_EV(0, 1); MT_EV(2, winN);
+        MT_QB(q0); MT_QC(4);
         int newWin = 0; nU = 0;
         for (int base = 0; base < winN; base += MT_WAVE) {
             const int m = (winN - base) < MT_WAVE ? (winN - base) : MT_WAVE;
@@ -281,7 +325,9 @@ struct MtEng {
                 const uint32_t mt = R[s].meta;
                 const bool removed = (mt & MT_M_REMOVED) != 0;
                 const int sq = R[s].seq, rs = R[s].rseq;
-                w.live = R[s].parent >= 0 && (sq > minSeq || (removed && rs > minSeq));
+                const bool linked = R[s].parent >= 0;
+                w.live = linked && (sq > minSeq || (removed && rs > minSeq));
+                w.recycle = !linked && !(mt & MT_M_HREF);
                 const bool vr = vis_rc(sq, mt, rs, R[s].ovl, r, c);
                 const bool vo = !removed;
                 w.delta = w.live ? ((vr ? R[s].len : 0) - (vo ? R[s].len : 0)) : 0;
@@ -291,11 +337,16 @@ struct MtEng {
             if (prune) {
                 auto rk = wave_rank(live);
                 const int cntLive = wave_count(live);
+                auto rc = wave_map(m, [&](int k) MT_LAM { return own(wi, k).recycle; });
+                auto rkr = wave_rank(rc);
+                const int cntR = wave_count(rc), f0 = rfN;
                 wave_for(m, [&](int k) MT_LAM {
                     const WinI w = own(wi, k);
                     if (w.live) win[newWin + own(rk, k)] = w.id;
                     else R[w.id].meta = R[w.id].meta & ~MT_M_INWIN;
+                    if (w.recycle && f0 + own(rkr, k) < MT_RFL) sc->rfree[f0 + own(rkr, k)] = w.id;
                 });
+                rfN = (f0 + cntR) < MT_RFL ? (f0 + cntR) : MT_RFL;
                 newWin += cntLive;
             }
             auto du = wave_map(m, [&](int k) MT_LAM { return own(wi, k).delta != 0; });
@@ -308,6 +359,7 @@ struct MtEng {
             nU += cntU;
         }
         if (prune) winN = newWin;
+        MT_EV(1, nU);
         wave_sync();
         // ancestor chains: uanc[u*MAXH + h] = block at height h above row u
         for (int base = 0; base < nU; base += MT_WAVE) {
@@ -324,6 +376,7 @@ struct MtEng {
         wave_sync();
         uValid = true; uRef = r; uCli = c;
         MT_PE(MT_PH_U, t0);
+        MT_QE(3, q0);
     }
     MT_HD int perspectiveLength(int r, int c) {
         if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
@@ -350,20 +403,27 @@ struct MtEng {
                 return o;
             });
         }
-        auto corr = wave_map(h.n, [&](int j) MT_LAM { return 0; });
-        const int hc = h.height - 1;
+        // Each U row (one per lane) finds the child it lies under and adds its
+        // delta into that child's LDS slot.
+        const int hc = h.height - 1, n = h.n;
+        int cid[MT_MAXN];
+#pragma unroll
+        for (int j = 0; j < MT_MAXN; j++) cid[j] = j < n ? wave_at(ch, j) : -2;
+        wave_for(MT_MAXN, [&](int j) MT_LAM { sc->corr[j] = 0; });
+        wave_sync();
         for (int base = 0; base < nU; base += MT_WAVE) {
             const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
-            auto an = wave_map(m, [&](int k) MT_LAM { return uanc[(size_t)(base + k) * MT_MAXH + hc]; });
-            auto dk = wave_map(m, [&](int k) MT_LAM { return udelta[base + k]; });
-            for (int j = 0; j < h.n; j++) {
-                const int cj = wave_at(ch, j);
-                const int sj = wave_sum(wave_map(m, [&](int k) MT_LAM { return own(an, k) == cj ? own(dk, k) : 0; }));
-                if (sj) corr = wave_map(h.n, [&](int jj) MT_LAM { return own(corr, jj) + (jj == j ? sj : 0); });
-            }
+            wave_for(m, [&](int k) MT_LAM {
+                const int a = uanc[(size_t)(base + k) * MT_MAXH + hc];
+                int jk = -1;
+#pragma unroll
+                for (int j = 0; j < MT_MAXN; j++) if (cid[j] == a) jk = j;
+                if (jk >= 0) lds_add(&sc->corr[jk], udelta[base + k]);
+            });
         }
-        return wave_map(h.n, [&](int j) MT_LAM {
-            ChildL o; o.len = blk[own(ch, j)].len + own(corr, j); o.tie = true; return o;
+        wave_sync();
+        return wave_map(n, [&](int j) MT_LAM {
+            ChildL o; o.len = blk[own(ch, j)].len + sc->corr[j]; o.tie = true; return o;
         });
     }
 
@@ -377,7 +437,7 @@ struct MtEng {
         const int ls = uni(R[s].len);
         const uint32_t mt = uni(R[s].meta);
         R[n].len = ls - pos; R[s].len = pos;
-        R[n].seq = R[s].seq; R[n].rseq = R[s].rseq; R[n].meta = mt & ~MT_M_INWIN; R[n].ovl = R[s].ovl;
+        R[n].seq = R[s].seq; R[n].rseq = R[s].rseq; R[n].meta = mt & ~(MT_M_INWIN | MT_M_HREF); R[n].ovl = R[s].ovl;
         R[n].toff = R[s].toff + pos; R[n].props = R[s].props; R[n].parent = R[s].parent;
         R[n].tcap = R[s].tcap - pos; R[s].tcap = pos;   // each row owns [toff, toff+tcap) of the arena
         if (mt & MT_M_INWIN) winAdd(n);
@@ -391,7 +451,7 @@ struct MtEng {
             const int B = uni(sc->pathB[L]);
             BlkH h;
             auto cur = blkLoad(B, h);
-            auto prv = wave_from(cur, -1);
+            auto prv = wave_from8<-1>(cur);
             auto nc = wave_map(8, [&](int i) MT_LAM { return i < idx ? own(cur, i) : (i == idx ? node : own(prv, i)); });
             const int n1 = h.n + 1;
             setChildParent(h.height, node, B);
@@ -402,9 +462,10 @@ struct MtEng {
                 return;
             }
             lastSplit = true;
+            MT_EV(6, 1);
             const int NB = allocBlock();
             if (NB < 0) return;
-            auto hi = wave_from(nc, 4);
+            auto hi = wave_from8<4>(nc);
             wave_for(8, [&](int i) MT_LAM {
                 blk[NB].c[i] = i < 4 ? own(hi, i) : -1;
                 blk[B].c[i] = i < 4 ? own(nc, i) : -1;
@@ -433,12 +494,17 @@ struct MtEng {
         int B = root, L = 0, p = pos;
         for (;;) {
             BlkH h;
+            MT_QB(q0); MT_QC(2);
             auto ch = blkLoad(B, h);
+            MT_QE(0, q0);
+            MT_EV(5, 1);
             sc->pathB[L] = B;
+            MT_QB(q1);
             auto cl = childLens(B, h, ch, r, c);
+            MT_QE(1, q1);
             auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
-            auto pre = wave_excl_scan(lens);
-            const int total = wave_sum(lens);
+            auto pre = wave_excl_scan8(lens);
+            const int total = wave_sum8(lens);
             const bool interior = h.height > 0;
             auto cond = wave_map(h.n, [&](int j) MT_LAM {
                 const int pj = p - own(pre, j), lj = own(cl, j).len;
@@ -494,6 +560,7 @@ struct MtEng {
         const int lseg = uni(heap[heapN].seg), lms = uni(heap[heapN].maxSeq);
         heapN--;
         heapTop = 0x7FFFFFFF;
+        MT_EV(3, 1); MT_EV(7, heapN);
         if (heapN >= 1) {
             int k = 1;
             heapTop = lms;
@@ -505,6 +572,7 @@ struct MtEng {
                     if (hm > hm1) { j++; hs = uni(heap[j].seg); hm = hm1; }
                 }
                 if (lms <= hm) break;
+                MT_EV(4, 1);
                 if (k == 1) heapTop = hm;
                 heap[k].seg = hs; heap[k].maxSeq = hm; k = j;
             }
@@ -514,7 +582,12 @@ struct MtEng {
     }
     MT_HD void addToLRUSet(int s, int sq) {                   // MT/mergeTree.ts:1262-1272
         const int p = uni(R[s].parent);
-        if (uni(blk[p].scour) != 1 && sq > curSeq) { blk[p].scour = 1; heapAdd(s, sq); }
+        const uint32_t m = uni(R[s].meta);
+        if (uni(blk[p].scour) != 1 && sq > curSeq) {
+            blk[p].scour = 1;
+            if ((m & MT_M_HREF) != MT_M_HREF) R[s].meta = m + MT_M_HREF1;   // saturated: never recycled
+            heapAdd(s, sq);
+        }
     }
     MT_HD bool propsMatch(int a, int b) {                      // matchProperties, MT/properties.ts:64-95
         if (a == b) return true;
@@ -620,7 +693,10 @@ struct MtEng {
             c_scour++;
             if (mt & MT_M_REMOVED) {
                 if (wave_at(fr, k) > minSeq) sc->hold[nh++] = s;
-                else R[s].parent = -1;                             // UNLINK
+                else {                                             // UNLINK
+                    R[s].parent = -1;
+                    if (!(mt & (MT_M_HREF | MT_M_INWIN))) freeRow(s);
+                }
                 prev = -1;
             } else if (wave_at(fs, k) <= minSeq) {
                 const int ls = wave_at(fl, k), ps = wave_at(fp, k);
@@ -630,6 +706,7 @@ struct MtEng {
                 if (can) {
                     appendText(prev, prevLen, prevToff, prevCap, s, ls, wave_at(ft, k), wave_at(fc, k));
                     R[s].parent = -1;
+                    if (!(mt & (MT_M_HREF | MT_M_INWIN))) freeRow(s);
                     prevLen += ls; prevLast = wave_at(fe, k);
                 } else {
                     sc->hold[nh++] = s;
@@ -703,11 +780,18 @@ struct MtEng {
         uValid = false;
         for (int i = 0; i < MT_ZMAX; i++) {
             if (heapN == 0 || heapTop > minSeq) break;
+            MT_QB(q0); MT_QC(6);
             const MtHeapE e = heapGet();
+            MT_QE(5, q0);
             const int p = uni(R[e.seg].parent);
+            uint32_t em = uni(R[e.seg].meta);
+            if ((em & MT_M_HREF) != MT_M_HREF) { em -= MT_M_HREF1; R[e.seg].meta = em; }
+            if (p < 0 && !(em & (MT_M_HREF | MT_M_INWIN))) freeRow(e.seg);
             if (p >= 0 && uni(blk[p].scour) != 0) {
                 const BlkH h = head(p);
+                MT_QB(q1);
                 const int nh = scourLeaf(p, h.n, 0);
+                MT_QE(7, q1);
                 blk[p].scour = 0;
                 if (nh < h.n) {
                     wave_for(8, [&](int j) MT_LAM { blk[p].c[j] = j < nh ? sc->hold[j] : -1; });
@@ -760,7 +844,7 @@ struct MtEng {
             const int at = wave_first(wave_map(n, [&](int i) MT_LAM { return own(kk, i) == key; }));
             if (nv < 0) {
                 if (at >= 0) {
-                    auto k1 = wave_from(kk, 1), v1 = wave_from(vv, 1);
+                    auto k1 = wave_from8<1>(kk), v1 = wave_from8<1>(vv);
                     kk = wave_map(8, [&](int i) MT_LAM { return i < at ? own(kk, i) : own(k1, i); });
                     vv = wave_map(8, [&](int i) MT_LAM { return i < at ? own(vv, i) : own(v1, i); });
                     n--;
@@ -802,7 +886,7 @@ struct MtEng {
             auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
             const int j0 = uni(sc->fJ[L]);
             auto lensFrom = wave_map(h.n, [&](int j) MT_LAM { return j >= j0 ? own(lens, j) : 0; });
-            auto pre = wave_excl_scan(lensFrom);
+            auto pre = wave_excl_scan8(lensFrom);
             const int st = uni(sc->fS[L]), en = uni(sc->fE[L]);
             auto cond = wave_map(h.n, [&](int j) MT_LAM {
                 const int lj = own(lens, j), pj = own(pre, j);
@@ -827,7 +911,7 @@ struct MtEng {
                             R[s].rseq = sq;
                             return R[s].len;
                         });
-                        obsDelta = -wave_sum(nd);
+                        obsDelta = -wave_sum8(nd);
                         wave_sync();
                         for (int j = 0; j < h.n; j++) if (wave_at(cond, j)) winAdd(wave_at(ch, j));
                     } else {

@@ -61,27 +61,46 @@ __device__ __forceinline__ int wave_rank(bool p) {
     uint64_t b = __ballot(p);
     return __popcll(b & ((1ull << __lane_id()) - 1ull));
 }
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-__device__ __forceinline__ int wave_excl_scan(int v) {
-    const int lane = __lane_id();
+// Scans and sums run on DPP (row_shr within 16-lane rows, then row_bcast:15/31
+// across rows): VALU-latency chains instead of ds_bpermute round trips.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ int dpp0(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, ROWS, 0xf, false); }
+__device__ __forceinline__ int wave_incl_scan(int v) {
     int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    return x - v;
+    x += dpp0<0x111>(x);          // row_shr:1
+    x += dpp0<0x112>(x);          // row_shr:2
+    x += dpp0<0x114>(x);          // row_shr:4
+    x += dpp0<0x118>(x);          // row_shr:8
+    x += dpp0<0x142, 0xa>(x);     // row_bcast:15 -> rows 1, 3
+    x += dpp0<0x143, 0xc>(x);     // row_bcast:31 -> rows 2, 3
+    return x;
 }
+__device__ __forceinline__ int wave_sum(int v) { return __builtin_amdgcn_readlane(wave_incl_scan(v), 63); }
+__device__ __forceinline__ int wave_excl_scan(int v) { return wave_incl_scan(v) - v; }
+// Same for data held in lanes 0..7 (a block's children): three row shifts.
+__device__ __forceinline__ int wave_incl_scan8(int v) {
+    int x = v;
+    x += dpp0<0x111>(x);
+    x += dpp0<0x112>(x);
+    x += dpp0<0x114>(x);
+    return x;
+}
+__device__ __forceinline__ int wave_sum8(int v) { return __builtin_amdgcn_readlane(wave_incl_scan8(v), 7); }
+__device__ __forceinline__ int wave_excl_scan8(int v) { return wave_incl_scan8(v) - v; }
 // lane i receives a[i + off] (0 outside [0, 64)); call from uniform control flow
 __device__ __forceinline__ int wave_from(int a, int off) {
     const int src = __lane_id() + off;
     const int v = __shfl(a, src & 63);
     return (src >= 0 && src < 64) ? v : 0;
 }
+// lanes 0..7 receive a[i + OFF] from within the first 16 lanes (DPP row shift)
+template <int OFF> __device__ __forceinline__ int wave_from8(int a) {
+    static_assert(OFF != 0 && OFF > -16 && OFF < 16, "row shift");
+    if constexpr (OFF < 0) return dpp0<0x110 | (-OFF)>(a);
+    else return dpp0<0x100 | OFF>(a);
+}
+// per-lane add into wave-private LDS (conflicting lanes serialize in hardware)
+__device__ __forceinline__ void lds_add(int* p, int v) { __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -137,10 +156,22 @@ inline LaneArr<int> wave_excl_scan(const LaneArr<int>& a) {
     for (int k = 0; k < MT_WAVE; k++) { r.v[k] = s; s += a.v[k]; }
     return r;
 }
+inline int wave_sum8(const LaneArr<int>& a) {
+    int s = 0;
+    for (int k = 0; k < 8; k++) s += a.v[k];
+    return s;
+}
+inline LaneArr<int> wave_excl_scan8(const LaneArr<int>& a) { return wave_excl_scan(a); }
 inline LaneArr<int> wave_from(const LaneArr<int>& a, int off) {
     LaneArr<int> r;
     for (int k = 0; k < MT_WAVE; k++) { const int s = k + off; r.v[k] = (s >= 0 && s < MT_WAVE) ? a.v[s] : 0; }
     return r;
 }
+template <int OFF> inline LaneArr<int> wave_from8(const LaneArr<int>& a) {
+    LaneArr<int> r;
+    for (int k = 0; k < MT_WAVE; k++) { const int s = (k & 15) + OFF; r.v[k] = (s >= 0 && s < 16) ? a.v[(k & ~15) + s] : 0; }
+    return r;
+}
+inline void lds_add(int* p, int v) { *p += v; }
 inline void wave_sync() {}
 #endif

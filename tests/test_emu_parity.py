@@ -6,7 +6,7 @@ repeats these checks on the real device.
 import numpy as np
 import pytest
 
-from fluidframework_amd.batch import PropTable
+from fluidframework_amd.batch import OpBatch, PropTable
 from oracle_lib import gen_params, generate, replay
 from emu_lib import emu_engine
 
@@ -104,3 +104,61 @@ def test_emu_matches_oracle_under_text_compaction_pressure():
     batch, st, kept = generate(p, props, keep=True)
     live = max(k.get_length() for k in kept)
     compare(batch, props, 3, text=live + 600)
+
+
+def split_batch(batch, k):
+    """Cut every document's run into k consecutive batches at message boundaries."""
+    out = [dict(doc=[], idx=[]) for _ in range(k)]
+    flags = batch.arrays["flags"]
+    for r, d in enumerate(batch.doc_ids):
+        a, b = int(batch.op_offsets[r]), int(batch.op_offsets[r + 1])
+        ends = [i + 1 for i in range(a, b) if flags[i] & 1]
+        cuts = [a] + [ends[min(len(ends) - 1, (j + 1) * len(ends) // k - 1)] for j in range(k - 1)] + [b]
+        for j in range(k):
+            if cuts[j + 1] > cuts[j]:
+                out[j]["doc"].append(d)
+                out[j]["idx"].append(np.arange(cuts[j], cuts[j + 1]))
+    res = []
+    for o in out:
+        idx = np.concatenate(o["idx"])
+        offs = np.concatenate([[0], np.cumsum([len(x) for x in o["idx"]])])
+        res.append(OpBatch.from_arrays(o["doc"], offs, batch.payload,
+                                       **{n: batch.arrays[n][idx] for n in batch.arrays}))
+    return res
+
+
+def test_emu_matches_oracle_across_batches():
+    # Per-document state that lives in LDS during a run (recycled-row stack)
+    # must survive the run boundary: replay the same streams in 5 batches.
+    props = ann_props()
+    p = gen_params(seed=23, n_docs=3, **CONFIGS["cfg2"])
+    batch, st, _ = generate(p, props)
+    eng = emu_engine(3, rows_per_doc=20000, window_per_doc=8192, propsets_per_doc=8192, text_per_doc=1 << 18)
+    eng.upload_props(props)
+    eng.upload_names(NAMES)
+    eng.open_docs(0, 3)
+    for b in split_batch(batch, 5):
+        eng.apply(b)
+    eng.sync()
+    assert (eng.status(range(3)) == 0).all()
+    oracle_docs = replay(batch, props, NAMES)
+    texts = eng.get_text(range(3))
+    for d in range(3):
+        assert texts[d] == oracle_docs[d][0].get_text()
+        assert np.array_equal(eng.dump(d), oracle_docs[d][0].dump())
+
+
+STRESS = {
+    "deep": dict(clients=4, lag=16, ins=92, rem=4, ins_len=3, rem_len=2, ops=6000, ann_sets=24, rewrite=10),
+    "lag128": dict(clients=16, lag=128, ins=55, rem=35, ins_len=8, rem_len=12, ops=3000, ann_sets=24, rewrite=5),
+    "shrink": dict(clients=8, lag=32, ins=35, rem=65, ins_len=8, rem_len=24, ops=3000),
+}
+
+
+@pytest.mark.parametrize("cfg", list(STRESS))
+def test_emu_matches_oracle_stress(cfg):
+    props = ann_props()
+    p = gen_params(seed=29, n_docs=2, **STRESS[cfg])
+    batch, st, _ = generate(p, props)
+    assert st == [0] * 2
+    compare(batch, props, 2)
