@@ -60,6 +60,22 @@ def algorithmic_bytes(cnt):
                + 64 * cnt["depth"].sum() + 64 * cnt["scoured"].sum())
 
 
+def measured_traffic(cfg_name, c):
+    """HBM bytes per replay launch from the committed rocprofv3 PMC passes
+    (profiles/<round>/<config>_traffic.json, written by tools/traffic_from_pmc.py)
+    when they were taken on this exact workload; None otherwise."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{cfg_name}_traffic.json"))):
+        try:
+            t = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if t.get("docs") == c["docs"] and t.get("msgs_per_doc") == c["ops"]:
+            best = (t["traffic_bytes"], os.path.relpath(f, ROOT))
+    return best
+
+
 def caps_for(c):
     ops = c["ops"]
     return dict(rows_per_doc=3 * ops + 64, blocks_per_doc=ops + 64, heap_per_doc=2 * ops + 64,
@@ -189,6 +205,7 @@ def main():
     achieved = bytes_per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
     if rank != 0:
         return
+    traffic = measured_traffic(args.config, c)
     out = {
         "metric": "sequenced merge-tree ops applied/sec (whole node) + achieved HBM GB/s",
         "value": value,
@@ -207,7 +224,9 @@ def main():
                                                                                    100 - c["ins"] - c["rem"]],
                    "parallelism": f"doc-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBPS,
+                     "traffic": traffic[0] if traffic else None,
+                     "traffic_source": traffic[1] if traffic else None,
                      "kernel": "mt_replay_kernel", "kernel_ms": kern_s * 1e3,
                      "bytes_per_launch": bytes_per_launch},
         "hbm_gbps_algorithmic": achieved,

@@ -12,14 +12,26 @@
 #ifndef MT_WAVES_PER_SIMD
 #define MT_WAVES_PER_SIMD 4
 #endif
-__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_kernel(MtState S, MtOps ops, MtGen gen) {
+// Replay: Client.applyMsg over each document's resident op run (the timed hot path).
+__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_kernel(MtState S, MtOps ops) {
+    __shared__ MtScratch sc;
+    const uint32_t run = blockIdx.x;
+    const uint32_t doc = ops.doc_ids[run];
+    MtEng e;
+    e.bind(S, doc, &sc);
+    mt_replay_run(e, ops, run, doc, nullptr, nullptr);
+    e.store(doc);
+}
+// Generation: the same engine acting as sequencer + observer, writing the op
+// records it applies (a separate symbol so profiles never mix it with replay).
+__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_generate_kernel(MtState S, MtOps ops, MtGen gen) {
     __shared__ MtScratch sc;
     __shared__ int lastRef[64];
     const uint32_t run = blockIdx.x;
     const uint32_t doc = ops.doc_ids[run];
     MtEng e;
     e.bind(S, doc, &sc);
-    mt_replay_run(e, ops, run, doc, gen.enabled ? &gen : nullptr, lastRef);
+    mt_replay_run(e, ops, run, doc, &gen, lastRef);
     e.store(doc);
 }
 __global__ __launch_bounds__(64) void mt_open_kernel(MtState S, uint32_t first) {
@@ -88,7 +100,8 @@ static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     hipStream_t s = (hipStream_t)c->stream;
     (void)hipGetLastError();
     (void)hipEventRecord((hipEvent_t)c->ev0, s);
-    hipLaunchKernelGGL(mt_replay_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, g);
+    if (g.enabled) hipLaunchKernelGGL(mt_generate_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, g);
+    else hipLaunchKernelGGL(mt_replay_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops);
     (void)hipEventRecord((hipEvent_t)c->ev1, s);
     c->ev_pending = true;
     return mtb_check(c);
