@@ -125,6 +125,8 @@ def main():
     ap.add_argument("--seed", type=int, default=20241015)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--residency", default="hbm", choices=["lds", "hbm"],
+                    help="hbm: HBM-pool kernel (default); lds: LDS-resident pools with HBM hand-over")
     ap.add_argument("--caps", default="", help="override pool caps, e.g. rows_per_doc=400,text_per_doc=16384")
     args = ap.parse_args()
 
@@ -151,6 +153,7 @@ def main():
         k, v = kv.split("=")
         caps[k] = int(v)
     eng = Engine(c["docs"], device=local, **caps)
+    eng.set_residency(args.residency == "lds")
     eng.upload_props(ann_props())
     eng.upload_names(['"c%d"' % i for i in range(64)])
     seed = args.seed ^ (rank * 0x9E3779B1)
@@ -222,7 +225,7 @@ def main():
         "config": {"workload": f"{args.config}: {c['desc']}", "docs_per_gpu": c["docs"], "msgs_per_doc": c["ops"],
                    "clients": c["clients"], "lag_max": c["lag"], "mix_ins_rem_ann": [c["ins"], c["rem"],
                                                                                    100 - c["ins"] - c["rem"]],
-                   "parallelism": f"doc-sharded x{world}"},
+                   "parallelism": f"doc-sharded x{world}", "residency": args.residency},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic[0] if traffic else None,

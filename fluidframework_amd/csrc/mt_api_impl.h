@@ -71,7 +71,7 @@ void MT_FN(destroy)(mt_ctx* c) {
     MtState& S = c->S;
     void* ps[] = {S.rows, S.blk, S.heap, S.win, S.uid, S.udelta, S.uanc, S.text, S.pset, S.hdr, S.hold};
     for (void* p : ps) if (p) mtb_free(p);
-    mt_ctx::DevBuf* bs[] = {&c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_pset_off,
+    mt_ctx::DevBuf* bs[] = {&c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_pset_off,
                             &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3};
     for (auto* b : bs) if (b->p) mtb_free(b->p);
     mtb_fini(c);
@@ -161,6 +161,8 @@ int MT_FN(upload_batch)(mt_ctx* c, const mt_op_batch* B) {
 }
 int MT_FN(replay_resident)(mt_ctx* c) {
     if (!c || !c->ops.op_off) return MT_E_INVALID;
+    int rc = mtb_ensure(c, c->b_cursor, 4ull * c->n_runs + 4);
+    if (rc) return rc;
     MtGen g{}; g.enabled = 0;
     return mtb_launch_replay(c, g, c->n_runs);
 }
@@ -169,15 +171,43 @@ int MT_FN(apply_batch)(mt_ctx* c, const mt_op_batch* B) {
     if (rc) return rc;
     return MT_FN(replay_resident)(c);
 }
+int MT_FN(set_residency)(mt_ctx* c, int use_lds, int rows, int blocks, int heap) {
+    if (!c || rows < 0 || blocks < 0 || heap < 0 || rows > MT_L_ROWS || blocks > MT_L_BLKS || heap > MT_L_HEAP)
+        return MT_E_INVALID;
+    c->use_lds = use_lds ? 1 : 0;
+    c->lds_rows = rows ? rows : MT_L_ROWS; c->lds_blks = blocks ? blocks : MT_L_BLKS; c->lds_heap = heap ? heap : MT_L_HEAP;
+    return MT_OK;
+}
 int MT_FN(last_replay_ms)(mt_ctx* c, float* ms) { if (!c || !ms) return MT_E_INVALID; *ms = c->last_ms; return MT_OK; }
 int MT_FN(sync)(mt_ctx* c) { if (!c) return MT_E_INVALID; return mtb_sync(c); }
 
 static int mt_read_hdrs(mt_ctx* c, uint32_t n, const uint32_t* docs, std::vector<MtDocHdr>& h) {
     h.resize(n);
     mtb_sync(c);
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
     for (uint32_t i = 0; i < n; i++) {
         if (docs[i] >= c->S.maxDocs) return MT_E_INVALID;
-        mtb_d2h(c, &h[i], c->S.hdr + docs[i], sizeof(MtDocHdr));
+        lo = docs[i] < lo ? docs[i] : lo; hi = docs[i] > hi ? docs[i] : hi;
+    }
+    if (n == 0) return MT_OK;
+    if (n < 8) {
+        for (uint32_t i = 0; i < n; i++) mtb_d2h(c, &h[i], c->S.hdr + docs[i], sizeof(MtDocHdr));
+        return MT_OK;
+    }
+    std::vector<MtDocHdr> all((size_t)(hi - lo + 1));      // one copy of the covering header range
+    mtb_d2h(c, all.data(), c->S.hdr + lo, sizeof(MtDocHdr) * all.size());
+    for (uint32_t i = 0; i < n; i++) h[i] = all[docs[i] - lo];
+    return MT_OK;
+}
+int MT_FN(doc_pools)(mt_ctx* c, uint32_t n, const uint32_t* docs, int32_t* out) {
+    if (!c || (n && (!docs || !out))) return MT_E_INVALID;
+    std::vector<MtDocHdr> h;
+    int rc = mt_read_hdrs(c, n, docs, h);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < n; i++) {
+        int32_t* o = out + 8 * (size_t)i;
+        o[0] = h[i].rowTop; o[1] = h[i].blkTop; o[2] = h[i].heapN; o[3] = h[i].winN;
+        o[4] = h[i].textTop; o[5] = h[i].psetTop; o[6] = h[i].height; o[7] = h[i].rfN;
     }
     return MT_OK;
 }

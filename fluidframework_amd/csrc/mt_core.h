@@ -35,6 +35,19 @@
 #define MT_ZMAX 2                     // zamboniSegmentsMaxCount, MT/mergeTree.ts:1058
 #define MT_NOREM 0x7FFFFFFF           // removedSeq "undefined"
 #define MT_RFL 128                    // recycled-row stack per document (LDS while a run executes)
+// LDS-resident pools (mt_replay_lds_kernel): a document whose rows, blocks, heap
+// and window fit runs entirely out of LDS; one that outgrows them mid-run is
+// written back to HBM and finished by the HBM-pool kernel (exact resume).
+#ifndef MT_L_ROWS
+#define MT_L_ROWS 256                 // rows (and window / U-set entries)
+#endif
+#ifndef MT_L_BLKS
+#define MT_L_BLKS 96                  // blocks (ids < 255: ancestor chains are bytes)
+#endif
+#ifndef MT_L_HEAP
+#define MT_L_HEAP 96                  // zamboni heap entries
+#endif
+#define MT_L_H 8                      // ancestor-chain levels (tree height < MT_L_H - 2)
 
 // Phase profiling (diagnostic builds only, -DMT_PROFILE): shader-clock cycles
 // accumulated per phase into MtDocHdr.prof; never compiled into the product.
@@ -107,7 +120,8 @@ struct __attribute__((aligned(16))) MtDocHdr {
     unsigned long long cnt[6];               // mt_doc_counters order
     int textHalf;                            // which half of the doc's text arena is live
     int rfN;                                 // recycled rows on the document's stack (hold pool)
-    int pad[6];
+    int blkFreeN;                            // blocks on the free list
+    int pad[5];
     unsigned long long prof[8];              // MT_PROFILE builds: s_memtime cycles per phase
 };
 
@@ -138,6 +152,18 @@ struct MtGen {                                // device stream generator paramet
     unsigned long long seed;
     uint32_t ops, clients, lag_max, pct_insert, pct_remove, ins_len_max, rem_len_max, n_ann_sets, pct_rewrite;
     int enabled;
+};
+
+struct __attribute__((aligned(16))) MtQ16 { uint32_t x, y, z, w; };
+// LDS home of a document's hot pools while mt_replay_lds_kernel runs it.
+struct __attribute__((aligned(16))) MtLdsPools {
+    MtRow rows[MT_L_ROWS];
+    MtBlk blk[MT_L_BLKS];
+    MtHeapE heap[MT_L_HEAP + 2];
+    int win[MT_L_ROWS];
+    int uid[MT_L_ROWS];
+    int udelta[MT_L_ROWS];
+    uint8_t uanc[MT_L_ROWS * MT_L_H];
 };
 
 // per-wave scratch (LDS on the device)
@@ -183,7 +209,17 @@ struct MtEngParams {
     const uint32_t* p_off; const uint16_t* p_key; const int32_t* p_val;
     const uint8_t* p_falsy; const uint32_t* p_class;
 };
-struct MtEng {
+// The LDS pools live in one file-scope __shared__ object, so every access of
+// the LDS-resident engine (MtEngT<true>) is a ds_* instruction; the host
+// emulation has one static instance (it runs one wave at a time).
+#if defined(__HIP_DEVICE_COMPILE__)
+__shared__ MtLdsPools mt_lds_pools_v;
+#else
+static MtLdsPools mt_lds_pools_v;
+#endif
+MT_INLINE MtLdsPools& mt_lds() { return mt_lds_pools_v; }
+
+template <bool LDS> struct MtEngT {
     MtEngParams S;
     MtDocHdr* hdrp;
     // doc-local views
@@ -191,6 +227,13 @@ struct MtEng {
     int *win, *uid, *udelta, *uanc;
     MtBlk* blk; MtHeapE* heap; uint16_t* text; MtPSet* pset;
     MtScratch* sc;
+    // pool accessors: LDS-resident (MtEngT<true>) or HBM (MtEngT<false>) homes
+    MT_HD MtRow& row(int s) const { if constexpr (LDS) return mt_lds().rows[s]; else return R[s]; }
+    MT_HD MtBlk& bk(int b) const { if constexpr (LDS) return mt_lds().blk[b]; else return blk[b]; }
+    MT_HD MtHeapE& hp(int k) const { if constexpr (LDS) return mt_lds().heap[k]; else return heap[k]; }
+    MT_HD int& wn(int k) const { if constexpr (LDS) return mt_lds().win[k]; else return win[k]; }
+    MT_HD int& ui(int k) const { if constexpr (LDS) return mt_lds().uid[k]; else return uid[k]; }
+    MT_HD int& ud(int k) const { if constexpr (LDS) return mt_lds().udelta[k]; else return udelta[k]; }
     // uniform document state (MtDocHdr)
     int root, height, minSeq, curSeq, rowTop, blkTop, blkFree, heapN, winN, textTop, psetTop;
     uint32_t status;
@@ -198,10 +241,15 @@ struct MtEng {
     unsigned long long prof[8];
     int textHalf; uint32_t blkCap;
     int nU; bool uValid; int uRef, uCli;
-    int heapTop;                        // heap[1].maxSeq cached (INT_MAX when empty)
+    int heapTop;                        // hp(1).maxSeq cached (INT_MAX when empty)
     int gcEpoch;                        // bumped by every text compaction
     int lastL, lastIdx; bool lastSplit; // landing spot of the last walk; did it split a block
     int rfN; int* rfHbm;                // recycled-row stack: depth, HBM home between runs
+    int blkFreeN;                       // blocks on the free list
+    // LDS residency (toLds/fromLds): LDS caps, and the HBM caps they stand in for
+    static constexpr bool kLds = LDS;
+    int lRows, lBlks, lHeap;
+    uint32_t gRowCap, gBlkCap, gHeapCap, gWinCap;
 
     MT_HD void bind(const MtState& st, uint32_t d, MtScratch* scratch) {
         S.rowCap = st.rowCap; S.heapCap = st.heapCap; S.winCap = st.winCap; S.textCap = st.textCap;
@@ -223,9 +271,10 @@ struct MtEng {
         for (int i = 0; i < 8; i++) prof[i] = h.prof[i];
         c_ops = h.cnt[0]; c_msgs = h.cnt[1]; c_ins = h.cnt[2]; c_rows = h.cnt[3]; c_depth = h.cnt[4]; c_scour = h.cnt[5];
         nU = 0; uValid = false; uRef = -1; uCli = -1;
-        heapTop = heapN > 0 ? uni(heap[1].maxSeq) : 0x7FFFFFFF;
+        heapTop = heapN > 0 ? uni(heap[1].maxSeq) : 0x7FFFFFFF;     // HBM home: bind precedes toLds
         lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0;
-        rfHbm = st.hold + (size_t)d * MT_RFL; rfN = uni(h.rfN);
+        rfHbm = st.hold + (size_t)d * MT_RFL; rfN = uni(h.rfN); blkFreeN = uni(h.blkFreeN);
+        lRows = lBlks = lHeap = 0; gRowCap = gBlkCap = gHeapCap = gWinCap = 0;
         if (rfN < 0 || rfN > MT_RFL) rfN = 0;
         { const int n = rfN; const int* src = rfHbm;
           for (int base = 0; base < n; base += MT_WAVE) {
@@ -238,7 +287,7 @@ struct MtEng {
         MtDocHdr& h = *hdrp;
         h.root = root; h.height = height; h.minSeq = minSeq; h.curSeq = curSeq; h.rowTop = rowTop;
         h.blkTop = blkTop; h.blkFree = blkFree; h.heapN = heapN; h.winN = winN; h.textTop = textTop;
-        h.psetTop = psetTop; h.status = status; h.textHalf = textHalf; h.rfN = rfN;
+        h.psetTop = psetTop; h.status = status; h.textHalf = textHalf; h.rfN = rfN; h.blkFreeN = blkFreeN;
         { const int n = rfN; int* dst = rfHbm;
           for (int base = 0; base < n; base += MT_WAVE) {
               const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
@@ -252,11 +301,12 @@ struct MtEng {
     MT_HD void open() {
         root = 0; height = 0; minSeq = 0; curSeq = 0; rowTop = 0; blkTop = 1; blkFree = -1;
         heapN = 0; winN = 0; textTop = 0; psetTop = 0; status = 0; textHalf = 0; heapTop = 0x7FFFFFFF; rfN = 0;
+        blkFreeN = 0;
         text = S.textBase;
         c_ops = c_msgs = c_ins = c_rows = c_depth = c_scour = 0;
         for (int i = 0; i < 8; i++) prof[i] = 0;
-        wave_for(8, [&](int i) MT_LAM { blk[0].c[i] = -1; });
-        blk[0].len = 0; blk[0].parent = -1; blk[0].n = 0; blk[0].height = 0; blk[0].scour = -1;
+        wave_for(8, [&](int i) MT_LAM { bk(0).c[i] = -1; });
+        bk(0).len = 0; bk(0).parent = -1; bk(0).n = 0; bk(0).height = 0; bk(0).scour = -1;
     }
 
     /* ---------------------------------------------------------- pools -- */
@@ -269,44 +319,106 @@ struct MtEng {
     }
     MT_HD void freeRow(int s) { if (rfN < MT_RFL) { sc->rfree[rfN] = s; rfN++; } }
     MT_HD int allocBlock() {
-        if (blkFree >= 0) { const int id = blkFree; blkFree = uni(blk[id].parent); return id; }
+        if (blkFree >= 0) { const int id = blkFree; blkFree = uni(bk(id).parent); blkFreeN--; return id; }
         if (blkTop >= (int)blkCap) { status |= MT_DS_OOM_BLOCKS; return -1; }
         return blkTop++;
     }
-    MT_HD void freeBlock(int id) { blk[id].parent = blkFree; blk[id].n = -1; blkFree = id; }
+    MT_HD void freeBlock(int id) { bk(id).parent = blkFree; bk(id).n = -1; blkFree = id; blkFreeN++; }
+
+    /* ---------------------------------------------------- LDS residency -- */
+    // Lane-parallel copy of n 16-byte quads.
+    MT_HD static void copyQ(MtQ16* dst, const MtQ16* src, int n) {
+        for (int base = 0; base < n; base += MT_WAVE) {
+            const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
+            wave_for(m, [&](int k) MT_LAM { dst[base + k] = src[base + k]; });
+        }
+    }
+    MT_HD static void copyI(int* dst, const int* src, int n) {
+        for (int base = 0; base < n; base += MT_WAVE) {
+            const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
+            wave_for(m, [&](int k) MT_LAM { dst[base + k] = src[base + k]; });
+        }
+    }
+    // MtEngT<true> only: move the document's rows, blocks, heap and window into
+    // the LDS pools (caps lr/lb/lh <= the MT_L_* array sizes).  False (nothing
+    // moved) if they do not fit.  R/blk/heap/win keep pointing at the HBM homes.
+    MT_HD bool toLds(int lr, int lb, int lh) {
+        static_assert(LDS, "LDS residency needs MtEngT<true>");
+        if (rowTop > lr || blkTop > lb || heapN > lh || winN > lr || height + 3 > MT_L_H || lb > 255) return false;
+        MtLdsPools& L = mt_lds();
+        copyQ((MtQ16*)L.rows, (const MtQ16*)R, rowTop * (int)(sizeof(MtRow) / 16));
+        copyQ((MtQ16*)L.blk, (const MtQ16*)blk, blkTop * (int)(sizeof(MtBlk) / 16));
+        copyI((int*)L.heap, (const int*)heap, 2 * (heapN + 1));
+        copyI(L.win, win, winN);
+        wave_sync();
+        gRowCap = S.rowCap; gBlkCap = blkCap; gHeapCap = S.heapCap; gWinCap = S.winCap;
+        S.rowCap = gRowCap < (uint32_t)lr ? gRowCap : (uint32_t)lr;
+        blkCap = gBlkCap < (uint32_t)lb ? gBlkCap : (uint32_t)lb;
+        S.heapCap = gHeapCap < (uint32_t)lh ? gHeapCap : (uint32_t)lh;
+        S.winCap = gWinCap < (uint32_t)lr ? gWinCap : (uint32_t)lr;
+        lRows = lr; lBlks = lb; lHeap = lh;
+        nU = 0; uValid = false;
+        return true;
+    }
+    MT_HD void fromLds() {
+        MtLdsPools& L = mt_lds();
+        copyQ((MtQ16*)R, (const MtQ16*)L.rows, rowTop * (int)(sizeof(MtRow) / 16));
+        copyQ((MtQ16*)blk, (const MtQ16*)L.blk, blkTop * (int)(sizeof(MtBlk) / 16));
+        copyI((int*)heap, (const int*)L.heap, 2 * (heapN + 1));
+        copyI(win, L.win, winN);
+        wave_sync();
+        S.rowCap = gRowCap; blkCap = gBlkCap; S.heapCap = gHeapCap; S.winCap = gWinCap;
+        nU = 0; uValid = false;
+    }
+    // Can the next op run without outgrowing the LDS pools?  Per op at most 2
+    // row splits + 1 new row, 2 split cascades of height+2 blocks and packParent
+    // regrowth; one heap entry per op plus one per message.
+    MT_HD bool ldsHeadroom() const {
+        if constexpr (!LDS) return true;
+        return (lRows - rowTop + rfN) >= 4 && (lBlks - blkTop + blkFreeN) >= 6 * (height + 2) + 8 &&
+               (lHeap - heapN) >= 4 && height + 3 <= MT_L_H;
+    }
+    MT_HD void ancPut(int u, int h, int a) {
+        if constexpr (LDS) mt_lds().uanc[u * MT_L_H + h] = (uint8_t)(a < 0 ? 255 : a);
+        else uanc[(size_t)u * MT_MAXH + h] = a;
+    }
+    MT_HD int ancGet(int u, int h) const {
+        if constexpr (LDS) { const int a = mt_lds().uanc[u * MT_L_H + h]; return a == 255 ? -1 : a; }
+        else return uanc[(size_t)u * MT_MAXH + h];
+    }
     MT_HD void winAdd(int s) {
-        const uint32_t mt = uni(R[s].meta);
+        const uint32_t mt = uni(row(s).meta);
         if (mt & MT_M_INWIN) return;
         if (winN >= (int)S.winCap) { status |= MT_DS_OOM_WINDOW; return; }
-        win[winN++] = s;
-        R[s].meta = mt | MT_M_INWIN;
+        wn(winN++) = s;
+        row(s).meta = mt | MT_M_INWIN;
     }
     // Scalar fields of a block (SGPRs) and its children (one per lane).
     MT_HD BlkH head(int B) const {
         BlkH h;
-        h.len = uni(blk[B].len); h.parent = uni(blk[B].parent); h.n = uni(blk[B].n);
-        h.height = uni(blk[B].height); h.scour = uni(blk[B].scour);
+        h.len = uni(bk(B).len); h.parent = uni(bk(B).parent); h.n = uni(bk(B).n);
+        h.height = uni(bk(B).height); h.scour = uni(bk(B).scour);
         return h;
     }
-    MT_HD LaneArr<int> kids(int B, int n) const { return wave_map(n, [&](int j) MT_LAM { return blk[B].c[j]; }); }
+    MT_HD LaneArr<int> kids(int B, int n) const { return wave_map(n, [&](int j) MT_LAM { return bk(B).c[j]; }); }
     // Whole 64-byte block record in one transaction: lane i loads dword i;
     // children stay in lanes 0..n-1, scalar fields are broadcast to SGPRs.
     MT_HD LaneArr<int> blkLoad(int B, BlkH& h) const {
-        auto w = wave_map(16, [&](int i) MT_LAM { return ((const int*)&blk[B])[i]; });
+        auto w = wave_map(16, [&](int i) MT_LAM { return ((const int*)&bk(B))[i]; });
         h.len = wave_at(w, 8); h.parent = wave_at(w, 9); h.n = wave_at(w, 10); h.height = wave_at(w, 11); h.scour = wave_at(w, 12);
         const int n = h.n;
         return wave_map(8, [&](int j) MT_LAM { return j < n ? own(w, j) : -1; });
     }
     MT_HD int childObsLen(int h, int id) const {
-        if (h == 0) return (R[id].meta & MT_M_REMOVED) ? 0 : R[id].len;
-        return blk[id].len;
+        if (h == 0) return (row(id).meta & MT_M_REMOVED) ? 0 : row(id).len;
+        return bk(id).len;
     }
     MT_HD int sumObs(int B, int n, int h) const {
-        auto v = wave_map(n, [&](int j) MT_LAM { return childObsLen(h, blk[B].c[j]); });
+        auto v = wave_map(n, [&](int j) MT_LAM { return childObsLen(h, bk(B).c[j]); });
         return wave_sum8(v);
     }
     MT_HD void setChildParent(int h, int id, int p) {
-        if (h == 0) R[id].parent = p; else blk[id].parent = p;
+        if (h == 0) row(id).parent = p; else bk(id).parent = p;
     }
 
     /* ------------------------------------- perspective window (U set) -- */
@@ -320,17 +432,17 @@ struct MtEng {
         for (int base = 0; base < winN; base += MT_WAVE) {
             const int m = (winN - base) < MT_WAVE ? (winN - base) : MT_WAVE;
             auto wi = wave_map(m, [&](int k) MT_LAM {
-                WinI w; w.id = win[base + k];
+                WinI w; w.id = wn(base + k);
                 const int s = w.id;
-                const uint32_t mt = R[s].meta;
+                const uint32_t mt = row(s).meta;
                 const bool removed = (mt & MT_M_REMOVED) != 0;
-                const int sq = R[s].seq, rs = R[s].rseq;
-                const bool linked = R[s].parent >= 0;
+                const int sq = row(s).seq, rs = row(s).rseq;
+                const bool linked = row(s).parent >= 0;
                 w.live = linked && (sq > minSeq || (removed && rs > minSeq));
                 w.recycle = !linked && !(mt & MT_M_HREF);
-                const bool vr = vis_rc(sq, mt, rs, R[s].ovl, r, c);
+                const bool vr = vis_rc(sq, mt, rs, row(s).ovl, r, c);
                 const bool vo = !removed;
-                w.delta = w.live ? ((vr ? R[s].len : 0) - (vo ? R[s].len : 0)) : 0;
+                w.delta = w.live ? ((vr ? row(s).len : 0) - (vo ? row(s).len : 0)) : 0;
                 return w;
             });
             auto live = wave_map(m, [&](int k) MT_LAM { return own(wi, k).live; });
@@ -342,8 +454,8 @@ struct MtEng {
                 const int cntR = wave_count(rc), f0 = rfN;
                 wave_for(m, [&](int k) MT_LAM {
                     const WinI w = own(wi, k);
-                    if (w.live) win[newWin + own(rk, k)] = w.id;
-                    else R[w.id].meta = R[w.id].meta & ~MT_M_INWIN;
+                    if (w.live) wn(newWin + own(rk, k)) = w.id;
+                    else row(w.id).meta = row(w.id).meta & ~MT_M_INWIN;
                     if (w.recycle && f0 + own(rkr, k) < MT_RFL) sc->rfree[f0 + own(rkr, k)] = w.id;
                 });
                 rfN = (f0 + cntR) < MT_RFL ? (f0 + cntR) : MT_RFL;
@@ -354,7 +466,7 @@ struct MtEng {
             const int cntU = wave_count(du);
             const int nu0 = nU;
             wave_for(m, [&](int k) MT_LAM {
-                if (own(du, k)) { uid[nu0 + own(rk2, k)] = own(wi, k).id; udelta[nu0 + own(rk2, k)] = own(wi, k).delta; }
+                if (own(du, k)) { ui(nu0 + own(rk2, k)) = own(wi, k).id; ud(nu0 + own(rk2, k)) = own(wi, k).delta; }
             });
             nU += cntU;
         }
@@ -366,10 +478,10 @@ struct MtEng {
             const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
             const int H = height;
             wave_for(m, [&](int k) MT_LAM {
-                int a = R[uid[base + k]].parent;
+                int a = row(ui(base + k)).parent;
                 for (int h = 0; h <= H; h++) {
-                    uanc[(size_t)(base + k) * MT_MAXH + h] = a;
-                    a = (a >= 0) ? blk[a].parent : -1;
+                    ancPut(base + k, h, a);
+                    a = (a >= 0) ? bk(a).parent : -1;
                 }
             });
         }
@@ -383,19 +495,19 @@ struct MtEng {
         int s = 0;
         for (int base = 0; base < nU; base += MT_WAVE) {
             const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
-            s += wave_sum(wave_map(m, [&](int k) MT_LAM { return udelta[base + k]; }));
+            s += wave_sum(wave_map(m, [&](int k) MT_LAM { return ud(base + k); }));
         }
-        return uni(blk[root].len) + s;
+        return uni(bk(root).len) + s;
     }
     // Perspective lengths of block B's children (nodeLength, MT/mergeTree.ts:1652-1692).
     MT_HD LaneArr<ChildL> childLens(int B, const BlkH& h, const LaneArr<int>& ch, int r, int c) {
         if (h.height == 0) {
             return wave_map(h.n, [&](int j) MT_LAM {
                 const int s = own(ch, j);
-                const uint32_t mt = R[s].meta;
-                const int rs = R[s].rseq;
+                const uint32_t mt = row(s).meta;
+                const int rs = row(s).rseq;
                 ChildL o;
-                o.len = vis_rc(R[s].seq, mt, rs, R[s].ovl, r, c) ? R[s].len : 0;
+                o.len = vis_rc(row(s).seq, mt, rs, row(s).ovl, r, c) ? row(s).len : 0;
                 // breakTie for a leaf at pos 0 (MT/mergeTree.ts:2270-2292): false if a
                 // removal the author has seen (removedSeq <= refSeq); true otherwise
                 // (every row has an assigned seq on the replay path).
@@ -414,16 +526,16 @@ struct MtEng {
         for (int base = 0; base < nU; base += MT_WAVE) {
             const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
             wave_for(m, [&](int k) MT_LAM {
-                const int a = uanc[(size_t)(base + k) * MT_MAXH + hc];
+                const int a = ancGet(base + k, hc);
                 int jk = -1;
 #pragma unroll
                 for (int j = 0; j < MT_MAXN; j++) if (cid[j] == a) jk = j;
-                if (jk >= 0) lds_add(&sc->corr[jk], udelta[base + k]);
+                if (jk >= 0) lds_add(&sc->corr[jk], ud(base + k));
             });
         }
         wave_sync();
         return wave_map(n, [&](int j) MT_LAM {
-            ChildL o; o.len = blk[own(ch, j)].len + sc->corr[j]; o.tie = true; return o;
+            ChildL o; o.len = bk(own(ch, j)).len + sc->corr[j]; o.tie = true; return o;
         });
     }
 
@@ -434,12 +546,12 @@ struct MtEng {
     MT_HD int splitRow(int s, int pos) {
         const int n = allocRow();
         if (n < 0) return -1;
-        const int ls = uni(R[s].len);
-        const uint32_t mt = uni(R[s].meta);
-        R[n].len = ls - pos; R[s].len = pos;
-        R[n].seq = R[s].seq; R[n].rseq = R[s].rseq; R[n].meta = mt & ~(MT_M_INWIN | MT_M_HREF); R[n].ovl = R[s].ovl;
-        R[n].toff = R[s].toff + pos; R[n].props = R[s].props; R[n].parent = R[s].parent;
-        R[n].tcap = R[s].tcap - pos; R[s].tcap = pos;   // each row owns [toff, toff+tcap) of the arena
+        const int ls = uni(row(s).len);
+        const uint32_t mt = uni(row(s).meta);
+        row(n).len = ls - pos; row(s).len = pos;
+        row(n).seq = row(s).seq; row(n).rseq = row(s).rseq; row(n).meta = mt & ~(MT_M_INWIN | MT_M_HREF); row(n).ovl = row(s).ovl;
+        row(n).toff = row(s).toff + pos; row(n).props = row(s).props; row(n).parent = row(s).parent;
+        row(n).tcap = row(s).tcap - pos; row(s).tcap = pos;   // each row owns [toff, toff+tcap) of the arena
         if (mt & MT_M_INWIN) winAdd(n);
         return n;
     }
@@ -452,13 +564,20 @@ struct MtEng {
             BlkH h;
             auto cur = blkLoad(B, h);
             auto prv = wave_from8<-1>(cur);
-            auto nc = wave_map(8, [&](int i) MT_LAM { return i < idx ? own(cur, i) : (i == idx ? node : own(prv, i)); });
+            const int nd = node, ix = idx;
+            // branch-free blend: a ?: chain here gets turned into a select of
+            // closure-field addresses, which forces the closure into scratch
+            auto nc = wave_map(8, [=](int i) MT_LAM {
+                const int a = own(cur, i), b = own(prv, i);
+                const int lt = -(int)(i < ix), eq = -(int)(i == ix);
+                return (a & lt) | (nd & eq) | (b & ~(lt | eq));
+            });
             const int n1 = h.n + 1;
             setChildParent(h.height, node, B);
             if (n1 < MT_MAXN) {
-                wave_for(8, [&](int i) MT_LAM { blk[B].c[i] = i < n1 ? own(nc, i) : -1; });
-                blk[B].n = n1; blk[B].len = h.len + delta;
-                for (int l = L - 1; l >= 0; l--) { const int pb = uni(sc->pathB[l]); blk[pb].len = uni(blk[pb].len) + delta; }
+                wave_for(8, [&](int i) MT_LAM { bk(B).c[i] = i < n1 ? own(nc, i) : -1; });
+                bk(B).n = n1; bk(B).len = h.len + delta;
+                for (int l = L - 1; l >= 0; l--) { const int pb = uni(sc->pathB[l]); bk(pb).len = uni(bk(pb).len) + delta; }
                 return;
             }
             lastSplit = true;
@@ -467,21 +586,21 @@ struct MtEng {
             if (NB < 0) return;
             auto hi = wave_from8<4>(nc);
             wave_for(8, [&](int i) MT_LAM {
-                blk[NB].c[i] = i < 4 ? own(hi, i) : -1;
-                blk[B].c[i] = i < 4 ? own(nc, i) : -1;
+                bk(NB).c[i] = i < 4 ? own(hi, i) : -1;
+                bk(B).c[i] = i < 4 ? own(nc, i) : -1;
             });
-            blk[NB].n = 4; blk[NB].height = h.height; blk[NB].scour = -1; blk[NB].parent = h.parent;
-            blk[B].n = 4;
+            bk(NB).n = 4; bk(NB).height = h.height; bk(NB).scour = -1; bk(NB).parent = h.parent;
+            bk(B).n = 4;
             wave_for(4, [&](int i) MT_LAM { setChildParent(h.height, own(hi, i), NB); });
             wave_sync();
             const int nbLen = sumObs(NB, 4, h.height), bLen = sumObs(B, 4, h.height);
-            blk[NB].len = nbLen; blk[B].len = bLen;
+            bk(NB).len = nbLen; bk(B).len = bLen;
             if (L == 0) {
                 const int R = allocBlock();
                 if (R < 0) return;
-                wave_for(8, [&](int i) MT_LAM { blk[R].c[i] = i == 0 ? B : (i == 1 ? NB : -1); });
-                blk[R].n = 2; blk[R].height = h.height + 1; blk[R].parent = -1; blk[R].scour = -1; blk[R].len = bLen + nbLen;
-                blk[B].parent = R; blk[NB].parent = R;
+                wave_for(8, [&](int i) MT_LAM { bk(R).c[i] = i == 0 ? B : (i == 1 ? NB : -1); });
+                bk(R).n = 2; bk(R).height = h.height + 1; bk(R).parent = -1; bk(R).scour = -1; bk(R).len = bLen + nbLen;
+                bk(B).parent = R; bk(NB).parent = R;
                 root = R; height = h.height + 1;
                 return;
             }
@@ -518,12 +637,15 @@ struct MtEng {
                 const int s = wave_at(ch, j);
                 lastL = L; lastSplit = false;
                 if (kind == MT_WALK_SPLIT) {
-                    if (pj > 0 && !(uni(R[s].meta) & MT_M_MARKER)) {
+                    if (pj > 0 && !(uni(row(s).meta) & MT_M_MARKER)) {
                         const int n = splitRow(s, pj);
                         if (n < 0) return MT_W_FAIL;
                         insertAtPath(L, j + 1, n, 0);
                         lastIdx = j + 1;                      // an insert at pos lands before the new right half
-                        uValid = false;
+                        // A row split keeps every row under the same ancestors unless a
+                        // block split moved some: U's per-ancestor delta sums stay exact
+                        // (s's delta covers both halves), so U stays valid.
+                        if (lastSplit) uValid = false;
                         return MT_W_OK;
                     }
                     lastIdx = j;
@@ -545,47 +667,93 @@ struct MtEng {
     }
 
     /* --------------------------------------------------------- zamboni -- */
-    MT_HD void heapAdd(int s, int ms) {                       // Heap.add + fixup, collections.ts:238-251
+    // Heap.add + fixup (collections.ts:238-251).  A heap of <= 63 entries is
+    // sifted in registers (lane k = entry k): one load, readlanes, one store.
+    MT_HD void heapAdd(int s, int ms) {
         if (heapN + 1 > (int)S.heapCap) { status |= MT_DS_OOM_HEAP; return; }
         int k = ++heapN;
-        while (k > 1) {
-            const int pm = uni(heap[k >> 1].maxSeq);
-            if (pm > ms) { heap[k].seg = heap[k >> 1].seg; heap[k].maxSeq = pm; k >>= 1; } else break;
+        if (heapN < MT_WAVE) {
+            const int n = heapN;
+            auto hs = wave_map(n, [&](int i) MT_LAM { return hp(i).seg; });
+            auto hm = wave_map(n, [&](int i) MT_LAM { return hp(i).maxSeq; });
+            while (k > 1) {
+                const int pm = wave_at(hm, k >> 1);
+                if (pm > ms) { hs = wave_set(hs, k, wave_at(hs, k >> 1)); hm = wave_set(hm, k, pm); k >>= 1; } else break;
+            }
+            hs = wave_set(hs, k, s); hm = wave_set(hm, k, ms);
+            const int n1 = n + 1;
+            wave_for(n1, [&](int i) MT_LAM { if (i >= k) { hp(i).seg = own(hs, i); hp(i).maxSeq = own(hm, i); } });
+            if (k == 1) heapTop = ms;
+            return;
         }
-        heap[k].seg = s; heap[k].maxSeq = ms;
+        while (k > 1) {
+            const int pm = uni(hp(k >> 1).maxSeq);
+            if (pm > ms) { hp(k).seg = hp(k >> 1).seg; hp(k).maxSeq = pm; k >>= 1; } else break;
+        }
+        hp(k).seg = s; hp(k).maxSeq = ms;
         if (k == 1) heapTop = ms;
     }
     MT_HD MtHeapE heapGet() {                                 // Heap.get + fixdown, collections.ts:230-268
-        MtHeapE x; x.seg = uni(heap[1].seg); x.maxSeq = uni(heap[1].maxSeq);
-        const int lseg = uni(heap[heapN].seg), lms = uni(heap[heapN].maxSeq);
+        MT_EV(3, 1); MT_EV(7, heapN - 1);
+        if (heapN < MT_WAVE) {
+            const int n0 = heapN + 1;
+            auto hs = wave_map(n0, [&](int i) MT_LAM { return hp(i).seg; });
+            auto hm = wave_map(n0, [&](int i) MT_LAM { return hp(i).maxSeq; });
+            MtHeapE x; x.seg = wave_at(hs, 1); x.maxSeq = wave_at(hm, 1);
+            const int lseg = wave_at(hs, heapN), lms = wave_at(hm, heapN);
+            heapN--;
+            heapTop = 0x7FFFFFFF;
+            if (heapN >= 1) {
+                const int n = heapN;
+                int k = 1;
+                heapTop = lms;
+                while ((k << 1) <= n) {
+                    int j = k << 1;
+                    int cs = wave_at(hs, j), cm = wave_at(hm, j);
+                    if (j < n) {
+                        const int cm1 = wave_at(hm, j + 1);
+                        if (cm > cm1) { j++; cs = wave_at(hs, j); cm = cm1; }
+                    }
+                    if (lms <= cm) break;
+                    MT_EV(4, 1);
+                    if (k == 1) heapTop = cm;
+                    hs = wave_set(hs, k, cs); hm = wave_set(hm, k, cm); k = j;
+                }
+                hs = wave_set(hs, k, lseg); hm = wave_set(hm, k, lms);
+                const int n1 = n + 1;
+                wave_for(n1, [&](int i) MT_LAM { if (i >= 1) { hp(i).seg = own(hs, i); hp(i).maxSeq = own(hm, i); } });
+            }
+            return x;
+        }
+        MtHeapE x; x.seg = uni(hp(1).seg); x.maxSeq = uni(hp(1).maxSeq);
+        const int lseg = uni(hp(heapN).seg), lms = uni(hp(heapN).maxSeq);
         heapN--;
         heapTop = 0x7FFFFFFF;
-        MT_EV(3, 1); MT_EV(7, heapN);
         if (heapN >= 1) {
             int k = 1;
             heapTop = lms;
             while ((k << 1) <= heapN) {
                 int j = k << 1;
-                int hs = uni(heap[j].seg), hm = uni(heap[j].maxSeq);
+                int hs = uni(hp(j).seg), hm = uni(hp(j).maxSeq);
                 if (j < heapN) {
-                    const int hm1 = uni(heap[j + 1].maxSeq);
-                    if (hm > hm1) { j++; hs = uni(heap[j].seg); hm = hm1; }
+                    const int hm1 = uni(hp(j + 1).maxSeq);
+                    if (hm > hm1) { j++; hs = uni(hp(j).seg); hm = hm1; }
                 }
                 if (lms <= hm) break;
                 MT_EV(4, 1);
                 if (k == 1) heapTop = hm;
-                heap[k].seg = hs; heap[k].maxSeq = hm; k = j;
+                hp(k).seg = hs; hp(k).maxSeq = hm; k = j;
             }
-            heap[k].seg = lseg; heap[k].maxSeq = lms;
+            hp(k).seg = lseg; hp(k).maxSeq = lms;
         }
         return x;
     }
     MT_HD void addToLRUSet(int s, int sq) {                   // MT/mergeTree.ts:1262-1272
-        const int p = uni(R[s].parent);
-        const uint32_t m = uni(R[s].meta);
-        if (uni(blk[p].scour) != 1 && sq > curSeq) {
-            blk[p].scour = 1;
-            if ((m & MT_M_HREF) != MT_M_HREF) R[s].meta = m + MT_M_HREF1;   // saturated: never recycled
+        const int p = uni(row(s).parent);
+        const uint32_t m = uni(row(s).meta);
+        if (uni(bk(p).scour) != 1 && sq > curSeq) {
+            bk(p).scour = 1;
+            if ((m & MT_M_HREF) != MT_M_HREF) row(s).meta = m + MT_M_HREF1;   // saturated: never recycled
             heapAdd(s, sq);
         }
     }
@@ -624,16 +792,16 @@ struct MtEng {
             const int m = (rowTop - base) < MT_WAVE ? (rowTop - base) : MT_WAVE;
             auto ln = wave_map(m, [&](int k) MT_LAM {
                 const int s = base + k;
-                return (R[s].parent >= 0 && !(R[s].meta & MT_M_MARKER)) ? R[s].len : 0;
+                return (row(s).parent >= 0 && !(row(s).meta & MT_M_MARKER)) ? row(s).len : 0;
             });
             auto pre = wave_excl_scan(ln);
             const int tot = wave_sum(ln);
             wave_for(m, [&](int k) MT_LAM {
                 const int s = base + k, l = own(ln, k);
                 if (l <= 0) return;
-                const int o = w + own(pre, k), t0 = R[s].toff;
+                const int o = w + own(pre, k), t0 = row(s).toff;
                 for (int q = 0; q < l; q++) dst[o + q] = text[t0 + q];
-                R[s].toff = o; R[s].tcap = l;
+                row(s).toff = o; row(s).tcap = l;
             });
             w += tot;
         }
@@ -652,14 +820,14 @@ struct MtEng {
     // region of twice the size (amortized O(appended chars)).
     // Returns the new (toff, tcap) of pv through references; lengths known by the caller.
     MT_HD void appendText(int pv, int lp, int& tp, int& cp, int s, int ls, int ts, int cs) {
-        if (ts == tp + lp && cp == lp) { R[pv].len = lp + ls; cp = lp + cs; R[pv].tcap = cp; return; }
-        if (lp + ls <= cp) { copyText(tp + lp, ts, ls); R[pv].len = lp + ls; return; }
+        if (ts == tp + lp && cp == lp) { row(pv).len = lp + ls; cp = lp + cs; row(pv).tcap = cp; return; }
+        if (lp + ls <= cp) { copyText(tp + lp, ts, ls); row(pv).len = lp + ls; return; }
         int nc = 2 * (lp + ls); if (nc < 16) nc = 16;
-        if (textTop + nc > (int)S.textCap) { textGC(); nc = lp + ls; tp = uni(R[pv].toff); ts = uni(R[s].toff); }
+        if (textTop + nc > (int)S.textCap) { textGC(); nc = lp + ls; tp = uni(row(pv).toff); ts = uni(row(s).toff); }
         const int o = textAlloc(nc);
         if (o < 0) return;
         copyText(o, tp, lp); copyText(o + lp, ts, ls);
-        R[pv].toff = o; R[pv].tcap = nc; R[pv].len = lp + ls;
+        row(pv).toff = o; row(pv).tcap = nc; row(pv).len = lp + ls;
         tp = o; cp = nc;
     }
     // scourNode for a block of rows (MT/mergeTree.ts:1278-1356); kept children
@@ -668,13 +836,13 @@ struct MtEng {
         // Prefetch every child's fields (and the last text unit) in parallel, then
         // run the sequential merge chain on registers.
         auto f = kids(B, n);
-        auto fm = wave_map(n, [&](int j) MT_LAM { return (int)R[own(f, j)].meta; });
-        auto fs = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].seq; });
-        auto fr = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].rseq; });
-        auto fl = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].len; });
-        auto fp = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].props; });
-        auto ft = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].toff; });
-        auto fc = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].tcap; });
+        auto fm = wave_map(n, [&](int j) MT_LAM { return (int)row(own(f, j)).meta; });
+        auto fs = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).seq; });
+        auto fr = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).rseq; });
+        auto fl = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).len; });
+        auto fp = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).props; });
+        auto ft = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).toff; });
+        auto fc = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).tcap; });
         auto fe = wave_map(n, [&](int j) MT_LAM {
             const int l = own(fl, j);
             return (!(own(fm, j) & MT_M_MARKER) && l > 0) ? (int)text[own(ft, j) + l - 1] : 0;
@@ -683,9 +851,9 @@ struct MtEng {
         int epoch = gcEpoch;
         for (int k = 0; k < n; k++) {
             if (epoch != gcEpoch) {                                // text moved: refresh prefetched offsets
-                ft = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].toff; });
-                fc = wave_map(n, [&](int j) MT_LAM { return R[own(f, j)].tcap; });
-                if (prev >= 0) { prevToff = uni(R[prev].toff); prevCap = uni(R[prev].tcap); }
+                ft = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).toff; });
+                fc = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).tcap; });
+                if (prev >= 0) { prevToff = uni(row(prev).toff); prevCap = uni(row(prev).tcap); }
                 epoch = gcEpoch;
             }
             const int s = wave_at(f, k);
@@ -694,7 +862,7 @@ struct MtEng {
             if (mt & MT_M_REMOVED) {
                 if (wave_at(fr, k) > minSeq) sc->hold[nh++] = s;
                 else {                                             // UNLINK
-                    R[s].parent = -1;
+                    row(s).parent = -1;
                     if (!(mt & (MT_M_HREF | MT_M_INWIN))) freeRow(s);
                 }
                 prev = -1;
@@ -705,7 +873,7 @@ struct MtEng {
                 if (can) can = propsMatch(prevProps, ps);
                 if (can) {
                     appendText(prev, prevLen, prevToff, prevCap, s, ls, wave_at(ft, k), wave_at(fc, k));
-                    R[s].parent = -1;
+                    row(s).parent = -1;
                     if (!(mt & (MT_M_HREF | MT_M_INWIN))) freeRow(s);
                     prevLen += ls; prevLast = wave_at(fe, k);
                 } else {
@@ -725,7 +893,7 @@ struct MtEng {
     MT_HD void updatePathLens(int B) {                        // blockUpdatePathLengths(..., newStructure)
         while (B >= 0) {
             const BlkH h = head(B);
-            blk[B].len = sumObs(B, h.n, h.height);
+            bk(B).len = sumObs(B, h.n, h.height);
             B = h.parent;
         }
     }
@@ -741,7 +909,7 @@ struct MtEng {
                 if (bh.height == 0) nh = scourLeaf(cb, bh.n, nh);
                 else {
                     const int base = nh;
-                    wave_for(bh.n, [&](int k) MT_LAM { sc->hold[base + k] = blk[cb].c[k]; });
+                    wave_for(bh.n, [&](int k) MT_LAM { sc->hold[base + k] = bk(cb).c[k]; });
                     nh += bh.n;
                 }
                 freeBlock(cb);
@@ -755,16 +923,16 @@ struct MtEng {
                 const int NB = allocBlock();
                 if (NB < 0) return;
                 const int r0 = rd;
-                wave_for(8, [&](int i) MT_LAM { blk[NB].c[i] = i < cntc ? sc->hold[r0 + i] : -1; });
+                wave_for(8, [&](int i) MT_LAM { bk(NB).c[i] = i < cntc ? sc->hold[r0 + i] : -1; });
                 wave_for(cntc, [&](int i) MT_LAM { setChildParent(chh, sc->hold[r0 + i], NB); });
                 rd += cntc;
-                blk[NB].n = cntc; blk[NB].height = chh; blk[NB].parent = P; blk[NB].scour = -1;
+                bk(NB).n = cntc; bk(NB).height = chh; bk(NB).parent = P; bk(NB).scour = -1;
                 wave_sync();
-                blk[NB].len = sumObs(NB, cntc, chh);
+                bk(NB).len = sumObs(NB, cntc, chh);
                 packed = wave_map(8, [&](int i) MT_LAM { return i == ni ? NB : own(packed, i); });
             }
-            wave_for(8, [&](int i) MT_LAM { blk[P].c[i] = own(packed, i); });
-            blk[P].n = cc;
+            wave_for(8, [&](int i) MT_LAM { bk(P).c[i] = own(packed, i); });
+            bk(P).n = cc;
             wave_sync();
             if (cc < MT_MAXN / 2 && ph.parent >= 0) { P = ph.parent; continue; }
             updatePathLens(P);
@@ -777,25 +945,25 @@ struct MtEng {
         MT_PE(MT_PH_ZAMBONI, t0);
     }
     MT_HD void zamboniInner() {
-        uValid = false;
         for (int i = 0; i < MT_ZMAX; i++) {
             if (heapN == 0 || heapTop > minSeq) break;
+            uValid = false;                                   // scour/pack may restructure
             MT_QB(q0); MT_QC(6);
             const MtHeapE e = heapGet();
             MT_QE(5, q0);
-            const int p = uni(R[e.seg].parent);
-            uint32_t em = uni(R[e.seg].meta);
-            if ((em & MT_M_HREF) != MT_M_HREF) { em -= MT_M_HREF1; R[e.seg].meta = em; }
+            const int p = uni(row(e.seg).parent);
+            uint32_t em = uni(row(e.seg).meta);
+            if ((em & MT_M_HREF) != MT_M_HREF) { em -= MT_M_HREF1; row(e.seg).meta = em; }
             if (p < 0 && !(em & (MT_M_HREF | MT_M_INWIN))) freeRow(e.seg);
-            if (p >= 0 && uni(blk[p].scour) != 0) {
+            if (p >= 0 && uni(bk(p).scour) != 0) {
                 const BlkH h = head(p);
                 MT_QB(q1);
                 const int nh = scourLeaf(p, h.n, 0);
                 MT_QE(7, q1);
-                blk[p].scour = 0;
+                bk(p).scour = 0;
                 if (nh < h.n) {
-                    wave_for(8, [&](int j) MT_LAM { blk[p].c[j] = j < nh ? sc->hold[j] : -1; });
-                    blk[p].n = nh;
+                    wave_for(8, [&](int j) MT_LAM { bk(p).c[j] = j < nh ? sc->hold[j] : -1; });
+                    bk(p).n = nh;
                     wave_sync();
                     if (nh < MT_MAXN / 2 && h.parent >= 0) packParent(h.parent);
                     else updatePathLens(p);
@@ -845,8 +1013,8 @@ struct MtEng {
             if (nv < 0) {
                 if (at >= 0) {
                     auto k1 = wave_from8<1>(kk), v1 = wave_from8<1>(vv);
-                    kk = wave_map(8, [&](int i) MT_LAM { return i < at ? own(kk, i) : own(k1, i); });
-                    vv = wave_map(8, [&](int i) MT_LAM { return i < at ? own(vv, i) : own(v1, i); });
+                    kk = wave_map(8, [&](int i) MT_LAM { const int a = own(kk, i), b = own(k1, i); return i < at ? a : b; });
+                    vv = wave_map(8, [&](int i) MT_LAM { const int a = own(vv, i), b = own(v1, i); return i < at ? a : b; });
                     n--;
                 }
             } else if (at >= 0) {
@@ -902,14 +1070,14 @@ struct MtEng {
                         auto nd = wave_map(h.n, [&](int j) MT_LAM {
                             if (!own(cond, j)) return 0;
                             const int s = own(ch, j);
-                            const uint32_t mt = R[s].meta;
+                            const uint32_t mt = row(s).meta;
                             if (mt & MT_M_REMOVED) {                   // overlapping remove: keep first remover
-                                R[s].ovl = R[s].ovl | (1ull << c);
+                                row(s).ovl = row(s).ovl | (1ull << c);
                                 return 0;
                             }
-                            R[s].meta = (mt & ~MT_M_RCLIENT) | MT_M_REMOVED | ((uint32_t)c << 8);
-                            R[s].rseq = sq;
-                            return R[s].len;
+                            row(s).meta = (mt & ~MT_M_RCLIENT) | MT_M_REMOVED | ((uint32_t)c << 8);
+                            row(s).rseq = sq;
+                            return row(s).len;
                         });
                         obsDelta = -wave_sum8(nd);
                         wave_sync();
@@ -918,16 +1086,16 @@ struct MtEng {
                         for (int j = 0; j < h.n; j++) {
                             if (!wave_at(cond, j)) continue;
                             const int s = wave_at(ch, j);
-                            const int old = uni(R[s].props);
+                            const int old = uni(row(s).props);
                             int nw;
                             if (old == uni(sc->lastOld)) nw = uni(sc->lastNew);
                             else { nw = applyPropSet(old, opset, rewrite); sc->lastOld = old; sc->lastNew = nw; }
-                            R[s].props = nw;
+                            row(s).props = nw;
                         }
                     }
                     addToLRUSet(wave_at(ch, first), sq);
                 }
-                if (mode == MT_MAP_REMOVE) blk[B].len = h.len + obsDelta;
+                if (mode == MT_MAP_REMOVE) bk(B).len = h.len + obsDelta;
                 const int d = uni(sc->fD[L]) + obsDelta;
                 L--;
                 if (L >= 0) {
@@ -946,7 +1114,7 @@ struct MtEng {
                 continue;
             }
             const int d = uni(sc->fD[L]);
-            if (d != 0) blk[B].len = h.len + d;
+            if (d != 0) bk(B).len = h.len + d;
             L--;
             if (L >= 0) {
                 sc->fD[L] = uni(sc->fD[L]) + d; sc->fS[L] = uni(sc->fS[L]) - uni(sc->fL[L]);
@@ -967,17 +1135,17 @@ struct MtEng {
         if (L > 0) {
             const int n = allocRow();
             if (n < 0) return;
-            R[n].len = L; R[n].seq = sq; R[n].rseq = MT_NOREM;
-            R[n].meta = (uint32_t)c | (marker ? MT_M_MARKER : 0u);
-            R[n].ovl = 0ull; R[n].parent = -1;
-            R[n].props = segProps >= 0 ? applyPropSet(-1, segProps, false) : -1;
-            R[n].tcap = marker ? 0 : plen;
-            if (marker) R[n].toff = refType;
+            row(n).len = L; row(n).seq = sq; row(n).rseq = MT_NOREM;
+            row(n).meta = (uint32_t)c | (marker ? MT_M_MARKER : 0u);
+            row(n).ovl = 0ull; row(n).parent = -1;
+            row(n).props = segProps >= 0 ? applyPropSet(-1, segProps, false) : -1;
+            row(n).tcap = marker ? 0 : plen;
+            if (marker) row(n).toff = refType;
             else {
-                R[n].parent = -1;                                  // not yet linked: excluded from compaction
+                row(n).parent = -1;                                  // not yet linked: excluded from compaction
                 const int t0 = textAlloc(plen);
                 if (t0 < 0) return;
-                R[n].toff = t0;
+                row(n).toff = t0;
                 for (int base = 0; base < plen; base += MT_WAVE) {
                     const int m = (plen - base) < MT_WAVE ? (plen - base) : MT_WAVE;
                     wave_for(m, [&](int k) MT_LAM { text[t0 + base + k] = src[base + k]; });
@@ -986,9 +1154,19 @@ struct MtEng {
             }
             wave_sync();
             MT_PB(t1);
-            w = walk(MT_WALK_INSERT, pos, r, c, n, L);
+            if ((w == MT_W_OK || w == MT_W_NOCHANGE) && !lastSplit) {
+                // The split walk (ensureIntervalBoundary) and the insert walk descend
+                // by the same rule; with no block split in between the insert walk
+                // would reach the same leaf slot: lastIdx (before the found row, at
+                // the block end, or before the new right half of a split row).
+                insertAtPath(lastL, lastIdx, n, L);
+                uValid = false;
+                w = MT_W_OK;
+            } else {
+                w = walk(MT_WALK_INSERT, pos, r, c, n, L);
+            }
             MT_PE(MT_PH_INSERT, t1);
-            if (w != MT_W_OK || R[n].parent < 0) { status |= MT_DS_INSERT_FAILED; return; }
+            if (w != MT_W_OK || row(n).parent < 0) { status |= MT_DS_INSERT_FAILED; return; }
             c_rows += 2;
             winAdd(n);
             if (sq > minSeq) addToLRUSet(n, sq);
@@ -1011,3 +1189,5 @@ struct MtEng {
         zamboni();
     }
 };
+using MtEng = MtEngT<false>;
+

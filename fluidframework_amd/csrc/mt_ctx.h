@@ -13,12 +13,14 @@ struct mt_ctx {
     std::string err;
     // device op batch (resident)
     struct DevBuf { void* p = nullptr; size_t cap = 0; };
-    DevBuf b_doc, b_off, b_rec, b_pay, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3;
+    DevBuf b_cursor, b_doc, b_off, b_rec, b_pay, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3;
     MtOps ops{};
     uint32_t n_runs = 0;
     MtGen gen{};
     uint32_t gen_docs = 0;
     float last_ms = 0.f;
+    // LDS residency of the replay (mt_set_residency): on/off and the pool caps
+    int use_lds = 0, lds_rows = MT_L_ROWS, lds_blks = MT_L_BLKS, lds_heap = MT_L_HEAP;
     void* stream = nullptr;
     void* ev0 = nullptr;
     void* ev1 = nullptr;

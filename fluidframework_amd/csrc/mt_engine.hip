@@ -12,14 +12,38 @@
 #ifndef MT_WAVES_PER_SIMD
 #define MT_WAVES_PER_SIMD 4
 #endif
-// Replay: Client.applyMsg over each document's resident op run (the timed hot path).
-__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_kernel(MtState S, MtOps ops) {
+// Replay: Client.applyMsg over each document's resident op run (the timed hot
+// path), in two launches.  mt_replay_lds_kernel moves the document's rows,
+// blocks, heap and window into LDS and runs as far as they fit (cursor[run] =
+// the first op not applied); mt_replay_kernel finishes any remainder with the
+// pools in HBM.
+#ifndef MT_LDS_WAVES_PER_SIMD
+#define MT_LDS_WAVES_PER_SIMD 1
+#endif
+__global__ __launch_bounds__(64, MT_LDS_WAVES_PER_SIMD) void mt_replay_lds_kernel(MtState S, MtOps ops, uint32_t* cursor, int lr, int lb, int lh) {
     __shared__ MtScratch sc;
     const uint32_t run = blockIdx.x;
     const uint32_t doc = ops.doc_ids[run];
+    const uint32_t o0 = ops.op_off[run];
+    MtEngT<true> e;
+    e.bind(S, doc, &sc);
+    uint32_t cur = o0;
+    if (e.toLds(lr, lb, lh)) {
+        cur = mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0);
+        e.fromLds();
+    }
+    cursor[run] = cur;
+    e.store(doc);
+}
+__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_kernel(MtState S, MtOps ops, const uint32_t* cursor) {
+    __shared__ MtScratch sc;
+    const uint32_t run = blockIdx.x;
+    const uint32_t o0 = cursor ? cursor[run] : ops.op_off[run];
+    if (o0 >= ops.op_off[run + 1]) return;
+    const uint32_t doc = ops.doc_ids[run];
     MtEng e;
     e.bind(S, doc, &sc);
-    mt_replay_run(e, ops, run, doc, nullptr, nullptr);
+    mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0);
     e.store(doc);
 }
 // Generation: the same engine acting as sequencer + observer, writing the op
@@ -31,7 +55,7 @@ __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_generate_kernel(MtSt
     const uint32_t doc = ops.doc_ids[run];
     MtEng e;
     e.bind(S, doc, &sc);
-    mt_replay_run(e, ops, run, doc, &gen, lastRef);
+    mt_replay_run(e, ops, run, doc, &gen, lastRef, ops.op_off[run]);
     e.store(doc);
 }
 __global__ __launch_bounds__(64) void mt_open_kernel(MtState S, uint32_t first) {
@@ -101,7 +125,11 @@ static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     (void)hipGetLastError();
     (void)hipEventRecord((hipEvent_t)c->ev0, s);
     if (g.enabled) hipLaunchKernelGGL(mt_generate_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, g);
-    else hipLaunchKernelGGL(mt_replay_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops);
+    else if (c->use_lds) {
+        hipLaunchKernelGGL(mt_replay_lds_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
+                           c->lds_rows, c->lds_blks, c->lds_heap);
+        hipLaunchKernelGGL(mt_replay_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (const uint32_t*)c->b_cursor.p);
+    } else hipLaunchKernelGGL(mt_replay_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (const uint32_t*)nullptr);
     (void)hipEventRecord((hipEvent_t)c->ev1, s);
     c->ev_pending = true;
     return mtb_check(c);

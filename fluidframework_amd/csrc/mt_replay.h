@@ -18,7 +18,8 @@ struct MtRng {                                     // splitmix64
 // Synthesize message i of document `doc` from the engine's own state (the
 // engine acts as sequencer + observer, so positions are valid under the
 // author's perspective), writing the op record into the batch arrays.
-MT_HD void mt_gen_op(MtEng& e, const MtOps& ops, uint32_t i, uint32_t k, uint32_t doc,
+template <class Eng>
+MT_HD void mt_gen_op(Eng& e, const MtOps& ops, uint32_t i, uint32_t k, uint32_t doc,
                             const MtGen& g, MtRng& rng, int* lastRef) {
     const uint32_t a = rng.u(g.clients);
     const uint32_t lag = rng.u(g.lag_max + 1);
@@ -58,15 +59,23 @@ MT_HD void mt_gen_op(MtEng& e, const MtOps& ops, uint32_t i, uint32_t k, uint32_
     wave_sync();
 }
 
-MT_HD void mt_replay_run(MtEng& e, const MtOps& ops, uint32_t run, uint32_t doc,
-                                const MtGen* g, int* lastRef) {
-    const uint32_t o0 = ops.op_off[run], o1 = ops.op_off[run + 1];
+// Applies ops [o0, op_off[run+1]) of the run.  With LDS pools (e.lds) it stops
+// before an op that could outgrow them and returns that op's index, so the HBM
+// kernel can resume there; otherwise it returns op_off[run+1].
+template <class Eng>
+MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t doc,
+                                const MtGen* g, int* lastRef, uint32_t o0) {
+    const uint32_t o1 = ops.op_off[run + 1];
     MtRng rng; rng.s = 0;
     if (g) {
         rng.s = g->seed ^ (0x9E3779B97F4A7C15ULL * (unsigned long long)(doc + 1));
         for (int c = 0; c < 64; c++) lastRef[c] = 0;
     }
+    // Replay prefetches op i+1's record while op i runs (generation writes the
+    // record at the top of each iteration, so it loads in place).
+    auto wn = wave_map(8, [&](int q) MT_LAM { return (!g && o0 < o1) ? ((const int*)&ops.rec[o0])[q] : 0; });
     for (uint32_t i = o0; i < o1; i++) {
+        if (Eng::kLds && !e.ldsHeadroom()) return i;
 #if defined(MT_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
         const unsigned long long tg = __builtin_amdgcn_s_memtime();
         if (g) mt_gen_op(e, ops, i, i - o0, doc, *g, rng, lastRef);
@@ -75,8 +84,10 @@ MT_HD void mt_replay_run(MtEng& e, const MtOps& ops, uint32_t run, uint32_t doc,
 #else
         if (g) mt_gen_op(e, ops, i, i - o0, doc, *g, rng, lastRef);
 #endif
-        // one 32-byte record: lanes 0..7 load a dword each, then broadcast
-        auto w = wave_map(8, [&](int q) MT_LAM { return ((const int*)&ops.rec[i])[q]; });
+        // one 32-byte record: lanes 0..7 hold a dword each, then broadcast
+        auto w = wn;
+        if (g) w = wave_map(8, [&](int q) MT_LAM { return ((const int*)&ops.rec[i])[q]; });
+        else if (i + 1 < o1) wn = wave_map(8, [&](int q) MT_LAM { return ((const int*)&ops.rec[i + 1])[q]; });
         const uint32_t w0 = (uint32_t)wave_at(w, 0);
         const int ty = (int)(w0 & 0xFF);
         const uint32_t fl = (w0 >> 8) & 0xFF;
@@ -116,4 +127,5 @@ MT_HD void mt_replay_run(MtEng& e, const MtOps& ops, uint32_t run, uint32_t doc,
         }
         if (e.status) break;
     }
+    return o1;
 }

@@ -46,7 +46,7 @@ __device__ __forceinline__ void wave_for(int n, F f) {
     const int k = __lane_id();
     if (k < n) f(k);
 }
-template <class T> __device__ __forceinline__ T own(const T& a, int) { return a; }
+template <class T> __device__ __forceinline__ T own(T a, int) { return a; }   // by value: no address-of, so no select-of-pointers
 __device__ __forceinline__ int wave_at(int a, int j) { return __builtin_amdgcn_readlane(a, j); }
 __device__ __forceinline__ uint32_t wave_at(uint32_t a, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)a, j); }
 __device__ __forceinline__ bool wave_at(bool a, int j) { return __builtin_amdgcn_readlane((int)a, j) != 0; }
@@ -99,6 +99,8 @@ template <int OFF> __device__ __forceinline__ int wave_from8(int a) {
     if constexpr (OFF < 0) return dpp0<0x110 | (-OFF)>(a);
     else return dpp0<0x100 | OFF>(a);
 }
+// lane k's value replaced by v (k uniform)
+__device__ __forceinline__ int wave_set(int a, int k, int v) { return __lane_id() == k ? v : a; }
 // per-lane add into wave-private LDS (conflicting lanes serialize in hardware)
 __device__ __forceinline__ void lds_add(int* p, int v) { __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
 __device__ __forceinline__ void wave_sync() {
@@ -172,6 +174,7 @@ template <int OFF> inline LaneArr<int> wave_from8(const LaneArr<int>& a) {
     for (int k = 0; k < MT_WAVE; k++) { const int s = (k & 15) + OFF; r.v[k] = (s >= 0 && s < 16) ? a.v[(k & ~15) + s] : 0; }
     return r;
 }
+inline LaneArr<int> wave_set(LaneArr<int> a, int k, int v) { if (k >= 0 && k < MT_WAVE) a.v[k] = v; return a; }
 inline void lds_add(int* p, int v) { *p += v; }
 inline void wave_sync() {}
 #endif

@@ -55,6 +55,8 @@ def _bind(lib, prefix: str):
         destroy=f("destroy", None, [P]),
         last_error=f("last_error", ctypes.c_char_p, [P]),
         docs_open=f("docs_open", ctypes.c_int, [P, U32, U32]),
+        doc_pools=f("doc_pools", ctypes.c_int, [P, U32, P, P]),
+        set_residency=f("set_residency", ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
         set_props=f("set_props", ctypes.c_int, [P, ctypes.POINTER(MtPropTable)]),
         set_client_names=f("set_client_names", ctypes.c_int, [P, U32, P]),
         apply_batch=f("apply_batch", ctypes.c_int, [P, ctypes.POINTER(MtOpBatch)]),
@@ -201,6 +203,18 @@ class Engine:
         self._check(self.fn["doc_counters_get"](self.h, len(d), d.ctypes.data, ctypes.addressof(out)),
                     "mt_doc_counters_get")
         return {f: np.array([getattr(x, f) for x in out], np.uint64) for f, _ in MtDocCounters._fields_}
+
+    def set_residency(self, use_lds: bool = True, rows: int = 0, blocks: int = 0, heap: int = 0):
+        """mt_set_residency: LDS-resident replay on/off and (lowered) LDS pool caps."""
+        self._check(self.fn["set_residency"](self.h, int(use_lds), rows, blocks, heap), "mt_set_residency")
+
+    def pools(self, docs) -> np.ndarray:
+        """Per-document pool occupancy (mt_doc_pools): columns rowTop, blkTop, heapN,
+        winN, textTop, psetTop, height, rfN."""
+        d = _u32(docs)
+        out = np.zeros((len(d), 8), np.int32)
+        self._check(self.fn["doc_pools"](self.h, len(d), d.ctypes.data, out.ctypes.data), "mt_doc_pools")
+        return out
 
     def update_seq(self, docs, msn, seq):
         d, m, s = _u32(docs), _i32(msn), _i32(seq)

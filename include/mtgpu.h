@@ -163,6 +163,12 @@ int  mt_apply_batch(mt_ctx* ctx, const mt_op_batch* batch);
  * documents it names without any host->device traffic (the bench's timed path). */
 int  mt_upload_batch(mt_ctx* ctx, const mt_op_batch* batch);
 int  mt_replay_resident(mt_ctx* ctx);
+/* Residency of the replay: with use_lds (default off) a document whose rows,
+ * blocks, zamboni heap and window fit the LDS caps runs out of LDS, and one that
+ * outgrows them is finished from HBM at the exact op it reached.  rows/blocks/
+ * heap (0 = compiled maximum) may only lower the caps; tests use small caps to
+ * force the hand-over. */
+int  mt_set_residency(mt_ctx* ctx, int use_lds, int rows, int blocks, int heap);
 /* Milliseconds of the last replay kernel(s), timed with HIP events on the
  * context stream. */
 int  mt_last_replay_ms(mt_ctx* ctx, float* ms);
@@ -173,6 +179,12 @@ int  mt_sync(mt_ctx* ctx);
 
 int  mt_doc_status(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, uint32_t* out_status);
 int  mt_doc_counters_get(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, mt_doc_counters* out);
+
+/* Pool occupancy per document, 8 int32 each: rows high-water (rowTop), blocks
+ * high-water, zamboni heap entries, window rows, text arena units in use,
+ * property sets, tree height, recycled rows held.  Used by hosts to size
+ * mt_limits for the next batch. */
+int  mt_doc_pools(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, int32_t* out);
 
 /* Perspective length (refSeq, client) of each document (mergeTree.ts:1569). */
 int  mt_get_length(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,

@@ -18,12 +18,38 @@ static void mtb_memset(void* p, int v, size_t n) { memset(p, v, n); }
 static void mtb_h2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static void mtb_d2h(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static int mtb_sync(mt_ctx*) { return MT_OK; }
+// Same two launches as the device (mt_engine.hip): LDS-resident pass, then the
+// HBM pass resuming at each run's cursor.
 static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
+    if (g.enabled) {
+        for (uint32_t run = 0; run < n_runs; run++) {
+            MtScratch sc; int lastRef[64];
+            const uint32_t doc = c->ops.doc_ids[run];
+            MtEng e; e.bind(c->S, doc, &sc);
+            mt_replay_run(e, c->ops, run, doc, &g, lastRef, c->ops.op_off[run]);
+            e.store(doc);
+        }
+        return MT_OK;
+    }
+    uint32_t* cursor = (uint32_t*)c->b_cursor.p;
     for (uint32_t run = 0; run < n_runs; run++) {
-        MtScratch sc; int lastRef[64];
+        const uint32_t doc = c->ops.doc_ids[run], o0 = c->ops.op_off[run];
+        uint32_t cur = o0;
+        if (c->use_lds) {
+            MtScratch sc; MtEngT<true> e; e.bind(c->S, doc, &sc);
+            if (e.toLds(c->lds_rows, c->lds_blks, c->lds_heap)) {
+                cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
+                e.fromLds();
+            }
+            e.store(doc);
+        }
+        cursor[run] = cur;
+    }
+    for (uint32_t run = 0; run < n_runs; run++) {
+        if (cursor[run] >= c->ops.op_off[run + 1]) continue;
         const uint32_t doc = c->ops.doc_ids[run];
-        MtEng e; e.bind(c->S, doc, &sc);
-        mt_replay_run(e, c->ops, run, doc, g.enabled ? &g : nullptr, lastRef);
+        MtScratch sc; MtEng e; e.bind(c->S, doc, &sc);
+        mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, cursor[run]);
         e.store(doc);
     }
     return MT_OK;

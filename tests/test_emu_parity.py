@@ -34,6 +34,8 @@ CONFIGS = {
 def compare(batch, props, n_docs, factory=None, **cap):
     eng = (factory or emu_engine)(n_docs, rows_per_doc=cap.get("rows", 20000), window_per_doc=cap.get("win", 8192),
                      propsets_per_doc=cap.get("psets", 8192), text_per_doc=cap.get("text", 1 << 18))
+    if "residency" in cap:
+        eng.set_residency(*cap["residency"])
     eng.upload_props(props)
     eng.upload_names(NAMES)
     eng.open_docs(0, n_docs)
@@ -71,6 +73,19 @@ def test_emu_matches_oracle(cfg):
     batch, st, _ = generate(p, props)
     assert st == [0] * 4
     compare(batch, props, 4)
+
+
+# LDS residency hand-over: tiny LDS caps make documents leave LDS mid-run (at
+# different ops, with different pools the binding one) and finish from HBM;
+# (0, ...) runs the HBM-pool kernel alone.  Results must not change.
+@pytest.mark.parametrize("res", [(1, 40, 40, 12), (1, 90, 48, 24), (1, 256, 96, 96), (0, 0, 0, 0)])
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "grow"])
+def test_emu_residency_handover_matches_oracle(cfg, res):
+    props = ann_props()
+    p = gen_params(seed=21, n_docs=3, **CONFIGS[cfg])
+    batch, st, _ = generate(p, props)
+    assert st == [0] * 3
+    compare(batch, props, 3, residency=res)
 
 
 @pytest.mark.parametrize("cfg", ["cfg1", "cfg3"])

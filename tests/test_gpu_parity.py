@@ -24,6 +24,17 @@ def test_gpu_matches_oracle(cfg):
     compare(batch, props, 8, factory=gpu_engine)
 
 
+@pytest.mark.parametrize("res", [(1, 40, 40, 12), (1, 90, 48, 24), (0, 0, 0, 0)])
+def test_gpu_residency_handover_matches_oracle(res):
+    # Small LDS caps: documents leave LDS mid-run and mt_replay_kernel finishes
+    # them from HBM at the exact op reached; (0, ...) is the HBM kernel alone.
+    props = ann_props()
+    p = gen_params(seed=21, n_docs=6, **CONFIGS["cfg2"])
+    batch, st, _ = generate(p, props)
+    assert st == [0] * 6
+    compare(batch, props, 6, factory=gpu_engine, residency=res)
+
+
 def test_gpu_deep_tree_matches_oracle():
     props = ann_props()
     cfg = dict(clients=8, lag=32, ins=70, rem=20, ins_len=8, rem_len=8, ops=20000, ann_sets=24, rewrite=5)

@@ -12,14 +12,18 @@ from fluidframework_amd.engine import Engine
 from fluidframework_amd.batch import MtGenParams
 import bench
 
-lib = os.path.join(ROOT, "fluidframework_amd", "libmtgpu_prof.so")
+flag = os.environ.get("MT_PROF_FLAG", "MT_PROFILE")
+lib = os.path.join(ROOT, "fluidframework_amd", f"libmtgpu_{flag.lower()}.so")
 if not os.path.exists(lib):
     subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared",
-                           "-DMT_PROFILE", "-o", lib, os.path.join(ROOT, "fluidframework_amd", "csrc", "mt_engine.hip")])
+                           f"-D{flag}", "-o", lib, os.path.join(ROOT, "fluidframework_amd", "csrc", "mt_engine.hip")])
 cfg = sys.argv[1] if len(sys.argv) > 1 else "config2"
 docs = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 c = dict(bench.CONFIGS[cfg]); c["docs"] = docs
+if len(sys.argv) > 3: c["ops"] = int(sys.argv[3])
+res = sys.argv[4] if len(sys.argv) > 4 else "lds"
 eng = Engine(docs, lib_path=lib, **bench.caps_for(c))
+eng.set_residency(res == "lds")
 eng.upload_props(bench.ann_props()); eng.upload_names(['"c%d"' % i for i in range(64)])
 p = MtGenParams(7, docs, c["ops"], c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"], c["rem_len"], c["ann_sets"], c["rewrite"])
 eng.generate(p); eng.sync(); eng.generated_to_resident()
@@ -35,6 +39,9 @@ fn.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
 fn(eng.h, docs, raw.ctypes.data)
 tot = raw.sum(axis=0).astype(float)
 names = ["computeU", "split-walks", "insert-walk", "rangeMap", "zamboni", "op-total", "gen", "textGC"]
+if flag == "MT_PROFILE2":
+    names = ["walk blkLoad", "walk childLens", "walk levels(n)", "computeU", "computeU(n)", "heapGet", "heapGet(n)", "scourLeaf"]
+print(f"{flag} residency={res} ops={c['ops']}")
 print(f"{cfg} docs={docs} replay wall {dt*1e3:.1f} ms; per-doc mean cycles per msg:")
 for i, n in enumerate(names):
     print(f"  {n:12s} {tot[i]/docs/c['ops']:10.0f} cyc/msg  ({100*tot[i]/max(tot[5],1):5.1f}% of op-total)")
