@@ -108,8 +108,14 @@ int MT_FN(set_props)(mt_ctx* c, const mt_prop_table* P) {
 }
 
 int MT_FN(set_client_names)(mt_ctx* c, uint32_t n, const char* const* cj) {
-    if (!c) return MT_E_INVALID;
+    if (!c || (n && !cj)) return MT_E_INVALID;
     c->names.client_json.assign(cj, cj + n);
+    return MT_OK;
+}
+int MT_FN(set_doc_client_names)(mt_ctx* c, uint32_t doc, uint32_t n, const char* const* cj) {
+    if (!c || doc >= c->S.maxDocs || (n && !cj)) return MT_E_INVALID;
+    if (n == 0) c->doc_clients.erase(doc);
+    else c->doc_clients[doc].assign(cj, cj + n);
     return MT_OK;
 }
 
@@ -290,7 +296,9 @@ int MT_FN(snapshot_v1)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_
     MtHostDoc h;
     for (uint32_t i = 0; i < n; i++) {
         mt_download_doc(c, docs[i], h);
-        std::vector<std::string> blobs = mtsnap::snapshot_blobs(h.view(), c->names);
+        auto dn = c->doc_clients.find(docs[i]);
+        std::vector<std::string> blobs = mtsnap::snapshot_blobs(h.view(), c->names,
+                                                                dn == c->doc_clients.end() ? nullptr : &dn->second);
         if (digest) digest[i] = mtsnap::blobs_digest(blobs);
         for (auto& b : blobs) { c->snap_arena += b; c->blob_off.push_back(c->snap_arena.size()); }
         c->blob_first.push_back((uint32_t)(c->blob_off.size() - 1));

@@ -1,6 +1,7 @@
 // mt_ctx.h — engine context (one per GPU) shared by the backends and the ABI.
 #pragma once
 #include <string>
+#include <unordered_map>
 #include <vector>
 #include "mt_replay.h"
 #include "mt_snapshot.h"
@@ -10,6 +11,7 @@ struct mt_ctx {
     mt_limits lim{};
     MtState S{};
     MtNames names;
+    std::unordered_map<uint32_t, std::vector<std::string>> doc_clients;   // mt_set_doc_client_names
     std::string err;
     // device op batch (resident)
     struct DevBuf { void* p = nullptr; size_t cap = 0; };

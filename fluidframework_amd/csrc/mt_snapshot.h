@@ -118,13 +118,15 @@ inline bool props_match(const MtSnapView& v, const MtNames& nm, int a, int b) {
     return true;
 }
 
-inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtNames& nm) {
+inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtNames& nm,
+                                               const std::vector<std::string>* doc_clients = nullptr) {
+    const std::vector<std::string>& cj = doc_clients ? *doc_clients : nm.client_json;
     const int minSeq = v.hdr.minSeq, curSeq = v.hdr.curSeq;
     std::vector<std::string> segs; std::vector<long long> lens;
     int prev = -1; std::vector<uint16_t> ptext; bool pcloned = false;
     auto client = [&](int c) -> const std::string& {
         static const std::string orig = "\"original\"";
-        return (c >= 0 && c < (int)nm.client_json.size()) ? nm.client_json[c] : orig;
+        return (c >= 0 && c < (int)cj.size()) ? cj[c] : orig;
     };
     auto pushPrev = [&]() {
         if (prev < 0) return;

@@ -59,6 +59,7 @@ def _bind(lib, prefix: str):
         set_residency=f("set_residency", ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
         set_props=f("set_props", ctypes.c_int, [P, ctypes.POINTER(MtPropTable)]),
         set_client_names=f("set_client_names", ctypes.c_int, [P, U32, P]),
+        set_doc_client_names=f("set_doc_client_names", ctypes.c_int, [P, U32, U32, P]),
         apply_batch=f("apply_batch", ctypes.c_int, [P, ctypes.POINTER(MtOpBatch)]),
         upload_batch=f("upload_batch", ctypes.c_int, [P, ctypes.POINTER(MtOpBatch)]),
         replay_resident=f("replay_resident", ctypes.c_int, [P]),
@@ -144,6 +145,12 @@ class Engine:
         self._names_c = arr
         self._check(self.fn["set_client_names"](self.h, len(lits), ctypes.cast(arr, ctypes.c_void_p)),
                     "mt_set_client_names")
+
+    def upload_doc_names(self, doc: int, literals: list[str]):
+        """mt_set_doc_client_names: this document's long client ids by index (JSON literals)."""
+        arr = (ctypes.c_char_p * max(1, len(literals)))(*[s.encode() for s in literals])
+        self._check(self.fn["set_doc_client_names"](self.h, doc, len(literals), ctypes.cast(arr, ctypes.c_void_p)),
+                    "mt_set_doc_client_names")
 
     # ---- replay ----
     def apply(self, batch: OpBatch):
@@ -278,6 +285,8 @@ class MergeTreeClient:
     def __init__(self, engine: Engine, doc_id: int, group: "ClientGroup"):
         self.engine, self.doc_id, self.group = engine, doc_id, group
         self.pending: list = []
+        self.names = ClientNames()       # per-document short client ids (client.ts:658-682)
+        self.names_uploaded = 0
         self.current_seq = 0
         self.min_seq = 0
         self.longClientId = None
@@ -345,15 +354,18 @@ class ClientGroup:
         busy = [c for c in self.clients if c.pending]
         if not busy:
             return
-        bb = BatchBuilder(self.engine.props, self.engine.names)
+        bb = BatchBuilder(self.engine.props, None)
         for c in busy:
+            bb.names = c.names
             bb.begin_doc(c.doc_id)
             for m in c.pending:
                 bb.add_message(m)
                 c.current_seq = int(m["sequenceNumber"])
                 c.min_seq = max(c.min_seq, int(m["minimumSequenceNumber"]))
             c.pending = []
+            if c.names_uploaded != len(c.names.names):
+                self.engine.upload_doc_names(c.doc_id, c.names.json_literals())
+                c.names_uploaded = len(c.names.names)
         batch = bb.build()
-        self.engine.upload_names()
         self.engine.apply(batch)
         self.engine.sync()

@@ -1,0 +1,299 @@
+"use strict";
+/*
+ * Node host of the MI355X merge-tree engine: the TypeScript/Node side of the
+ * drop-in boundary (SURVEY.md §8(b)).
+ *
+ * It mirrors the reference merge-tree `Client` (packages/dds/merge-tree/src/
+ * client.ts, MT/ below) for the passive-observer replay path:
+ *   MergeTreeClient.applyMsg(msg)            Client.applyMsg          MT/client.ts:819
+ *   MergeTreeClient.updateSeqNumbers(m, s)   Client.updateSeqNumbers  MT/client.ts:843
+ *   MergeTreeClient.getLength()              Client.getLength         MT/client.ts:1071
+ *   MergeTreeClient.getText()                createTextHelper().getText  MT/client.ts:917
+ *   MergeTreeClient.snapshot()               Client.snapshot (SnapshotV1) MT/client.ts:923
+ *   MergeTreeClient.startOrUpdateCollaboration  MT/client.ts:1073
+ * Messages are queued per document and applied in device batches: reads flush
+ * every queued document of the group in one mt_apply_batch.  Protocol violations
+ * the reference reports by throwing (assert, common-utils assert.ts:12-16) are
+ * thrown here as Errors when the document's status is read.
+ *
+ * Packing restates Client.applyMsg's dispatch (client.ts:790-841): long client
+ * ids become per-document indices, GROUP members share the message's seq, and
+ * property sets are interned with JS semantics (Object.keys order, JSON.stringify
+ * text, falsiness for "rewrite", matchProperties classes, MT/properties.ts:64-95).
+ */
+const path = require("path");
+
+// MTGPU_NAPI: an alternate build of this addon (the tests' host-emulation build)
+const addon = require(process.env.MTGPU_NAPI || path.join(__dirname, "mtgpu.node"));
+
+const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_GROUP = 3;
+const F_END = 1, F_MARKER = 2, F_REWRITE = 4, F_SEG_PROPS = 8, F_COMBINE = 16;
+const STATUS = {
+    0x01: "ASSERT_SEQ", 0x02: "ASSERT_MSN", 0x04: "INSERT_FAILED", 0x08: "UNSUPPORTED",
+    0x10: "OOM_ROWS", 0x20: "OOM_BLOCKS", 0x40: "OOM_TEXT", 0x80: "OOM_PROPS",
+    0x100: "OOM_HEAP", 0x200: "OOM_WINDOW", 0x400: "PROPS_TOO_MANY",
+};
+function statusNames(st) {
+    return Object.keys(STATUS).filter((b) => st & Number(b)).map((b) => STATUS[b]);
+}
+
+function arrayIndex(k) {
+    // canonical array index (OrdinaryOwnPropertyKeys orders these first)
+    if (!/^(0|[1-9][0-9]{0,9})$/.test(k)) return undefined;
+    const v = Number(k);
+    return v < 4294967295 ? v : undefined;
+}
+
+// matchProperties equivalence (MT/properties.ts:64-95): objects compare
+// order-insensitively and recursively, primitives with ===.
+function matchClassKey(v) {
+    if (v !== null && typeof v === "object") {
+        return "o{" + Object.keys(v).sort().map((k) => JSON.stringify(k) + ":" + matchClassKey(v[k])).join(",") + "}";
+    }
+    if (typeof v === "number") return "n" + String(v);
+    if (typeof v === "boolean") return "b" + String(v);
+    if (typeof v === "string") return "s" + JSON.stringify(v);
+    return "z";
+}
+
+class PropTable {
+    constructor() {
+        this.keyIds = new Map(); this.keys = [];
+        this.valueIds = new Map(); this.valueJson = []; this.valueFalsy = []; this.valueClass = [];
+        this.classIds = new Map();
+        this.setIds = new Map(); this.sets = [];
+    }
+    keyId(k) {
+        let i = this.keyIds.get(k);
+        if (i === undefined) { i = this.keys.length; this.keyIds.set(k, i); this.keys.push(k); }
+        return i;
+    }
+    valueId(v) {
+        if (v === null) return -1;                       // null deletes the key
+        const txt = JSON.stringify(v);
+        let i = this.valueIds.get(txt);
+        if (i === undefined) {
+            i = this.valueJson.length;
+            this.valueIds.set(txt, i);
+            this.valueJson.push(txt);
+            this.valueFalsy.push(v ? 0 : 1);
+            const ck = matchClassKey(v);
+            let c = this.classIds.get(ck);
+            if (c === undefined) { c = this.classIds.size; this.classIds.set(ck, c); }
+            this.valueClass.push(c);
+        }
+        return i;
+    }
+    intern(props) {
+        const pairs = Object.keys(props).map((k) => [this.keyId(k), this.valueId(props[k])]);
+        const sig = pairs.map((p) => p.join(":")).join(",");
+        let i = this.setIds.get(sig);
+        if (i === undefined) { i = this.sets.length; this.setIds.set(sig, i); this.sets.push(pairs); }
+        return i;
+    }
+    toNative() {
+        const setOff = new Uint32Array(this.sets.length + 1);
+        const key = [], value = [];
+        this.sets.forEach((s, i) => { setOff[i + 1] = setOff[i] + s.length; for (const [k, v] of s) { key.push(k); value.push(v); } });
+        return {
+            setOff, key: Uint16Array.from(key.length ? key : [0]), value: Int32Array.from(value.length ? value : [0]),
+            keyJson: this.keys.map((k) => JSON.stringify(k)),
+            keyIndex: Uint32Array.from(this.keys.length ? this.keys.map((k) => { const a = arrayIndex(k); return a === undefined ? 0xFFFFFFFF : a; }) : [0]),
+            valueJson: this.valueJson,
+            valueFalsy: Uint8Array.from(this.valueFalsy.length ? this.valueFalsy : [0]),
+            valueClass: Uint32Array.from(this.valueClass.length ? this.valueClass : [0]),
+        };
+    }
+}
+
+class ClientNames {
+    constructor() { this.ids = new Map(); this.names = []; }
+    index(longId) {
+        let i = this.ids.get(longId);
+        if (i === undefined) { i = this.names.length; this.ids.set(longId, i); this.names.push(longId); }
+        return i;
+    }
+}
+
+const COLS = [["type", Uint8Array], ["flags", Uint8Array], ["client", Uint16Array], ["seq", Int32Array],
+    ["refSeq", Int32Array], ["msn", Int32Array], ["pos1", Int32Array], ["pos2", Int32Array],
+    ["payloadOff", Uint32Array], ["payloadLen", Uint32Array], ["propId", Int32Array]];
+
+/** Packs ISequencedDocumentMessages (protocol.ts:126-166) into mt_op_batch runs. */
+class BatchBuilder {
+    constructor(props, names) {
+        this.props = props; this.names = names;
+        this.cols = {}; for (const [n] of COLS) this.cols[n] = [];
+        this.payload = []; this.docIds = []; this.offsets = [0];
+    }
+    beginDoc(docId) { this.docIds.push(docId); this.offsets.push(this.offsets[this.offsets.length - 1]); }
+    emit(o) {
+        for (const [n] of COLS) this.cols[n].push(o[n] || 0);
+        this.offsets[this.offsets.length - 1] += 1;
+    }
+    member(op, client, seq, ref, msn, last) {
+        let fl = last ? F_END : 0;
+        const common = { client, seq, refSeq: ref, msn, propId: -1 };
+        if (op.type === OP_INSERT) {
+            const seg = op.seg;
+            if (seg === undefined && op.register !== undefined) throw new Error("register-based insert (client.ts:425-440) is not on the batch path");
+            if (!seg) { this.emit({ ...common, type: OP_NOOP, flags: fl }); return; }   // `if (op.seg)` falsy: no tree change
+            if (op.pos1 === undefined) throw new Error("relativePos1 inserts (mergeTree.ts:1949) are not on the batch path");
+            let text = null, props, pos2 = 0;
+            if (typeof seg === "string") text = seg;
+            else if (seg.text !== undefined) { text = seg.text; props = seg.props; }
+            else if (seg.marker !== undefined) { props = seg.props; fl |= F_MARKER; pos2 = seg.marker.refType || 0; }
+            else throw new Error("Unrecognized IJSONSegment type");
+            let pid = -1;
+            if (props) { pid = this.props.intern(props); fl |= F_SEG_PROPS; }
+            const off = this.payload.length;
+            if (text !== null) for (let i = 0; i < text.length; i++) this.payload.push(text.charCodeAt(i));
+            this.emit({ ...common, type: OP_INSERT, flags: fl, pos1: op.pos1, pos2, payloadOff: off,
+                payloadLen: text !== null ? text.length : 0, propId: pid });
+        } else if (op.type === OP_REMOVE || op.type === OP_ANNOTATE) {
+            if (op.pos1 === undefined || op.pos2 === undefined) throw new Error("relative positions are not on the batch path");
+            let pid = -1;
+            if (op.type === OP_ANNOTATE) {
+                if (op.combiningOp) fl |= op.combiningOp.name === "rewrite" ? F_REWRITE : F_COMBINE;
+                pid = this.props.intern(op.props);
+            }
+            this.emit({ ...common, type: op.type, flags: fl, pos1: op.pos1, pos2: op.pos2, propId: pid });
+        } else {
+            this.emit({ ...common, type: OP_NOOP, flags: fl });
+        }
+    }
+    /** One sequenced message (Client.applyMsg, client.ts:819-841). */
+    addMessage(msg) {
+        const client = this.names.index(msg.clientId);
+        const seq = msg.sequenceNumber, ref = msg.referenceSequenceNumber, msn = msg.minimumSequenceNumber;
+        if ((msg.type === undefined ? "op" : msg.type) !== "op") {
+            this.emit({ type: OP_NOOP, flags: F_END, client, seq, refSeq: ref, msn, propId: -1 });
+            return;
+        }
+        const op = msg.contents;
+        const members = (op.type === OP_GROUP ? op.ops : [op]).filter((m) => m.type === OP_INSERT || m.type === OP_REMOVE || m.type === OP_ANNOTATE);
+        if (!members.length) { this.emit({ type: OP_NOOP, flags: F_END, client, seq, refSeq: ref, msn, propId: -1 }); return; }
+        members.forEach((m, i) => this.member(m, client, seq, ref, msn, i === members.length - 1));
+    }
+    build() {
+        const b = { docIds: Uint32Array.from(this.docIds), opOffsets: Uint32Array.from(this.offsets),
+            payload: Uint16Array.from(this.payload.length ? this.payload : [0]) };
+        for (const [n, T] of COLS) b[n] = T.from(this.cols[n]);
+        return b;
+    }
+}
+
+const DEFAULT_LIMITS = { rowsPerDoc: 8192, windowPerDoc: 4096, propsetsPerDoc: 8192, textPerDoc: 1 << 16 };
+
+/** One engine context (one GPU) and the documents it holds. */
+class Engine {
+    constructor(maxDocs, limits = {}, device = 0) {
+        this.maxDocs = maxDocs;
+        this.h = addon.create(device, { ...DEFAULT_LIMITS, ...limits, maxDocs });
+        this.props = new PropTable();
+        this.uploadedSets = -1;
+    }
+    close() { if (this.h) { addon.destroy(this.h); this.h = null; } }
+    openDocs(first, n) { addon.docsOpen(this.h, first, n); }
+    setClientNames(jsonLiterals) { addon.setClientNames(this.h, jsonLiterals); }
+    apply(batch) {
+        if (this.uploadedSets !== this.props.sets.length) {
+            addon.setProps(this.h, this.props.toNative());
+            this.uploadedSets = this.props.sets.length;
+        }
+        addon.applyBatch(this.h, batch);
+    }
+    sync() { addon.sync(this.h); }
+    syncAsync() { return addon.syncAsync(this.h); }
+    status(docs) { return addon.docStatus(this.h, Uint32Array.from(docs)); }
+    getLength(docs, refSeq, client) { return addon.getLength(this.h, Uint32Array.from(docs), Int32Array.from(refSeq), Int32Array.from(client)); }
+    updateSeq(docs, msn, seq) { addon.updateSeq(this.h, Uint32Array.from(docs), Int32Array.from(msn), Int32Array.from(seq)); }
+    snapshot(docs, msn, seq) { return addon.snapshotV1(this.h, Uint32Array.from(docs), Int32Array.from(msn), Int32Array.from(seq)); }
+    getText(docs) { return addon.getText(this.h, Uint32Array.from(docs)); }
+}
+
+/**
+ * Drop-in subset of merge-tree `Client` for a passive observer.  All clients of
+ * a group share one engine; every read flushes the group's queued messages in
+ * one device batch, so thousands of documents replay together.
+ */
+class MergeTreeClient {
+    constructor(group, docId) {
+        this.group = group; this.docId = docId;
+        this.pending = []; this.names = new ClientNames();
+        this.currentSeq = 0; this.minSeq = 0; this.longClientId = undefined;
+    }
+    startOrUpdateCollaboration(longClientId, minSeq = 0, currentSeq = 0) {
+        this.longClientId = longClientId;
+    }
+    applyMsg(msg) {
+        this.pending.push(msg);
+        this.currentSeq = msg.sequenceNumber;
+        this.minSeq = msg.minimumSequenceNumber;
+    }
+    getCurrentSeq() { return this.currentSeq; }
+    checkStatus() {
+        const st = this.group.engine.status([this.docId])[0];
+        if (st) throw new Error(`document ${this.docId}: ${statusNames(st).join(", ")}`);
+    }
+    updateSeqNumbers(min, seq) {
+        this.group.flush();
+        this.group.engine.updateSeq([this.docId], [min], [seq]);
+        this.minSeq = min; this.currentSeq = seq;
+        this.checkStatus();
+    }
+    getLength() {
+        this.group.flush();
+        this.checkStatus();
+        return this.group.engine.getLength([this.docId], [0x7FFFFFFF], [-1])[0];
+    }
+    getText() {
+        this.group.flush();
+        this.checkStatus();
+        return this.group.engine.getText([this.docId])[0];
+    }
+    /** ITree of SnapshotV1 blobs (MT/snapshotV1.ts:98-163): header, body_0, ... */
+    snapshot() {
+        this.group.flush();
+        this.checkStatus();
+        const { blobs } = this.group.engine.snapshot([this.docId], [this.minSeq], [this.currentSeq])[0];
+        return {
+            entries: blobs.map((contents, i) => ({
+                mode: "100644", path: i === 0 ? "header" : `body_${i - 1}`, type: "Blob",
+                value: { contents, encoding: "utf-8" },
+            })),
+        };
+    }
+}
+
+/** Many documents on one engine: `newClient()` per document, `flush()` batches. */
+class ClientGroup {
+    constructor(engine) { this.engine = engine; this.clients = []; }
+    newClient() {
+        const d = this.clients.length;
+        if (d >= this.engine.maxDocs) throw new Error("engine document capacity exhausted");
+        this.engine.openDocs(d, 1);
+        const c = new MergeTreeClient(this, d);
+        this.clients.push(c);
+        return c;
+    }
+    flush() {
+        const busy = this.clients.filter((c) => c.pending.length);
+        if (!busy.length) return;
+        const bb = new BatchBuilder(this.engine.props, null);
+        for (const c of busy) {
+            bb.names = c.names;
+            bb.beginDoc(c.docId);
+            for (const m of c.pending) bb.addMessage(m);
+            c.pending = [];
+            if (c.namesUploaded !== c.names.names.length) {     // snapshot "client" fields use long ids
+                addon.setDocClientNames(this.engine.h, c.docId, c.names.names.map((n) => JSON.stringify(n)));
+                c.namesUploaded = c.names.names.length;
+            }
+        }
+        this.engine.apply(bb.build());
+        this.engine.sync();
+    }
+}
+
+module.exports = { addon, Engine, ClientGroup, MergeTreeClient, BatchBuilder, PropTable, ClientNames, statusNames };

@@ -193,6 +193,10 @@ int  mt_get_length(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
 /* Client long-id strings (JSON literals) by per-document client index; used for
  * the snapshot's "client"/"removedClient" fields (snapshotV1.ts:229, :237). */
 int  mt_set_client_names(mt_ctx* ctx, uint32_t n, const char* const* client_json);
+/* Per-document client names (each Client interns its own long ids in first-seen
+ * order, MT/client.ts:658-682); they override the table above for that
+ * document.  n = 0 removes the override. */
+int  mt_set_doc_client_names(mt_ctx* ctx, uint32_t doc_id, uint32_t n, const char* const* client_json);
 
 /*
  * SnapshotV1 of each document: runs updateSeqNumbers(msn[i], seq[i]) first

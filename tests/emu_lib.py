@@ -20,3 +20,28 @@ def build_emu(force=False):
 
 def emu_engine(max_docs, **kw):
     return Engine(max_docs, lib_path=build_emu(), prefix="emu_", **kw)
+
+
+NAPI_EMU = os.path.join(ROOT, "tests", "emu", "mtgpu_emu.node")
+
+
+def build_emu_napi():
+    """The product N-API addon source compiled against the host emulation
+    (every mt_* call renamed to emu_* by a forced include): lets CPU tests run
+    the Node host end to end.  Returns None if Node headers are absent."""
+    import re
+    if not os.path.exists("/usr/include/node/node_api.h"):
+        return None
+    lib = build_emu()
+    src = os.path.join(ROOT, "fluidframework_amd", "napi", "mtgpu_napi.cpp")
+    hdr = os.path.join(ROOT, "include", "mtgpu.h")
+    ren = os.path.join(ROOT, "tests", "emu", "emu_rename.h")
+    names = sorted(set(re.findall(r"\b(mt_[a-z0-9_]+)\s*\(", open(hdr).read())))
+    text = "".join(f"#define {n} emu_{n[3:]}\n" for n in names)
+    if not os.path.exists(ren) or open(ren).read() != text:
+        open(ren, "w").write(text)
+    deps = [src, hdr, lib, ren]
+    if not os.path.exists(NAPI_EMU) or any(os.path.getmtime(NAPI_EMU) < os.path.getmtime(d) for d in deps):
+        subprocess.check_call(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-I/usr/include/node", "-include", ren,
+                               "-o", NAPI_EMU, src, lib, "-Wl,-rpath," + os.path.dirname(lib)])
+    return NAPI_EMU

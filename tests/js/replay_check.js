@@ -1,0 +1,30 @@
+"use strict";
+// Test driver for the Node host (fluidframework_amd/js): replays sequenced
+// message lists, one ClientGroup document per list, through MergeTreeClient
+// (the Client drop-in) and prints what the parity tests compare against the
+// oracle: text, length, SnapshotV1 ITree blobs and digests.
+// usage: node replay_check.js IN.json OUT.json
+const fs = require("fs");
+const path = require("path");
+const mt = require(path.join(__dirname, "..", "..", "fluidframework_amd", "js"));
+
+const [inPath, outPath] = process.argv.slice(2);
+const spec = JSON.parse(fs.readFileSync(inPath, "utf8"));
+const eng = new mt.Engine(spec.docs.length, spec.limits || {});
+const group = new mt.ClientGroup(eng);
+const clients = spec.docs.map(() => {
+    const c = group.newClient();
+    c.startOrUpdateCollaboration("observer");
+    return c;
+});
+spec.docs.forEach((msgs, d) => { for (const m of msgs) clients[d].applyMsg(m); });
+const out = { texts: [], lengths: [], blobs: [], digests: [] };
+for (const c of clients) {
+    out.texts.push(c.getText());
+    out.lengths.push(c.getLength());
+    out.blobs.push(c.snapshot().entries.map((e) => [e.path, e.value.contents]));
+}
+const snaps = eng.snapshot(clients.map((c) => c.docId), clients.map((c) => c.minSeq), clients.map((c) => c.getCurrentSeq()));
+out.digests = snaps.map((s) => s.digest.toString(16));
+fs.writeFileSync(outPath, JSON.stringify(out));
+eng.close();

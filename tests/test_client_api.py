@@ -1,0 +1,56 @@
+"""The Python Client drop-in (fluidframework_amd.engine.ClientGroup /
+MergeTreeClient, mirroring MT/client.ts) against the oracle, on the host
+emulation (CPU) and on the device (GPU)."""
+import pytest
+
+from emu_lib import emu_engine
+from fluidframework_amd.engine import ClientGroup, Engine, MergeTreeError
+from js_lib import batch_to_messages
+from oracle_lib import gen_params, generate
+from test_emu_parity import CONFIGS, ann_props
+
+LIMITS = dict(rows_per_doc=20000, window_per_doc=8192, propsets_per_doc=8192, text_per_doc=1 << 18)
+
+
+def check(factory, cfg, n_docs):
+    props = ann_props()
+    p = gen_params(seed=41, n_docs=n_docs, **CONFIGS[cfg])
+    batch, st, kept = generate(p, props, keep=True)
+    g = ClientGroup(factory(n_docs, **LIMITS))
+    clients = [g.new_client() for _ in range(n_docs)]
+    for d, c in enumerate(clients):
+        c.startOrUpdateCollaboration("observer")
+        for m in batch_to_messages(batch, props, d):
+            c.applyMsg(m)
+    last = batch.op_offsets[1:] - 1
+    for d, c in enumerate(clients):
+        od = kept[d]
+        assert c.getText() == od.get_text()
+        assert c.getLength() == od.get_length()
+        blobs, _ = od.snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]))
+        tree = c.snapshot()
+        assert [e["path"] for e in tree["entries"]] == ["header"] + [f"body_{i}" for i in range(len(blobs) - 1)]
+        assert [e["value"]["contents"].encode() for e in tree["entries"]] == blobs
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
+def test_client_group_on_emulation_matches_oracle(cfg):
+    check(emu_engine, cfg, 3)
+
+
+def test_client_assert_seq_raises():
+    # completeAndLogOp asserts currentSeq < seq (MT/client.ts:482): the drop-in throws.
+    g = ClientGroup(emu_engine(1, **LIMITS))
+    c = g.new_client()
+    c.applyMsg(dict(clientId="a", sequenceNumber=2, referenceSequenceNumber=0, minimumSequenceNumber=0, type="op",
+                    contents={"type": 0, "pos1": 0, "seg": "ab"}))
+    c.applyMsg(dict(clientId="a", sequenceNumber=2, referenceSequenceNumber=0, minimumSequenceNumber=0, type="op",
+                    contents={"type": 0, "pos1": 0, "seg": "cd"}))
+    with pytest.raises(MergeTreeError, match="ASSERT_SEQ"):
+        c.getText()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
+def test_client_group_on_gpu_matches_oracle(cfg):
+    check(lambda n, **kw: Engine(n, device=0, **kw), cfg, 4)

@@ -1,0 +1,62 @@
+"""The Node host (fluidframework_amd/js + the N-API addon) against the oracle.
+
+CPU: the addon source built against the host emulation of the engine runs the
+whole Node path (message packing, per-document client ids, property interning,
+snapshot ITree) and must match the oracle bit for bit.  GPU: the product addon
+(mtgpu.node over libmtgpu.so) does the same on the device.
+"""
+import json
+import os
+import subprocess
+
+import pytest
+
+from emu_lib import build_emu_napi
+from js_lib import NODE, ROOT, batch_to_messages, run_node
+from oracle_lib import gen_params, generate
+from test_emu_parity import CONFIGS, ann_props
+
+pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
+
+EXPORTS = ["applyBatch", "create", "destroy", "docStatus", "docsOpen", "getLength", "getText", "lastError",
+           "setClientNames", "setDocClientNames", "setProps", "setResidency", "snapshotV1", "sync", "syncAsync",
+           "updateSeq"]
+
+
+def check(cfg, n_docs, addon, seed=31):
+    props = ann_props()
+    p = gen_params(seed=seed, n_docs=n_docs, **CONFIGS[cfg])
+    batch, st, kept = generate(p, props, keep=True)
+    assert st == [0] * n_docs
+    msgs = [batch_to_messages(batch, props, d) for d in range(n_docs)]
+    got = run_node(msgs, addon=addon, limits=dict(rowsPerDoc=20000, windowPerDoc=8192, propsetsPerDoc=8192,
+                                                  textPerDoc=1 << 18))
+    last = batch.op_offsets[1:] - 1
+    for d in range(n_docs):
+        od = kept[d]
+        assert got["texts"][d] == od.get_text(), f"doc {d} text"
+        assert got["lengths"][d] == od.get_length()
+        blobs, dig = od.snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]))
+        want = [("header" if i == 0 else f"body_{i - 1}", b.decode("utf-8")) for i, b in enumerate(blobs)]
+        assert [tuple(x) for x in got["blobs"][d]] == want, f"doc {d} snapshot"
+        assert int(got["digests"][d], 16) == dig
+
+
+def test_product_addon_loads_and_exports():
+    import __graft_entry__
+    __graft_entry__.build_engine()
+    path = __graft_entry__.build_napi()
+    out = subprocess.run([NODE, "-e", f"console.log(JSON.stringify(Object.keys(require({json.dumps(path)})).sort()))"],
+                         check=True, capture_output=True, text=True).stdout
+    assert json.loads(out) == sorted(EXPORTS)
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
+def test_node_host_on_emulation_matches_oracle(cfg):
+    check(cfg, 3, build_emu_napi())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["cfg1", "cfg2", "cfg3"])
+def test_node_host_on_gpu_matches_oracle(cfg):
+    check(cfg, 6, os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"))
