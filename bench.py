@@ -201,6 +201,13 @@ def main():
         dt = float(t.item())
     st = eng.status(range(c["docs"]))
     cnt2 = eng.counters(range(c["docs"]))
+    # SnapshotV1 of every document at its current window (reported, not timed as ops)
+    t1 = time.perf_counter()
+    sthreads = min(16, os.cpu_count() or 1)
+    neg = np.full(c["docs"], -1, np.int32)
+    digs = eng.snapshot_digests(range(c["docs"]), neg, neg, threads=sthreads)
+    snap_ms = (time.perf_counter() - t1) * 1e3
+    dig_xor = int(np.bitwise_xor.reduce(digs)) if len(digs) else 0
     ok = (not st.any()) and int(cnt2["msgs"].sum()) == msgs
     total_msgs = msgs * world * args.steps
     value = total_msgs / dt
@@ -234,6 +241,8 @@ def main():
                      "bytes_per_launch": bytes_per_launch},
         "hbm_gbps_algorithmic": achieved,
         "parity": "status words clean" if ok else "STATUS ERROR",
+        "snapshot": {"docs": c["docs"], "ms": snap_ms, "host_threads": sthreads, "digest_xor": f"{dig_xor:016x}",
+                     "note": "mt_snapshot_digests after the timed steps: staged download + SnapshotV1 JSON + xxh64"},
         "gen_seconds": gen_s,
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -15,6 +15,8 @@
 //   mtb_launch_get_length(ctx, S, docs, ref, cli, out, n)
 //   mtb_event_start / mtb_event_stop_ms
 #pragma once
+#include <algorithm>
+#include <thread>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -36,42 +38,80 @@ extern "C" {
 
 const char* MT_FN(last_error)(mt_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
-int MT_FN(create)(int device, const mt_limits* L, mt_ctx** out) {
-    if (!L || !out || L->max_docs == 0) return MT_E_INVALID;
+// Pools of every document, laid out back to back with per-document capacities.
+static void mt_caps_default(mt_limits& q) {
+    if (!q.rows_per_doc) q.rows_per_doc = 4096;
+    if (!q.blocks_per_doc) q.blocks_per_doc = q.rows_per_doc / 2 + 64;
+    if (!q.heap_per_doc) q.heap_per_doc = q.rows_per_doc;
+    if (!q.window_per_doc) q.window_per_doc = 4096;
+    if (!q.text_per_doc) q.text_per_doc = q.rows_per_doc * 8;
+    if (!q.propsets_per_doc) q.propsets_per_doc = 1024;
+}
+static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bool uniform, mt_ctx** out) {
     mt_ctx* c = new mt_ctx();
-    c->device = device; c->lim = *L;
-    if (mtb_init(c) != 0) { *out = c; return MT_E_HIP; }
+    *out = c;
+    c->device = device; c->lim = caps[0]; c->lim.max_docs = n_docs;
+    if (mtb_init(c) != 0) return MT_E_HIP;
     MtState& S = c->S;
-    S.maxDocs = L->max_docs;
-    S.rowCap = L->rows_per_doc ? L->rows_per_doc : 4096;
-    S.blkCap = L->blocks_per_doc ? L->blocks_per_doc : S.rowCap / 2 + 64;
-    S.heapCap = L->heap_per_doc ? L->heap_per_doc : S.rowCap;
-    S.winCap = L->window_per_doc ? L->window_per_doc : 4096;
-    S.textCap = L->text_per_doc ? L->text_per_doc : S.rowCap * 8;
-    S.psetCap = L->propsets_per_doc ? L->propsets_per_doc : 1024;
+    S.maxDocs = n_docs;
     S.holdCap = MT_RFL;
-    const size_t D = S.maxDocs, R = (size_t)D * S.rowCap;
+    c->layout_h.resize(n_docs);
+    MtDocLayout tot{};
+    for (uint32_t d = 0; d < n_docs; d++) {
+        mt_limits q = caps[uniform ? 0 : d];
+        mt_caps_default(q);
+        if (q.rows_per_doc > (1u << 30) || q.text_per_doc > (1u << 30) || q.window_per_doc > (1u << 26)) {
+            c->err = "per-document capacity too large"; return MT_E_INVALID;
+        }
+        MtDocLayout& y = c->layout_h[d];
+        y.row = tot.row; y.blk = tot.blk; y.heap = tot.heap; y.win = tot.win; y.anc = tot.anc; y.text = tot.text; y.pset = tot.pset;
+        y.rowCap = q.rows_per_doc; y.blkCap = q.blocks_per_doc; y.heapCap = q.heap_per_doc; y.winCap = q.window_per_doc;
+        y.textCap = q.text_per_doc; y.psetCap = q.propsets_per_doc;
+        tot.row += y.rowCap; tot.blk += y.blkCap; tot.heap += y.heapCap + 1; tot.win += y.winCap;
+        tot.anc += (unsigned long long)y.winCap * MT_MAXH; tot.text += 2ull * y.textCap; tot.pset += y.psetCap;
+        S.rowCap = std::max(S.rowCap, y.rowCap); S.blkCap = std::max(S.blkCap, y.blkCap); S.heapCap = std::max(S.heapCap, y.heapCap);
+        S.winCap = std::max(S.winCap, y.winCap); S.textCap = std::max(S.textCap, y.textCap); S.psetCap = std::max(S.psetCap, y.psetCap);
+    }
+    const size_t D = S.maxDocs;
     void* p;
 #define MT_ALLOC(field, T, count) \
-    if (mtb_malloc(&p, sizeof(T) * (size_t)(count)) != 0) { c->err = "pool allocation failed: " #field; *out = c; return MT_E_OOM; } \
+    if (mtb_malloc(&p, sizeof(T) * (size_t)(count)) != 0) { c->err = "pool allocation failed: " #field; return MT_E_OOM; } \
     S.field = (T*)p;
-    MT_ALLOC(rows, MtRow, R)
-    MT_ALLOC(blk, MtBlk, D * S.blkCap) MT_ALLOC(heap, MtHeapE, D * (S.heapCap + 1)) MT_ALLOC(win, int, D * S.winCap)
-    MT_ALLOC(uid, int, D * S.winCap) MT_ALLOC(udelta, int, D * S.winCap) MT_ALLOC(uanc, int, D * S.winCap * MT_MAXH)
-    MT_ALLOC(text, uint16_t, D * 2 * S.textCap) MT_ALLOC(pset, MtPSet, D * S.psetCap) MT_ALLOC(hdr, MtDocHdr, D)
+    MT_ALLOC(rows, MtRow, tot.row)
+    MT_ALLOC(blk, MtBlk, tot.blk) MT_ALLOC(heap, MtHeapE, tot.heap) MT_ALLOC(win, int, tot.win)
+    MT_ALLOC(uid, int, tot.win) MT_ALLOC(udelta, int, tot.win) MT_ALLOC(uanc, int, tot.anc)
+    MT_ALLOC(text, uint16_t, tot.text) MT_ALLOC(pset, MtPSet, tot.pset) MT_ALLOC(hdr, MtDocHdr, D)
     MT_ALLOC(hold, int, D * MT_RFL)
 #undef MT_ALLOC
+    if (mtb_malloc(&p, sizeof(MtDocLayout) * D) != 0) { c->err = "pool allocation failed: layout"; return MT_E_OOM; }
+    S.layout = (const MtDocLayout*)p;
+    mtb_h2d(c, p, c->layout_h.data(), sizeof(MtDocLayout) * D);
     mtb_memset(S.hdr, 0, sizeof(MtDocHdr) * D);
-    *out = c;
+    c->pool_bytes = sizeof(MtRow) * tot.row + sizeof(MtBlk) * tot.blk + sizeof(MtHeapE) * tot.heap + 12ull * tot.win +
+                    4ull * tot.anc + 2ull * tot.text + sizeof(MtPSet) * tot.pset + (sizeof(MtDocHdr) + 4ull * MT_RFL + sizeof(MtDocLayout)) * D;
+    return MT_OK;
+}
+
+int MT_FN(create)(int device, const mt_limits* L, mt_ctx** out) {
+    if (!L || !out || L->max_docs == 0) return MT_E_INVALID;
+    return mt_create_impl(device, L->max_docs, L, true, out);
+}
+int MT_FN(create_docs)(int device, uint32_t n_docs, const mt_limits* per_doc, mt_ctx** out) {
+    if (!per_doc || !out || n_docs == 0) return MT_E_INVALID;
+    return mt_create_impl(device, n_docs, per_doc, false, out);
+}
+int MT_FN(pool_bytes)(mt_ctx* c, uint64_t* bytes) {
+    if (!c || !bytes) return MT_E_INVALID;
+    *bytes = c->pool_bytes;
     return MT_OK;
 }
 
 void MT_FN(destroy)(mt_ctx* c) {
     if (!c) return;
     MtState& S = c->S;
-    void* ps[] = {S.rows, S.blk, S.heap, S.win, S.uid, S.udelta, S.uanc, S.text, S.pset, S.hdr, S.hold};
+    void* ps[] = {S.rows, S.blk, S.heap, S.win, S.uid, S.udelta, S.uanc, S.text, S.pset, S.hdr, S.hold, (void*)S.layout};
     for (void* p : ps) if (p) mtb_free(p);
-    mt_ctx::DevBuf* bs[] = {&c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_pset_off,
+    mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_pset_off,
                             &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3};
     for (auto* b : bs) if (b->p) mtb_free(b->p);
     mtb_fini(c);
@@ -273,16 +313,49 @@ struct MtHostDoc {
 };
 static int mt_download_doc(mt_ctx* c, uint32_t d, MtHostDoc& h) {
     const MtState& S = c->S;
+    const MtDocLayout& y = c->layout_h[d];
     mtb_d2h(c, &h.hdr, S.hdr + d, sizeof(MtDocHdr));
-    const size_t R = (size_t)h.hdr.rowTop, r0 = (size_t)d * S.rowCap;
+    const size_t R = (size_t)h.hdr.rowTop;
     h.rows.resize(R + 1);
-    if (R) mtb_d2h(c, h.rows.data(), S.rows + r0, sizeof(MtRow) * R);
+    if (R) mtb_d2h(c, h.rows.data(), S.rows + y.row, sizeof(MtRow) * R);
     h.blk.resize((size_t)h.hdr.blkTop + 1);
-    mtb_d2h(c, h.blk.data(), S.blk + (size_t)d * S.blkCap, sizeof(MtBlk) * (size_t)h.hdr.blkTop);
+    mtb_d2h(c, h.blk.data(), S.blk + y.blk, sizeof(MtBlk) * (size_t)h.hdr.blkTop);
     h.text.resize((size_t)h.hdr.textTop + 1);
-    if (h.hdr.textTop) mtb_d2h(c, h.text.data(), S.text + ((size_t)d * 2 + (size_t)h.hdr.textHalf) * S.textCap, 2 * (size_t)h.hdr.textTop);
+    if (h.hdr.textTop) mtb_d2h(c, h.text.data(), S.text + y.text + (size_t)h.hdr.textHalf * y.textCap, 2 * (size_t)h.hdr.textTop);
     h.pset.resize((size_t)h.hdr.psetTop + 1);
-    if (h.hdr.psetTop) mtb_d2h(c, h.pset.data(), S.pset + (size_t)d * S.psetCap, sizeof(MtPSet) * (size_t)h.hdr.psetTop);
+    if (h.hdr.psetTop) mtb_d2h(c, h.pset.data(), S.pset + y.pset, sizeof(MtPSet) * (size_t)h.hdr.psetTop);
+    return MT_OK;
+}
+
+// Gather documents' live state into host memory with two kernels and one copy
+// (mt_pack.h); views[i] points into `host`.
+static int mt_stage_docs(mt_ctx* c, uint32_t n, const uint32_t* docs, std::vector<uint8_t>& host,
+                         std::vector<MtSnapView>& views) {
+    views.clear(); host.clear();
+    if (n == 0) return MT_OK;
+    for (uint32_t i = 0; i < n; i++) if (docs[i] >= c->S.maxDocs) { c->err = "doc id out of range"; return MT_E_INVALID; }
+    int rc;
+    if ((rc = mtb_ensure(c, c->b_pack_docs, 4ull * n))) return rc;
+    if ((rc = mtb_ensure(c, c->b_pack_sz, sizeof(MtPackSize) * n))) return rc;
+    if ((rc = mtb_ensure(c, c->b_pack_off, 8ull * n))) return rc;
+    mtb_h2d(c, c->b_pack_docs.p, docs, 4ull * n);
+    if ((rc = mtb_launch_pack_size(c, (const uint32_t*)c->b_pack_docs.p, (MtPackSize*)c->b_pack_sz.p, n))) return rc;
+    std::vector<MtPackSize> sz(n);
+    mtb_d2h(c, sz.data(), c->b_pack_sz.p, sizeof(MtPackSize) * n);
+    std::vector<uint64_t> off(n + 1, 0);
+    for (uint32_t i = 0; i < n; i++) off[i + 1] = off[i] + mt_pack_bytes(sz[i]);
+    if ((rc = mtb_ensure(c, c->b_stage, off[n] + 16))) return rc;
+    mtb_h2d(c, c->b_pack_off.p, off.data(), 8ull * n);
+    if ((rc = mtb_launch_pack(c, (const uint32_t*)c->b_pack_docs.p, (const uint64_t*)c->b_pack_off.p, (uint8_t*)c->b_stage.p, n))) return rc;
+    if ((rc = mtb_sync(c))) return rc;
+    host.resize(off[n] + 16);
+    mtb_d2h(c, host.data(), c->b_stage.p, off[n]);
+    views.resize(n);
+    for (uint32_t i = 0; i < n; i++) {
+        const MtStagedDoc sd = MtStagedDoc::at(host.data() + off[i]);
+        MtSnapView& v = views[i];
+        v.hdr = sd.hdr; v.R = sd.R; v.blk = sd.blk; v.text = sd.text; v.pset = sd.pset;
+    }
     return MT_OK;
 }
 
@@ -291,13 +364,12 @@ int MT_FN(snapshot_v1)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_
     if (!c) return MT_E_INVALID;
     int rc = MT_FN(update_seq)(c, n, docs, msn, seq);       // Client.snapshot: updateSeqNumbers first (client.ts:936)
     if (rc) return rc;
-    mtb_sync(c);
+    std::vector<uint8_t> host; std::vector<MtSnapView> views;
+    if ((rc = mt_stage_docs(c, n, docs, host, views))) return rc;
     c->snap_arena.clear(); c->blob_off.assign(1, 0); c->blob_first.assign(1, 0);
-    MtHostDoc h;
     for (uint32_t i = 0; i < n; i++) {
-        mt_download_doc(c, docs[i], h);
         auto dn = c->doc_clients.find(docs[i]);
-        std::vector<std::string> blobs = mtsnap::snapshot_blobs(h.view(), c->names,
+        std::vector<std::string> blobs = mtsnap::snapshot_blobs(views[i], c->names,
                                                                 dn == c->doc_clients.end() ? nullptr : &dn->second);
         if (digest) digest[i] = mtsnap::blobs_digest(blobs);
         for (auto& b : blobs) { c->snap_arena += b; c->blob_off.push_back(c->snap_arena.size()); }
@@ -309,14 +381,39 @@ int MT_FN(snapshot_v1)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_
     return MT_OK;
 }
 
+// Digests only, serialized on `threads` host threads (no blob arena).
+int MT_FN(snapshot_digests)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t* msn, const int32_t* seq,
+                            uint64_t* digest, int threads) {
+    if (!c || (n && (!docs || !msn || !seq || !digest))) return MT_E_INVALID;
+    int rc = MT_FN(update_seq)(c, n, docs, msn, seq);
+    if (rc) return rc;
+    std::vector<uint8_t> host; std::vector<MtSnapView> views;
+    if ((rc = mt_stage_docs(c, n, docs, host, views))) return rc;
+    if (threads < 1) threads = 1;
+    if ((uint32_t)threads > n) threads = (int)(n ? n : 1);
+    auto work = [&](int t) {
+        for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)threads) {
+            auto dn = c->doc_clients.find(docs[i]);
+            digest[i] = mtsnap::blobs_digest(mtsnap::snapshot_blobs(views[i], c->names,
+                                                                    dn == c->doc_clients.end() ? nullptr : &dn->second));
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+    return MT_OK;
+}
+
 int MT_FN(get_text)(mt_ctx* c, uint32_t n, const uint32_t* docs, const uint16_t** arena, const uint64_t** off) {
     if (!c) return MT_E_INVALID;
-    mtb_sync(c);
+    int rc = mtb_sync(c);
+    if (rc) return rc;
+    std::vector<uint8_t> host; std::vector<MtSnapView> views;
+    if ((rc = mt_stage_docs(c, n, docs, host, views))) return rc;
     c->text_arena.clear(); c->text_off.assign(1, 0);
-    MtHostDoc h;
     for (uint32_t i = 0; i < n; i++) {
-        mt_download_doc(c, docs[i], h);
-        mtsnap::observer_text(h.view(), c->text_arena);
+        mtsnap::observer_text(views[i], c->text_arena);
         c->text_off.push_back(c->text_arena.size());
     }
     if (arena) *arena = c->text_arena.data();
@@ -348,33 +445,56 @@ int MT_FN(prof_get)(mt_ctx* c, uint32_t n, unsigned long long* out) {
     return MT_OK;
 }
 
-int MT_FN(generate)(mt_ctx* c, const mt_gen_params* P) {
-    if (!c || !P || P->n_docs == 0 || P->n_docs > c->S.maxDocs || P->clients == 0 || P->clients > 64 ||
-        P->ins_len_max == 0 || P->rem_len_max == 0 || P->n_ann_sets == 0) return MT_E_INVALID;
+// Stream generation with per-document op counts and client counts (null arrays:
+// P->ops_per_doc / P->clients for every document).
+int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_per_doc, const uint32_t* clients_per_doc) {
+    if (!c || !P || P->n_docs == 0 || P->n_docs > c->S.maxDocs || P->ins_len_max == 0 || P->rem_len_max == 0 ||
+        P->n_ann_sets == 0) return MT_E_INVALID;
     if (P->pct_insert + P->pct_remove < 100 && P->n_ann_sets > c->S.p_nsets) { c->err = "annotate prop sets not uploaded"; return MT_E_INVALID; }
-    const size_t N = (size_t)P->n_docs * P->ops_per_doc;
+    std::vector<uint32_t> docs(P->n_docs), off(P->n_docs + 1), cl(P->n_docs);
+    off[0] = 0;
+    for (uint32_t i = 0; i < P->n_docs; i++) {
+        docs[i] = i;
+        const uint64_t n = ops_per_doc ? ops_per_doc[i] : P->ops_per_doc;
+        cl[i] = clients_per_doc ? clients_per_doc[i] : P->clients;
+        if (cl[i] == 0 || cl[i] > 64) { c->err = "clients per document must be in [1, 64]"; return MT_E_INVALID; }
+        if ((uint64_t)off[i] + n > 0xFFFFFFFFull) { c->err = "more than 2^32 ops in one batch"; return MT_E_INVALID; }
+        off[i + 1] = (uint32_t)(off[i] + n);
+    }
+    const size_t N = off[P->n_docs];
+    if ((uint64_t)N * P->ins_len_max >= 0xFFFFFFFFull) { c->err = "payload arena exceeds 2^32 units"; return MT_E_INVALID; }
     const size_t PU = N * P->ins_len_max + 1;
     int rc;
 #define AL(buf, bytes) if ((rc = mtb_ensure(c, c->buf, (bytes)))) return rc;
-    AL(b_doc, 4ull * P->n_docs) AL(b_off, 4ull * (P->n_docs + 1)) AL(b_rec, sizeof(MtOpRec) * N) AL(b_pay, 2 * PU)
+    AL(b_doc, 4ull * P->n_docs) AL(b_off, 4ull * (P->n_docs + 1)) AL(b_rec, sizeof(MtOpRec) * (N + 1)) AL(b_pay, 2 * PU)
+    AL(b_gencl, 4ull * P->n_docs)
 #undef AL
-    std::vector<uint32_t> docs(P->n_docs), off(P->n_docs + 1);
-    for (uint32_t i = 0; i < P->n_docs; i++) { docs[i] = i; off[i] = (uint32_t)((size_t)i * P->ops_per_doc); }
-    off[P->n_docs] = (uint32_t)N;
     mtb_h2d(c, c->b_doc.p, docs.data(), 4ull * P->n_docs);
     mtb_h2d(c, c->b_off.p, off.data(), 4ull * (P->n_docs + 1));
+    mtb_h2d(c, c->b_gencl.p, cl.data(), 4ull * P->n_docs);
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs;
     c->n_runs = P->n_docs;
+    c->gen_off.assign(off.begin(), off.end());
     rc = MT_FN(docs_open)(c, 0, P->n_docs);
     if (rc) return rc;
     MtGen g{};
     g.seed = P->seed; g.ops = P->ops_per_doc; g.clients = P->clients; g.lag_max = P->lag_max;
     g.pct_insert = P->pct_insert; g.pct_remove = P->pct_remove; g.ins_len_max = P->ins_len_max;
     g.rem_len_max = P->rem_len_max; g.n_ann_sets = P->n_ann_sets; g.pct_rewrite = P->pct_rewrite; g.enabled = 1;
+    g.clients_per_run = (const uint32_t*)c->b_gencl.p; g.total_ops = N;
     c->gen = g; c->gen_docs = P->n_docs;
     return mtb_launch_replay(c, g, P->n_docs);
+}
+int MT_FN(generate)(mt_ctx* c, const mt_gen_params* P) {
+    if (!P || P->clients == 0 || P->clients > 64) return MT_E_INVALID;
+    return MT_FN(generate_docs)(c, P, nullptr, nullptr);
+}
+int MT_FN(generated_ops)(mt_ctx* c, uint64_t* n_ops) {
+    if (!c || !n_ops || !c->gen_docs) return MT_E_INVALID;
+    *n_ops = c->gen.total_ops;
+    return MT_OK;
 }
 
 int MT_FN(generated_download)(mt_ctx* c, uint8_t* type, uint8_t* flags, uint16_t* client, int32_t* seq, int32_t* ref,
@@ -382,7 +502,7 @@ int MT_FN(generated_download)(mt_ctx* c, uint8_t* type, uint8_t* flags, uint16_t
                               uint16_t* payload) {
     if (!c || !c->gen_docs) return MT_E_INVALID;
     mtb_sync(c);
-    const size_t N = (size_t)c->gen_docs * c->gen.ops;
+    const size_t N = c->gen.total_ops;
     std::vector<MtOpRec> rec(N ? N : 1);
     mtb_d2h(c, rec.data(), c->ops.rec, sizeof(MtOpRec) * N);
     for (size_t i = 0; i < N; i++) {

@@ -125,11 +125,21 @@ struct __attribute__((aligned(16))) MtDocHdr {
     unsigned long long prof[8];              // MT_PROFILE builds: s_memtime cycles per phase
 };
 
+// Where one document's pools live (element offsets into the MtState pools) and
+// their capacities: documents of one context may be sized differently
+// (mt_create_docs), e.g. by their op counts.
+struct __attribute__((aligned(16))) MtDocLayout {
+    unsigned long long row, blk, heap, win, anc, text, pset;   // heap: cap+1 entries; text: 2 halves
+    uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap;
+    uint32_t pad[2];
+};
+
 struct MtState {                              // device pools, doc-major
     MtRow* rows;
     MtBlk* blk; MtHeapE* heap; int* win; int* uid; int* udelta; int* uanc;
     uint16_t* text; MtPSet* pset; MtDocHdr* hdr; int* hold;   // text: 2 halves of textCap per doc; hold: recycled-row stacks
-    uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap, holdCap, maxDocs;
+    uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap, holdCap, maxDocs;   // largest per-doc caps
+    const MtDocLayout* layout;                // [maxDocs]
     // interned op property sets (mt_prop_table)
     const uint32_t* p_off; const uint16_t* p_key; const int32_t* p_val;
     const uint8_t* p_falsy; const uint32_t* p_class; uint32_t p_nsets;
@@ -152,6 +162,8 @@ struct MtGen {                                // device stream generator paramet
     unsigned long long seed;
     uint32_t ops, clients, lag_max, pct_insert, pct_remove, ins_len_max, rem_len_max, n_ann_sets, pct_rewrite;
     int enabled;
+    const uint32_t* clients_per_run;          // per-document authoring clients (mt_generate_docs), or null
+    uint64_t total_ops;                       // ops over all runs (payload stride base)
 };
 
 struct __attribute__((aligned(16))) MtQ16 { uint32_t x, y, z, w; };
@@ -252,22 +264,26 @@ template <bool LDS> struct MtEngT {
     uint32_t gRowCap, gBlkCap, gHeapCap, gWinCap;
 
     MT_HD void bind(const MtState& st, uint32_t d, MtScratch* scratch) {
-        S.rowCap = st.rowCap; S.heapCap = st.heapCap; S.winCap = st.winCap; S.textCap = st.textCap;
-        S.psetCap = st.psetCap; S.p_nsets = st.p_nsets; S.p_off = st.p_off; S.p_key = st.p_key; S.p_val = st.p_val;
-        S.p_falsy = st.p_falsy; S.p_class = st.p_class; S.textBase = st.text + (size_t)d * 2 * st.textCap;
-        blkCap = st.blkCap; hdrp = st.hdr + d;
-        const size_t r = (size_t)d * st.rowCap;
-        R = st.rows + r;
-        blk = st.blk + (size_t)d * st.blkCap; heap = st.heap + (size_t)d * (st.heapCap + 1);
-        win = st.win + (size_t)d * st.winCap; uid = st.uid + (size_t)d * st.winCap;
-        udelta = st.udelta + (size_t)d * st.winCap; uanc = st.uanc + (size_t)d * st.winCap * MT_MAXH;
-        pset = st.pset + (size_t)d * st.psetCap;
+        const MtDocLayout* Ly = st.layout + d;
+        auto off = [&](const unsigned long long* p) -> size_t {
+            const uint32_t* w = (const uint32_t*)p;
+            return (size_t)uni(w[0]) | ((size_t)uni(w[1]) << 32);
+        };
+        S.rowCap = uni(Ly->rowCap); S.heapCap = uni(Ly->heapCap); S.winCap = uni(Ly->winCap); S.textCap = uni(Ly->textCap);
+        S.psetCap = uni(Ly->psetCap); S.p_nsets = st.p_nsets; S.p_off = st.p_off; S.p_key = st.p_key; S.p_val = st.p_val;
+        S.p_falsy = st.p_falsy; S.p_class = st.p_class; S.textBase = st.text + off(&Ly->text);
+        blkCap = uni(Ly->blkCap); hdrp = st.hdr + d;
+        R = st.rows + off(&Ly->row);
+        blk = st.blk + off(&Ly->blk); heap = st.heap + off(&Ly->heap);
+        const size_t wo = off(&Ly->win);
+        win = st.win + wo; uid = st.uid + wo; udelta = st.udelta + wo; uanc = st.uanc + off(&Ly->anc);
+        pset = st.pset + off(&Ly->pset);
         sc = scratch;
         const MtDocHdr& h = *hdrp;
         root = uni(h.root); height = uni(h.height); minSeq = uni(h.minSeq); curSeq = uni(h.curSeq); rowTop = uni(h.rowTop);
         blkTop = uni(h.blkTop); blkFree = uni(h.blkFree); heapN = uni(h.heapN); winN = uni(h.winN); textTop = uni(h.textTop);
         psetTop = uni(h.psetTop); status = uni(h.status); textHalf = uni(h.textHalf);
-        text = S.textBase + (size_t)textHalf * st.textCap;
+        text = S.textBase + (size_t)textHalf * S.textCap;
         for (int i = 0; i < 8; i++) prof[i] = h.prof[i];
         c_ops = h.cnt[0]; c_msgs = h.cnt[1]; c_ins = h.cnt[2]; c_rows = h.cnt[3]; c_depth = h.cnt[4]; c_scour = h.cnt[5];
         nU = 0; uValid = false; uRef = -1; uCli = -1;

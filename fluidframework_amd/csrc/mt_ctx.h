@@ -5,21 +5,25 @@
 #include <vector>
 #include "mt_replay.h"
 #include "mt_snapshot.h"
+#include "mt_pack.h"
 
 struct mt_ctx {
     int device = 0;
     mt_limits lim{};
     MtState S{};
     MtNames names;
+    std::vector<MtDocLayout> layout_h;                                     // host copy of S.layout
+    uint64_t pool_bytes = 0;
     std::unordered_map<uint32_t, std::vector<std::string>> doc_clients;   // mt_set_doc_client_names
     std::string err;
     // device op batch (resident)
     struct DevBuf { void* p = nullptr; size_t cap = 0; };
-    DevBuf b_cursor, b_doc, b_off, b_rec, b_pay, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3;
+    DevBuf b_stage, b_pack_docs, b_pack_sz, b_pack_off, b_gencl, b_cursor, b_doc, b_off, b_rec, b_pay, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3;
     MtOps ops{};
     uint32_t n_runs = 0;
     MtGen gen{};
     uint32_t gen_docs = 0;
+    std::vector<uint32_t> gen_off;     // op offsets of the generated runs
     float last_ms = 0.f;
     // LDS residency of the replay (mt_set_residency): on/off and the pool caps
     int use_lds = 0, lds_rows = MT_L_ROWS, lds_blks = MT_L_BLKS, lds_heap = MT_L_HEAP;

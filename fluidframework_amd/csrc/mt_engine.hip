@@ -71,8 +71,7 @@ __global__ __launch_bounds__(64) void mt_update_seq_kernel(MtState S, const uint
     const uint32_t doc = docs[blockIdx.x];
     MtEng e;
     e.bind(S, doc, &sc);
-    if (e.curSeq > seq[blockIdx.x]) e.status |= MT_DS_ASSERT_SEQ;
-    else { e.curSeq = seq[blockIdx.x]; e.setMinSeq(msn[blockIdx.x]); }
+    mt_update_seq_doc(e, msn[blockIdx.x], seq[blockIdx.x]);
     e.store(doc);
 }
 __global__ __launch_bounds__(64) void mt_get_length_kernel(MtState S, const uint32_t* docs, const int32_t* ref, const int32_t* cli, int32_t* out) {
@@ -82,6 +81,21 @@ __global__ __launch_bounds__(64) void mt_get_length_kernel(MtState S, const uint
     e.bind(S, doc, &sc);
     const int l = e.perspectiveLength(ref[blockIdx.x], cli[blockIdx.x] < 0 ? 255 : cli[blockIdx.x]);
     if (__lane_id() == 0) out[blockIdx.x] = l;
+}
+
+// Staging for host-side serialization (mt_pack.h): sizes, then the packed copy.
+__global__ __launch_bounds__(64) void mt_pack_size_kernel(MtState S, const uint32_t* docs, MtPackSize* out) {
+    __shared__ MtScratch sc;
+    MtEng e;
+    e.bind(S, docs[blockIdx.x], &sc);
+    const MtPackSize z = mt_pack_size(e);
+    if (__lane_id() == 0) out[blockIdx.x] = z;
+}
+__global__ __launch_bounds__(64) void mt_pack_kernel(MtState S, const uint32_t* docs, const uint64_t* off, uint8_t* stage) {
+    __shared__ MtScratch sc;
+    MtEng e;
+    e.bind(S, docs[blockIdx.x], &sc);
+    mt_pack_doc(e, stage + off[blockIdx.x]);
 }
 
 // ----------------------------------------------------- backend plumbing ----
@@ -149,6 +163,19 @@ static int mtb_launch_get_length(mt_ctx* c, const uint32_t* docs, const int32_t*
     if (!n) return MT_OK;
     (void)hipGetLastError();
     hipLaunchKernelGGL(mt_get_length_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, ref, cli, out);
+    return mtb_check(c);
+}
+
+static int mtb_launch_pack_size(mt_ctx* c, const uint32_t* docs, MtPackSize* out, uint32_t n) {
+    if (!n) return MT_OK;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(mt_pack_size_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, out);
+    return mtb_check(c);
+}
+static int mtb_launch_pack(mt_ctx* c, const uint32_t* docs, const uint64_t* off, uint8_t* stage, uint32_t n) {
+    if (!n) return MT_OK;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(mt_pack_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, off, stage);
     return mtb_check(c);
 }
 

@@ -19,9 +19,9 @@ struct MtRng {                                     // splitmix64
 // engine acts as sequencer + observer, so positions are valid under the
 // author's perspective), writing the op record into the batch arrays.
 template <class Eng>
-MT_HD void mt_gen_op(Eng& e, const MtOps& ops, uint32_t i, uint32_t k, uint32_t doc,
+MT_HD void mt_gen_op(Eng& e, const MtOps& ops, uint32_t i, uint32_t nc,
                             const MtGen& g, MtRng& rng, int* lastRef) {
-    const uint32_t a = rng.u(g.clients);
+    const uint32_t a = rng.u(nc);
     const uint32_t lag = rng.u(g.lag_max + 1);
     int r = e.curSeq - (int)lag;
     if (r < lastRef[a]) r = lastRef[a];
@@ -33,7 +33,7 @@ MT_HD void mt_gen_op(Eng& e, const MtOps& ops, uint32_t i, uint32_t k, uint32_t 
     int ty = tsel < g.pct_insert ? MT_OP_INSERT : (tsel < g.pct_insert + g.pct_remove ? MT_OP_REMOVE : MT_OP_ANNOTATE);
     if (L == 0) ty = MT_OP_INSERT;
     int s1 = 0, s2 = 0, pid = -1; uint32_t plen = 0; uint8_t fl = MT_OPF_END_OF_MSG;
-    const uint32_t poff = (uint32_t)((size_t)doc * g.ops * g.ins_len_max + (size_t)k * g.ins_len_max);
+    const uint32_t poff = (uint32_t)((size_t)i * g.ins_len_max);      // fixed stride per op record
     MtOpRec& o = ops.rec[i];
     if (ty == MT_OP_INSERT) {
         s1 = (int)rng.u((uint32_t)L + 1);
@@ -52,7 +52,7 @@ MT_HD void mt_gen_op(Eng& e, const MtOps& ops, uint32_t i, uint32_t k, uint32_t 
         }
     }
     int mn = lastRef[0];
-    for (uint32_t c = 1; c < g.clients; c++) mn = lastRef[c] < mn ? lastRef[c] : mn;
+    for (uint32_t c = 1; c < nc; c++) mn = lastRef[c] < mn ? lastRef[c] : mn;
     o.type = (uint8_t)ty; o.flags = fl; o.client = (uint16_t)a;
     o.seq = e.curSeq + 1; o.ref_seq = r; o.msn = mn;
     o.pos1 = s1; o.pos2 = s2; o.payload_off = poff; o.payload_len = (uint16_t)plen; o.prop_id = (int16_t)pid;
@@ -67,6 +67,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
                                 const MtGen* g, int* lastRef, uint32_t o0) {
     const uint32_t o1 = ops.op_off[run + 1];
     MtRng rng; rng.s = 0;
+    const uint32_t nc = g ? (g->clients_per_run ? g->clients_per_run[run] : g->clients) : 0;
     if (g) {
         rng.s = g->seed ^ (0x9E3779B97F4A7C15ULL * (unsigned long long)(doc + 1));
         for (int c = 0; c < 64; c++) lastRef[c] = 0;
@@ -78,11 +79,11 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
         if (Eng::kLds && !e.ldsHeadroom()) return i;
 #if defined(MT_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
         const unsigned long long tg = __builtin_amdgcn_s_memtime();
-        if (g) mt_gen_op(e, ops, i, i - o0, doc, *g, rng, lastRef);
+        if (g) mt_gen_op(e, ops, i, nc, *g, rng, lastRef);
         e.prof[MT_PH_GEN] += __builtin_amdgcn_s_memtime() - tg;
         const unsigned long long top = __builtin_amdgcn_s_memtime();
 #else
-        if (g) mt_gen_op(e, ops, i, i - o0, doc, *g, rng, lastRef);
+        if (g) mt_gen_op(e, ops, i, nc, *g, rng, lastRef);
 #endif
         // one 32-byte record: lanes 0..7 hold a dword each, then broadcast
         auto w = wn;
@@ -128,4 +129,14 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
         if (e.status) break;
     }
     return o1;
+}
+
+// Client.updateSeqNumbers(min, seq) (MT/client.ts:843-850) on one document;
+// seq < 0 leaves the document's window as it is (mt_snapshot_* "current").
+template <class Eng>
+MT_HD void mt_update_seq_doc(Eng& e, int msn, int seq) {
+    if (seq < 0) return;
+    if (e.curSeq > seq) { e.status |= MT_DS_ASSERT_SEQ; return; }
+    e.curSeq = seq;
+    e.setMinSeq(msn);
 }

@@ -52,6 +52,8 @@ def _bind(lib, prefix: str):
 
     return dict(
         create=f("create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(MtLimits), ctypes.POINTER(P)]),
+        create_docs=f("create_docs", ctypes.c_int, [ctypes.c_int, U32, P, ctypes.POINTER(P)]),
+        pool_bytes=f("pool_bytes", ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64)]),
         destroy=f("destroy", None, [P]),
         last_error=f("last_error", ctypes.c_char_p, [P]),
         docs_open=f("docs_open", ctypes.c_int, [P, U32, U32]),
@@ -71,10 +73,13 @@ def _bind(lib, prefix: str):
         get_length=f("get_length", ctypes.c_int, [P, U32, P, P, P, P]),
         snapshot_v1=f("snapshot_v1", ctypes.c_int, [P, U32, P, P, P, P, ctypes.POINTER(P), ctypes.POINTER(P),
                                                     ctypes.POINTER(P)]),
+        snapshot_digests=f("snapshot_digests", ctypes.c_int, [P, U32, P, P, P, P, ctypes.c_int]),
         get_text=f("get_text", ctypes.c_int, [P, U32, P, ctypes.POINTER(P), ctypes.POINTER(P)]),
         dump_segments=f("dump_segments", ctypes.c_int, [P, U32, ctypes.POINTER(P), ctypes.POINTER(U32)]),
         free=f("free", None, [P]),
         generate=f("generate", ctypes.c_int, [P, ctypes.POINTER(MtGenParams)]),
+        generate_docs=f("generate_docs", ctypes.c_int, [P, ctypes.POINTER(MtGenParams), P, P]),
+        generated_ops=f("generated_ops", ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64)]),
         generated_download=f("generated_download", ctypes.c_int, [P] + [P] * 12),
         generated_to_resident=f("generated_to_resident", ctypes.c_int, [P]),
     )
@@ -93,7 +98,10 @@ class Engine:
 
     def __init__(self, max_docs: int, rows_per_doc: int = 4096, blocks_per_doc: int = 0, text_per_doc: int = 0,
                  propsets_per_doc: int = 0, heap_per_doc: int = 0, window_per_doc: int = 0, device: int = 0,
-                 lib_path: str | None = None, prefix: str = "mt_"):
+                 lib_path: str | None = None, prefix: str = "mt_", per_doc: dict | None = None):
+        """per_doc: optional dict of per-document capacity arrays (keys rows_per_doc,
+        blocks_per_doc, text_per_doc, propsets_per_doc, heap_per_doc, window_per_doc;
+        missing keys use the scalar arguments) -> mt_create_docs."""
         # MTGPU_LIB: an alternate build of the same HIP engine (e.g. another occupancy target)
         path = lib_path or os.environ.get("MTGPU_LIB") or LIB_PATH
         if not os.path.exists(path):
@@ -104,7 +112,17 @@ class Engine:
         lim = MtLimits(max_docs, rows_per_doc, blocks_per_doc, text_per_doc, propsets_per_doc, heap_per_doc,
                        window_per_doc)
         h = ctypes.c_void_p()
-        rc = self.fn["create"](device, ctypes.byref(lim), ctypes.byref(h))
+        if per_doc:
+            arr = (MtLimits * max_docs)()
+            scal = dict(rows_per_doc=rows_per_doc, blocks_per_doc=blocks_per_doc, text_per_doc=text_per_doc,
+                        propsets_per_doc=propsets_per_doc, heap_per_doc=heap_per_doc, window_per_doc=window_per_doc)
+            cols = {k: (np.asarray(per_doc[k], np.uint32) if k in per_doc else None) for k in scal}
+            for i in range(max_docs):
+                for k, v in scal.items():
+                    setattr(arr[i], k, int(cols[k][i]) if cols[k] is not None else v)
+            rc = self.fn["create_docs"](device, max_docs, ctypes.cast(arr, ctypes.c_void_p), ctypes.byref(h))
+        else:
+            rc = self.fn["create"](device, ctypes.byref(lim), ctypes.byref(h))
         self.h = h
         if rc != 0:
             err = self.fn["last_error"](h).decode() if h.value else "create failed"
@@ -176,13 +194,27 @@ class Engine:
         self.fn["last_replay_ms"](self.h, ctypes.byref(v))
         return float(v.value)
 
-    def generate(self, params: MtGenParams):
+    def generate(self, params: MtGenParams, ops_per_doc=None, clients_per_doc=None):
+        """Device stream generation (mt_generate / mt_generate_docs with per-document
+        message and client counts)."""
         self._gen = params
-        self._check(self.fn["generate"](self.h, ctypes.byref(params)), "mt_generate")
+        n = params.n_docs
+        self._gen_ops = (np.full(n, params.ops_per_doc, np.uint32) if ops_per_doc is None
+                         else np.ascontiguousarray(ops_per_doc, np.uint32))
+        if ops_per_doc is None and clients_per_doc is None:
+            self._check(self.fn["generate"](self.h, ctypes.byref(params)), "mt_generate")
+            return
+        o = self._gen_ops
+        c = None if clients_per_doc is None else np.ascontiguousarray(clients_per_doc, np.uint32)
+        self._gen_keep = (o, c)
+        self._check(self.fn["generate_docs"](self.h, ctypes.byref(params), o.ctypes.data,
+                                             c.ctypes.data if c is not None else None), "mt_generate_docs")
 
     def generated_download(self) -> OpBatch:
         p = self._gen
-        n = p.n_docs * p.ops_per_doc
+        v = ctypes.c_uint64()
+        self._check(self.fn["generated_ops"](self.h, ctypes.byref(v)), "mt_generated_ops")
+        n = int(v.value)
         a = dict(type=np.zeros(n, np.uint8), flags=np.zeros(n, np.uint8), client=np.zeros(n, np.uint16),
                  seq=np.zeros(n, np.int32), ref_seq=np.zeros(n, np.int32), msn=np.zeros(n, np.int32),
                  pos1=np.zeros(n, np.int32), pos2=np.zeros(n, np.int32), payload_off=np.zeros(n, np.uint32),
@@ -191,7 +223,8 @@ class Engine:
         self._check(self.fn["generated_download"](self.h, *(a[k].ctypes.data for k in (
             "type", "flags", "client", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_off", "payload_len",
             "prop_id")), pay.ctypes.data), "mt_generated_download")
-        offs = np.arange(p.n_docs + 1, dtype=np.uint32) * p.ops_per_doc
+        offs = np.zeros(p.n_docs + 1, np.uint32)
+        offs[1:] = np.cumsum(self._gen_ops, dtype=np.uint64).astype(np.uint32)
         return OpBatch.from_arrays(np.arange(p.n_docs, dtype=np.uint32), offs, pay, **a)
 
     def generated_to_resident(self):
@@ -214,6 +247,11 @@ class Engine:
     def set_residency(self, use_lds: bool = True, rows: int = 0, blocks: int = 0, heap: int = 0):
         """mt_set_residency: LDS-resident replay on/off and (lowered) LDS pool caps."""
         self._check(self.fn["set_residency"](self.h, int(use_lds), rows, blocks, heap), "mt_set_residency")
+
+    def pool_bytes(self) -> int:
+        v = ctypes.c_uint64()
+        self._check(self.fn["pool_bytes"](self.h, ctypes.byref(v)), "mt_pool_bytes")
+        return int(v.value)
 
     def pools(self, docs) -> np.ndarray:
         """Per-document pool occupancy (mt_doc_pools): columns rowTop, blkTop, heapN,
@@ -251,6 +289,15 @@ class Engine:
         for i in range(len(d)):
             blobs = [raw[offs[j]:offs[j + 1]] for j in range(first[i], first[i + 1])]
             out.append((blobs, int(dig[i])))
+        return out
+
+    def snapshot_digests(self, docs, msn, seq, threads: int = 8) -> np.ndarray:
+        """mt_snapshot_digests: SnapshotV1 digests of many documents (one staged download,
+        host serialization on `threads` threads)."""
+        d, m, s = _u32(docs), _i32(msn), _i32(seq)
+        out = np.zeros(len(d), np.uint64)
+        self._check(self.fn["snapshot_digests"](self.h, len(d), d.ctypes.data, m.ctypes.data, s.ctypes.data,
+                                                out.ctypes.data, threads), "mt_snapshot_digests")
         return out
 
     def get_text(self, docs) -> list[str]:

@@ -145,6 +145,11 @@ typedef struct mt_doc_counters {
 } mt_doc_counters;
 
 int  mt_create(int device, const mt_limits* limits, mt_ctx** out);
+/* As mt_create, with capacities per document (per_doc[i] for document i; its
+ * max_docs field is ignored), e.g. sized from each document's op count. */
+int  mt_create_docs(int device, uint32_t n_docs, const mt_limits* per_doc, mt_ctx** out);
+/* HBM bytes held by the context's document pools. */
+int  mt_pool_bytes(mt_ctx* ctx, uint64_t* bytes);
 void mt_destroy(mt_ctx* ctx);
 const char* mt_last_error(mt_ctx* ctx);
 
@@ -173,6 +178,8 @@ int  mt_set_residency(mt_ctx* ctx, int use_lds, int rows, int blocks, int heap);
  * context stream. */
 int  mt_last_replay_ms(mt_ctx* ctx, float* ms);
 
+/* seq[i] < 0 leaves document i's (minSeq, currentSeq) unchanged; the snapshot
+ * entry points take the same convention for "snapshot at the current window". */
 int  mt_update_seq(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
                    const int32_t* msn, const int32_t* seq);
 int  mt_sync(mt_ctx* ctx);
@@ -211,6 +218,10 @@ int  mt_snapshot_v1(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
                     uint64_t* out_digest,
                     const char** arena, const uint64_t** blob_off,
                     const uint32_t** blob_first);
+/* Digests only (same values as mt_snapshot_v1's), for many documents: one staged
+ * download, serialization spread over `threads` host threads. */
+int  mt_snapshot_digests(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, const int32_t* msn,
+                         const int32_t* seq, uint64_t* out_digest, int threads);
 /* Observer text (UTF-16) of each document into a library-owned arena. */
 int  mt_get_text(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
                  const uint16_t** arena, const uint64_t** off);
@@ -241,8 +252,16 @@ typedef struct mt_gen_params {
     uint32_t pct_rewrite;        /* annotate rewrite percentage                   */
 } mt_gen_params;
 int  mt_generate(mt_ctx* ctx, const mt_gen_params* params);
-/* Copy the generated stream to host memory (arrays sized n_docs*ops_per_doc,
- * payload sized n_docs*ops_per_doc*ins_len_max). */
+/* As mt_generate with per-document message counts and authoring-client counts
+ * (either array may be null: params->ops_per_doc / params->clients).  Runs are
+ * documents 0..n_docs-1 with op offsets = prefix sums of the counts. */
+int  mt_generate_docs(mt_ctx* ctx, const mt_gen_params* params, const uint32_t* ops_per_doc,
+                      const uint32_t* clients_per_doc);
+/* Total op records of the last generation. */
+int  mt_generated_ops(mt_ctx* ctx, uint64_t* n_ops);
+/* Copy the generated stream to host memory (arrays sized mt_generated_ops,
+ * payload sized mt_generated_ops * ins_len_max; op i's payload starts at
+ * i * ins_len_max). */
 int  mt_generated_download(mt_ctx* ctx, uint8_t* type, uint8_t* flags, uint16_t* client,
                            int32_t* seq, int32_t* ref_seq, int32_t* msn, int32_t* pos1,
                            int32_t* pos2, uint32_t* payload_off, uint32_t* payload_len,

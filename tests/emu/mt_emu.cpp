@@ -61,7 +61,7 @@ static int mtb_launch_open(mt_ctx* c, uint32_t first, uint32_t n) {
 static int mtb_launch_update_seq(mt_ctx* c, const uint32_t* docs, const int32_t* msn, const int32_t* seq, uint32_t n) {
     for (uint32_t i = 0; i < n; i++) {
         MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc);
-        if (e.curSeq > seq[i]) e.status |= MT_DS_ASSERT_SEQ; else { e.curSeq = seq[i]; e.setMinSeq(msn[i]); }
+        mt_update_seq_doc(e, msn[i], seq[i]);
         e.store(docs[i]);
     }
     return MT_OK;
@@ -71,6 +71,14 @@ static int mtb_launch_get_length(mt_ctx* c, const uint32_t* docs, const int32_t*
         MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc);
         out[i] = e.perspectiveLength(ref[i], cli[i] < 0 ? 255 : cli[i]);
     }
+    return MT_OK;
+}
+static int mtb_launch_pack_size(mt_ctx* c, const uint32_t* docs, MtPackSize* out, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) { MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc); out[i] = mt_pack_size(e); }
+    return MT_OK;
+}
+static int mtb_launch_pack(mt_ctx* c, const uint32_t* docs, const uint64_t* off, uint8_t* stage, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) { MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc); mt_pack_doc(e, stage + off[i]); }
     return MT_OK;
 }
 #define MT_FN(name) emu_##name

@@ -7,13 +7,13 @@ from fluidframework_amd.engine import Engine
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "emu", "mt_emu.cpp")
 LIB = os.path.join(ROOT, "tests", "emu", "libmtemu.so")
-DEPS = [SRC] + [os.path.join(ROOT, "fluidframework_amd", "csrc", f) for f in
-                ("mt_core.h", "mt_replay.h", "mt_snapshot.h", "mt_api_impl.h", "mt_ctx.h", "wave.h")]
+DEPS = [SRC, os.path.join(ROOT, "include", "mtgpu.h")] + [os.path.join(ROOT, "fluidframework_amd", "csrc", f) for f in
+                ("mt_core.h", "mt_replay.h", "mt_snapshot.h", "mt_pack.h", "mt_api_impl.h", "mt_ctx.h", "wave.h")]
 
 
 def build_emu(force=False):
     if force or not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(d) for d in DEPS):
-        subprocess.check_call(["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
+        subprocess.check_call(["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wno-unknown-pragmas",
                                "-o", LIB, SRC])
     return LIB
 

@@ -165,23 +165,30 @@ def gen_params(seed=1, n_docs=1, ops=1000, clients=2, lag=8, ins=55, rem=45, ins
     return MtGenParams(seed, n_docs, ops, clients, lag, ins, rem, ins_len, rem_len, ann_sets, rewrite)
 
 
-def generate(params: MtGenParams, props: PropTable, docs=None, keep=False):
-    """Generate streams with the oracle as sequencer+observer; returns (OpBatch, [status], [OracleDoc])."""
+def generate(params: MtGenParams, props: PropTable, docs=None, keep=False, ops_per_doc=None, clients_per_doc=None):
+    """Generate streams with the oracle as sequencer+observer; returns (OpBatch, [status], [OracleDoc]).
+    ops_per_doc / clients_per_doc: per-document counts (indexed by position in docs),
+    as mt_generate_docs takes them."""
     L = lib()
     docs = list(range(params.n_docs)) if docs is None else list(docs)
-    n = params.ops_per_doc
     cols = {k: [] for k in ("type", "flags", "client", "seq", "ref_seq", "msn", "pos1", "pos2",
                             "payload_off", "payload_len", "prop_id")}
     payloads, offs, stats, kept = [], [0], [], []
     base = 0
-    for d in docs:
+    for j, d in enumerate(docs):
+        pj = MtGenParams(*(getattr(params, f) for f, _ in MtGenParams._fields_))
+        if ops_per_doc is not None:
+            pj.ops_per_doc = int(ops_per_doc[j])
+        if clients_per_doc is not None:
+            pj.clients = int(clients_per_doc[j])
+        n = pj.ops_per_doc
         a = dict(type=np.zeros(n, np.uint8), flags=np.zeros(n, np.uint8), client=np.zeros(n, np.uint16),
                  seq=np.zeros(n, np.int32), ref_seq=np.zeros(n, np.int32), msn=np.zeros(n, np.int32),
                  pos1=np.zeros(n, np.int32), pos2=np.zeros(n, np.int32), payload_off=np.zeros(n, np.uint32),
                  payload_len=np.zeros(n, np.uint32), prop_id=np.zeros(n, np.int32))
         pay = np.zeros(max(1, n * params.ins_len_max), np.uint16)
         kp = ctypes.c_void_p()
-        st = L.ora_generate_doc(ctypes.byref(params), d, ctypes.byref(props.to_c()),
+        st = L.ora_generate_doc(ctypes.byref(pj), d, ctypes.byref(props.to_c()),
                                 *(a[k].ctypes.data for k in ("type", "flags", "client", "seq", "ref_seq", "msn",
                                                              "pos1", "pos2", "payload_off", "payload_len", "prop_id")),
                                 pay.ctypes.data, base, ctypes.byref(kp) if keep else None)

@@ -57,12 +57,14 @@ def compare(batch, props, n_docs, factory=None, **cap):
         bad = np.nonzero((ed != odump).any(axis=1))[0]
         assert len(bad) == 0, f"doc {d} first differing row {bad[:3]}: emu {ed[bad[0]]} oracle {odump[bad[0]]}"
     snaps = eng.snapshot(range(n_docs), msn, seq)
+    digs = eng.snapshot_digests(range(n_docs), msn, seq, threads=3)
     for d in range(n_docs):
         od, _ = oracle_docs[d]
         oblobs, odig = od.snapshot(int(msn[d]), int(seq[d]))
         eblobs, edig = snaps[d]
         assert eblobs == oblobs, f"doc {d} snapshot"
         assert edig == odig
+        assert int(digs[d]) == odig, f"doc {d} mt_snapshot_digests"
     return eng
 
 
@@ -177,3 +179,53 @@ def test_emu_matches_oracle_stress(cfg):
     batch, st, _ = generate(p, props)
     assert st == [0] * 2
     compare(batch, props, 2)
+
+
+def test_emu_per_document_capacities_match_oracle():
+    # mt_create_docs: documents of one context with different pool sizes (sized
+    # from each document's op count, as config 5's Zipf documents are).
+    props = ann_props()
+    p = gen_params(seed=17, n_docs=4, **CONFIGS["cfg3"])
+    batch, st, _ = generate(p, props)
+    n = 4
+    per_doc = dict(rows_per_doc=[3000 + 500 * d for d in range(n)], window_per_doc=[2048 + 64 * d for d in range(n)],
+                   text_per_doc=[40000 + 1000 * d for d in range(n)], propsets_per_doc=[4000 + 7 * d for d in range(n)])
+    from fluidframework_amd.engine import Engine
+    from emu_lib import build_emu
+    eng = Engine(n, lib_path=build_emu(), prefix="emu_", per_doc=per_doc)
+    assert eng.pool_bytes() > 0
+    eng.upload_props(props)
+    eng.upload_names(NAMES)
+    eng.open_docs(0, n)
+    eng.apply(batch)
+    eng.sync()
+    assert (eng.status(range(n)) == 0).all()
+    oracle_docs = replay(batch, props, NAMES)
+    texts = eng.get_text(range(n))
+    last = batch.op_offsets[1:] - 1
+    snaps = eng.snapshot(range(n), batch.arrays["msn"][last], batch.arrays["seq"][last])
+    for d in range(n):
+        assert texts[d] == oracle_docs[d][0].get_text()
+        assert np.array_equal(eng.dump(d), oracle_docs[d][0].dump())
+        assert snaps[d][0] == oracle_docs[d][0].snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]))[0]
+
+
+def test_emu_generator_per_document_counts_matches_oracle():
+    # mt_generate_docs: skewed per-document message counts and client counts
+    # (config 5's Zipf documents) produce the oracle generator's streams.
+    props = ann_props()
+    ops = [8, 300, 1200, 57, 2000]
+    cl = [2, 16, 5, 9, 3]
+    p = gen_params(seed=19, n_docs=5, **{**CONFIGS["cfg2"], "ops": 100})
+    ob, st, _ = generate(p, props, ops_per_doc=ops, clients_per_doc=cl)
+    assert st == [0] * 5
+    eng = emu_engine(5, rows_per_doc=8192, window_per_doc=4096, propsets_per_doc=8192, text_per_doc=1 << 16)
+    eng.upload_props(props)
+    eng.upload_names(NAMES)
+    eng.generate(p, ops_per_doc=ops, clients_per_doc=cl)
+    eng.sync()
+    assert (eng.status(range(5)) == 0).all()
+    gb = eng.generated_download()
+    assert np.array_equal(gb.op_offsets, ob.op_offsets)
+    for k in ("type", "flags", "client", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_len", "prop_id"):
+        assert np.array_equal(gb.arrays[k], ob.arrays[k]), k

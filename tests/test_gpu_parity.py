@@ -95,3 +95,40 @@ def test_gpu_get_length_matches_oracle():
             got = eng.get_length(range(4), refs, [c] * 4)
             want = [kept[d].get_length(int(refs[d]), c) for d in range(4)]
             assert list(got) == want
+
+
+def test_gpu_per_document_capacities_and_generator_counts():
+    # mt_create_docs (per-document pool sizes) + mt_generate_docs (per-document
+    # message and client counts): device streams equal the oracle generator's,
+    # and replaying them on differently sized documents is bit-exact.
+    props = ann_props()
+    ops = [8, 300, 1200, 57, 2000, 640]
+    cl = [2, 16, 5, 9, 3, 8]
+    n = len(ops)
+    p = gen_params(seed=19, n_docs=n, **{**CONFIGS["cfg2"], "ops": 100})
+    ob, st, kept = generate(p, props, ops_per_doc=ops, clients_per_doc=cl, keep=True)
+    assert st == [0] * n
+    per_doc = dict(rows_per_doc=[3 * o + 64 for o in ops], window_per_doc=[2048] * n,
+                   text_per_doc=[8 * o + 4096 for o in ops], propsets_per_doc=[64] * n, blocks_per_doc=[o + 64 for o in ops],
+                   heap_per_doc=[2 * o + 64 for o in ops])
+    eng = Engine(n, device=0, per_doc=per_doc)
+    eng.upload_props(props)
+    eng.upload_names(NAMES)
+    eng.generate(p, ops_per_doc=ops, clients_per_doc=cl)
+    eng.sync()
+    assert (eng.status(range(n)) == 0).all()
+    gb = eng.generated_download()
+    assert np.array_equal(gb.op_offsets, ob.op_offsets)
+    for k in ("type", "flags", "client", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_len", "prop_id"):
+        assert np.array_equal(gb.arrays[k], ob.arrays[k]), k
+    eng.generated_to_resident()
+    eng.open_docs(0, n)
+    eng.replay_resident()
+    eng.sync()
+    assert (eng.status(range(n)) == 0).all()
+    last = ob.op_offsets[1:] - 1
+    digs = eng.snapshot_digests(range(n), ob.arrays["msn"][last], ob.arrays["seq"][last], threads=4)
+    texts = eng.get_text(range(n))
+    for d in range(n):
+        assert texts[d] == kept[d].get_text()
+        assert int(digs[d]) == kept[d].snapshot(int(ob.arrays["msn"][last[d]]), int(ob.arrays["seq"][last[d]]))[1]
