@@ -40,6 +40,10 @@ CONFIGS = {
                     desc="16384 docs x 8 clients x 4k msgs, lag U[0,4], 30/30/40 ins/rem/annotate, zamboni-heavy"),
     "config1": dict(docs=1, ops=10000, clients=2, lag=8, ins=55, rem=45, ins_len=8, rem_len=16, ann_sets=1, rewrite=0,
                     desc="1 doc x 2 clients x 10k msgs (reference plumbing case)"),
+    # docs = per GPU (weak scaling; 8 GPUs = 1,048,576 docs); ops ~ Zipf(1.5) on [8, 65536], clients U[2,16]
+    "config5": dict(docs=131072, ops=0, clients=0, lag=32, ins=60, rem=40, ins_len=8, rem_len=8, ann_sets=1, rewrite=0,
+                    desc="Zipf(1.5)-sized docs (8..65536 msgs, clients U[2,16]), 131072 docs per GPU, rank-0 ingest, "
+                         "LPT rebalance + digest gather over RCCL"),
 }
 
 
@@ -83,8 +87,9 @@ def caps_for(c):
                 propsets_per_doc=(2 * ops + 64) if c["ins"] + c["rem"] < 100 else 64)
 
 
-def cpu_baseline(eng, c, params_cls, seed, target_s, threads):
-    """Oracle ('port' of the reference algorithm) on a bounded sample of the same streams."""
+def cpu_baseline(eng, c, params_cls, seed, target_s, threads, ops_fn=None):
+    """Oracle ('port' of the reference algorithm) on a bounded sample of the same streams.
+    ops_fn(n) -> (ops_per_doc, clients_per_doc) for skewed workloads (config 5)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes
     from oracle_lib import lib as oracle
@@ -94,7 +99,11 @@ def cpu_baseline(eng, c, params_cls, seed, target_s, threads):
     def run(n_docs):
         p = params_cls(seed, n_docs, c["ops"], c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"],
                        c["rem_len"], c["ann_sets"], c["rewrite"])
-        eng.generate(p)
+        if ops_fn is None:
+            eng.generate(p)
+        else:
+            o, k = ops_fn(n_docs)
+            eng.generate(p, ops_per_doc=o, clients_per_doc=k)
         eng.sync()
         b = eng.generated_download()
         st = np.zeros(n_docs, np.uint32)
@@ -110,8 +119,108 @@ def cpu_baseline(eng, c, params_cls, seed, target_s, threads):
         if docs > pilot_docs:
             t, n = run(docs)
     return {"value": n / t, "unit": "ops/s", "cores": threads, "kind": "port",
-            "sample": f"{docs} docs x {c['ops']} msgs of the same workload, oracle (C++ restatement of "
+            "sample": f"{docs} docs ({n} msgs) of the same workload, oracle (C++ restatement of "
                       f"MT/mergeTree.ts + partialLengths.ts) on {threads} host threads, {t:.1f} s"}
+
+
+def run_config5(args, c, world, rank, local):
+    """Config 5: Zipf-sized documents ingested on rank 0, LPT-rebalanced across the
+    ranks over RCCL (one all_to_all_single of op records + payloads), replayed per
+    rank, SnapshotV1 digests gathered to rank 0 (fluidframework_amd/shard.py)."""
+    import torch
+    from fluidframework_amd.batch import MtGenParams
+    from fluidframework_amd.engine import Engine
+    from fluidframework_amd.shard import SoloDist, build_sharded, clients_per_doc, zipf_op_counts
+    if world > 1:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = tdist
+    else:
+        dist = SoloDist()
+    device = torch.device("cuda", local)
+    total_docs = c["docs"] * world
+    gen_kw = dict(lag_max=c["lag"], pct_insert=c["ins"], pct_remove=c["rem"], ins_len_max=c["ins_len"],
+                  rem_len_max=c["rem_len"], n_ann_sets=c["ann_sets"], pct_rewrite=c["rewrite"])
+    names = ['"c%d"' % i for i in range(64)]
+    fac = lambda n, caps: Engine(n, device=local, per_doc=caps)
+    t0 = time.time()
+    sh = build_sharded(dist, device, fac, total_docs, args.seed, MtGenParams, gen_kw, names=names)
+    setup_s = time.time() - t0
+    eng = sh.engine
+    eng.set_residency(args.residency == "lds")
+    my_msgs = int(sh.ops.sum())
+    for _ in range(args.warmup):
+        sh.replay()
+    eng.sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        sh.replay()
+        eng.sync()
+        kms.append(eng.last_replay_ms())
+    eng.sync()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    st = eng.status(range(sh.n_docs))
+    cnt = eng.counters(range(sh.n_docs))
+    bytes_per_launch = algorithmic_bytes(cnt)
+    digs = sh.gather_digests(dist, device, threads=min(16, os.cpu_count() or 1))
+    bad = torch.tensor([int(st.any()) + int(int(cnt["msgs"].sum()) != my_msgs)], dtype=torch.int32, device=device)
+    if world > 1:
+        dist.all_reduce(bad)
+    if rank != 0:
+        return
+    total_msgs = int(sh.all_ops.sum())
+    kern_s = float(np.mean(kms)) / 1e3
+    achieved = bytes_per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
+    out = {
+        "metric": "sequenced merge-tree ops applied/sec (whole node) + achieved HBM GB/s",
+        "value": total_msgs * args.steps / dt, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic (device-generated sequenced op streams, SURVEY.md §8(d) config-5 rules)",
+        "config": {"workload": f"config5: {c['desc']}", "docs_per_gpu": c["docs"], "docs_total": total_docs,
+                   "msgs_total": total_msgs, "msgs_mean": total_msgs / total_docs,
+                   "msgs_max": int(sh.all_ops.max()), "parallelism": f"doc-sharded x{world} (LPT)",
+                   "residency": args.residency},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "mt_replay_kernel (rank 0)",
+                     "kernel_ms": kern_s * 1e3, "bytes_per_launch": bytes_per_launch},
+        "parity": "status words clean on every rank" if int(bad.item()) == 0 else "STATUS ERROR",
+        "sharding": {"rebalance_ms": sh.timings.get("rebalance_ms"), "rebalance_bytes": sh.timings.get("rebalance_bytes"),
+                     "digest_gather_ms": sh.timings.get("digest_ms"), "ingest_generate_s": sh.timings.get("generate_s"),
+                     "setup_s": setup_s, "digest_xor": f"{int(np.bitwise_xor.reduce(digs)):016x}",
+                     "docs_per_rank_max": int(np.bincount(sh.owner).max())},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline_config5(args, c, local)
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline_config5(args, c, local):
+    """Oracle on a bounded sample of config-5 documents (same Zipf sizes)."""
+    from fluidframework_amd.batch import MtGenParams
+    from fluidframework_amd.engine import Engine
+    from fluidframework_amd.shard import clients_per_doc, generation_caps, zipf_op_counts
+    threads = min(16, os.cpu_count() or 1)
+    n = 4000
+    ops = zipf_op_counts(n, args.seed ^ 0x5A)
+    cl = clients_per_doc(n, args.seed ^ 0x5A)
+    eng = Engine(n, device=local, per_doc=generation_caps(ops, c["ins_len"]))
+    eng.upload_props(ann_props())
+    eng.upload_names(['"c%d"' % i for i in range(64)])
+    cc = dict(c)
+    cc["docs"] = n
+    res = cpu_baseline(eng, cc, MtGenParams, args.seed ^ 0x5A, args.cpu_seconds, threads,
+                       ops_fn=lambda k: (ops[:k], cl[:k]))
+    eng.close()
+    return res
 
 
 def main():
@@ -133,6 +242,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config == "config5":
+        c = dict(CONFIGS["config5"])
+        if args.docs:
+            c["docs"] = args.docs
+        return run_config5(args, c, world, rank, local)
     dist = None
     if world > 1:
         import torch
@@ -205,7 +319,7 @@ def main():
     t1 = time.perf_counter()
     sthreads = min(16, os.cpu_count() or 1)
     neg = np.full(c["docs"], -1, np.int32)
-    digs = eng.snapshot_digests(range(c["docs"]), neg, neg, threads=sthreads)
+    digs = eng.snapshot_digests(range(c["docs"]), neg, neg, threads=sthreads) if eng.fn["snapshot_digests"] else np.zeros(1, np.uint64)
     snap_ms = (time.perf_counter() - t1) * 1e3
     dig_xor = int(np.bitwise_xor.reduce(digs)) if len(digs) else 0
     ok = (not st.any()) and int(cnt2["msgs"].sum()) == msgs

@@ -56,7 +56,7 @@ class MtPropTable(ctypes.Structure):
 class MtGenParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64 if n == "seed" else ctypes.c_uint32) for n in (
         "seed", "n_docs", "ops_per_doc", "clients", "lag_max", "pct_insert", "pct_remove",
-        "ins_len_max", "rem_len_max", "n_ann_sets", "pct_rewrite")]
+        "ins_len_max", "rem_len_max", "n_ann_sets", "pct_rewrite", "doc_id_base")]
 
 
 def _ptr(a: np.ndarray) -> int:

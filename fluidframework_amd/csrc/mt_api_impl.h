@@ -251,9 +251,10 @@ int MT_FN(doc_pools)(mt_ctx* c, uint32_t n, const uint32_t* docs, int32_t* out) 
     int rc = mt_read_hdrs(c, n, docs, h);
     if (rc) return rc;
     for (uint32_t i = 0; i < n; i++) {
-        int32_t* o = out + 8 * (size_t)i;
+        int32_t* o = out + 10 * (size_t)i;
         o[0] = h[i].rowTop; o[1] = h[i].blkTop; o[2] = h[i].heapN; o[3] = h[i].winN;
         o[4] = h[i].textTop; o[5] = h[i].psetTop; o[6] = h[i].height; o[7] = h[i].rfN;
+        o[8] = h[i].heapHW; o[9] = h[i].winHW;
     }
     return MT_OK;
 }
@@ -483,7 +484,7 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     g.seed = P->seed; g.ops = P->ops_per_doc; g.clients = P->clients; g.lag_max = P->lag_max;
     g.pct_insert = P->pct_insert; g.pct_remove = P->pct_remove; g.ins_len_max = P->ins_len_max;
     g.rem_len_max = P->rem_len_max; g.n_ann_sets = P->n_ann_sets; g.pct_rewrite = P->pct_rewrite; g.enabled = 1;
-    g.clients_per_run = (const uint32_t*)c->b_gencl.p; g.total_ops = N;
+    g.clients_per_run = (const uint32_t*)c->b_gencl.p; g.total_ops = N; g.doc_id_base = P->doc_id_base;
     c->gen = g; c->gen_docs = P->n_docs;
     return mtb_launch_replay(c, g, P->n_docs);
 }
@@ -512,6 +513,41 @@ int MT_FN(generated_download)(mt_ctx* c, uint8_t* type, uint8_t* flags, uint16_t
     }
     mtb_d2h(c, payload, c->ops.payload, 2 * (N * c->gen.ins_len_max));
     return MT_OK;
+}
+static_assert(sizeof(mt_op_rec) == sizeof(MtOpRec) && sizeof(mt_op_rec) == 32, "op record layout");
+int MT_FN(generated_copy_dev)(mt_ctx* c, uint32_t first, uint32_t n, mt_op_rec* rec, uint16_t* payload) {
+    if (!c || !c->gen_docs || (uint64_t)first + n > c->gen_off.size() - 1 || (n && (!rec || !payload))) return MT_E_INVALID;
+    int rc = mtb_sync(c);
+    if (rc) return rc;
+    const uint64_t o0 = c->gen_off[first], o1 = c->gen_off[first + n];
+    const uint64_t L = c->gen.ins_len_max;
+    mtb_d2d(c, rec, c->ops.rec + o0, sizeof(MtOpRec) * (o1 - o0));
+    mtb_d2d(c, payload, c->ops.payload + o0 * L, 2 * (o1 - o0) * L);
+    return MT_OK;
+}
+int MT_FN(upload_batch_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids, const uint32_t* op_offsets,
+                            const mt_op_rec* rec, const uint16_t* payload, uint64_t payload_units) {
+    if (!c || !op_offsets || (n_runs && !doc_ids)) return MT_E_INVALID;
+    for (uint32_t r = 0; r < n_runs; r++) {
+        if (doc_ids[r] >= c->S.maxDocs) { c->err = "doc id out of range"; return MT_E_INVALID; }
+        if (op_offsets[r] > op_offsets[r + 1]) { c->err = "op_offsets not monotone"; return MT_E_INVALID; }
+    }
+    const uint64_t N = op_offsets[n_runs];
+    if (N && (!rec || !payload)) return MT_E_INVALID;
+    int rc;
+#define UP(buf, bytes) if ((rc = mtb_ensure(c, c->buf, (bytes)))) return rc;
+    UP(b_doc, 4ull * n_runs + 4) UP(b_off, 4ull * (n_runs + 1)) UP(b_rec, sizeof(MtOpRec) * N + 32) UP(b_pay, 2 * payload_units + 2)
+#undef UP
+    mtb_h2d(c, c->b_doc.p, doc_ids, 4ull * n_runs);
+    mtb_h2d(c, c->b_off.p, op_offsets, 4ull * (n_runs + 1));
+    if (N) mtb_d2d(c, c->b_rec.p, rec, sizeof(MtOpRec) * N);
+    if (payload_units) mtb_d2d(c, c->b_pay.p, payload, 2 * payload_units);
+    MtOps& o = c->ops;
+    o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
+    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs;
+    c->n_runs = n_runs;
+    c->gen.enabled = 0;
+    return mtb_sync(c);
 }
 int MT_FN(generated_to_resident)(mt_ctx* c) {
     if (!c || !c->gen.enabled) return MT_E_INVALID;

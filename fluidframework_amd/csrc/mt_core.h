@@ -64,6 +64,14 @@
 #else
 #define MT_EV(i, v)
 #endif
+// Second event set (host-emulation diagnostic builds only, -DMT_EVCOUNT2): 0 packParent,
+// 1 updatePathLens levels, 2 copyText units, 3 copyText calls, 4 textGC, 5 splitRow,
+// 6 zamboni calls that popped, 7 rangeMap leaf blocks.
+#if defined(MT_EVCOUNT2)
+#define MT_EV2(i, v) prof[i] += (unsigned long long)(v)
+#else
+#define MT_EV2(i, v)
+#endif
 // Fine-grained latency probes (device diagnostic builds only, -DMT_PROFILE2):
 // 0 walk blkLoad cyc, 1 walk childLens cyc, 2 walk levels, 3 computeU cyc,
 // 4 computeU calls, 5 heapGet cyc, 6 heapGet calls, 7 scourLeaf cyc.
@@ -121,7 +129,8 @@ struct __attribute__((aligned(16))) MtDocHdr {
     int textHalf;                            // which half of the doc's text arena is live
     int rfN;                                 // recycled rows on the document's stack (hold pool)
     int blkFreeN;                            // blocks on the free list
-    int pad[5];
+    int heapHW, winHW;                       // high-water marks (pool sizing, mt_doc_pools)
+    int pad[3];
     unsigned long long prof[8];              // MT_PROFILE builds: s_memtime cycles per phase
 };
 
@@ -163,6 +172,7 @@ struct MtGen {                                // device stream generator paramet
     uint32_t ops, clients, lag_max, pct_insert, pct_remove, ins_len_max, rem_len_max, n_ann_sets, pct_rewrite;
     int enabled;
     const uint32_t* clients_per_run;          // per-document authoring clients (mt_generate_docs), or null
+    uint32_t doc_id_base;                     // run i is seeded as document doc_id_base + i
     uint64_t total_ops;                       // ops over all runs (payload stride base)
 };
 
@@ -258,6 +268,7 @@ template <bool LDS> struct MtEngT {
     int lastL, lastIdx; bool lastSplit; // landing spot of the last walk; did it split a block
     int rfN; int* rfHbm;                // recycled-row stack: depth, HBM home between runs
     int blkFreeN;                       // blocks on the free list
+    int heapHW, winHW;                  // high-water marks of heapN / winN
     // LDS residency (toLds/fromLds): LDS caps, and the HBM caps they stand in for
     static constexpr bool kLds = LDS;
     int lRows, lBlks, lHeap;
@@ -290,6 +301,7 @@ template <bool LDS> struct MtEngT {
         heapTop = heapN > 0 ? uni(heap[1].maxSeq) : 0x7FFFFFFF;     // HBM home: bind precedes toLds
         lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0;
         rfHbm = st.hold + (size_t)d * MT_RFL; rfN = uni(h.rfN); blkFreeN = uni(h.blkFreeN);
+        heapHW = uni(h.heapHW); winHW = uni(h.winHW);
         lRows = lBlks = lHeap = 0; gRowCap = gBlkCap = gHeapCap = gWinCap = 0;
         if (rfN < 0 || rfN > MT_RFL) rfN = 0;
         { const int n = rfN; const int* src = rfHbm;
@@ -304,6 +316,7 @@ template <bool LDS> struct MtEngT {
         h.root = root; h.height = height; h.minSeq = minSeq; h.curSeq = curSeq; h.rowTop = rowTop;
         h.blkTop = blkTop; h.blkFree = blkFree; h.heapN = heapN; h.winN = winN; h.textTop = textTop;
         h.psetTop = psetTop; h.status = status; h.textHalf = textHalf; h.rfN = rfN; h.blkFreeN = blkFreeN;
+        h.heapHW = heapHW; h.winHW = winHW;
         { const int n = rfN; int* dst = rfHbm;
           for (int base = 0; base < n; base += MT_WAVE) {
               const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
@@ -317,7 +330,7 @@ template <bool LDS> struct MtEngT {
     MT_HD void open() {
         root = 0; height = 0; minSeq = 0; curSeq = 0; rowTop = 0; blkTop = 1; blkFree = -1;
         heapN = 0; winN = 0; textTop = 0; psetTop = 0; status = 0; textHalf = 0; heapTop = 0x7FFFFFFF; rfN = 0;
-        blkFreeN = 0;
+        blkFreeN = 0; heapHW = 0; winHW = 0;
         text = S.textBase;
         c_ops = c_msgs = c_ins = c_rows = c_depth = c_scour = 0;
         for (int i = 0; i < 8; i++) prof[i] = 0;
@@ -407,6 +420,7 @@ template <bool LDS> struct MtEngT {
         if (mt & MT_M_INWIN) return;
         if (winN >= (int)S.winCap) { status |= MT_DS_OOM_WINDOW; return; }
         wn(winN++) = s;
+        if (winN > winHW) winHW = winN;
         row(s).meta = mt | MT_M_INWIN;
     }
     // Scalar fields of a block (SGPRs) and its children (one per lane).
@@ -560,6 +574,7 @@ template <bool LDS> struct MtEngT {
     // createSplitSegmentAt textSegment.ts:103-111): the right half copies every
     // attribute; the property map is immutable here, so both halves share it.
     MT_HD int splitRow(int s, int pos) {
+        MT_EV2(5, 1);
         const int n = allocRow();
         if (n < 0) return -1;
         const int ls = uni(row(s).len);
@@ -688,6 +703,7 @@ template <bool LDS> struct MtEngT {
     MT_HD void heapAdd(int s, int ms) {
         if (heapN + 1 > (int)S.heapCap) { status |= MT_DS_OOM_HEAP; return; }
         int k = ++heapN;
+        if (heapN > heapHW) heapHW = heapN;
         if (heapN < MT_WAVE) {
             const int n = heapN;
             auto hs = wave_map(n, [&](int i) MT_LAM { return hp(i).seg; });
@@ -787,10 +803,13 @@ template <bool LDS> struct MtEngT {
         });
         return wave_count(ok) == na;
     }
-    MT_HD void copyText(int dst, int src, int n) {
+    // text[dst, dst+n1+n2) = text[src1, src1+n1) ++ text[src2, src2+n2), 64 units a pass.
+    MT_HD void copyText(int dst, int src1, int n1, int src2 = 0, int n2 = 0) {
+        const int n = n1 + n2;
+        MT_EV2(2, n); MT_EV2(3, 1);
         for (int base = 0; base < n; base += MT_WAVE) {
             const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
-            auto v = wave_map(m, [&](int k) MT_LAM { return (int)text[src + base + k]; });
+            auto v = wave_map(m, [&](int k) MT_LAM { const int q = base + k; return (int)text[q < n1 ? src1 + q : src2 + (q - n1)]; });
             wave_sync();
             wave_for(m, [&](int k) MT_LAM { text[dst + base + k] = (uint16_t)own(v, k); });
         }
@@ -800,6 +819,7 @@ template <bool LDS> struct MtEngT {
     // half of the document's arena (rows are immutable slices, so garbage from
     // relocated or unlinked rows accumulates until the half is full).
     MT_HD void textGC() {
+        MT_EV2(4, 1);
         MT_PB(t0);
         const int other = textHalf ^ 1;
         uint16_t* dst = S.textBase + (size_t)other * S.textCap;
@@ -842,7 +862,7 @@ template <bool LDS> struct MtEngT {
         if (textTop + nc > (int)S.textCap) { textGC(); nc = lp + ls; tp = uni(row(pv).toff); ts = uni(row(s).toff); }
         const int o = textAlloc(nc);
         if (o < 0) return;
-        copyText(o, tp, lp); copyText(o + lp, ts, ls);
+        copyText(o, tp, lp, ts, ls);
         row(pv).toff = o; row(pv).tcap = nc; row(pv).len = lp + ls;
         tp = o; cp = nc;
     }
@@ -908,12 +928,14 @@ template <bool LDS> struct MtEngT {
     }
     MT_HD void updatePathLens(int B) {                        // blockUpdatePathLengths(..., newStructure)
         while (B >= 0) {
+            MT_EV2(1, 1);
             const BlkH h = head(B);
             bk(B).len = sumObs(B, h.n, h.height);
             B = h.parent;
         }
     }
     MT_HD void packParent(int P) {                            // MT/mergeTree.ts:1359-1410
+        MT_EV2(0, 1);
         for (;;) {
             BlkH ph;
             auto pch = blkLoad(P, ph);
@@ -964,6 +986,7 @@ template <bool LDS> struct MtEngT {
         for (int i = 0; i < MT_ZMAX; i++) {
             if (heapN == 0 || heapTop > minSeq) break;
             uValid = false;                                   // scour/pack may restructure
+            MT_EV2(6, 1);
             MT_QB(q0); MT_QC(6);
             const MtHeapE e = heapGet();
             MT_QE(5, q0);
@@ -1077,6 +1100,7 @@ template <bool LDS> struct MtEngT {
                 return j >= j0 && (en - pj) > 0 && lj > 0 && (st - pj) < lj;
             });
             if (h.height == 0) {
+                MT_EV2(7, 1);
                 const int first = wave_first(cond);
                 int obsDelta = 0;
                 if (first >= 0) {

@@ -116,6 +116,7 @@ static int mtb_malloc(void** p, size_t n) { return hipMalloc(p, n) == hipSuccess
 static void mtb_free(void* p) { (void)hipFree(p); }
 static void mtb_memset(void* p, int v, size_t n) { (void)hipMemset(p, v, n); }
 static void mtb_h2d(mt_ctx* c, void* d, const void* s, size_t n) { (void)hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, (hipStream_t)c->stream); (void)hipStreamSynchronize((hipStream_t)c->stream); }
+static void mtb_d2d(mt_ctx* c, void* d, const void* s, size_t n) { (void)hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, (hipStream_t)c->stream); (void)hipStreamSynchronize((hipStream_t)c->stream); }
 static void mtb_d2h(mt_ctx* c, void* d, const void* s, size_t n) { (void)hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, (hipStream_t)c->stream); (void)hipStreamSynchronize((hipStream_t)c->stream); }
 static int mtb_sync(mt_ctx* c) {
     hipError_t e = hipStreamSynchronize((hipStream_t)c->stream);

@@ -58,7 +58,7 @@ MT_HD void mt_pack_doc(Eng& e, uint8_t* dst) {
             MtRow r = e.R[s];
             if (l > 0) {
                 const int o = w + own(pre, k);
-                for (int q = 0; q < l; q++) text[o + q] = e.text[r.toff + q];
+                lane_copy16(text + o, e.text + r.toff, l);
                 r.toff = o; r.tcap = l;
             }
             rows[s] = r;

@@ -69,7 +69,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
     MtRng rng; rng.s = 0;
     const uint32_t nc = g ? (g->clients_per_run ? g->clients_per_run[run] : g->clients) : 0;
     if (g) {
-        rng.s = g->seed ^ (0x9E3779B97F4A7C15ULL * (unsigned long long)(doc + 1));
+        rng.s = g->seed ^ (0x9E3779B97F4A7C15ULL * (unsigned long long)(g->doc_id_base + doc + 1));
         for (int c = 0; c < 64; c++) lastRef[c] = 0;
     }
     // Replay prefetches op i+1's record while op i runs (generation writes the

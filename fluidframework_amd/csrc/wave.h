@@ -24,6 +24,20 @@
 
 #define MT_WAVE 64
 
+// One lane copies n UTF-16 units with 8 independent loads in flight per step
+// (a per-unit load->store chain would pay a full memory round trip per unit).
+MT_INLINE void lane_copy16(uint16_t* dst, const uint16_t* src, int n) {
+    int q = 0;
+    for (; q + 8 <= n; q += 8) {
+        uint16_t t[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) t[j] = src[q + j];
+#pragma unroll
+        for (int j = 0; j < 8; j++) dst[q + j] = t[j];
+    }
+    for (; q < n; q++) dst[q] = src[q];
+}
+
 #if defined(__HIP_DEVICE_COMPILE__)
 // ---------------------------------------------------------------- device ----
 template <class T> using LaneArr = T;

@@ -46,7 +46,10 @@ def _bind(lib, prefix: str):
     P, U32, I32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32
 
     def f(name, res, args):
-        fn = getattr(lib, prefix + name)
+        try:
+            fn = getattr(lib, prefix + name)
+        except AttributeError:      # an older build of the library (A/B runs): fails only if called
+            return None
         fn.restype, fn.argtypes = res, args
         return fn
 
@@ -82,6 +85,8 @@ def _bind(lib, prefix: str):
         generated_ops=f("generated_ops", ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64)]),
         generated_download=f("generated_download", ctypes.c_int, [P] + [P] * 12),
         generated_to_resident=f("generated_to_resident", ctypes.c_int, [P]),
+        generated_copy_dev=f("generated_copy_dev", ctypes.c_int, [P, U32, U32, P, P]),
+        upload_batch_dev=f("upload_batch_dev", ctypes.c_int, [P, U32, P, P, P, P, ctypes.c_uint64]),
     )
 
 
@@ -227,6 +232,18 @@ class Engine:
         offs[1:] = np.cumsum(self._gen_ops, dtype=np.uint64).astype(np.uint32)
         return OpBatch.from_arrays(np.arange(p.n_docs, dtype=np.uint32), offs, pay, **a)
 
+    def generated_copy_dev(self, first_run: int, n_runs: int, rec_ptr: int, payload_ptr: int):
+        """mt_generated_copy_dev: op records / payload of generated runs into caller
+        buffers (device pointers, e.g. torch tensors' data_ptr())."""
+        self._check(self.fn["generated_copy_dev"](self.h, first_run, n_runs, rec_ptr, payload_ptr),
+                    "mt_generated_copy_dev")
+
+    def upload_batch_dev(self, doc_ids, op_offsets, rec_ptr: int, payload_ptr: int, payload_units: int):
+        """mt_upload_batch_dev: a batch already in device memory becomes resident."""
+        d, o = _u32(doc_ids), _u32(op_offsets)
+        self._check(self.fn["upload_batch_dev"](self.h, len(d), d.ctypes.data, o.ctypes.data, rec_ptr, payload_ptr,
+                                                int(payload_units)), "mt_upload_batch_dev")
+
     def generated_to_resident(self):
         self._check(self.fn["generated_to_resident"](self.h), "mt_generated_to_resident")
 
@@ -255,9 +272,9 @@ class Engine:
 
     def pools(self, docs) -> np.ndarray:
         """Per-document pool occupancy (mt_doc_pools): columns rowTop, blkTop, heapN,
-        winN, textTop, psetTop, height, rfN."""
+        winN, textTop, psetTop, height, rfN, heapHW, winHW."""
         d = _u32(docs)
-        out = np.zeros((len(d), 8), np.int32)
+        out = np.zeros((len(d), 10), np.int32)
         self._check(self.fn["doc_pools"](self.h, len(d), d.ctypes.data, out.ctypes.data), "mt_doc_pools")
         return out
 

@@ -1,0 +1,263 @@
+"""Document sharding across GPUs (BASELINE config 5).
+
+Documents are fully independent (one `Client` per DDS, packages/dds/sequence/
+src/sequence.ts:131-134), so the engine shards them across ranks with no
+per-op communication.  The two exchanges are the ones the north star names,
+both over torch.distributed (backend "nccl" = RCCL over xGMI on ROCm; "gloo"
+in the CPU tests):
+
+1. a one-shot size-balanced redistribution: rank 0 holds every document's
+   sequenced op stream (the ingest point); every rank computes the same LPT
+   (longest-processing-time) plan from the broadcast op counts, and rank 0
+   sends each rank its documents' packed 32-byte op records and UTF-16
+   payloads in one all_to_all_single each (per-link bound on xGMI: each
+   destination's share travels on its own link);
+2. the gather of per-document SnapshotV1 digests to rank 0.
+
+Pool capacities are exact: generation runs the same deterministic engine, so
+its high-water marks (mt_doc_pools) are what a replay of the same stream needs.
+"""
+from __future__ import annotations
+
+import heapq
+import time
+
+import numpy as np
+
+REC_BYTES = 32           # mt_op_rec
+
+
+def zipf_op_counts(n_docs: int, seed: int, s: float = 1.5, lo: int = 8, hi: int = 65536) -> np.ndarray:
+    """Messages per document ~ Zipf(s) truncated to [lo, hi] (SURVEY §8(d) config 5;
+    mean ≈ 700 for the defaults), deterministic in seed."""
+    k = np.arange(lo, hi + 1, dtype=np.float64)
+    cdf = np.cumsum(k ** -s)
+    cdf /= cdf[-1]
+    u = np.random.Generator(np.random.PCG64(seed)).random(n_docs)
+    return (lo + np.searchsorted(cdf, u, side="left")).astype(np.uint32)
+
+
+def clients_per_doc(n_docs: int, seed: int, lo: int = 2, hi: int = 16) -> np.ndarray:
+    """Authoring clients per document ~ U[lo, hi] (config 5)."""
+    return np.random.Generator(np.random.PCG64(seed ^ 0xC11E)).integers(lo, hi + 1, n_docs).astype(np.uint32)
+
+
+def lpt_assign(costs: np.ndarray, world: int) -> np.ndarray:
+    """LPT bins: documents by decreasing cost (ties by id) each go to the least
+    loaded rank (ties by rank).  Deterministic, so every rank computes the same plan."""
+    order = np.lexsort((np.arange(len(costs)), -np.asarray(costs, np.int64)))
+    heap = [(0, r) for r in range(world)]
+    owner = np.empty(len(costs), np.int32)
+    for d in order:
+        load, r = heapq.heappop(heap)
+        owner[d] = r
+        heapq.heappush(heap, (load + int(costs[d]), r))
+    return owner
+
+
+def generation_caps(ops: np.ndarray, ins_len: int) -> dict:
+    """Generous per-document pools for the generating context."""
+    o = np.asarray(ops, np.int64)
+    return dict(rows_per_doc=3 * o + 64, blocks_per_doc=o + 64, heap_per_doc=2 * o + 64,
+                window_per_doc=np.minimum(o + 64, 1024), text_per_doc=ins_len * o + 4096,
+                propsets_per_doc=np.full(len(o), 64))
+
+
+def replay_caps(pools: np.ndarray, gen_caps: dict, idx) -> np.ndarray:
+    """[n, 6] caps (rows, blocks, heap, window, text, psets) from the generation's
+    high-water marks (mt_doc_pools columns 0, 1, 8, 9, 5); text keeps the generation cap."""
+    p = np.asarray(pools, np.int64)
+    cap = np.stack([np.maximum(p[:, 0], 1), np.maximum(p[:, 1], 1), np.maximum(p[:, 8], 1), np.maximum(p[:, 9], 1),
+                    np.asarray(gen_caps["text_per_doc"])[idx], np.maximum(p[:, 5], 1)], axis=1)
+    return cap.astype(np.int32)
+
+
+def rank_order(owner: np.ndarray, ops: np.ndarray) -> np.ndarray:
+    """Documents grouped by owning rank; within a rank, largest first (so the
+    longest streams start first and set less of the tail), then by id."""
+    return np.lexsort((np.arange(len(ops)), -np.asarray(ops, np.int64), np.asarray(owner)))
+
+
+class SoloDist:
+    """The torch.distributed subset build_sharded uses, for a single process."""
+
+    def get_world_size(self):
+        return 1
+
+    def get_rank(self):
+        return 0
+
+    def broadcast(self, t, src):
+        pass
+
+    def barrier(self):
+        pass
+
+    def all_to_all_single(self, out, inp, out_split, in_split):
+        out.copy_(inp)
+
+    def all_gather(self, outs, t):
+        outs[0].copy_(t)
+
+
+CAP_KEYS = ("rows_per_doc", "blocks_per_doc", "heap_per_doc", "window_per_doc", "text_per_doc", "propsets_per_doc")
+
+
+class ShardedReplay:
+    """One rank's share of a sharded replay: an Engine holding its documents with
+    their op streams resident, plus the plan (owner of every global document)."""
+
+    def __init__(self, engine, owned: np.ndarray, all_ops: np.ndarray, owner: np.ndarray, timings: dict):
+        self.engine, self.owned, self.all_ops, self.owner, self.timings = engine, owned, all_ops, owner, timings
+        self.ops = all_ops[owned]          # engine document slot i holds global document owned[i]
+
+    @property
+    def n_docs(self) -> int:
+        return len(self.owned)
+
+    def replay(self):
+        self.engine.open_docs(0, self.n_docs)
+        self.engine.replay_resident()
+
+    def gather_digests(self, dist, device, threads: int = 8):
+        """SnapshotV1 digests of every document at its current window, gathered to
+        rank 0 in global document order (None on other ranks)."""
+        import torch
+        t0 = time.perf_counter()
+        n = self.n_docs
+        neg = np.full(n, -1, np.int32)
+        dig = self.engine.snapshot_digests(range(n), neg, neg, threads=threads) if n else np.zeros(0, np.uint64)
+        world, rank = dist.get_world_size(), dist.get_rank()
+        counts = np.bincount(self.owner, minlength=world)
+        mx = int(counts.max()) if len(counts) else 0
+        buf = torch.zeros(mx, dtype=torch.int64, device=device)
+        if n:
+            buf[:n] = torch.from_numpy(dig.view(np.int64)).to(device)
+        out = [torch.zeros(mx, dtype=torch.int64, device=device) for _ in range(world)]
+        dist.all_gather(out, buf)
+        self.timings["digest_ms"] = (time.perf_counter() - t0) * 1e3
+        if rank != 0:
+            return None
+        res = np.zeros(len(self.owner), np.uint64)
+        order = rank_order(self.owner, self.all_ops)
+        own_sorted = self.owner[order]
+        for r in range(world):
+            docs_r = order[own_sorted == r]
+            res[docs_r] = out[r][:len(docs_r)].cpu().numpy().view(np.uint64)
+        return res
+
+
+def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_params_cls, gen_kw: dict,
+                  props=None, names=None, chunk_docs: int = 131072, counts=None, clients=None) -> ShardedReplay:
+    """Rank 0 generates every document's stream (the ingest point), every rank
+    gets its LPT share by RCCL/gloo collectives, and each rank's engine ends up
+    holding its documents with their streams resident.
+
+    engine_factory(n_docs, per_doc_caps: dict) -> Engine;  gen_kw: MtGenParams
+    fields other than seed/n_docs/ops_per_doc/clients."""
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    L = int(gen_kw["ins_len_max"])
+    tm = {}
+    # -- op counts / clients: known at the ingest point, broadcast to all ranks
+    t0 = time.perf_counter()
+    cnt_t = torch.zeros(docs_total, dtype=torch.int32, device=device)
+    cli_t = torch.zeros(docs_total, dtype=torch.int32, device=device)
+    if rank == 0:
+        c0 = zipf_op_counts(docs_total, seed) if counts is None else np.asarray(counts, np.uint32)
+        k0 = clients_per_doc(docs_total, seed) if clients is None else np.asarray(clients, np.uint32)
+        cnt_t.copy_(torch.from_numpy(c0.astype(np.int32)))
+        cli_t.copy_(torch.from_numpy(k0.astype(np.int32)))
+    dist.broadcast(cnt_t, 0)
+    dist.broadcast(cli_t, 0)
+    ops = cnt_t.cpu().numpy().astype(np.uint32)
+    cli = cli_t.cpu().numpy().astype(np.uint32)
+    owner = lpt_assign(ops, world)
+    op_off = np.zeros(docs_total + 1, np.int64)
+    op_off[1:] = np.cumsum(ops, dtype=np.int64)
+    n_total = int(op_off[-1])
+    tm["plan_ms"] = (time.perf_counter() - t0) * 1e3
+
+    # -- rank 0: generate all streams in chunks (untimed ingest), staging in device tensors
+    caps_t = torch.zeros((docs_total, 6), dtype=torch.int32, device=device)
+    if rank == 0:
+        t0 = time.perf_counter()
+        rec_all = torch.empty((n_total, REC_BYTES), dtype=torch.uint8, device=device)
+        pay_all = torch.empty((n_total, 2 * L), dtype=torch.uint8, device=device)     # UTF-16 units as bytes
+        gcaps = generation_caps(ops, L)
+        for a in range(0, docs_total, chunk_docs):
+            b = min(docs_total, a + chunk_docs)
+            idx = np.arange(a, b)
+            eng = engine_factory(b - a, {k: np.asarray(v)[idx] for k, v in gcaps.items()})
+            if props is not None:
+                eng.upload_props(props)
+            if names is not None:
+                eng.upload_names(names)
+            p = gen_params_cls(**{**gen_kw, "seed": seed, "n_docs": b - a, "ops_per_doc": 0, "clients": 2,
+                                  "doc_id_base": a})
+            eng.generate(p, ops_per_doc=ops[idx], clients_per_doc=cli[idx])
+            eng.sync()
+            st = eng.status(range(b - a))
+            if st.any():
+                raise RuntimeError(f"generation failed for docs {a}..{b}: status {np.unique(st)}")
+            caps_t[a:b] = torch.from_numpy(replay_caps(eng.pools(range(b - a)), gcaps, idx)).to(device)
+            o0, o1 = int(op_off[a]), int(op_off[b])
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            eng.generated_copy_dev(0, b - a, rec_all[o0:o1].data_ptr(), pay_all[o0:o1].data_ptr())
+            eng.close()
+        tm["generate_s"] = time.perf_counter() - t0
+    dist.broadcast(caps_t, 0)
+    caps = caps_t.cpu().numpy()
+
+    # -- redistribution: rank 0 -> every rank, one all_to_all_single per array
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    dist.barrier()
+    t0 = time.perf_counter()
+    order = rank_order(owner, ops)
+    owned = order[owner[order] == rank]
+    per_rank_ops = np.array([int(ops[owner == r].sum()) for r in range(world)], np.int64)
+    my_ops = int(per_rank_ops[rank])
+    rec_recv = torch.empty((my_ops, REC_BYTES), dtype=torch.uint8, device=device)
+    pay_recv = torch.empty((my_ops, 2 * L), dtype=torch.uint8, device=device)
+    if rank == 0:
+        starts = op_off[order]
+        lens = ops[order].astype(np.int64)
+        op_idx = np.repeat(starts - np.concatenate(([0], np.cumsum(lens)[:-1])), lens) + np.arange(int(lens.sum()))
+        sel = torch.from_numpy(op_idx).to(device)
+        rec_send = rec_all.index_select(0, sel)
+        pay_send = pay_all.index_select(0, sel)
+        del rec_all, pay_all, sel
+        in_split = per_rank_ops.tolist()
+    else:
+        rec_send = torch.empty((0, REC_BYTES), dtype=torch.uint8, device=device)
+        pay_send = torch.empty((0, 2 * L), dtype=torch.uint8, device=device)
+        in_split = [0] * world
+    out_split = [my_ops if r == 0 else 0 for r in range(world)]
+    dist.all_to_all_single(rec_recv, rec_send, out_split, in_split)
+    dist.all_to_all_single(pay_recv, pay_send, out_split, in_split)
+    del rec_send, pay_send
+    # payload offsets follow the new op order (fixed stride L per op record)
+    if my_ops:
+        rec_recv.view(torch.int32)[:, 6] = torch.arange(my_ops, dtype=torch.int32, device=device) * L
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    tm["rebalance_ms"] = (time.perf_counter() - t0) * 1e3
+    tm["rebalance_bytes"] = int(per_rank_ops.sum()) * (REC_BYTES + 2 * L)
+
+    # -- this rank's engine, sized exactly, with the received stream resident
+    mine = caps[owned]
+    eng = engine_factory(len(owned), {k: mine[:, i] for i, k in enumerate(CAP_KEYS)})
+    if props is not None:
+        eng.upload_props(props)
+    if names is not None:
+        eng.upload_names(names)
+    loc_off = np.zeros(len(owned) + 1, np.int64)
+    loc_off[1:] = np.cumsum(ops[owned], dtype=np.int64)
+    if my_ops >= 2 ** 32:
+        raise RuntimeError("more than 2^32 ops on one rank")
+    eng.upload_batch_dev(np.arange(len(owned)), loc_off.astype(np.uint32),
+                         rec_recv.data_ptr() if my_ops else 0, pay_recv.data_ptr() if my_ops else 0, my_ops * L)
+    del rec_recv, pay_recv
+    return ShardedReplay(eng, owned, ops, owner, tm)

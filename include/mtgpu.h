@@ -101,6 +101,18 @@ typedef struct mt_op_batch {
     uint64_t        payload_units;
 } mt_op_batch;
 
+/* The packed 32-byte op record the device replays (one per op member), for
+ * hosts that move op streams between devices without a host round trip
+ * (mt_generated_copy_dev / mt_upload_batch_dev). */
+typedef struct mt_op_rec {
+    uint8_t  type, flags;
+    uint16_t client;
+    int32_t  seq, ref_seq, msn, pos1, pos2;
+    uint32_t payload_off;
+    uint16_t payload_len;
+    int16_t  prop_id;
+} mt_op_rec;
+
 /*
  * Host-interned property sets (the `props` of an annotate op or of an inserted
  * segment spec), already in JS Object.keys() order.  Values are interned JS
@@ -187,10 +199,12 @@ int  mt_sync(mt_ctx* ctx);
 int  mt_doc_status(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, uint32_t* out_status);
 int  mt_doc_counters_get(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, mt_doc_counters* out);
 
-/* Pool occupancy per document, 8 int32 each: rows high-water (rowTop), blocks
+/* Pool occupancy per document, 10 int32 each: rows high-water (rowTop), blocks
  * high-water, zamboni heap entries, window rows, text arena units in use,
- * property sets, tree height, recycled rows held.  Used by hosts to size
- * mt_limits for the next batch. */
+ * property sets, tree height, recycled rows held, heap high-water, window
+ * high-water.  Allocation is deterministic, so replaying the same stream needs
+ * exactly these row/block/heap/window capacities (hosts size mt_create_docs
+ * from a generation or earlier replay). */
 int  mt_doc_pools(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, int32_t* out);
 
 /* Perspective length (refSeq, client) of each document (mergeTree.ts:1569). */
@@ -250,6 +264,7 @@ typedef struct mt_gen_params {
     uint32_t rem_len_max;        /* remove/annotate length U[1, rem_len_max]      */
     uint32_t n_ann_sets;         /* annotate prop sets drawn from table [0, n)    */
     uint32_t pct_rewrite;        /* annotate rewrite percentage                   */
+    uint32_t doc_id_base;        /* stream of run i is seeded as document doc_id_base + i */
 } mt_gen_params;
 int  mt_generate(mt_ctx* ctx, const mt_gen_params* params);
 /* As mt_generate with per-document message counts and authoring-client counts
@@ -266,6 +281,17 @@ int  mt_generated_download(mt_ctx* ctx, uint8_t* type, uint8_t* flags, uint16_t*
                            int32_t* seq, int32_t* ref_seq, int32_t* msn, int32_t* pos1,
                            int32_t* pos2, uint32_t* payload_off, uint32_t* payload_len,
                            int32_t* prop_id, uint16_t* payload);
+/* Copy the op records of generated runs [first_run, first_run + n_runs) into a
+ * caller-owned device buffer (records in run order), and their payloads (op i of
+ * the copy at payload_dev + i * ins_len_max; payload_off fields are left as
+ * generated).  Device pointers of this context's GPU. */
+int  mt_generated_copy_dev(mt_ctx* ctx, uint32_t first_run, uint32_t n_runs, mt_op_rec* rec_dev,
+                           uint16_t* payload_dev);
+/* Make a device-resident batch the resident batch (as mt_upload_batch, without
+ * the host copy): doc_ids/op_offsets are host arrays, records and payload are
+ * device buffers that the engine copies. */
+int  mt_upload_batch_dev(mt_ctx* ctx, uint32_t n_runs, const uint32_t* doc_ids, const uint32_t* op_offsets,
+                         const mt_op_rec* rec_dev, const uint16_t* payload_dev, uint64_t payload_units);
 /* Make the generated stream the resident batch (docs 0..n_docs-1). */
 int  mt_generated_to_resident(mt_ctx* ctx);
 

@@ -17,6 +17,7 @@ static void mtb_free(void* p) { free(p); }
 static void mtb_memset(void* p, int v, size_t n) { memset(p, v, n); }
 static void mtb_h2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static void mtb_d2h(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
+static void mtb_d2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static int mtb_sync(mt_ctx*) { return MT_OK; }
 // Same two launches as the device (mt_engine.hip): LDS-resident pass, then the
 // HBM pass resuming at each run's cursor.
