@@ -40,6 +40,11 @@ CONFIGS = {
                     desc="16384 docs x 8 clients x 4k msgs, lag U[0,4], 30/30/40 ins/rem/annotate, zamboni-heavy"),
     "config1": dict(docs=1, ops=10000, clients=2, lag=8, ins=55, rem=45, ins_len=8, rem_len=16, ann_sets=1, rewrite=0,
                     desc="1 doc x 2 clients x 10k msgs (reference plumbing case)"),
+    # 256 long docs pre-built (untimed) by 200k 5-char appends with alternating segment props
+    # (200k segments, 1M chars), then 50k measured ops with lag U[0,1024] (window ~1k)
+    "config4": dict(docs=256, ops=50000, clients=8, lag=1024, ins=60, rem=40, ins_len=8, rem_len=8, ann_sets=2,
+                    rewrite=0, prebuild=200000,
+                    desc="256 long docs (pre-built to 200k segments / 1M chars) x 50k msgs, 8 clients, lag U[0,1024]"),
     # docs = per GPU (weak scaling; 8 GPUs = 1,048,576 docs); ops ~ Zipf(1.5) on [8, 65536], clients U[2,16]
     "config5": dict(docs=131072, ops=0, clients=0, lag=32, ins=60, rem=40, ins_len=8, rem_len=8, ann_sets=1, rewrite=0,
                     desc="Zipf(1.5)-sized docs (8..65536 msgs, clients U[2,16]), 131072 docs per GPU, rank-0 ingest, "
@@ -121,6 +126,144 @@ def cpu_baseline(eng, c, params_cls, seed, target_s, threads, ops_fn=None):
     return {"value": n / t, "unit": "ops/s", "cores": threads, "kind": "port",
             "sample": f"{docs} docs ({n} msgs) of the same workload, oracle (C++ restatement of "
                       f"MT/mergeTree.ts + partialLengths.ts) on {threads} host threads, {t:.1f} s"}
+
+
+def run_config4(args, c, world, rank, local):
+    """Config 4: long documents.  Untimed: pre-build every document by
+    c['prebuild'] appends (5 chars, segment props alternating between two sets,
+    so nothing coalesces), checkpoint that state, generate the measured stream
+    on top of it.  A step = restore the pre-built documents (device copy) +
+    replay the measured stream."""
+    from fluidframework_amd.batch import MtGenParams
+    from fluidframework_amd.engine import Engine
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo")  # rank coordination only: replicas, no data-path collective
+        dist = (torch, tdist)
+    n, pre, ops = c["docs"], c["prebuild"], c["ops"]
+    rows = pre + 3 * ops + 64
+    eng = Engine(n, device=local, rows_per_doc=rows, blocks_per_doc=rows // 2 + 64, heap_per_doc=rows,
+                 window_per_doc=16384, text_per_doc=5 * pre + c["ins_len"] * ops + 4096,
+                 propsets_per_doc=pre + ops + 64)
+    eng.set_residency(args.residency == "lds")
+    eng.upload_props(ann_props())
+    eng.upload_names(['"c%d"' % i for i in range(64)])
+    seed = args.seed ^ (rank * 0x9E3779B1)
+    t0 = time.time()
+    pa = MtGenParams(seed, n, pre, 1, 0, 100, 0, 5, 1, 1, 0)
+    pa.ins_len_min, pa.seg_prop_sets, pa.ins_at_end = 5, 2, 1
+    eng.generate(pa)
+    eng.sync()
+    if eng.status(range(n)).any():
+        raise SystemExit(f"prebuild failed: {np.unique(eng.status(range(n)))}")
+    cnt_a = eng.counters(range(n))
+    eng.checkpoint()
+    pb = MtGenParams(seed ^ 0xB, n, ops, c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"], c["rem_len"],
+                     c["ann_sets"], c["rewrite"])
+    pb.continue_docs = 1
+    eng.generate(pb)
+    eng.sync()
+    if eng.status(range(n)).any():
+        raise SystemExit(f"stream generation failed: {np.unique(eng.status(range(n)))}")
+    cnt_b = eng.counters(range(n))
+    pools = eng.pools(range(n))
+    gen_s = time.time() - t0
+    diff = {k: cnt_b[k] - cnt_a[k] for k in cnt_b}
+    msgs = int(diff["msgs"].sum())
+    bytes_per_launch = algorithmic_bytes(diff)
+    eng.generated_to_resident()
+
+    def step():
+        eng.restore()
+        eng.replay_resident()
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    if dist:
+        dist[1].barrier()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        step()
+        eng.sync()
+        kms.append(eng.last_replay_ms())
+    eng.sync()
+    if dist:
+        dist[1].barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        torch, tdist = dist
+        t = torch.tensor([dt], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    st = eng.status(range(n))
+    cnt = eng.counters(range(n))
+    ok = (not st.any()) and int((cnt["msgs"] - cnt_a["msgs"]).sum()) == msgs
+    neg = np.full(n, -1, np.int32)
+    t1 = time.perf_counter()
+    digs = eng.snapshot_digests(range(n), neg, neg, threads=min(16, os.cpu_count() or 1))
+    snap_ms = (time.perf_counter() - t1) * 1e3
+    if rank != 0:
+        return
+    kern_s = float(np.mean(kms)) / 1e3
+    achieved = bytes_per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
+    out = {
+        "metric": "sequenced merge-tree ops applied/sec (whole node) + achieved HBM GB/s",
+        "value": msgs * world * args.steps / dt, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic (device-generated: pre-built documents + sequenced op stream, SURVEY.md §8(d) config-4 rules)",
+        "config": {"workload": f"config4: {c['desc']}", "docs_per_gpu": n, "msgs_per_doc": ops, "prebuild_appends": pre,
+                   "clients": c["clients"], "lag_max": c["lag"], "tree_height_max": int(pools[:, 6].max()),
+                   "rows_per_doc_max": int(pools[:, 0].max()), "window_max": int(pools[:, 9].max()),
+                   "parallelism": f"doc-sharded x{world}", "residency": args.residency,
+                   "step": "mt_restore (device copy of the pre-built documents) + replay"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "mt_replay_kernel",
+                     "kernel_ms": kern_s * 1e3, "bytes_per_launch": bytes_per_launch},
+        "parity": "status words clean" if ok else "STATUS ERROR",
+        "snapshot": {"docs": n, "ms": snap_ms, "digest_xor": f"{int(np.bitwise_xor.reduce(digs)):016x}"},
+        "gen_seconds": gen_s,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_config4(eng, c, pa, pb, min(16, os.cpu_count() or 1))
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline_config4(eng, c, pa, pb, threads):
+    """Oracle ('port') on one pre-built document per host thread: time(prebuild +
+    stream) - time(prebuild), i.e. the measured stream alone, in ops/s."""
+    import ctypes
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fluidframework_amd.batch import MtGenParams
+    from oracle_lib import lib as oracle
+    L = oracle()
+    props = eng.props
+    k = threads
+    sa = MtGenParams(*(getattr(pa, f) for f, _ in MtGenParams._fields_))
+    sa.n_docs = k
+    sb = MtGenParams(*(getattr(pb, f) for f, _ in MtGenParams._fields_))
+    sb.n_docs = k
+    eng.generate(sa)
+    eng.sync()
+    a = eng.generated_download()
+    eng.generate(sb)
+    eng.sync()
+    b = eng.generated_download()
+    from fluidframework_amd.batch import concat_runs
+    both = concat_runs(a, b)
+    st = np.zeros(k, np.uint32)
+    t_a = L.ora_replay_batch(ctypes.byref(a.to_c()), ctypes.byref(props.to_c()), threads, None, st.ctypes.data)
+    t_ab = L.ora_replay_batch(ctypes.byref(both.to_c()), ctypes.byref(props.to_c()), threads, None, st.ctypes.data)
+    n_b = int(b.op_offsets[-1])
+    dt = max(t_ab - t_a, 1e-6)
+    return {"value": n_b / dt, "unit": "ops/s", "cores": threads, "kind": "port",
+            "sample": f"{k} pre-built docs ({int(a.op_offsets[-1])} prebuild + {n_b} measured msgs), oracle (C++ "
+                      f"restatement of MT/mergeTree.ts + partialLengths.ts) on {threads} host threads; "
+                      f"measured-stream time = {t_ab:.1f} s - {t_a:.1f} s"}
 
 
 def run_config5(args, c, world, rank, local):
@@ -232,6 +375,7 @@ def main():
     ap.add_argument("--docs", type=int, default=0, help="override documents per GPU")
     ap.add_argument("--ops", type=int, default=0, help="override messages per document")
     ap.add_argument("--seed", type=int, default=20241015)
+    ap.add_argument("--prebuild", type=int, default=0, help="config4: override pre-build appends per document")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--residency", default="hbm", choices=["lds", "hbm"],
@@ -242,6 +386,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config == "config4":
+        c = dict(CONFIGS["config4"])
+        if args.docs:
+            c["docs"] = args.docs
+        if args.ops:
+            c["ops"] = args.ops
+        if args.prebuild:
+            c["prebuild"] = args.prebuild
+        return run_config4(args, c, world, rank, local)
     if args.config == "config5":
         c = dict(CONFIGS["config5"])
         if args.docs:

@@ -56,7 +56,8 @@ class MtPropTable(ctypes.Structure):
 class MtGenParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64 if n == "seed" else ctypes.c_uint32) for n in (
         "seed", "n_docs", "ops_per_doc", "clients", "lag_max", "pct_insert", "pct_remove",
-        "ins_len_max", "rem_len_max", "n_ann_sets", "pct_rewrite", "doc_id_base")]
+        "ins_len_max", "rem_len_max", "n_ann_sets", "pct_rewrite", "doc_id_base", "ins_len_min", "seg_prop_sets",
+        "ins_at_end", "continue_docs")]
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -283,3 +284,22 @@ class BatchBuilder:
         arrays = {n: np.asarray(self.cols[n], dtype=t) for n, t in _FIELDS}
         return OpBatch(np.asarray(self.doc_ids, np.uint32), np.asarray(self.offsets, np.uint32), arrays,
                        np.asarray(self.payload or [0], np.uint16))
+
+
+def concat_runs(a: OpBatch, b: OpBatch) -> OpBatch:
+    """Per document: a's ops then b's ops (one run per document; payloads re-packed)."""
+    sl = []
+    for d in range(len(a.doc_ids)):
+        sl.append((a, int(a.op_offsets[d]), int(a.op_offsets[d + 1]), 0))
+        sl.append((b, int(b.op_offsets[d]), int(b.op_offsets[d + 1]), len(a.payload)))
+    cols = {k: np.concatenate([src.arrays[k][lo:hi] for src, lo, hi, _ in sl]) for k, _ in _FIELDS}
+    po = np.concatenate([src.arrays["payload_off"][lo:hi].astype(np.int64) + base for src, lo, hi, base in sl])
+    pl = cols["payload_len"].astype(np.int64)
+    out_off = np.concatenate(([0], np.cumsum(pl)[:-1])) if len(pl) else np.zeros(0, np.int64)
+    src_pay = np.concatenate([a.payload, b.payload])
+    idx = np.repeat(po - out_off, pl) + np.arange(int(pl.sum()))
+    cols["payload_off"] = out_off.astype(np.uint32)
+    offs = np.zeros(len(a.doc_ids) + 1, np.uint32)
+    offs[1:] = np.cumsum((a.op_offsets[1:] - a.op_offsets[:-1]) + (b.op_offsets[1:] - b.op_offsets[:-1]))
+    payload = src_pay[idx] if len(idx) else np.zeros(1, np.uint16)
+    return OpBatch.from_arrays(a.doc_ids, offs, payload, **cols)

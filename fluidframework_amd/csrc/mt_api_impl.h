@@ -87,6 +87,7 @@ static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bo
     S.layout = (const MtDocLayout*)p;
     mtb_h2d(c, p, c->layout_h.data(), sizeof(MtDocLayout) * D);
     mtb_memset(S.hdr, 0, sizeof(MtDocHdr) * D);
+    c->tot = tot;
     c->pool_bytes = sizeof(MtRow) * tot.row + sizeof(MtBlk) * tot.blk + sizeof(MtHeapE) * tot.heap + 12ull * tot.win +
                     4ull * tot.anc + 2ull * tot.text + sizeof(MtPSet) * tot.pset + (sizeof(MtDocHdr) + 4ull * MT_RFL + sizeof(MtDocLayout)) * D;
     return MT_OK;
@@ -100,6 +101,36 @@ int MT_FN(create_docs)(int device, uint32_t n_docs, const mt_limits* per_doc, mt
     if (!per_doc || !out || n_docs == 0) return MT_E_INVALID;
     return mt_create_impl(device, n_docs, per_doc, false, out);
 }
+// Device-side checkpoint of every document's state (rows, blocks, heap, window,
+// text, property sets, headers, recycled-row stacks): the engine's equivalent of
+// a summary to resume from (SURVEY.md §5 checkpoint/resume), used by benchmarks
+// that replay the same stream on the same starting state.
+struct MtCkPart { void** ck; void* live; size_t bytes; };
+static std::vector<MtCkPart> mt_ck_parts(mt_ctx* c) {
+    const MtState& S = c->S; const MtDocLayout& t = c->tot; const size_t D = S.maxDocs;
+    return {{&c->ck_rows, S.rows, sizeof(MtRow) * t.row}, {&c->ck_blk, S.blk, sizeof(MtBlk) * t.blk},
+            {&c->ck_heap, S.heap, sizeof(MtHeapE) * t.heap}, {&c->ck_win, S.win, 4ull * t.win},
+            {&c->ck_text, S.text, 2ull * t.text}, {&c->ck_pset, S.pset, sizeof(MtPSet) * t.pset},
+            {&c->ck_hdr, S.hdr, sizeof(MtDocHdr) * D}, {&c->ck_hold, S.hold, 4ull * MT_RFL * D}};
+}
+int MT_FN(checkpoint)(mt_ctx* c) {
+    if (!c) return MT_E_INVALID;
+    int rc = mtb_sync(c);
+    if (rc) return rc;
+    for (auto& p : mt_ck_parts(c)) {
+        if (!*p.ck && mtb_malloc(p.ck, p.bytes ? p.bytes : 16) != 0) { c->err = "checkpoint allocation failed"; return MT_E_OOM; }
+        if (p.bytes) mtb_d2d(c, *p.ck, p.live, p.bytes);
+    }
+    c->ck_valid = true;
+    return MT_OK;
+}
+int MT_FN(restore)(mt_ctx* c) {
+    if (!c || !c->ck_valid) return MT_E_INVALID;
+    int rc = mtb_sync(c);
+    if (rc) return rc;
+    for (auto& p : mt_ck_parts(c)) if (p.bytes) mtb_d2d(c, p.live, *p.ck, p.bytes);
+    return MT_OK;
+}
 int MT_FN(pool_bytes)(mt_ctx* c, uint64_t* bytes) {
     if (!c || !bytes) return MT_E_INVALID;
     *bytes = c->pool_bytes;
@@ -109,7 +140,8 @@ int MT_FN(pool_bytes)(mt_ctx* c, uint64_t* bytes) {
 void MT_FN(destroy)(mt_ctx* c) {
     if (!c) return;
     MtState& S = c->S;
-    void* ps[] = {S.rows, S.blk, S.heap, S.win, S.uid, S.udelta, S.uanc, S.text, S.pset, S.hdr, S.hold, (void*)S.layout};
+    void* ps[] = {S.rows, S.blk, S.heap, S.win, S.uid, S.udelta, S.uanc, S.text, S.pset, S.hdr, S.hold, (void*)S.layout,
+                  c->ck_rows, c->ck_blk, c->ck_heap, c->ck_win, c->ck_text, c->ck_pset, c->ck_hdr, c->ck_hold};
     for (void* p : ps) if (p) mtb_free(p);
     mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_pset_off,
                             &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3};
@@ -478,13 +510,18 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs;
     c->n_runs = P->n_docs;
     c->gen_off.assign(off.begin(), off.end());
-    rc = MT_FN(docs_open)(c, 0, P->n_docs);
-    if (rc) return rc;
+    if (!P->continue_docs) {
+        rc = MT_FN(docs_open)(c, 0, P->n_docs);
+        if (rc) return rc;
+    }
+    if (P->ins_len_min > P->ins_len_max) { c->err = "ins_len_min > ins_len_max"; return MT_E_INVALID; }
+    if (P->seg_prop_sets > c->S.p_nsets) { c->err = "segment prop sets not uploaded"; return MT_E_INVALID; }
     MtGen g{};
     g.seed = P->seed; g.ops = P->ops_per_doc; g.clients = P->clients; g.lag_max = P->lag_max;
     g.pct_insert = P->pct_insert; g.pct_remove = P->pct_remove; g.ins_len_max = P->ins_len_max;
     g.rem_len_max = P->rem_len_max; g.n_ann_sets = P->n_ann_sets; g.pct_rewrite = P->pct_rewrite; g.enabled = 1;
     g.clients_per_run = (const uint32_t*)c->b_gencl.p; g.total_ops = N; g.doc_id_base = P->doc_id_base;
+    g.ins_len_min = P->ins_len_min; g.seg_prop_sets = P->seg_prop_sets; g.ins_at_end = P->ins_at_end;
     c->gen = g; c->gen_docs = P->n_docs;
     return mtb_launch_replay(c, g, P->n_docs);
 }

@@ -173,6 +173,7 @@ struct MtGen {                                // device stream generator paramet
     int enabled;
     const uint32_t* clients_per_run;          // per-document authoring clients (mt_generate_docs), or null
     uint32_t doc_id_base;                     // run i is seeded as document doc_id_base + i
+    uint32_t ins_len_min, seg_prop_sets, ins_at_end;
     uint64_t total_ops;                       // ops over all runs (payload stride base)
 };
 

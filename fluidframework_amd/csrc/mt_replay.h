@@ -19,7 +19,7 @@ struct MtRng {                                     // splitmix64
 // engine acts as sequencer + observer, so positions are valid under the
 // author's perspective), writing the op record into the batch arrays.
 template <class Eng>
-MT_HD void mt_gen_op(Eng& e, const MtOps& ops, uint32_t i, uint32_t nc,
+MT_HD void mt_gen_op(Eng& e, const MtOps& ops, uint32_t i, uint32_t k, uint32_t nc,
                             const MtGen& g, MtRng& rng, int* lastRef) {
     const uint32_t a = rng.u(nc);
     const uint32_t lag = rng.u(g.lag_max + 1);
@@ -36,8 +36,10 @@ MT_HD void mt_gen_op(Eng& e, const MtOps& ops, uint32_t i, uint32_t nc,
     const uint32_t poff = (uint32_t)((size_t)i * g.ins_len_max);      // fixed stride per op record
     MtOpRec& o = ops.rec[i];
     if (ty == MT_OP_INSERT) {
-        s1 = (int)rng.u((uint32_t)L + 1);
-        plen = 1 + rng.u(g.ins_len_max);
+        s1 = g.ins_at_end ? L : (int)rng.u((uint32_t)L + 1);
+        const uint32_t lo = g.ins_len_min > 1 ? g.ins_len_min : 1;
+        plen = lo + rng.u(g.ins_len_max - lo + 1);
+        if (g.seg_prop_sets) { pid = (int)(k % g.seg_prop_sets); fl |= MT_OPF_SEG_PROPS; }
         for (uint32_t q = 0; q < plen; q++) {
             const uint16_t ch = (uint16_t)('a' + rng.u(26));
             ops.payload[poff + q] = ch;
@@ -70,7 +72,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
     const uint32_t nc = g ? (g->clients_per_run ? g->clients_per_run[run] : g->clients) : 0;
     if (g) {
         rng.s = g->seed ^ (0x9E3779B97F4A7C15ULL * (unsigned long long)(g->doc_id_base + doc + 1));
-        for (int c = 0; c < 64; c++) lastRef[c] = 0;
+        for (int c = 0; c < 64; c++) lastRef[c] = e.minSeq;   // 0 for fresh documents; continue_docs keeps MSN monotone
     }
     // Replay prefetches op i+1's record while op i runs (generation writes the
     // record at the top of each iteration, so it loads in place).
@@ -79,11 +81,11 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
         if (Eng::kLds && !e.ldsHeadroom()) return i;
 #if defined(MT_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
         const unsigned long long tg = __builtin_amdgcn_s_memtime();
-        if (g) mt_gen_op(e, ops, i, nc, *g, rng, lastRef);
+        if (g) mt_gen_op(e, ops, i, i - o0, nc, *g, rng, lastRef);
         e.prof[MT_PH_GEN] += __builtin_amdgcn_s_memtime() - tg;
         const unsigned long long top = __builtin_amdgcn_s_memtime();
 #else
-        if (g) mt_gen_op(e, ops, i, nc, *g, rng, lastRef);
+        if (g) mt_gen_op(e, ops, i, i - o0, nc, *g, rng, lastRef);
 #endif
         // one 32-byte record: lanes 0..7 hold a dword each, then broadcast
         auto w = wn;

@@ -57,6 +57,8 @@ def _bind(lib, prefix: str):
         create=f("create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(MtLimits), ctypes.POINTER(P)]),
         create_docs=f("create_docs", ctypes.c_int, [ctypes.c_int, U32, P, ctypes.POINTER(P)]),
         pool_bytes=f("pool_bytes", ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64)]),
+        checkpoint=f("checkpoint", ctypes.c_int, [P]),
+        restore=f("restore", ctypes.c_int, [P]),
         destroy=f("destroy", None, [P]),
         last_error=f("last_error", ctypes.c_char_p, [P]),
         docs_open=f("docs_open", ctypes.c_int, [P, U32, U32]),
@@ -264,6 +266,14 @@ class Engine:
     def set_residency(self, use_lds: bool = True, rows: int = 0, blocks: int = 0, heap: int = 0):
         """mt_set_residency: LDS-resident replay on/off and (lowered) LDS pool caps."""
         self._check(self.fn["set_residency"](self.h, int(use_lds), rows, blocks, heap), "mt_set_residency")
+
+    def checkpoint(self):
+        """mt_checkpoint: device copy of every document's state."""
+        self._check(self.fn["checkpoint"](self.h), "mt_checkpoint")
+
+    def restore(self):
+        """mt_restore: documents back to the last checkpoint."""
+        self._check(self.fn["restore"](self.h), "mt_restore")
 
     def pool_bytes(self) -> int:
         v = ctypes.c_uint64()

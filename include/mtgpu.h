@@ -162,6 +162,10 @@ int  mt_create(int device, const mt_limits* limits, mt_ctx** out);
 int  mt_create_docs(int device, uint32_t n_docs, const mt_limits* per_doc, mt_ctx** out);
 /* HBM bytes held by the context's document pools. */
 int  mt_pool_bytes(mt_ctx* ctx, uint64_t* bytes);
+/* Device-side checkpoint of every document's state, and restore to it (the
+ * engine's resume point: replay a stream on the same starting documents). */
+int  mt_checkpoint(mt_ctx* ctx);
+int  mt_restore(mt_ctx* ctx);
 void mt_destroy(mt_ctx* ctx);
 const char* mt_last_error(mt_ctx* ctx);
 
@@ -265,6 +269,11 @@ typedef struct mt_gen_params {
     uint32_t n_ann_sets;         /* annotate prop sets drawn from table [0, n)    */
     uint32_t pct_rewrite;        /* annotate rewrite percentage                   */
     uint32_t doc_id_base;        /* stream of run i is seeded as document doc_id_base + i */
+    uint32_t ins_len_min;        /* insert length U[max(1, ins_len_min), ins_len_max] */
+    uint32_t seg_prop_sets;      /* > 0: insert k carries segment props set k % n   */
+    uint32_t ins_at_end;         /* 1: every insert appends at the author's length  */
+    uint32_t continue_docs;      /* 1: continue the documents' current state (no     */
+                                 /*    reopen; seqs continue from currentSeq)       */
 } mt_gen_params;
 int  mt_generate(mt_ctx* ctx, const mt_gen_params* params);
 /* As mt_generate with per-document message counts and authoring-client counts

@@ -1164,7 +1164,10 @@ uint32_t ora_generate_doc(const mt_gen_params* p, uint32_t doc, const mt_prop_ta
         if (L == 0) ty = MT_OP_INSERT;
         int s1, s2 = 0; uint32_t plen = 0; int pid = -1; uint8_t fl = MT_OPF_END_OF_MSG;
         if (ty == MT_OP_INSERT) {
-            s1 = (int)rng.u((uint32_t)L + 1); plen = 1 + rng.u(p->ins_len_max);
+            s1 = p->ins_at_end ? L : (int)rng.u((uint32_t)L + 1);
+            const uint32_t lo = p->ins_len_min > 1 ? p->ins_len_min : 1;
+            plen = lo + rng.u(p->ins_len_max - lo + 1);
+            if (p->seg_prop_sets) { pid = (int)(k % p->seg_prop_sets); fl |= MT_OPF_SEG_PROPS; }
             for (uint32_t c = 0; c < plen; c++) payload[pw + c] = (uint16_t)(u'a' + rng.u(26));
         } else {
             s1 = (int)rng.u((uint32_t)L); uint32_t n = 1 + rng.u(p->rem_len_max); s2 = std::min(L, s1 + (int)n);

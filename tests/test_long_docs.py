@@ -1,0 +1,75 @@
+"""Config 4 machinery on the host emulation vs the oracle: documents pre-built by
+append-only inserts with alternating segment properties (no coalescing), a
+device checkpoint of that state, then a deep-window stream generated on top of
+it (continue_docs) and replayed from the restored checkpoint."""
+import numpy as np
+import pytest
+
+from emu_lib import emu_engine
+from fluidframework_amd.batch import concat_runs as concat
+from oracle_lib import gen_params, generate, replay
+from test_emu_parity import NAMES, ann_props
+
+
+
+def prebuild_params(n_docs, ops):
+    p = gen_params(seed=404, n_docs=n_docs, ops=ops, clients=4, lag=0, ins=100, rem=0, ins_len=5, rem_len=1)
+    p.ins_len_min, p.seg_prop_sets, p.ins_at_end = 5, 2, 1
+    return p
+
+
+def test_prebuild_generator_matches_oracle():
+    props = ann_props()
+    p = prebuild_params(3, 600)
+    ob, st, kept = generate(p, props, keep=True)
+    assert st == [0] * 3
+    assert (ob.arrays["flags"] & 8).all() and (ob.arrays["payload_len"] == 5).all()
+    eng = emu_engine(3, rows_per_doc=4096, window_per_doc=1024, propsets_per_doc=4096, text_per_doc=1 << 14)
+    eng.upload_props(props)
+    eng.upload_names(NAMES)
+    eng.generate(p)
+    eng.sync()
+    assert (eng.status(range(3)) == 0).all()
+    gb = eng.generated_download()
+    for k in ("type", "flags", "client", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_len", "prop_id"):
+        assert np.array_equal(gb.arrays[k], ob.arrays[k]), k
+    for d in range(3):
+        assert len(kept[d].dump()) == 600          # alternating props: no two neighbours coalesce
+        assert np.array_equal(eng.dump(d), kept[d].dump())
+
+
+@pytest.mark.parametrize("lag", [64, 512])
+def test_deep_window_on_checkpoint_matches_oracle(lag):
+    props = ann_props()
+    n = 2
+    eng = emu_engine(n, rows_per_doc=12000, window_per_doc=8192, propsets_per_doc=8192, text_per_doc=1 << 16)
+    eng.upload_props(props)
+    eng.upload_names(NAMES)
+    pa = prebuild_params(n, 3000)
+    eng.generate(pa)
+    eng.sync()
+    a = eng.generated_download()
+    eng.checkpoint()
+    pb = gen_params(seed=505, n_docs=n, ops=1500, clients=8, lag=lag, ins=60, rem=40, ins_len=8, rem_len=8)
+    pb.continue_docs = 1
+    eng.generate(pb)
+    eng.sync()
+    assert (eng.status(range(n)) == 0).all()
+    b = eng.generated_download()
+    assert (b.arrays["seq"][b.op_offsets[:-1]] == 3001).all()        # continues the pre-built documents
+    neg = np.full(n, -1, np.int32)
+    dig_gen = eng.snapshot_digests(range(n), neg, neg, threads=2)
+    eng.restore()
+    eng.generated_to_resident()
+    eng.replay_resident()
+    eng.sync()
+    assert (eng.status(range(n)) == 0).all()
+    dig_replay = eng.snapshot_digests(range(n), neg, neg, threads=2)
+    assert np.array_equal(dig_gen, dig_replay)
+    both = concat(a, b)
+    last = both.op_offsets[1:] - 1
+    for d, (od, st) in enumerate(replay(both, props, NAMES)):
+        assert st == 0
+        assert eng.get_text([d])[0] == od.get_text()
+        assert np.array_equal(eng.dump(d), od.dump())
+        assert int(dig_replay[d]) == od.snapshot(int(both.arrays["msn"][last[d]]), int(both.arrays["seq"][last[d]]))[1]
