@@ -609,7 +609,8 @@ template <bool LDS> struct MtEngT {
             if (n1 < MT_MAXN) {
                 wave_for(8, [&](int i) MT_LAM { bk(B).c[i] = i < n1 ? own(nc, i) : -1; });
                 bk(B).n = n1; bk(B).len = h.len + delta;
-                for (int l = L - 1; l >= 0; l--) { const int pb = uni(sc->pathB[l]); bk(pb).len = uni(bk(pb).len) + delta; }
+                // ancestors on the path: one lane per level (distinct blocks), one round trip
+                if (delta != 0) wave_for(L, [&](int l) MT_LAM { const int pb = sc->pathB[l]; bk(pb).len = bk(pb).len + delta; });
                 return;
             }
             lastSplit = true;
@@ -782,6 +783,7 @@ template <bool LDS> struct MtEngT {
         return x;
     }
     MT_HD void addToLRUSet(int s, int sq) {                   // MT/mergeTree.ts:1262-1272
+        if (!(sq > curSeq)) return;
         const int p = uni(row(s).parent);
         const uint32_t m = uni(row(s).meta);
         if (uni(bk(p).scour) != 1 && sq > curSeq) {
@@ -808,6 +810,9 @@ template <bool LDS> struct MtEngT {
     MT_HD void copyText(int dst, int src1, int n1, int src2 = 0, int n2 = 0) {
         const int n = n1 + n2;
         MT_EV2(2, n); MT_EV2(3, 1);
+#ifdef MT_EXPERIMENT_NOCOPY
+        return;                            // timing experiment only: results are wrong
+#endif
         for (int base = 0; base < n; base += MT_WAVE) {
             const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
             auto v = wave_map(m, [&](int k) MT_LAM { const int q = base + k; return (int)text[q < n1 ? src1 + q : src2 + (q - n1)]; });
