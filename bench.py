@@ -30,7 +30,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+HBM_PEAK_GBPS = 8000.0
+RESIDENCY = {"hbm": 0, "lds": 1, "blk": 2}
+REPLAY_KERNEL = {"hbm": "mt_replay_kernel", "lds": "mt_replay_lds_kernel + mt_replay_kernel",
+                 "blk": "mt_replay_blk_kernel"}  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 
 CONFIGS = {
     # name: (docs, ops, clients, lag, ins%, rem%, ins_len, rem_len, ann_sets, rewrite%)
@@ -69,7 +72,7 @@ def algorithmic_bytes(cnt):
                + 64 * cnt["depth"].sum() + 64 * cnt["scoured"].sum())
 
 
-def measured_traffic(cfg_name, c):
+def measured_traffic(cfg_name, c, kernel):
     """HBM bytes per replay launch from the committed rocprofv3 PMC passes
     (profiles/<round>/<config>_traffic.json, written by tools/traffic_from_pmc.py)
     when they were taken on this exact workload; None otherwise."""
@@ -80,7 +83,7 @@ def measured_traffic(cfg_name, c):
             t = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if t.get("docs") == c["docs"] and t.get("msgs_per_doc") == c["ops"]:
+        if t.get("docs") == c["docs"] and t.get("msgs_per_doc") == c["ops"] and t.get("kernel") == kernel:
             best = (t["traffic_bytes"], os.path.relpath(f, ROOT))
     return best
 
@@ -147,7 +150,7 @@ def run_config4(args, c, world, rank, local):
     eng = Engine(n, device=local, rows_per_doc=rows, blocks_per_doc=rows // 2 + 64, heap_per_doc=rows,
                  window_per_doc=16384, text_per_doc=5 * pre + c["ins_len"] * ops + 4096,
                  propsets_per_doc=pre + ops + 64)
-    eng.set_residency(args.residency == "lds")
+    eng.set_residency(RESIDENCY[args.residency])
     eng.upload_props(ann_props())
     eng.upload_names(['"c%d"' % i for i in range(64)])
     seed = args.seed ^ (rank * 0x9E3779B1)
@@ -222,7 +225,7 @@ def run_config4(args, c, world, rank, local):
                    "parallelism": f"doc-sharded x{world}", "residency": args.residency,
                    "step": "mt_restore (device copy of the pre-built documents) + replay"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "mt_replay_kernel",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": REPLAY_KERNEL[args.residency],
                      "kernel_ms": kern_s * 1e3, "bytes_per_launch": bytes_per_launch},
         "parity": "status words clean" if ok else "STATUS ERROR",
         "snapshot": {"docs": n, "ms": snap_ms, "digest_xor": f"{int(np.bitwise_xor.reduce(digs)):016x}"},
@@ -291,7 +294,7 @@ def run_config5(args, c, world, rank, local):
     sh = build_sharded(dist, device, fac, total_docs, args.seed, MtGenParams, gen_kw, names=names)
     setup_s = time.time() - t0
     eng = sh.engine
-    eng.set_residency(args.residency == "lds")
+    eng.set_residency(RESIDENCY[args.residency])
     my_msgs = int(sh.ops.sum())
     for _ in range(args.warmup):
         sh.replay()
@@ -333,7 +336,7 @@ def run_config5(args, c, world, rank, local):
                    "msgs_max": int(sh.all_ops.max()), "parallelism": f"doc-sharded x{world} (LPT)",
                    "residency": args.residency},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "mt_replay_kernel (rank 0)",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": REPLAY_KERNEL[args.residency] + " (rank 0)",
                      "kernel_ms": kern_s * 1e3, "bytes_per_launch": bytes_per_launch},
         "parity": "status words clean on every rank" if int(bad.item()) == 0 else "STATUS ERROR",
         "sharding": {"rebalance_ms": sh.timings.get("rebalance_ms"), "rebalance_bytes": sh.timings.get("rebalance_bytes"),
@@ -378,8 +381,9 @@ def main():
     ap.add_argument("--prebuild", type=int, default=0, help="config4: override pre-build appends per document")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--residency", default="hbm", choices=["lds", "hbm"],
-                    help="hbm: HBM-pool kernel (default); lds: LDS-resident pools with HBM hand-over")
+    ap.add_argument("--residency", default="blk", choices=["lds", "hbm", "blk"],
+                    help="blk: blocks + heap in LDS, in-wave HBM continuation (default); hbm: every pool in HBM; "
+                         "lds: rows/blocks/heap/window in LDS")
     ap.add_argument("--caps", default="", help="override pool caps, e.g. rows_per_doc=400,text_per_doc=16384")
     args = ap.parse_args()
 
@@ -420,7 +424,7 @@ def main():
         k, v = kv.split("=")
         caps[k] = int(v)
     eng = Engine(c["docs"], device=local, **caps)
-    eng.set_residency(args.residency == "lds")
+    eng.set_residency(RESIDENCY[args.residency])
     eng.upload_props(ann_props())
     eng.upload_names(['"c%d"' % i for i in range(64)])
     seed = args.seed ^ (rank * 0x9E3779B1)
@@ -468,6 +472,10 @@ def main():
         dt = float(t.item())
     st = eng.status(range(c["docs"]))
     cnt2 = eng.counters(range(c["docs"]))
+    handover = None
+    if args.residency != "hbm":
+        cur = eng.last_cursors(c["docs"]).astype(np.int64)
+        handover = int((cur < (np.arange(c["docs"]) + 1) * c["ops"]).sum())
     # SnapshotV1 of every document at its current window (reported, not timed as ops)
     t1 = time.perf_counter()
     sthreads = min(16, os.cpu_count() or 1)
@@ -482,7 +490,7 @@ def main():
     achieved = bytes_per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
     if rank != 0:
         return
-    traffic = measured_traffic(args.config, c)
+    traffic = measured_traffic(args.config, c, REPLAY_KERNEL[args.residency])
     out = {
         "metric": "sequenced merge-tree ops applied/sec (whole node) + achieved HBM GB/s",
         "value": value,
@@ -499,12 +507,13 @@ def main():
         "config": {"workload": f"{args.config}: {c['desc']}", "docs_per_gpu": c["docs"], "msgs_per_doc": c["ops"],
                    "clients": c["clients"], "lag_max": c["lag"], "mix_ins_rem_ann": [c["ins"], c["rem"],
                                                                                    100 - c["ins"] - c["rem"]],
-                   "parallelism": f"doc-sharded x{world}", "residency": args.residency},
+                   "parallelism": f"doc-sharded x{world}", "residency": args.residency,
+                   "lds_handover_docs": handover},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic[0] if traffic else None,
                      "traffic_source": traffic[1] if traffic else None,
-                     "kernel": "mt_replay_kernel", "kernel_ms": kern_s * 1e3,
+                     "kernel": REPLAY_KERNEL[args.residency], "kernel_ms": kern_s * 1e3,
                      "bytes_per_launch": bytes_per_launch},
         "hbm_gbps_algorithmic": achieved,
         "parity": "status words clean" if ok else "STATUS ERROR",

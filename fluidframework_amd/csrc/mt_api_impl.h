@@ -250,10 +250,22 @@ int MT_FN(apply_batch)(mt_ctx* c, const mt_op_batch* B) {
     return MT_FN(replay_resident)(c);
 }
 int MT_FN(set_residency)(mt_ctx* c, int use_lds, int rows, int blocks, int heap) {
-    if (!c || rows < 0 || blocks < 0 || heap < 0 || rows > MT_L_ROWS || blocks > MT_L_BLKS || heap > MT_L_HEAP)
+    if (!c || use_lds < 0 || use_lds > 2 || rows < 0 || blocks < 0 || heap < 0 || rows > MT_L_ROWS ||
+        blocks > (use_lds == 2 ? MT_B_BLKS : MT_L_BLKS) || heap > (use_lds == 2 ? MT_B_HEAP : MT_L_HEAP))
         return MT_E_INVALID;
-    c->use_lds = use_lds ? 1 : 0;
-    c->lds_rows = rows ? rows : MT_L_ROWS; c->lds_blks = blocks ? blocks : MT_L_BLKS; c->lds_heap = heap ? heap : MT_L_HEAP;
+    c->use_lds = use_lds;
+    c->lds_rows = rows ? rows : MT_L_ROWS;
+    c->lds_blks = blocks ? blocks : (use_lds == 2 ? MT_B_BLKS : MT_L_BLKS);
+    c->lds_heap = heap ? heap : (use_lds == 2 ? MT_B_HEAP : MT_L_HEAP);
+    return MT_OK;
+}
+// Where each run of the last LDS-resident replay handed over to the HBM kernel
+// (op index; op_offsets[run+1] = finished in LDS).  Diagnostic.
+int MT_FN(last_cursors)(mt_ctx* c, uint32_t n, uint32_t* out) {
+    if (!c || !out || n > c->n_runs || !c->b_cursor.p) return MT_E_INVALID;
+    int rc = mtb_sync(c);
+    if (rc) return rc;
+    mtb_d2h(c, out, c->b_cursor.p, 4ull * n);
     return MT_OK;
 }
 int MT_FN(last_replay_ms)(mt_ctx* c, float* ms) { if (!c || !ms) return MT_E_INVALID; *ms = c->last_ms; return MT_OK; }

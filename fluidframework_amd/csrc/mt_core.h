@@ -48,6 +48,15 @@
 #define MT_L_HEAP 96                  // zamboni heap entries
 #endif
 #define MT_L_H 8                      // ancestor-chain levels (tree height < MT_L_H - 2)
+// Block residency (mt_replay_blk_kernel): only blocks and the zamboni heap move to
+// LDS (rows, window and U set stay in HBM), small enough for 4 waves per SIMD.
+#ifndef MT_B_BLKS
+#define MT_B_BLKS 112
+#endif
+#ifndef MT_B_HEAP
+#define MT_B_HEAP 126
+#endif
+enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2 };
 
 // Phase profiling (diagnostic builds only, -DMT_PROFILE): shader-clock cycles
 // accumulated per phase into MtDocHdr.prof; never compiled into the product.
@@ -189,6 +198,12 @@ struct __attribute__((aligned(16))) MtLdsPools {
     uint8_t uanc[MT_L_ROWS * MT_L_H];
 };
 
+// LDS home of a document's blocks and heap while mt_replay_blk_kernel runs it.
+struct __attribute__((aligned(16))) MtLdsBlk {
+    MtBlk blk[MT_B_BLKS];
+    MtHeapE heap[MT_B_HEAP + 2];
+};
+
 // per-wave scratch (LDS on the device)
 struct MtScratch {
     int pathB[MT_MAXH + 2], pathJ[MT_MAXH + 2];
@@ -233,7 +248,7 @@ struct MtEngParams {
     const uint8_t* p_falsy; const uint32_t* p_class;
 };
 // The LDS pools live in one file-scope __shared__ object, so every access of
-// the LDS-resident engine (MtEngT<true>) is a ds_* instruction; the host
+// the LDS-resident engine (MtEngT<MT_RES_LDS / MT_RES_BLK>) is a ds_* instruction; the host
 // emulation has one static instance (it runs one wave at a time).
 #if defined(__HIP_DEVICE_COMPILE__)
 __shared__ MtLdsPools mt_lds_pools_v;
@@ -241,8 +256,18 @@ __shared__ MtLdsPools mt_lds_pools_v;
 static MtLdsPools mt_lds_pools_v;
 #endif
 MT_INLINE MtLdsPools& mt_lds() { return mt_lds_pools_v; }
+#if defined(__HIP_DEVICE_COMPILE__)
+__shared__ MtLdsBlk mt_ldsb_v;
+#else
+static MtLdsBlk mt_ldsb_v;
+#endif
+MT_INLINE MtLdsBlk& mt_ldsb() { return mt_ldsb_v; }
 
-template <bool LDS> struct MtEngT {
+// RES: MT_RES_HBM (every pool in HBM), MT_RES_LDS (rows, blocks, heap, window,
+// U set in LDS) or MT_RES_BLK (blocks and heap in LDS).
+template <int RES> struct MtEngT {
+    static constexpr bool LDS = RES == MT_RES_LDS;      // all hot pools in LDS
+    static constexpr bool BLKL = RES != MT_RES_HBM;     // blocks + heap in LDS
     MtEngParams S;
     MtDocHdr* hdrp;
     // doc-local views
@@ -250,10 +275,14 @@ template <bool LDS> struct MtEngT {
     int *win, *uid, *udelta, *uanc;
     MtBlk* blk; MtHeapE* heap; uint16_t* text; MtPSet* pset;
     MtScratch* sc;
-    // pool accessors: LDS-resident (MtEngT<true>) or HBM (MtEngT<false>) homes
+    // pool accessors: LDS (MT_RES_LDS, MT_RES_BLK for blocks + heap) or HBM homes
     MT_HD MtRow& row(int s) const { if constexpr (LDS) return mt_lds().rows[s]; else return R[s]; }
-    MT_HD MtBlk& bk(int b) const { if constexpr (LDS) return mt_lds().blk[b]; else return blk[b]; }
-    MT_HD MtHeapE& hp(int k) const { if constexpr (LDS) return mt_lds().heap[k]; else return heap[k]; }
+    MT_HD MtBlk& bk(int b) const {
+        if constexpr (LDS) return mt_lds().blk[b]; else if constexpr (BLKL) return mt_ldsb().blk[b]; else return blk[b];
+    }
+    MT_HD MtHeapE& hp(int k) const {
+        if constexpr (LDS) return mt_lds().heap[k]; else if constexpr (BLKL) return mt_ldsb().heap[k]; else return heap[k];
+    }
     MT_HD int& wn(int k) const { if constexpr (LDS) return mt_lds().win[k]; else return win[k]; }
     MT_HD int& ui(int k) const { if constexpr (LDS) return mt_lds().uid[k]; else return uid[k]; }
     MT_HD int& ud(int k) const { if constexpr (LDS) return mt_lds().udelta[k]; else return udelta[k]; }
@@ -271,7 +300,7 @@ template <bool LDS> struct MtEngT {
     int blkFreeN;                       // blocks on the free list
     int heapHW, winHW;                  // high-water marks of heapN / winN
     // LDS residency (toLds/fromLds): LDS caps, and the HBM caps they stand in for
-    static constexpr bool kLds = LDS;
+    static constexpr bool kLds = BLKL;                  // runs check ldsHeadroom before each op
     int lRows, lBlks, lHeap;
     uint32_t gRowCap, gBlkCap, gHeapCap, gWinCap;
 
@@ -369,11 +398,26 @@ template <bool LDS> struct MtEngT {
             wave_for(m, [&](int k) MT_LAM { dst[base + k] = src[base + k]; });
         }
     }
-    // MtEngT<true> only: move the document's rows, blocks, heap and window into
+    // MT_RES_LDS: move the document's rows, blocks, heap and window into
     // the LDS pools (caps lr/lb/lh <= the MT_L_* array sizes).  False (nothing
     // moved) if they do not fit.  R/blk/heap/win keep pointing at the HBM homes.
     MT_HD bool toLds(int lr, int lb, int lh) {
-        static_assert(LDS, "LDS residency needs MtEngT<true>");
+        static_assert(BLKL, "LDS residency needs MtEngT<MT_RES_LDS or MT_RES_BLK>");
+        if constexpr (!LDS) {                                   // MT_RES_BLK: blocks + heap only
+            if (lb > MT_B_BLKS) lb = MT_B_BLKS;
+            if (lh > MT_B_HEAP) lh = MT_B_HEAP;
+            if (blkTop > lb || heapN > lh) return false;
+            MtLdsBlk& B = mt_ldsb();
+            copyQ((MtQ16*)B.blk, (const MtQ16*)blk, blkTop * (int)(sizeof(MtBlk) / 16));
+            copyI((int*)B.heap, (const int*)heap, 2 * (heapN + 1));
+            wave_sync();
+            gRowCap = S.rowCap; gBlkCap = blkCap; gHeapCap = S.heapCap; gWinCap = S.winCap;
+            blkCap = gBlkCap < (uint32_t)lb ? gBlkCap : (uint32_t)lb;
+            S.heapCap = gHeapCap < (uint32_t)lh ? gHeapCap : (uint32_t)lh;
+            lRows = 0x7FFFFFFF; lBlks = lb; lHeap = lh;
+            nU = 0; uValid = false;
+            return true;
+        }
         if (rowTop > lr || blkTop > lb || heapN > lh || winN > lr || height + 3 > MT_L_H || lb > 255) return false;
         MtLdsPools& L = mt_lds();
         copyQ((MtQ16*)L.rows, (const MtQ16*)R, rowTop * (int)(sizeof(MtRow) / 16));
@@ -391,6 +435,15 @@ template <bool LDS> struct MtEngT {
         return true;
     }
     MT_HD void fromLds() {
+        if constexpr (!LDS) {
+            MtLdsBlk& B = mt_ldsb();
+            copyQ((MtQ16*)blk, (const MtQ16*)B.blk, blkTop * (int)(sizeof(MtBlk) / 16));
+            copyI((int*)heap, (const int*)B.heap, 2 * (heapN + 1));
+            wave_sync();
+            blkCap = gBlkCap; S.heapCap = gHeapCap;
+            nU = 0; uValid = false;
+            return;
+        }
         MtLdsPools& L = mt_lds();
         copyQ((MtQ16*)R, (const MtQ16*)L.rows, rowTop * (int)(sizeof(MtRow) / 16));
         copyQ((MtQ16*)blk, (const MtQ16*)L.blk, blkTop * (int)(sizeof(MtBlk) / 16));
@@ -404,7 +457,8 @@ template <bool LDS> struct MtEngT {
     // row splits + 1 new row, 2 split cascades of height+2 blocks and packParent
     // regrowth; one heap entry per op plus one per message.
     MT_HD bool ldsHeadroom() const {
-        if constexpr (!LDS) return true;
+        if constexpr (!BLKL) return true;
+        if constexpr (!LDS) return (lBlks - blkTop + blkFreeN) >= 6 * (height + 2) + 8 && (lHeap - heapN) >= 4;
         return (lRows - rowTop + rfN) >= 4 && (lBlks - blkTop + blkFreeN) >= 6 * (height + 2) + 8 &&
                (lHeap - heapN) >= 4 && height + 3 <= MT_L_H;
     }
@@ -1235,5 +1289,5 @@ template <bool LDS> struct MtEngT {
         zamboni();
     }
 };
-using MtEng = MtEngT<false>;
+using MtEng = MtEngT<MT_RES_HBM>;
 

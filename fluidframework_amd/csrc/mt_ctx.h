@@ -31,7 +31,7 @@ struct mt_ctx {
     std::vector<uint32_t> gen_off;     // op offsets of the generated runs
     float last_ms = 0.f;
     // LDS residency of the replay (mt_set_residency): on/off and the pool caps
-    int use_lds = 0, lds_rows = MT_L_ROWS, lds_blks = MT_L_BLKS, lds_heap = MT_L_HEAP;
+    int use_lds = 2, lds_rows = MT_L_ROWS, lds_blks = MT_B_BLKS, lds_heap = MT_B_HEAP;
     void* stream = nullptr;
     void* ev0 = nullptr;
     void* ev1 = nullptr;

@@ -25,7 +25,7 @@ __global__ __launch_bounds__(64, MT_LDS_WAVES_PER_SIMD) void mt_replay_lds_kerne
     const uint32_t run = blockIdx.x;
     const uint32_t doc = ops.doc_ids[run];
     const uint32_t o0 = ops.op_off[run];
-    MtEngT<true> e;
+    MtEngT<MT_RES_LDS> e;
     e.bind(S, doc, &sc);
     uint32_t cur = o0;
     if (e.toLds(lr, lb, lh)) {
@@ -34,6 +34,30 @@ __global__ __launch_bounds__(64, MT_LDS_WAVES_PER_SIMD) void mt_replay_lds_kerne
     }
     cursor[run] = cur;
     e.store(doc);
+}
+// Blocks + heap in LDS (~9.5 KB per workgroup, 4 waves per SIMD), rows/window in HBM.
+__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(MtState S, MtOps ops, uint32_t* cursor, int lb, int lh) {
+    __shared__ MtScratch sc;
+    const uint32_t run = blockIdx.x;
+    const uint32_t doc = ops.doc_ids[run];
+    const uint32_t o0 = ops.op_off[run];
+    MtEngT<MT_RES_BLK> e;
+    e.bind(S, doc, &sc);
+    uint32_t cur = o0;
+    if (e.toLds(0, lb, lh)) {
+        cur = mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0);
+        e.fromLds();
+    }
+    cursor[run] = cur;
+    e.store(doc);
+    // A document that outgrew LDS continues here with its pools in HBM (no
+    // second launch: long documents, which outgrow it first, keep their head start).
+    if (cur < ops.op_off[run + 1]) {
+        MtEng h;
+        h.bind(S, doc, &sc);
+        mt_replay_run(h, ops, run, doc, nullptr, nullptr, cur);
+        h.store(doc);
+    }
 }
 __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_kernel(MtState S, MtOps ops, const uint32_t* cursor) {
     __shared__ MtScratch sc;
@@ -140,7 +164,10 @@ static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     (void)hipGetLastError();
     (void)hipEventRecord((hipEvent_t)c->ev0, s);
     if (g.enabled) hipLaunchKernelGGL(mt_generate_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, g);
-    else if (c->use_lds) {
+    else if (c->use_lds == 2) {
+        hipLaunchKernelGGL(mt_replay_blk_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
+                           c->lds_blks, c->lds_heap);
+    } else if (c->use_lds) {
         hipLaunchKernelGGL(mt_replay_lds_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
                            c->lds_rows, c->lds_blks, c->lds_heap);
         hipLaunchKernelGGL(mt_replay_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (const uint32_t*)c->b_cursor.p);

@@ -70,6 +70,7 @@ def _bind(lib, prefix: str):
         apply_batch=f("apply_batch", ctypes.c_int, [P, ctypes.POINTER(MtOpBatch)]),
         upload_batch=f("upload_batch", ctypes.c_int, [P, ctypes.POINTER(MtOpBatch)]),
         replay_resident=f("replay_resident", ctypes.c_int, [P]),
+        last_cursors=f("last_cursors", ctypes.c_int, [P, U32, P]),
         last_replay_ms=f("last_replay_ms", ctypes.c_int, [P, ctypes.POINTER(ctypes.c_float)]),
         update_seq=f("update_seq", ctypes.c_int, [P, U32, P, P, P]),
         sync=f("sync", ctypes.c_int, [P]),
@@ -193,6 +194,12 @@ class Engine:
     def replay_resident(self):
         self._check(self.fn["replay_resident"](self.h), "mt_replay_resident")
 
+    def last_cursors(self, n_runs: int) -> np.ndarray:
+        """mt_last_cursors: op index where each run left LDS in the last replay."""
+        out = np.zeros(n_runs, np.uint32)
+        self._check(self.fn["last_cursors"](self.h, n_runs, out.ctypes.data), "mt_last_cursors")
+        return out
+
     def sync(self):
         self._check(self.fn["sync"](self.h), "mt_sync")
 
@@ -263,8 +270,9 @@ class Engine:
                     "mt_doc_counters_get")
         return {f: np.array([getattr(x, f) for x in out], np.uint64) for f, _ in MtDocCounters._fields_}
 
-    def set_residency(self, use_lds: bool = True, rows: int = 0, blocks: int = 0, heap: int = 0):
-        """mt_set_residency: LDS-resident replay on/off and (lowered) LDS pool caps."""
+    def set_residency(self, use_lds=True, rows: int = 0, blocks: int = 0, heap: int = 0):
+        """mt_set_residency: 0/False HBM pools, 1/True LDS-resident, 2 blocks+heap in LDS;
+        optional (lowered) LDS pool caps."""
         self._check(self.fn["set_residency"](self.h, int(use_lds), rows, blocks, heap), "mt_set_residency")
 
     def checkpoint(self):

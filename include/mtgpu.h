@@ -184,12 +184,17 @@ int  mt_apply_batch(mt_ctx* ctx, const mt_op_batch* batch);
  * documents it names without any host->device traffic (the bench's timed path). */
 int  mt_upload_batch(mt_ctx* ctx, const mt_op_batch* batch);
 int  mt_replay_resident(mt_ctx* ctx);
-/* Residency of the replay: with use_lds (default off) a document whose rows,
- * blocks, zamboni heap and window fit the LDS caps runs out of LDS, and one that
- * outgrows them is finished from HBM at the exact op it reached.  rows/blocks/
- * heap (0 = compiled maximum) may only lower the caps; tests use small caps to
- * force the hand-over. */
+/* Residency of the replay.  use_lds = 2 (default): blocks and zamboni heap move
+ * to LDS (9.6 KB per document, 4 waves per SIMD), rows/window/text stay in HBM,
+ * and a document that outgrows the LDS blocks continues from HBM in the same
+ * wave at the exact op it reached; 0: every pool in HBM; 1: rows, blocks, heap
+ * and window all in LDS (finished by a second HBM launch when outgrown).
+ * rows/blocks/heap (0 = compiled maximum) may only lower the caps; tests use
+ * small caps to force the hand-over. */
 int  mt_set_residency(mt_ctx* ctx, int use_lds, int rows, int blocks, int heap);
+/* Per run of the last LDS-resident replay: the op index where it handed over to
+ * the HBM kernel (== the run's end when it finished in LDS).  Diagnostic. */
+int  mt_last_cursors(mt_ctx* ctx, uint32_t n_runs, uint32_t* out);
 /* Milliseconds of the last replay kernel(s), timed with HIP events on the
  * context stream. */
 int  mt_last_replay_ms(mt_ctx* ctx, float* ms);

@@ -36,8 +36,21 @@ static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     for (uint32_t run = 0; run < n_runs; run++) {
         const uint32_t doc = c->ops.doc_ids[run], o0 = c->ops.op_off[run];
         uint32_t cur = o0;
-        if (c->use_lds) {
-            MtScratch sc; MtEngT<true> e; e.bind(c->S, doc, &sc);
+        if (c->use_lds == 2) {
+            MtScratch sc; MtEngT<MT_RES_BLK> e; e.bind(c->S, doc, &sc);
+            if (e.toLds(0, c->lds_blks, c->lds_heap)) {
+                cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
+                e.fromLds();
+            }
+            e.store(doc);
+            if (cur < c->ops.op_off[run + 1]) {               // continues in HBM within the same "wave"
+                MtEng h; h.bind(c->S, doc, &sc);
+                mt_replay_run(h, c->ops, run, doc, nullptr, nullptr, cur);
+                h.store(doc);
+                // cursor keeps the hand-over point (diagnostic); the HBM pass below skips it
+            }
+        } else if (c->use_lds) {
+            MtScratch sc; MtEngT<MT_RES_LDS> e; e.bind(c->S, doc, &sc);
             if (e.toLds(c->lds_rows, c->lds_blks, c->lds_heap)) {
                 cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
                 e.fromLds();
@@ -46,7 +59,7 @@ static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
         }
         cursor[run] = cur;
     }
-    for (uint32_t run = 0; run < n_runs; run++) {
+    for (uint32_t run = 0; run < n_runs && c->use_lds != 2; run++) {
         if (cursor[run] >= c->ops.op_off[run + 1]) continue;
         const uint32_t doc = c->ops.doc_ids[run];
         MtScratch sc; MtEng e; e.bind(c->S, doc, &sc);
