@@ -25,6 +25,7 @@
 // Every function below is executed by all 64 lanes of the document's wave with
 // wave-uniform control flow (see wave.h); data-parallel steps use wave_map().
 #pragma once
+#include <type_traits>
 #include "wave.h"
 #include "../../include/mtgpu.h"
 
@@ -51,8 +52,9 @@
 // Block residency (mt_replay_blk_kernel): only blocks and the zamboni heap move to
 // LDS (rows, window and U set stay in HBM), small enough for 4 waves per SIMD.
 #ifndef MT_B_BLKS
-#define MT_B_BLKS 112
+#define MT_B_BLKS 104
 #endif
+#define MT_B_U 64                     // U-set entries kept in LDS (the rest, if any, in HBM)
 #ifndef MT_B_HEAP
 #define MT_B_HEAP 126
 #endif
@@ -202,6 +204,8 @@ struct __attribute__((aligned(16))) MtLdsPools {
 struct __attribute__((aligned(16))) MtLdsBlk {
     MtBlk blk[MT_B_BLKS];
     MtHeapE heap[MT_B_HEAP + 2];
+    int uid[MT_B_U], udelta[MT_B_U];
+    uint8_t uanc[MT_B_U * MT_L_H];    // block ids < MT_B_BLKS < 255; 255 = none
 };
 
 // per-wave scratch (LDS on the device)
@@ -286,6 +290,27 @@ template <int RES> struct MtEngT {
     MT_HD int& wn(int k) const { if constexpr (LDS) return mt_lds().win[k]; else return win[k]; }
     MT_HD int& ui(int k) const { if constexpr (LDS) return mt_lds().uid[k]; else return uid[k]; }
     MT_HD int& ud(int k) const { if constexpr (LDS) return mt_lds().udelta[k]; else return udelta[k]; }
+    // MT_RES_BLK keeps the first MT_B_U U-set entries in LDS.  U loops run per
+    // 64-entry chunk (chunks never straddle MT_B_U), so each chunk picks its home
+    // at compile time: forU calls f(std::bool_constant<inLds>, base, m).
+    static constexpr bool UL = RES == MT_RES_BLK;
+    template <bool L> MT_HD int uiAt(int k) const { if constexpr (UL && L) return mt_ldsb().uid[k]; else return ui(k); }
+    template <bool L> MT_HD int udAt(int k) const { if constexpr (UL && L) return mt_ldsb().udelta[k]; else return ud(k); }
+    template <bool L> MT_HD void ancPutAt(int u, int h, int a) {
+        if constexpr (UL && L) mt_ldsb().uanc[u * MT_L_H + h] = (uint8_t)(a < 0 ? 255 : a);
+        else ancPut(u, h, a);
+    }
+    template <bool L> MT_HD int ancGetAt(int u, int h) const {
+        if constexpr (UL && L) { const int a = mt_ldsb().uanc[u * MT_L_H + h]; return a == 255 ? -1 : a; }
+        else return ancGet(u, h);
+    }
+    template <class F> MT_HD void forU(F f) const {
+        for (int base = 0; base < nU; base += MT_WAVE) {
+            const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
+            if (UL && base < MT_B_U) f(std::true_type{}, base, m);
+            else f(std::false_type{}, base, m);
+        }
+    }
     // uniform document state (MtDocHdr)
     int root, height, minSeq, curSeq, rowTop, blkTop, blkFree, heapN, winN, textTop, psetTop;
     uint32_t status;
@@ -406,7 +431,7 @@ template <int RES> struct MtEngT {
         if constexpr (!LDS) {                                   // MT_RES_BLK: blocks + heap only
             if (lb > MT_B_BLKS) lb = MT_B_BLKS;
             if (lh > MT_B_HEAP) lh = MT_B_HEAP;
-            if (blkTop > lb || heapN > lh) return false;
+            if (blkTop > lb || heapN > lh || height + 3 > MT_L_H) return false;
             MtLdsBlk& B = mt_ldsb();
             copyQ((MtQ16*)B.blk, (const MtQ16*)blk, blkTop * (int)(sizeof(MtBlk) / 16));
             copyI((int*)B.heap, (const int*)heap, 2 * (heapN + 1));
@@ -458,7 +483,8 @@ template <int RES> struct MtEngT {
     // regrowth; one heap entry per op plus one per message.
     MT_HD bool ldsHeadroom() const {
         if constexpr (!BLKL) return true;
-        if constexpr (!LDS) return (lBlks - blkTop + blkFreeN) >= 6 * (height + 2) + 8 && (lHeap - heapN) >= 4;
+        if constexpr (!LDS) return (lBlks - blkTop + blkFreeN) >= 6 * (height + 2) + 8 && (lHeap - heapN) >= 4 &&
+                                   height + 3 <= MT_L_H;
         return (lRows - rowTop + rfN) >= 4 && (lBlks - blkTop + blkFreeN) >= 6 * (height + 2) + 8 &&
                (lHeap - heapN) >= 4 && height + 3 <= MT_L_H;
     }
@@ -551,7 +577,13 @@ template <int RES> struct MtEngT {
             const int cntU = wave_count(du);
             const int nu0 = nU;
             wave_for(m, [&](int k) MT_LAM {
-                if (own(du, k)) { ui(nu0 + own(rk2, k)) = own(wi, k).id; ud(nu0 + own(rk2, k)) = own(wi, k).delta; }
+                if (own(du, k)) {
+                    const int pos = nu0 + own(rk2, k);
+                    if constexpr (UL) {
+                        if (pos < MT_B_U) { mt_ldsb().uid[pos] = own(wi, k).id; mt_ldsb().udelta[pos] = own(wi, k).delta; }
+                        else { ui(pos) = own(wi, k).id; ud(pos) = own(wi, k).delta; }
+                    } else { ui(pos) = own(wi, k).id; ud(pos) = own(wi, k).delta; }
+                }
             });
             nU += cntU;
         }
@@ -559,17 +591,17 @@ template <int RES> struct MtEngT {
         MT_EV(1, nU);
         wave_sync();
         // ancestor chains: uanc[u*MAXH + h] = block at height h above row u
-        for (int base = 0; base < nU; base += MT_WAVE) {
-            const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
-            const int H = height;
+        const int H = height;
+        forU([&](auto inL, int base, int m) MT_LAM {
+            constexpr bool L = decltype(inL)::value;
             wave_for(m, [&](int k) MT_LAM {
-                int a = row(ui(base + k)).parent;
+                int a = row(uiAt<L>(base + k)).parent;
                 for (int h = 0; h <= H; h++) {
-                    ancPut(base + k, h, a);
+                    ancPutAt<L>(base + k, h, a);
                     a = (a >= 0) ? bk(a).parent : -1;
                 }
             });
-        }
+        });
         wave_sync();
         uValid = true; uRef = r; uCli = c;
         MT_PE(MT_PH_U, t0);
@@ -578,10 +610,10 @@ template <int RES> struct MtEngT {
     MT_HD int perspectiveLength(int r, int c) {
         if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
         int s = 0;
-        for (int base = 0; base < nU; base += MT_WAVE) {
-            const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
-            s += wave_sum(wave_map(m, [&](int k) MT_LAM { return ud(base + k); }));
-        }
+        forU([&](auto inL, int base, int m) MT_LAM {
+            constexpr bool L = decltype(inL)::value;
+            s += wave_sum(wave_map(m, [&](int k) MT_LAM { return udAt<L>(base + k); }));
+        });
         return uni(bk(root).len) + s;
     }
     // Perspective lengths of block B's children (nodeLength, MT/mergeTree.ts:1652-1692).
@@ -608,16 +640,16 @@ template <int RES> struct MtEngT {
         for (int j = 0; j < MT_MAXN; j++) cid[j] = j < n ? wave_at(ch, j) : -2;
         wave_for(MT_MAXN, [&](int j) MT_LAM { sc->corr[j] = 0; });
         wave_sync();
-        for (int base = 0; base < nU; base += MT_WAVE) {
-            const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
+        forU([&](auto inL, int base, int m) MT_LAM {
+            constexpr bool L = decltype(inL)::value;
             wave_for(m, [&](int k) MT_LAM {
-                const int a = ancGet(base + k, hc);
+                const int a = ancGetAt<L>(base + k, hc);
                 int jk = -1;
 #pragma unroll
                 for (int j = 0; j < MT_MAXN; j++) if (cid[j] == a) jk = j;
-                if (jk >= 0) lds_add(&sc->corr[jk], ud(base + k));
+                if (jk >= 0) lds_add(&sc->corr[jk], udAt<L>(base + k));
             });
-        }
+        });
         wave_sync();
         return wave_map(n, [&](int j) MT_LAM {
             ChildL o; o.len = bk(own(ch, j)).len + sc->corr[j]; o.tie = true; return o;
