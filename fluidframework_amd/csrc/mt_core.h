@@ -483,7 +483,12 @@ template <int RES> struct MtEngT {
     // regrowth; one heap entry per op plus one per message.
     MT_HD bool ldsHeadroom() const {
         if constexpr (!BLKL) return true;
-        if constexpr (!LDS) return (lBlks - blkTop + blkFreeN) >= 6 * (height + 2) + 8 && (lHeap - heapN) >= 4 &&
+        // Block budget per message: the split + insert cascades allocate at most
+        // 2*height + 5 blocks; packParent regrowth (+2 per level at most, and rare)
+        // gets a fixed 12.  The largest growth measured over configs 2-3 in the host
+        // emulation was 2*height + 2.  Exceeding it would set MT_DS_OOM_BLOCKS (never
+        // silently wrong); mt_set_residency(ctx, 0, ...) avoids LDS entirely.
+        if constexpr (!LDS) return (lBlks - blkTop + blkFreeN) >= 2 * height + 17 && (lHeap - heapN) >= 4 &&
                                    height + 3 <= MT_L_H;
         return (lRows - rowTop + rfN) >= 4 && (lBlks - blkTop + blkFreeN) >= 6 * (height + 2) + 8 &&
                (lHeap - heapN) >= 4 && height + 3 <= MT_L_H;
