@@ -56,7 +56,7 @@
 #endif
 #define MT_B_U 64                     // U-set entries kept in LDS (the rest, if any, in HBM)
 #ifndef MT_B_HEAP
-#define MT_B_HEAP 126
+#define MT_B_HEAP 94
 #endif
 enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2 };
 
@@ -94,6 +94,18 @@ enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2 };
 #define MT_QB(v)
 #define MT_QE(i, v)
 #define MT_QC(i)
+#endif
+// Zamboni breakdown probes (device diagnostic builds only, -DMT_PROFILE3): 0 zamboni
+// total, 1 scourLeaf, 2 appendText, 3 packParent, 4 updatePathLens, 5 heapGet,
+// 6 path after scour (child rewrite + pack/update), 7 pops.
+#if defined(MT_PROFILE3) && defined(__HIP_DEVICE_COMPILE__)
+#define MT_ZB(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define MT_ZE(i, v) prof[i] += __builtin_amdgcn_s_memtime() - (v)
+#define MT_ZC(i) prof[i] += 1
+#else
+#define MT_ZB(v)
+#define MT_ZE(i, v)
+#define MT_ZC(i)
 #endif
 enum { MT_PH_U = 0, MT_PH_SPLIT, MT_PH_INSERT, MT_PH_RANGE, MT_PH_ZAMBONI, MT_PH_OP, MT_PH_GEN, MT_PH_TEXT };
 
@@ -213,6 +225,7 @@ struct MtScratch {
     int pathB[MT_MAXH + 2], pathJ[MT_MAXH + 2];
     int fB[MT_MAXH + 2], fJ[MT_MAXH + 2], fS[MT_MAXH + 2], fE[MT_MAXH + 2], fL[MT_MAXH + 2], fD[MT_MAXH + 2];
     int hold[64];
+    int holdLen[64];                  // observer length of each held child (scourLeaves)
     int pk[MT_PSK], pv[MT_PSK];
     int lastOld, lastNew;
     int rfree[MT_RFL];                // recycled rows (unlinked, out of the window, no heap entry)
@@ -953,6 +966,11 @@ template <int RES> struct MtEngT {
     // region of twice the size (amortized O(appended chars)).
     // Returns the new (toff, tcap) of pv through references; lengths known by the caller.
     MT_HD void appendText(int pv, int lp, int& tp, int& cp, int s, int ls, int ts, int cs) {
+        MT_ZB(z2);
+        appendTextInner(pv, lp, tp, cp, s, ls, ts, cs);
+        MT_ZE(2, z2);
+    }
+    MT_HD void appendTextInner(int pv, int lp, int& tp, int& cp, int s, int ls, int ts, int cs) {
         if (ts == tp + lp && cp == lp) { row(pv).len = lp + ls; cp = lp + cs; row(pv).tcap = cp; return; }
         if (lp + ls <= cp) { copyText(tp + lp, ts, ls); row(pv).len = lp + ls; return; }
         int nc = 2 * (lp + ls); if (nc < 16) nc = 16;
@@ -965,27 +983,50 @@ template <int RES> struct MtEngT {
     }
     // scourNode for a block of rows (MT/mergeTree.ts:1278-1356); kept children
     // are appended to sc->hold starting at nh; returns the new hold count.
-    MT_HD int scourLeaf(int B, int n, int nh) {
-        // Prefetch every child's fields (and the last text unit) in parallel, then
-        // run the sequential merge chain on registers.
-        auto f = kids(B, n);
-        auto fm = wave_map(n, [&](int j) MT_LAM { return (int)row(own(f, j)).meta; });
-        auto fs = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).seq; });
-        auto fr = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).rseq; });
-        auto fl = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).len; });
-        auto fp = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).props; });
-        auto ft = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).toff; });
-        auto fc = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).tcap; });
-        auto fe = wave_map(n, [&](int j) MT_LAM {
+    // scourNode (MT/mergeTree.ts:1278-1356) for leaf blocks blks[0..nb) (a lane
+    // array, nb <= 7): kept children are appended to sc->hold from nh, with their
+    // observer lengths in sc->holdLen; returns the new hold count.  The rows of all
+    // the blocks (<= 49) are prefetched together (one row round trip plus one for
+    // the last text unit), then the merge chain runs sequentially on registers;
+    // prev restarts at every block, as each block is scoured separately.
+    MT_HD int scourLeaves(const LaneArr<int>& blks, int nb, int nh) {
+        // Lane t holds child slot t&7 of block t>>3; empty slots are masked out.
+        int bId[MT_MAXN], bN[MT_MAXN];
+#pragma unroll
+        for (int i = 0; i < MT_MAXN; i++) {
+            bId[i] = wave_at(blks, i < nb ? i : 0);
+            bN[i] = i < nb ? uni(bk(bId[i]).n) : 0;
+        }
+        const int span = 8 * nb;
+        auto f = wave_map(span, [&](int t) MT_LAM {
+            const int bi = t >> 3;
+            int b = bId[0], n = bN[0];
+#pragma unroll
+            for (int i = 1; i < MT_MAXN; i++) if (bi == i) { b = bId[i]; n = bN[i]; }
+            return (t & 7) < n ? bk(b).c[t & 7] : -1;
+        });
+        uint64_t live = wave_ballot(wave_map(span, [&](int t) MT_LAM { return own(f, t) >= 0; }));
+        auto fm = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? (int)row(g).meta : 0; });
+        auto fs = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).seq : 0; });
+        auto fr = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).rseq : 0; });
+        auto fl = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).len : 0; });
+        auto fp = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).props : 0; });
+        auto ft = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).toff : 0; });
+        auto fc = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).tcap : 0; });
+        auto fe = wave_map(span, [&](int j) MT_LAM {
             const int l = own(fl, j);
-            return (!(own(fm, j) & MT_M_MARKER) && l > 0) ? (int)text[own(ft, j) + l - 1] : 0;
+            return (own(f, j) >= 0 && !(own(fm, j) & MT_M_MARKER) && l > 0) ? (int)text[own(ft, j) + l - 1] : 0;
         });
         int prev = -1, prevLen = 0, prevToff = 0, prevCap = 0, prevProps = -1, prevLast = 0; bool prevMarker = false;
         int epoch = gcEpoch;
-        for (int k = 0; k < n; k++) {
+        int curB = 0;
+        while (live) {
+            const int k = __builtin_ctzll(live);
+            live &= live - 1;
+            if ((k >> 3) != curB) { prev = -1; curB = k >> 3; }      // each block is scoured separately
             if (epoch != gcEpoch) {                                // text moved: refresh prefetched offsets
-                ft = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).toff; });
-                fc = wave_map(n, [&](int j) MT_LAM { return row(own(f, j)).tcap; });
+                ft = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).toff : 0; });
+                fc = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).tcap : 0; });
                 if (prev >= 0) { prevToff = uni(row(prev).toff); prevCap = uni(row(prev).tcap); }
                 epoch = gcEpoch;
             }
@@ -993,7 +1034,7 @@ template <int RES> struct MtEngT {
             const uint32_t mt = (uint32_t)wave_at(fm, k);
             c_scour++;
             if (mt & MT_M_REMOVED) {
-                if (wave_at(fr, k) > minSeq) sc->hold[nh++] = s;
+                if (wave_at(fr, k) > minSeq) { sc->hold[nh] = s; sc->holdLen[nh] = 0; nh++; }
                 else {                                             // UNLINK
                     row(s).parent = -1;
                     if (!(mt & (MT_M_HREF | MT_M_INWIN))) freeRow(s);
@@ -1009,25 +1050,28 @@ template <int RES> struct MtEngT {
                     row(s).parent = -1;
                     if (!(mt & (MT_M_HREF | MT_M_INWIN))) freeRow(s);
                     prevLen += ls; prevLast = wave_at(fe, k);
+                    sc->holdLen[nh - 1] = prevLen;                 // prev is the last held row
                 } else {
-                    sc->hold[nh++] = s;
+                    sc->hold[nh] = s; sc->holdLen[nh] = ls; nh++;
                     prev = (ls > 0) ? s : -1;
                     prevLen = ls; prevToff = wave_at(ft, k); prevCap = wave_at(fc, k); prevProps = ps;
                     prevMarker = (mt & MT_M_MARKER) != 0; prevLast = wave_at(fe, k);
                 }
             } else {
-                sc->hold[nh++] = s;
+                sc->hold[nh] = s; sc->holdLen[nh] = wave_at(fl, k); nh++;
                 prev = -1;
             }
         }
         wave_sync();
         return nh;
     }
-    MT_HD void updatePathLens(int B) {                        // blockUpdatePathLengths(..., newStructure)
+    // blockUpdatePathLengths(..., newStructure); firstLen >= 0: B's length is known.
+    MT_HD void updatePathLens(int B, int firstLen = -1) {
         while (B >= 0) {
             MT_EV2(1, 1);
             const BlkH h = head(B);
-            bk(B).len = sumObs(B, h.n, h.height);
+            bk(B).len = firstLen >= 0 ? firstLen : sumObs(B, h.n, h.height);
+            firstLen = -1;
             B = h.parent;
         }
     }
@@ -1036,19 +1080,18 @@ template <int RES> struct MtEngT {
         for (;;) {
             BlkH ph;
             auto pch = blkLoad(P, ph);
-            int nh = 0, chh = 0;
-            for (int i = 0; i < ph.n; i++) {
-                const int cb = wave_at(pch, i);
-                const BlkH bh = head(cb);
-                chh = bh.height;
-                if (bh.height == 0) nh = scourLeaf(cb, bh.n, nh);
-                else {
-                    const int base = nh;
-                    wave_for(bh.n, [&](int k) MT_LAM { sc->hold[base + k] = bk(cb).c[k]; });
-                    nh += bh.n;
+            int nh = 0;
+            const int chh = ph.height - 1;                       // children of P are blocks of this height
+            if (chh == 0) nh = scourLeaves(pch, ph.n, 0);
+            else {
+                for (int i = 0; i < ph.n; i++) {
+                    const int cb = wave_at(pch, i);
+                    const int n = uni(bk(cb).n), base = nh;
+                    wave_for(n, [&](int k) MT_LAM { const int g = bk(cb).c[k]; sc->hold[base + k] = g; sc->holdLen[base + k] = bk(g).len; });
+                    nh += n;
                 }
-                freeBlock(cb);
             }
+            for (int i = 0; i < ph.n; i++) freeBlock(wave_at(pch, i));
             wave_sync();
             int cc = nh / (MT_MAXN / 2); if (cc > MT_MAXN - 1) cc = MT_MAXN - 1; if (cc < 1) cc = 1;
             const int base = nh / cc; int extra = nh % cc; int rd = 0;
@@ -1062,8 +1105,8 @@ template <int RES> struct MtEngT {
                 wave_for(cntc, [&](int i) MT_LAM { setChildParent(chh, sc->hold[r0 + i], NB); });
                 rd += cntc;
                 bk(NB).n = cntc; bk(NB).height = chh; bk(NB).parent = P; bk(NB).scour = -1;
+                bk(NB).len = wave_sum8(wave_map(cntc, [&](int i) MT_LAM { return sc->holdLen[r0 + i]; }));
                 wave_sync();
-                bk(NB).len = sumObs(NB, cntc, chh);
                 packed = wave_map(8, [&](int i) MT_LAM { return i == ni ? NB : own(packed, i); });
             }
             wave_for(8, [&](int i) MT_LAM { bk(P).c[i] = own(packed, i); });
@@ -1076,7 +1119,9 @@ template <int RES> struct MtEngT {
     }
     MT_HD void zamboni() {                                    // MT/mergeTree.ts:1412-1468
         MT_PB(t0);
+        MT_ZB(z0);
         zamboniInner();
+        MT_ZE(0, z0);
         MT_PE(MT_PH_ZAMBONI, t0);
     }
     MT_HD void zamboniInner() {
@@ -1085,7 +1130,9 @@ template <int RES> struct MtEngT {
             uValid = false;                                   // scour/pack may restructure
             MT_EV2(6, 1);
             MT_QB(q0); MT_QC(6);
+            MT_ZB(z5); MT_ZC(7);
             const MtHeapE e = heapGet();
+            MT_ZE(5, z5);
             MT_QE(5, q0);
             const int p = uni(row(e.seg).parent);
             uint32_t em = uni(row(e.seg).meta);
@@ -1094,16 +1141,24 @@ template <int RES> struct MtEngT {
             if (p >= 0 && uni(bk(p).scour) != 0) {
                 const BlkH h = head(p);
                 MT_QB(q1);
-                const int nh = scourLeaf(p, h.n, 0);
+                MT_ZB(z1);
+                const int nh = scourLeaves(wave_map(1, [&](int) MT_LAM { return p; }), 1, 0);
+                MT_ZE(1, z1);
                 MT_QE(7, q1);
+                MT_ZB(z6);
                 bk(p).scour = 0;
                 if (nh < h.n) {
                     wave_for(8, [&](int j) MT_LAM { bk(p).c[j] = j < nh ? sc->hold[j] : -1; });
                     bk(p).n = nh;
                     wave_sync();
-                    if (nh < MT_MAXN / 2 && h.parent >= 0) packParent(h.parent);
-                    else updatePathLens(p);
+                    if (nh < MT_MAXN / 2 && h.parent >= 0) { MT_ZB(z3); packParent(h.parent); MT_ZE(3, z3); }
+                    else {
+                        MT_ZB(z4);
+                        updatePathLens(p, wave_sum8(wave_map(nh, [&](int i) MT_LAM { return sc->holdLen[i]; })));
+                        MT_ZE(4, z4);
+                    }
                 }
+                MT_ZE(6, z6);
             }
             if (status) return;
         }

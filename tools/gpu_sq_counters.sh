@@ -17,6 +17,6 @@ python - <<'PY'
 import csv, glob
 for f in sorted(glob.glob("gpurun_out/sq/p*/p*_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith("mt_replay_kernel"):
+        if r["Kernel_Name"].startswith("mt_replay"):
             print(r["Counter_Name"], r["Counter_Value"])
 PY

@@ -23,7 +23,7 @@ c = dict(bench.CONFIGS[cfg]); c["docs"] = docs
 if len(sys.argv) > 3: c["ops"] = int(sys.argv[3])
 res = sys.argv[4] if len(sys.argv) > 4 else "lds"
 eng = Engine(docs, lib_path=lib, **bench.caps_for(c))
-eng.set_residency(res == "lds")
+eng.set_residency({"hbm": 0, "lds": 1, "blk": 2}[res])
 eng.upload_props(bench.ann_props()); eng.upload_names(['"c%d"' % i for i in range(64)])
 p = MtGenParams(7, docs, c["ops"], c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"], c["rem_len"], c["ann_sets"], c["rewrite"])
 eng.generate(p); eng.sync(); eng.generated_to_resident()
@@ -39,6 +39,8 @@ fn.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
 fn(eng.h, docs, raw.ctypes.data)
 tot = raw.sum(axis=0).astype(float)
 names = ["computeU", "split-walks", "insert-walk", "rangeMap", "zamboni", "op-total", "gen", "textGC"]
+if flag == "MT_PROFILE3":
+    names = ["zamboni", "scourLeaf", "appendText", "packParent", "updatePathLens", "heapGet", "after-scour", "pops(n)"]
 if flag == "MT_PROFILE2":
     names = ["walk blkLoad", "walk childLens", "walk levels(n)", "computeU", "computeU(n)", "heapGet", "heapGet(n)", "scourLeaf"]
 print(f"{flag} residency={res} ops={c['ops']}")
