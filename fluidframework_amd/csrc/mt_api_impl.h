@@ -144,7 +144,8 @@ void MT_FN(destroy)(mt_ctx* c) {
                   c->ck_rows, c->ck_blk, c->ck_heap, c->ck_win, c->ck_text, c->ck_pset, c->ck_hdr, c->ck_hold};
     for (void* p : ps) if (p) mtb_free(p);
     mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_pset_off,
-                            &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3};
+                            &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3,
+                            &c->b_ld_meta, &c->b_ld_seg, &c->b_ld_pay, &c->b_ld_plan, &c->b_ld_poff};
     for (auto* b : bs) if (b->p) mtb_free(b->p);
     mtb_fini(c);
     delete c;
@@ -248,6 +249,102 @@ int MT_FN(apply_batch)(mt_ctx* c, const mt_op_batch* B) {
     int rc = MT_FN(upload_batch)(c, B);
     if (rc) return rc;
     return MT_FN(replay_resident)(c);
+}
+// SnapshotLoader.loadBody's insertSegments calls as a device plan
+// (MT/snapshotLoader.ts:162-206).  Universal NonCollab segments collect in a
+// batch that every flush appends as one insertSegments call; the batch is never
+// emptied, so a later flush re-appends already-linked segments: such a flush
+// becomes one REFLUSH step (a no-op where the reference's walk falls off the
+// tree, aliasing -> MT_DS_UNSUPPORTED where it would link a segment twice).
+static bool mt_load_seg_ok(const mt_load_seg& g, int ms, int cs) {
+    if ((g.flags & MT_LS_CLIENT) && g.client >= 64) return false;
+    if (g.flags & MT_LS_SEQ) {
+        if (g.seq < 0 || g.seq > cs) return false;
+        if (g.seq != 0 && g.seq <= ms) return false;     // neither universal nor in the collab window
+    }
+    if (g.flags & MT_LS_REMOVED) {
+        if (g.removed_client >= 64 || g.removed_seq <= ms || g.removed_seq > cs) return false;
+    }
+    return true;
+}
+static void mt_load_plan(const mt_load_batch* B, uint32_t i, std::vector<MtLoadStep>& plan) {
+    const uint32_t s0 = B->seg_offsets[i], s1 = B->seg_offsets[i + 1], nh = B->header_segments[i];
+    const int ms = B->min_seq[i], cs = B->seq[i];
+    bool ok = ms >= 0 && ms <= cs;
+    for (uint32_t k = s0; k < s1 && ok; k++) ok = mt_load_seg_ok(B->segs[k], ms, cs);
+    if (!ok) { plan.push_back({0, MT_LD_UNSUPPORTED, 0, 0}); return; }
+    auto seglen = [&](uint32_t k) -> int {
+        const mt_load_seg& g = B->segs[s0 + k];
+        return (g.flags & MT_LS_MARKER) ? 1 : (int)g.payload_len;
+    };
+    std::vector<uint32_t> batch;
+    size_t linked = 0;                                   // batch entries appended by earlier flushes
+    auto flush = [&]() {
+        if (batch.empty()) return;
+        bool oldLinked = false;
+        for (size_t j = 0; j < linked; j++) if (seglen(batch[j]) > 0) { oldLinked = true; break; }
+        if (oldLinked) plan.push_back({0, batch.size() > linked ? MT_LD_REFLUSH_NEW : MT_LD_REFLUSH, MT_NONCOLLAB, 0});
+        else
+            for (size_t j = linked; j < batch.size(); j++)
+                plan.push_back({(int)batch[j], j == linked ? MT_LD_START : MT_LD_CONT, MT_NONCOLLAB, 0});
+        linked = batch.size();
+    };
+    for (uint32_t k = nh; k < s1 - s0; k++) {
+        const mt_load_seg& g = B->segs[s0 + k];
+        const int cli = (g.flags & MT_LS_CLIENT) ? (int)g.client : MT_NONCOLLAB;
+        const int sq = (g.flags & MT_LS_SEQ) ? g.seq : 0;
+        if (cli == MT_NONCOLLAB && sq == 0) batch.push_back(k);
+        else { flush(); plan.push_back({(int)k, MT_LD_START, cli, sq}); }
+    }
+    flush();
+}
+int MT_FN(load_snapshot)(mt_ctx* c, const mt_load_batch* B) {
+    if (!c || !B || !B->seg_offsets || (B->n_docs && (!B->doc_ids || !B->header_segments || !B->min_seq || !B->seq)))
+        { if (c) c->err = "null load batch arrays"; return MT_E_INVALID; }
+    const uint32_t n = B->n_docs;
+    if (n == 0) return MT_OK;
+    const uint32_t nseg = B->seg_offsets[n];
+    std::vector<uint32_t> meta(5ull * n + 1);           // docs | seg_off (n+1) | nhdr | ms | cs
+    std::vector<uint32_t> plan_off(n + 1, 0);
+    std::vector<MtLoadStep> plan;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t s0 = B->seg_offsets[i], s1 = B->seg_offsets[i + 1];
+        if (B->doc_ids[i] >= c->S.maxDocs) { c->err = "doc id out of range"; return MT_E_INVALID; }
+        if (s1 < s0 || s1 > nseg || B->header_segments[i] > s1 - s0) { c->err = "bad seg_offsets/header_segments"; return MT_E_INVALID; }
+        uint64_t expect = ~0ull;                          // text payloads contiguous per document
+        for (uint32_t k = s0; k < s1; k++) {
+            const mt_load_seg& g = B->segs[k];
+            if (g.flags & MT_LS_MARKER) continue;
+            if ((uint64_t)g.payload_off + g.payload_len > B->payload_units) { c->err = "payload out of range"; return MT_E_INVALID; }
+            if (expect != ~0ull && g.payload_off != expect) { c->err = "document text payloads must be contiguous"; return MT_E_INVALID; }
+            expect = (uint64_t)g.payload_off + g.payload_len;
+        }
+        for (uint32_t k = s0; k < s1; k++)
+            if (B->segs[k].prop_id >= 0 && (uint32_t)B->segs[k].prop_id >= c->S.p_nsets) { c->err = "prop_id out of range (mt_set_props first)"; return MT_E_INVALID; }
+        plan_off[i] = (uint32_t)plan.size();
+        mt_load_plan(B, i, plan);
+    }
+    plan_off[n] = (uint32_t)plan.size();
+    for (uint32_t i = 0; i < n; i++) {
+        meta[i] = B->doc_ids[i]; meta[n + i] = B->seg_offsets[i];
+        meta[2ull * n + 1 + i] = B->header_segments[i];
+        meta[3ull * n + 1 + i] = (uint32_t)B->min_seq[i]; meta[4ull * n + 1 + i] = (uint32_t)B->seq[i];
+    }
+    meta[2ull * n] = nseg;
+    int rc;
+#define UP(buf, src, bytes) if ((rc = mtb_ensure(c, c->buf, (bytes)))) return rc; if ((bytes) && (src)) mtb_h2d(c, c->buf.p, (src), (bytes));
+    static_assert(sizeof(mt_load_seg) == sizeof(MtLoadSeg) && sizeof(MtLoadSeg) == 32, "load segment layout");
+    UP(b_ld_meta, meta.data(), 4 * meta.size()) UP(b_ld_seg, B->segs, sizeof(MtLoadSeg) * nseg)
+    UP(b_ld_pay, B->payload, 2 * B->payload_units) UP(b_ld_plan, plan.data(), sizeof(MtLoadStep) * plan.size())
+    UP(b_ld_poff, plan_off.data(), 4ull * (n + 1))
+#undef UP
+    MtLoad L;
+    const uint32_t* m = (const uint32_t*)c->b_ld_meta.p;
+    L.docs = m; L.seg_off = m + n; L.nhdr = m + 2 * n + 1;
+    L.ms = (const int32_t*)(m + 3 * n + 1); L.cs = (const int32_t*)(m + 4 * n + 1);
+    L.segs = (const MtLoadSeg*)c->b_ld_seg.p; L.payload = (const uint16_t*)c->b_ld_pay.p;
+    L.plan_off = (const uint32_t*)c->b_ld_poff.p; L.plan = (const MtLoadStep*)c->b_ld_plan.p;
+    return mtb_launch_load(c, L, n);
 }
 int MT_FN(set_residency)(mt_ctx* c, int use_lds, int rows, int blocks, int heap) {
     if (!c || use_lds < 0 || use_lds > 2 || rows < 0 || blocks < 0 || heap < 0 || rows > MT_L_ROWS ||

@@ -190,6 +190,31 @@ struct MtOps {                                // device copy of an mt_op_batch
     uint32_t n_runs;
 };
 
+// Snapshot load (mt_load_snapshot): the segments of each document (mt_load_seg)
+// and the host's plan of loadBody's insertSegments calls (MT/snapshotLoader.ts:162-206).
+struct __attribute__((aligned(16))) MtLoadSeg {
+    uint8_t flags, pad0; uint16_t client;
+    int32_t seq, rseq;
+    uint16_t rclient; int16_t prop;
+    uint32_t poff, plen;
+    uint32_t pad1[2];
+};
+// One step of the body plan: START = first segment of an insertSegments call
+// (ensureIntervalBoundary at the observer's length, then insert), CONT = a later
+// segment of the same call (insertPos += previous cachedLength, blockInsert
+// :2207-2241), REFLUSH[_NEW] = a flush of loadBody's never-emptied batch that
+// would insert already-linked segments [followed by new ones], UNSUPPORTED =
+// the host rejected the document (nothing is loaded).
+enum { MT_LD_START = 0, MT_LD_CONT = 1, MT_LD_REFLUSH = 2, MT_LD_REFLUSH_NEW = 3, MT_LD_UNSUPPORTED = 4 };
+struct MtLoadStep { int seg, kind, cli, seq; };
+struct MtLoad {
+    const uint32_t* docs; const uint32_t* seg_off; const uint32_t* nhdr;
+    const int32_t* ms; const int32_t* cs;
+    const MtLoadSeg* segs; const uint16_t* payload;
+    const uint32_t* plan_off; const MtLoadStep* plan;
+};
+#define MT_NONCOLLAB 254              // NonCollabClient (MT/constants.ts) in the 8-bit client field
+
 struct MtGen {                                // device stream generator parameters
     unsigned long long seed;
     uint32_t ops, clients, lag_max, pct_insert, pct_remove, ins_len_max, rem_len_max, n_ann_sets, pct_rewrite;
@@ -243,7 +268,7 @@ MT_INLINE bool vis_rc(int seq, uint32_t meta, int rseq, unsigned long long ovl, 
     if (!(cl == c || seq <= r)) return false;
     if (meta & MT_M_REMOVED) {
         const int rc = (int)((meta & MT_M_RCLIENT) >> 8);
-        if (rc == c || ((ovl >> c) & 1ull) || rseq <= r) return false;
+        if (rc == c || (c < 64 && ((ovl >> c) & 1ull)) || rseq <= r) return false;
     }
     return true;
 }
@@ -1316,6 +1341,145 @@ template <int RES> struct MtEngT {
         uValid = false;
     }
     /* -------------------------------------------------------- op apply -- */
+    /* ---------------------------------------------------- snapshot load -- */
+    // The header chunk (SnapshotLoader.loadHeader, MT/snapshotLoader.ts:126-160):
+    // specToSegment per segment (:93-124) into rows 0..nh-1, reloadFromSegments
+    // (mergeTree.ts:1185-1238: blocks of 7 children built level by level from
+    // the leaves), then startCollaboration(minSeq, currentSeq) (:1243).  The
+    // collab window gets every row with seq > minSeq or a removal.  Runs on a
+    // freshly opened document.
+    MT_HD void loadHeader(const MtLoad& Ld, uint32_t s0, int nh, int ms, int cs) {
+        minSeq = ms; curSeq = cs;
+        if (nh == 0) return;                                  // root stays open()'s empty block
+        if (nh > (int)S.rowCap) { status |= MT_DS_OOM_ROWS; return; }
+        const MtLoadSeg* G = Ld.segs + s0;
+        const uint32_t pbase = uni(G[0].poff);
+        int ttot = 0;
+        for (int base = 0; base < nh; base += MT_WAVE) {
+            const int m = (nh - base) < MT_WAVE ? (nh - base) : MT_WAVE;
+            auto tl = wave_map(m, [&](int k) MT_LAM {
+                const MtLoadSeg g = G[base + k];
+                return (g.flags & MT_LS_MARKER) ? 0 : (int)g.plen;
+            });
+            ttot += wave_sum(tl);
+        }
+        if (ttot > (int)S.textCap) { status |= MT_DS_OOM_TEXT; return; }
+        const int t0 = textTop;
+        for (int base = 0; base < nh; base += MT_WAVE) {
+            const int m = (nh - base) < MT_WAVE ? (nh - base) : MT_WAVE;
+            wave_for(m, [&](int k) MT_LAM {
+                const MtLoadSeg g = G[base + k];
+                const int s = base + k;
+                const bool mk = (g.flags & MT_LS_MARKER) != 0, rm = (g.flags & MT_LS_REMOVED) != 0;
+                const int cl = (g.flags & MT_LS_CLIENT) ? (int)g.client : MT_NONCOLLAB;
+                MtRow& w = row(s);
+                w.len = mk ? 1 : (int)g.plen;
+                w.seq = (g.flags & MT_LS_SEQ) ? g.seq : 0;
+                w.rseq = rm ? g.rseq : MT_NOREM;
+                w.meta = (uint32_t)cl | (rm ? (((uint32_t)g.rclient << 8) | MT_M_REMOVED) : 0u) | (mk ? MT_M_MARKER : 0u);
+                w.ovl = 0ull; w.props = -1; w.parent = -1;
+                w.toff = mk ? (int)g.plen : t0 + (int)(g.poff - pbase);
+                w.tcap = mk ? 0 : (int)g.plen;
+            });
+        }
+        for (int base = 0; base < ttot; base += MT_WAVE) {
+            const int m = (ttot - base) < MT_WAVE ? (ttot - base) : MT_WAVE;
+            wave_for(m, [&](int k) MT_LAM { text[t0 + base + k] = Ld.payload[pbase + base + k]; });
+        }
+        textTop = t0 + ttot; rowTop = nh; c_ins += (uint64_t)ttot;
+        wave_sync();
+        for (int i = 0; i < nh; i++) {                        // TextSegment.make / Marker.make: addProperties(props)
+            const int pid = uni((int)G[i].prop);
+            if (pid >= 0) { const int ps = applyPropSet(-1, pid, false); row(i).props = ps; }
+        }
+        if (status) return;
+        for (int base = 0; base < nh; base += MT_WAVE) {      // collab window
+            const int m = (nh - base) < MT_WAVE ? (nh - base) : MT_WAVE;
+            auto inw = wave_map(m, [&](int k) MT_LAM {
+                const int s = base + k;
+                return row(s).seq > minSeq || (row(s).meta & MT_M_REMOVED) != 0;
+            });
+            const int cnt = wave_count(inw);
+            if (winN + cnt > (int)S.winCap) { status |= MT_DS_OOM_WINDOW; return; }
+            auto rk = wave_rank(inw);
+            const int w0 = winN;
+            wave_for(m, [&](int k) MT_LAM {
+                if (own(inw, k)) { const int s = base + k; wn(w0 + own(rk, k)) = s; row(s).meta = row(s).meta | MT_M_INWIN; }
+            });
+            winN += cnt;
+        }
+        if (winN > winHW) winHW = winN;
+        // reloadFromSegments: level h groups the nodes of level h-1 seven at a time
+        blkTop = 0; blkFree = -1; blkFreeN = 0;
+        int first = 0, count = nh, h = 0;
+        for (;;) {
+            const int nb = (count + MT_MAXN - 2) / (MT_MAXN - 1);
+            if (blkTop + nb > (int)blkCap) { status |= MT_DS_OOM_BLOCKS; return; }
+            const int b0 = blkTop; blkTop += nb;
+            const int lvl = h, f0 = first, cnt = count;
+            for (int base = 0; base < nb; base += MT_WAVE) {
+                const int m = (nb - base) < MT_WAVE ? (nb - base) : MT_WAVE;
+                wave_for(m, [&](int k) MT_LAM {
+                    const int B = b0 + base + k, c0 = (base + k) * (MT_MAXN - 1);
+                    const int n = (cnt - c0) < (MT_MAXN - 1) ? (cnt - c0) : (MT_MAXN - 1);
+                    int len = 0;
+                    for (int i = 0; i < MT_MAXN; i++) {
+                        const int id = i < n ? f0 + c0 + i : -1;
+                        if (id >= 0) {
+                            if (lvl == 0) { row(id).parent = B; len += (row(id).meta & MT_M_REMOVED) ? 0 : row(id).len; }
+                            else { bk(id).parent = B; len += bk(id).len; }
+                        }
+                        bk(B).c[i] = id;
+                    }
+                    bk(B).n = n; bk(B).len = len; bk(B).height = lvl; bk(B).parent = -1; bk(B).scour = -1;
+                });
+            }
+            wave_sync();
+            if (nb == 1) { root = b0; height = lvl; return; }
+            first = b0; count = nb; h++;
+        }
+    }
+    // One segment of a loadBody insertSegments call (mergeTree.ts:1974-2011,
+    // blockInsert :2159-2242) at `pos` under perspective (UniversalSequenceNumber,
+    // cli); `boundary`: first segment of the call (ensureIntervalBoundary first).
+    // Returns the segment's cachedLength (0: skipped, as blockInsert skips it).
+    MT_HD int loadInsert(const MtLoad& Ld, uint32_t gi, int pos, int cli, int sq, bool boundary) {
+        if (boundary) { walk(MT_WALK_SPLIT, pos, 0, cli, -1, 0); if (status) return 0; }
+        const MtLoadSeg* g = Ld.segs + gi;
+        const uint32_t fl = uni((uint32_t)g->flags);
+        const bool mk = (fl & MT_LS_MARKER) != 0, rm = (fl & MT_LS_REMOVED) != 0;
+        const int plen = mk ? 0 : uni((int)g->plen);
+        const int L = mk ? 1 : plen;
+        if (L == 0) return 0;
+        const int n = allocRow();
+        if (n < 0) return 0;
+        row(n).len = L; row(n).seq = sq; row(n).rseq = rm ? uni(g->rseq) : MT_NOREM;
+        row(n).meta = (uint32_t)cli | (rm ? (((uint32_t)uni((int)g->rclient) << 8) | MT_M_REMOVED) : 0u) | (mk ? MT_M_MARKER : 0u);
+        row(n).ovl = 0ull; row(n).parent = -1; row(n).props = -1;
+        row(n).tcap = plen;
+        if (mk) row(n).toff = uni((int)g->plen);
+        else {
+            const int t0 = textAlloc(plen);
+            if (t0 < 0) return 0;
+            row(n).toff = t0;
+            const uint16_t* src = Ld.payload + uni((int)g->poff);
+            for (int base = 0; base < plen; base += MT_WAVE) {
+                const int m = (plen - base) < MT_WAVE ? (plen - base) : MT_WAVE;
+                wave_for(m, [&](int k) MT_LAM { text[t0 + base + k] = src[base + k]; });
+            }
+            c_ins += (uint64_t)plen;
+        }
+        const int pid = uni((int)g->prop);
+        if (pid >= 0) { const int ps = applyPropSet(-1, pid, false); row(n).props = ps; }
+        wave_sync();
+        if (status) return 0;
+        const int w = walk(MT_WALK_INSERT, pos, 0, cli, n, rm ? 0 : L);
+        if (w != MT_W_OK || uni(row(n).parent) < 0) { status |= MT_DS_INSERT_FAILED; return 0; }
+        c_rows += 2;
+        if (sq > minSeq || rm) winAdd(n);
+        if (sq > minSeq) addToLRUSet(n, sq);
+        return L;
+    }
     MT_HD void opInsert(int pos, int r, int c, int sq, const uint16_t* src, int plen, bool marker, int refType, int segProps) {
         // MergeTree.insertSegments (MT/mergeTree.ts:1974-2011)
         MT_PB(t0);
@@ -1382,4 +1546,30 @@ template <int RES> struct MtEngT {
     }
 };
 using MtEng = MtEngT<MT_RES_HBM>;
+
+// SnapshotLoader for document i of a load batch (MT/snapshotLoader.ts:39-222) on
+// a freshly opened engine document: header, collaboration start, body plan.
+template <class Eng>
+MT_HD void mt_load_doc(Eng& e, const MtLoad& Ld, uint32_t i) {
+    const uint32_t s0 = Ld.seg_off[i], p0 = Ld.plan_off[i], p1 = Ld.plan_off[i + 1];
+    if (p1 > p0 && uni(Ld.plan[p0].kind) == MT_LD_UNSUPPORTED) { e.status |= MT_DS_UNSUPPORTED; return; }
+    e.loadHeader(Ld, s0, (int)Ld.nhdr[i], Ld.ms[i], Ld.cs[i]);
+    int pos = 0, prevLen = 0;
+    for (uint32_t k = p0; k < p1 && !e.status; k++) {
+        const MtLoadStep st = Ld.plan[k];
+        const int kind = uni(st.kind);
+        if (kind == MT_LD_REFLUSH || kind == MT_LD_REFLUSH_NEW) {
+            // The batch's first segment is already linked: the walk links it a
+            // second time iff the observer length is within the NonCollab view.
+            const int p = uni(e.bk(e.root).len);
+            if (p <= e.perspectiveLength(0, MT_NONCOLLAB)) e.status |= MT_DS_UNSUPPORTED;
+            else if (kind == MT_LD_REFLUSH_NEW) e.status |= MT_DS_INSERT_FAILED;   // a new segment falls off
+            continue;
+        }
+        if (kind == MT_LD_UNSUPPORTED) { e.status |= MT_DS_UNSUPPORTED; break; }
+        pos = kind == MT_LD_START ? uni(e.bk(e.root).len) : pos + prevLen;
+        prevLen = e.loadInsert(Ld, s0 + (uint32_t)uni(st.seg), pos, uni(st.cli), uni(st.seq), kind == MT_LD_START);
+        if (!e.status) e.zamboni();            // insertSegments ends with zamboniSegments (:2007-2010)
+    }
+}
 

@@ -90,6 +90,16 @@ __global__ __launch_bounds__(64) void mt_open_kernel(MtState S, uint32_t first) 
     e.open();
     e.store(doc);
 }
+// Snapshot load (mt_load_snapshot): one wave per document, pools in HBM.
+__global__ __launch_bounds__(64) void mt_load_kernel(MtState S, MtLoad Ld) {
+    __shared__ MtScratch sc;
+    const uint32_t doc = Ld.docs[blockIdx.x];
+    MtEng e;
+    e.bind(S, doc, &sc);
+    e.open();
+    mt_load_doc(e, Ld, blockIdx.x);
+    e.store(doc);
+}
 __global__ __launch_bounds__(64) void mt_update_seq_kernel(MtState S, const uint32_t* docs, const int32_t* msn, const int32_t* seq) {
     __shared__ MtScratch sc;
     const uint32_t doc = docs[blockIdx.x];
@@ -179,6 +189,12 @@ static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
 static int mtb_launch_open(mt_ctx* c, uint32_t first, uint32_t n) {
     (void)hipGetLastError();
     hipLaunchKernelGGL(mt_open_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, first);
+    return mtb_check(c);
+}
+static int mtb_launch_load(mt_ctx* c, const MtLoad& L, uint32_t n) {
+    if (!n) return MT_OK;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(mt_load_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, L);
     return mtb_check(c);
 }
 static int mtb_launch_update_seq(mt_ctx* c, const uint32_t* docs, const int32_t* msn, const int32_t* seq, uint32_t n) {

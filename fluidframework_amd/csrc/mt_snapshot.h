@@ -233,7 +233,7 @@ inline void dump_rows(const MtSnapView& v, const MtNames& nm, std::vector<int32_
     auto f = [&](int s) {
         int32_t r[12];
         const uint32_t mt = v.R[s].meta;
-        r[0] = v.R[s].len; r[1] = v.R[s].seq; r[2] = (int32_t)(mt & MT_M_CLIENT);
+        r[0] = v.R[s].len; r[1] = v.R[s].seq; r[2] = (mt & MT_M_CLIENT) == MT_NONCOLLAB ? -1 : (int32_t)(mt & MT_M_CLIENT);
         const bool removed = (mt & MT_M_REMOVED) != 0;
         r[3] = removed ? v.R[s].rseq : INT32_MIN; r[4] = removed ? (int32_t)((mt & MT_M_RCLIENT) >> 8) : -1;
         r[5] = (int32_t)(v.R[s].ovl & 0xFFFFFFFFull); r[6] = (int32_t)(v.R[s].ovl >> 32);

@@ -90,6 +90,7 @@ def _bind(lib, prefix: str):
         generated_to_resident=f("generated_to_resident", ctypes.c_int, [P]),
         generated_copy_dev=f("generated_copy_dev", ctypes.c_int, [P, U32, U32, P, P]),
         upload_batch_dev=f("upload_batch_dev", ctypes.c_int, [P, U32, P, P, P, P, ctypes.c_uint64]),
+        load_snapshot=f("load_snapshot", ctypes.c_int, [P, P]),
     )
 
 
@@ -295,6 +296,11 @@ class Engine:
         out = np.zeros((len(d), 10), np.int32)
         self._check(self.fn["doc_pools"](self.h, len(d), d.ctypes.data, out.ctypes.data), "mt_doc_pools")
         return out
+
+    def load_snapshot(self, batch):
+        """mt_load_snapshot of a snapshot_load.LoadBatch (upload_props first if it interned props)."""
+        self.upload_props()
+        self._check(self.fn["load_snapshot"](self.h, ctypes.byref(batch.to_c())), "mt_load_snapshot")
 
     def update_seq(self, docs, msn, seq):
         d, m, s = _u32(docs), _i32(msn), _i32(seq)

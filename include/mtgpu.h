@@ -26,6 +26,11 @@
  *   mt_get_text                 `createTextHelper().getText(currentSeq, obs)`
  *                               MT/textSegment.ts:163-181
  *   mt_dump_segments            walkAllSegments (mergeTree.ts:2998) row dump, parity
+ *   mt_load_snapshot            `SnapshotLoader.initialize` + `loadBody`
+ *                               (MT/snapshotLoader.ts:39-222): reloadFromSegments
+ *                               (mergeTree.ts:1185-1238) of the header chunk,
+ *                               startOrUpdateCollaboration, then the body chunks
+ *                               appended through insertSegments (mergeTree.ts:1974)
  *
  * Conventions: every function returns an int status (MT_OK == 0); no exception
  * crosses the ABI.  Per-document errors (the reference's `assert` throws,
@@ -145,6 +150,44 @@ typedef struct mt_limits {
 
 typedef struct mt_ctx mt_ctx;
 
+/* ---- snapshot load (MT/snapshotLoader.ts) ------------------------------- */
+/* One snapshot segment, i.e. one element of a chunk's `segments` array after
+ * the host's JSON.parse (IJSONSegment or IJSONSegmentWithMergeInfo,
+ * MT/snapshotChunks.ts:63-76), as SnapshotLoader.specToSegment reads it
+ * (MT/snapshotLoader.ts:93-124). 32 bytes. */
+#define MT_LS_SEQ     0x01u   /* spec.seq present (else UniversalSequenceNumber 0)  */
+#define MT_LS_CLIENT  0x02u   /* spec.client present (else NonCollabClient)         */
+#define MT_LS_REMOVED 0x04u   /* spec.removedSeq/removedClient present               */
+#define MT_LS_MARKER  0x08u   /* {"marker":{"refType":n}} (else a text segment)      */
+typedef struct mt_load_seg {
+    uint8_t  flags;           /* MT_LS_*                                              */
+    uint8_t  pad0;
+    uint16_t client;          /* per-document client index (MT_LS_CLIENT)            */
+    int32_t  seq;             /* MT_LS_SEQ                                            */
+    int32_t  removed_seq;     /* MT_LS_REMOVED                                        */
+    uint16_t removed_client;  /* MT_LS_REMOVED                                        */
+    int16_t  prop_id;         /* mt_set_props set of spec.props, -1: none             */
+    uint32_t payload_off;     /* text: UTF-16 offset into payload                      */
+    uint32_t payload_len;     /* text: UTF-16 units; marker: refType                   */
+    uint32_t pad1[2];
+} mt_load_seg;
+/* Per document: segments [seg_offsets[i], seg_offsets[i+1]) in chunk order
+ * (header chunk first, then body_0, body_1, ...), the first header_segments[i]
+ * of them from the header chunk; min_seq/seq = headerMetadata.minSequenceNumber
+ * (sequenceNumber when absent) / .sequenceNumber.  The text payloads of one
+ * document must be contiguous and in segment order in `payload`. */
+typedef struct mt_load_batch {
+    uint32_t           n_docs;
+    const uint32_t*    doc_ids;          /* [n_docs] engine document slots       */
+    const uint32_t*    seg_offsets;      /* [n_docs+1]                            */
+    const uint32_t*    header_segments;  /* [n_docs]                              */
+    const int32_t*     min_seq;          /* [n_docs]                              */
+    const int32_t*     seq;              /* [n_docs]                              */
+    const mt_load_seg* segs;
+    const uint16_t*    payload;
+    uint64_t           payload_units;
+} mt_load_batch;
+
 /* Counters the engine accumulates per document (algorithmic-byte accounting,
  * B_op = 32 + 4 L_ins + 32 (R_r + R_w) + 64 D + 64 Z). */
 typedef struct mt_doc_counters {
@@ -251,6 +294,18 @@ int  mt_get_text(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
 /* walkAllSegments order dump: per row {len, seq, client, removed_seq (INT32_MIN =
  * undefined), removed_client, overlap_mask_lo, overlap_mask_hi, prop_set(-1 none),
  * marker_ref_type(-1 text), text_off, parent_block, flags}. 12 int32 per row. */
+/* SnapshotLoader (MT/snapshotLoader.ts:39-222) for each document of the batch:
+ * the slot is reset, the header segments are built bottom-up into the B-tree
+ * (reloadFromSegments, mergeTree.ts:1185-1238), collaboration starts at
+ * (min_seq, seq) (client.ts:1073, mergeTree.ts:1243), and the body segments are
+ * appended as loadBody does (snapshotLoader.ts:162-206: runs of universal
+ * segments batched, others one by one, at the observer's length under
+ * perspective (UniversalSequenceNumber, segment client)).  Where the reference
+ * would throw ("MergeTree insert failed", mergeTree.ts:2228) the document gets
+ * MT_DS_INSERT_FAILED; where its never-emptied loadBody batch would link one
+ * segment object twice the document gets MT_DS_UNSUPPORTED.  Stream-ordered;
+ * status words after mt_sync. */
+int  mt_load_snapshot(mt_ctx* ctx, const mt_load_batch* batch);
 int  mt_dump_segments(mt_ctx* ctx, uint32_t doc_id, int32_t** rows, uint32_t* n_rows);
 void mt_free(void* p);
 

@@ -645,6 +645,54 @@ struct Tree {
     void ensureIntervalBoundary(int pos, int refSeq, int clientId) {                        // :2260
         updateRoot(insertingWalk(root, pos, refSeq, clientId, TreeMaintSeq, LEAF_SPLIT, nullptr));
     }
+    // reloadFromSegments (MT/mergeTree.ts:1185-1238): blocks of MaxNodesInBlock-1
+    // children, built layer by layer from the leaves; collaboration not yet started.
+    void reloadFromSegments(const std::vector<Seg*>& segsIn) {
+        const int maxChildren = MaxNodesInBlock - 1;
+        if (segsIn.empty()) { root = makeBlock(0); return; }
+        std::vector<Node*> nodes(segsIn.begin(), segsIn.end());
+        for (;;) {
+            const int blockCount = ((int)nodes.size() + maxChildren - 1) / maxChildren;
+            std::vector<Node*> blocksL(blockCount);
+            size_t nodeIndex = 0;
+            for (int bi = 0; bi < blockCount; bi++) {
+                Block* b = makeBlock(0);
+                blocksL[bi] = b;
+                for (int ci = 0; ci < maxChildren && nodeIndex < nodes.size(); ci++, nodeIndex++) {   // addNode :1176-1183
+                    int idx = b->childCount++;
+                    assignChild(b, nodes[nodeIndex], idx);
+                }
+                blockUpdate(b);
+            }
+            if (blockCount == 1) { root = (Block*)blocksL[0]; return; }
+            nodes = blocksL;
+        }
+    }
+    // insertSegments with several segments as SnapshotLoader.loadBody calls it
+    // (mergeTree.ts:1974-2011, blockInsert :2159-2242).  loadBody never empties its
+    // batch (snapshotLoader.ts:188-206), so a segment may come back already
+    // linked: its walk either falls off the tree (no-op: parent is still set, so
+    // no throw) or would link the same object twice, which the oracle does not
+    // model (MT_DS_UNSUPPORTED).
+    void insertSegmentsLoad(int pos, const std::vector<Seg*>& in, int refSeq, int clientId, int seq) {
+        ensureIntervalBoundary(pos, refSeq, clientId);
+        int insertPos = pos;
+        for (Seg* seg : in) {
+            if (seg->cachedLength > 0) {
+                seg->seq = seq; seg->clientId = clientId;
+                if (seg->parent) {
+                    if (insertPos <= getLength(refSeq, clientId)) { status |= MT_DS_UNSUPPORTED; return; }
+                } else {
+                    Block* sn = insertingWalk(root, insertPos, refSeq, clientId, seq, LEAF_INSERT, seg);
+                    if (!seg->parent) { status |= MT_DS_INSERT_FAILED; return; }
+                    updateRoot(sn);
+                    if (collaborating && seg->seq > minSeq) addToLRUSet(seg, seg->seq);
+                }
+                insertPos += seg->cachedLength;
+            }
+        }
+        if (collaborating && seq != UnassignedSeq) zamboni();
+    }
     void addToLRUSet(Seg* s, int seq) {                                                      // :1262-1272
         if (s->parent->needsScour != 1 && seq > currentSeq) { s->parent->needsScour = 1; heapAdd({s, seq}); }
     }
@@ -1041,6 +1089,107 @@ static long long g_verify_bad = 0, g_verify_checks = 0;
 
 extern "C" {
 
+/* ---- SnapshotLoader (MT/snapshotLoader.ts:39-222) ---- */
+static const JVal* jget(const JVal& o, const char16_t* k) {
+    if (o.t != JVal::Obj) return nullptr;
+    int i = obj_find(o, u16s(k));
+    return i >= 0 ? &o.ovals[i] : nullptr;
+}
+static std::string jquote(const u16s& s) { std::string o; quote(o, s); return o; }
+// getOrAddShortClientId for a long id met in a snapshot (client.ts:658-682).
+static int load_short_id(Doc& d, const u16s& longId) {
+    std::string nm = jquote(longId);
+    auto it = d.nameToShort.find(nm);
+    if (it != d.nameToShort.end()) return it->second;
+    int id = (int)d.shortToName.size();
+    d.nameToShort[nm] = id; d.shortToName.push_back(nm);
+    int stream = -1;
+    for (int i = 0; i < (int)d.names.size(); i++) if (d.names[i] == nm) { stream = i; break; }
+    d.shortToStream.push_back(stream);
+    if (stream >= 0) { if ((int)d.streamToShort.size() <= stream) d.streamToShort.resize(stream + 1, -1); d.streamToShort[stream] = id; }
+    return id;
+}
+// SharedStringFactory.segmentFromSpec (sequenceFactory.ts:31-37): TextSegment.fromJSONObject
+// (textSegment.ts:31-39), else Marker.fromJSONObject (mergeTree.ts:655-662).
+static Seg* segFromSpec(Doc& d, const JVal& spec) {
+    const JVal* props = nullptr;
+    Seg* s = nullptr;
+    if (spec.t == JVal::Str) { s = d.t.makeSeg(); s->text = spec.s; s->cachedLength = (int)spec.s.size(); }
+    else if (spec.t == JVal::Obj && jget(spec, u"text")) {
+        const JVal* tx = jget(spec, u"text");
+        if (tx->t != JVal::Str) return nullptr;
+        s = d.t.makeSeg(); s->text = tx->s; s->cachedLength = (int)tx->s.size();
+        props = jget(spec, u"props");
+    } else if (spec.t == JVal::Obj && jget(spec, u"marker")) {
+        const JVal* mk = jget(spec, u"marker"); const JVal* rt = mk ? jget(*mk, u"refType") : nullptr;
+        if (!rt || rt->t != JVal::Num) return nullptr;
+        s = d.t.makeSeg(); s->marker = true; s->refType = (int)rt->n; s->cachedLength = 1;
+        props = jget(spec, u"props");
+    } else return nullptr;
+    if (props && truthy(props)) {                                    // make(..., props) -> addProperties(props)
+        if (props->t != JVal::Obj) return nullptr;
+        s->hasProps = true; s->props = make_obj();
+        for (int i : obj_order(*props)) {
+            if (props->ovals[i].t == JVal::Null) obj_del(s->props, props->okeys[i]);
+            else obj_set(s->props, props->okeys[i], props->ovals[i]);
+        }
+    }
+    return s;
+}
+// SnapshotLoader.specToSegment (snapshotLoader.ts:93-124).
+static Seg* loadSpec(Doc& d, const JVal& spec) {
+    const JVal* js = spec.t == JVal::Obj ? jget(spec, u"json") : nullptr;     // hasMergeInfo, snapshotChunks.ts:74-76
+    if (!js) {
+        Seg* s = segFromSpec(d, spec);
+        if (s) { s->seq = UniversalSeq; s->clientId = NonCollabClient; }
+        return s;
+    }
+    Seg* s = segFromSpec(d, *js);
+    if (!s) return nullptr;
+    const JVal* cl = jget(spec, u"client"); const JVal* sq = jget(spec, u"seq");
+    const JVal* rs = jget(spec, u"removedSeq"); const JVal* rc = jget(spec, u"removedClient");
+    s->clientId = (cl && cl->t == JVal::Str) ? load_short_id(d, cl->s) : NonCollabClient;
+    s->seq = (sq && sq->t == JVal::Num) ? (int)sq->n : UniversalSeq;
+    if (rs && rs->t == JVal::Num) { s->hasRemoved = true; s->removedSeq = (int)rs->n; }
+    if (rc && rc->t == JVal::Str) { s->hasRemoved = true; s->removedClientId = load_short_id(d, rc->s); }
+    return s;
+}
+// toLatestVersion (snapshotChunks.ts:137-160): a V1 chunk, or a legacy chunk
+// (version undefined) with its header metadata built as
+// buildHeaderMetadataForLegecyChunk does (:162-180).
+struct LoadChunk { bool ok = false; const JVal* segs = nullptr; int segmentCount = 0, length = 0;
+                   bool hasMeta = false; bool hasMin = false; int minSeq = 0, seq = 0, totalLength = 0, totalSegmentCount = 0, nChunks = 1; };
+static LoadChunk load_chunk(const JVal& c, bool header) {
+    LoadChunk r;
+    const JVal* ver = jget(c, u"version");
+    auto num = [&](const JVal* v, int& out) { if (v && v->t == JVal::Num) { out = (int)v->n; return true; } return false; };
+    if (ver && ver->t == JVal::Str && ver->s == u"1") {
+        r.segs = jget(c, u"segments"); num(jget(c, u"segmentCount"), r.segmentCount); num(jget(c, u"length"), r.length);
+        const JVal* hm = header ? jget(c, u"headerMetadata") : nullptr;
+        if (hm && hm->t == JVal::Obj) {
+            r.hasMeta = true; r.hasMin = num(jget(*hm, u"minSequenceNumber"), r.minSeq); num(jget(*hm, u"sequenceNumber"), r.seq);
+            num(jget(*hm, u"totalLength"), r.totalLength); num(jget(*hm, u"totalSegmentCount"), r.totalSegmentCount);
+            const JVal* oc = jget(*hm, u"orderedChunkMetadata"); r.nChunks = (oc && oc->t == JVal::Arr) ? (int)oc->arr.size() : 1;
+        }
+    } else if (!ver) {
+        r.segs = jget(c, u"segmentTexts"); num(jget(c, u"chunkSegmentCount"), r.segmentCount); num(jget(c, u"chunkLengthChars"), r.length);
+        if (header) {
+            const JVal* hm = jget(c, u"headerMetadata");
+            if (hm && hm->t == JVal::Obj) {
+                r.hasMeta = true; r.hasMin = num(jget(*hm, u"minSequenceNumber"), r.minSeq); num(jget(*hm, u"sequenceNumber"), r.seq);
+                num(jget(*hm, u"totalLength"), r.totalLength); num(jget(*hm, u"totalSegmentCount"), r.totalSegmentCount);
+                const JVal* oc = jget(*hm, u"orderedChunkMetadata"); r.nChunks = (oc && oc->t == JVal::Arr) ? (int)oc->arr.size() : 1;
+            } else {
+                r.hasMeta = true; r.hasMin = num(jget(c, u"chunkMinSequenceNumber"), r.minSeq); num(jget(c, u"chunkSequenceNumber"), r.seq);
+                num(jget(c, u"totalLengthChars"), r.totalLength); num(jget(c, u"totalSegmentCount"), r.totalSegmentCount);
+                r.nChunks = r.length < r.totalLength ? 2 : 1;
+            }
+        }
+    } else return r;
+    r.ok = r.segs && r.segs->t == JVal::Arr;
+    return r;
+}
+
 ora_doc* ora_new(int collaborating) {
     ora_doc* o = new ora_doc();
     if (collaborating) {                                                                         // startOrUpdateCollaboration("obs")
@@ -1082,6 +1231,42 @@ int ora_local_remove(ora_doc* o, int32_t start, int32_t end) {
 }
 int ora_local_annotate(ora_doc* o, int32_t start, int32_t end, int32_t ps, int32_t rewrite) {
     Tree& t = o->d.t; t.annotateRange(start, end, o->d.props, ps, rewrite != 0, t.currentSeq, t.cwClientId, t.collaborating ? UnassignedSeq : UniversalSeq); return (int)t.status;
+}
+int ora_load_snapshot(ora_doc* o, uint32_t n_blobs, const char* const* blobs) {
+    Doc& d = o->d; Tree& t = d.t;
+    if (t.collaborating || n_blobs == 0) return MT_DS_UNSUPPORTED;
+    std::vector<JVal> js(n_blobs);
+    for (uint32_t i = 0; i < n_blobs; i++) js[i] = json_parse(blobs[i]);
+    LoadChunk h = load_chunk(js[0], true);
+    if (!h.ok || !h.hasMeta) { t.status |= MT_DS_UNSUPPORTED; return (int)t.status; }   // "header metadata not available"
+    // loadHeader (:126-160)
+    std::vector<Seg*> hs;
+    for (const JVal& sp : h.segs->arr) { Seg* s = loadSpec(d, sp); if (!s) { t.status |= MT_DS_UNSUPPORTED; return (int)t.status; } hs.push_back(s); }
+    t.reloadFromSegments(hs);
+    {   // startOrUpdateCollaboration("obs", minSeq ?? seq, seq)
+        int obs = load_short_id(d, u"obs");
+        d.shortToStream[obs] = -1;
+        t.startCollaboration(obs, h.hasMin ? h.minSeq : h.seq, h.seq);
+    }
+    // loadBody (:162-206)
+    if (h.segmentCount == h.totalSegmentCount) return (int)t.status;
+    std::vector<Seg*> segs;
+    for (int ci = 1; ci < h.nChunks; ci++) {
+        if ((uint32_t)ci >= n_blobs) { t.status |= MT_DS_UNSUPPORTED; return (int)t.status; }
+        LoadChunk c = load_chunk(js[ci], false);
+        if (!c.ok) { t.status |= MT_DS_UNSUPPORTED; return (int)t.status; }
+        for (const JVal& sp : c.segs->arr) { Seg* s = loadSpec(d, sp); if (!s) { t.status |= MT_DS_UNSUPPORTED; return (int)t.status; } segs.push_back(s); }
+    }
+    std::vector<Seg*> batch;
+    auto append = [&](const std::vector<Seg*>& v, int cli, int seq) { t.insertSegmentsLoad(t.root->cachedLength, v, UniversalSeq, cli, seq); };
+    auto flushBatch = [&]() { if (!batch.empty()) append(batch, NonCollabClient, UniversalSeq); };
+    for (Seg* s : segs) {
+        if (t.status) break;
+        if (s->clientId == NonCollabClient && s->seq == UniversalSeq) batch.push_back(s);
+        else { flushBatch(); if (!t.status) append({s}, s->clientId, s->seq); }
+    }
+    if (!t.status) flushBatch();
+    return (int)t.status;
 }
 int32_t ora_get_length(ora_doc* o, int32_t ref, int32_t client) {
     // A client that has not sent a message yet owns no segment: any unused id gives its view.

@@ -31,6 +31,12 @@ int      ora_local_insert(ora_doc* d, int32_t pos, const uint16_t* text, uint32_
                           int32_t marker_ref_type, int32_t prop_set);
 int      ora_local_remove(ora_doc* d, int32_t start, int32_t end);
 int      ora_local_annotate(ora_doc* d, int32_t start, int32_t end, int32_t prop_set, int32_t rewrite);
+/* SnapshotLoader (MT/snapshotLoader.ts:39-222) on a document made with
+ * ora_new(0): blobs[0] = the "header" blob, then the body chunks in
+ * orderedChunkMetadata order (V1 or legacy chunks, snapshotChunks.ts:137-180);
+ * the observer is "obs".  Returns the MT_DS_* status (INSERT_FAILED where the
+ * reference throws, UNSUPPORTED for aliased loadBody segments / bad specs). */
+int      ora_load_snapshot(ora_doc* d, uint32_t n_blobs, const char* const* blobs);
 int32_t  ora_get_length(ora_doc* d, int32_t ref_seq, int32_t client); /* client -1: observer */
 /* Snapshot: returns a malloc'd buffer: u32 n_blobs, then per blob u64 len + bytes. */
 uint8_t* ora_snapshot_v1(ora_doc* d, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total_bytes);

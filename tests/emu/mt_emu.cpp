@@ -72,6 +72,14 @@ static int mtb_launch_open(mt_ctx* c, uint32_t first, uint32_t n) {
     for (uint32_t d = first; d < first + n; d++) { MtScratch sc; MtEng e; e.bind(c->S, d, &sc); e.open(); e.store(d); }
     return MT_OK;
 }
+static int mtb_launch_load(mt_ctx* c, const MtLoad& L, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) {
+        MtScratch sc; MtEng e; e.bind(c->S, L.docs[i], &sc); e.open();
+        mt_load_doc(e, L, i);
+        e.store(L.docs[i]);
+    }
+    return MT_OK;
+}
 static int mtb_launch_update_seq(mt_ctx* c, const uint32_t* docs, const int32_t* msn, const int32_t* seq, uint32_t n) {
     for (uint32_t i = 0; i < n; i++) {
         MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc);

@@ -44,6 +44,8 @@ def lib():
         L.ora_local_insert.argtypes = [P, I32, P, U32, I32, I32]
         L.ora_local_remove.argtypes = [P, I32, I32]
         L.ora_local_annotate.argtypes = [P, I32, I32, I32, I32]
+        L.ora_load_snapshot.restype = ctypes.c_int
+        L.ora_load_snapshot.argtypes = [P, U32, P]
         L.ora_get_length.restype = I32
         L.ora_get_length.argtypes = [P, I32, I32]
         L.ora_snapshot_v1.restype = P
@@ -129,6 +131,13 @@ class OracleDoc:
 
     def remove_range(self, start: int, end: int):
         return self.L.ora_local_remove(self.h, start, end)
+
+    def load_snapshot(self, blobs: list) -> int:
+        """SnapshotLoader on a document made with collaborating=False: blobs[0] is
+        the header blob, then the body chunks in orderedChunkMetadata order."""
+        enc = [b if isinstance(b, bytes) else b.encode() for b in blobs]
+        arr = (ctypes.c_char_p * len(enc))(*enc)
+        return int(self.L.ora_load_snapshot(self.h, len(enc), ctypes.cast(arr, ctypes.c_void_p)))
 
     def get_length(self, ref_seq: int = 0, client: int = -1) -> int:
         return int(self.L.ora_get_length(self.h, ref_seq, client))
