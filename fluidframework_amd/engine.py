@@ -363,6 +363,22 @@ class _Pending:
     msgs: list
 
 
+def catchup_ops(blobs: dict, snap) -> list:
+    """The catch-up messages blob of a legacy snapshot (snapshotLoader.ts:69-92):
+    the one blob that is neither the header nor a listed chunk."""
+    import json as _json
+    from .snapshot_load import _latest, _parse
+    md = _latest(_parse(blobs["header"]), True)["headerMetadata"] or {}
+    ids = {c["id"] for c in md.get("orderedChunkMetadata", [])} | {"header"}
+    rest = [k for k in blobs if k not in ids]
+    if len(rest) > 1:
+        raise MergeTreeError("Unexpected blobs in snapshot")
+    if not rest:
+        return []
+    raw = blobs[rest[0]]
+    return _json.loads(raw.decode("utf-8") if isinstance(raw, (bytes, bytearray)) else raw)
+
+
 class MergeTreeClient:
     """Drop-in subset of merge-tree ``Client`` (MT/client.ts:44) for a passive observer.
 
@@ -420,6 +436,25 @@ class MergeTreeClient:
 
     def getCurrentSeq(self) -> int:
         return self.current_seq
+
+    def load(self, blobs: dict, longClientId: str = "snapshot") -> dict:
+        """Client.load (MT/client.ts:958) through SnapshotLoader (snapshotLoader.ts:39-222):
+        `blobs` maps blob paths (header, body_0.. or body) to contents.  Returns
+        {"catchupOps": [...]} (legacy catch-up blob) for the caller to apply."""
+        from .snapshot_load import LoadBatchBuilder, parse_snapshot
+        self.group.flush()
+        chunks = {k: v for k, v in blobs.items()}
+        snap = parse_snapshot(chunks)
+        lb = LoadBatchBuilder(self.engine.props)
+        lb.add(self.doc_id, snap, self.names)
+        self.engine.upload_doc_names(self.doc_id, self.names.json_literals())
+        self.names_uploaded = len(self.names.names)
+        self.engine.load_snapshot(lb.build())
+        self.engine.sync()
+        self._raise_status()
+        self.longClientId = longClientId
+        self.min_seq, self.current_seq = snap.min_seq, snap.seq
+        return {"catchupOps": catchup_ops(blobs, snap)}
 
 
 class ClientGroup:

@@ -183,6 +183,128 @@ class BatchBuilder {
     }
 }
 
+// ---- snapshot load: the JSON half of SnapshotLoader (MT/snapshotLoader.ts) ----
+const LS_SEQ = 1, LS_CLIENT = 2, LS_REMOVED = 4, LS_MARKER = 8;
+
+/** toLatestVersion (MT/snapshotChunks.ts:137-180) of one parsed chunk. */
+function latestChunk(chunk, header) {
+    if (chunk.version === "1") {
+        return { segments: chunk.segments, segmentCount: chunk.segmentCount,
+            headerMetadata: header ? chunk.headerMetadata : undefined };
+    }
+    if (chunk.version === undefined) {
+        let md;
+        if (header) {
+            md = chunk.headerMetadata;
+            if (md === undefined) {
+                const ids = [{ id: "header" }];
+                if (chunk.chunkLengthChars < chunk.totalLengthChars) ids.push({ id: "body" });
+                md = { orderedChunkMetadata: ids, minSequenceNumber: chunk.chunkMinSequenceNumber,
+                    sequenceNumber: chunk.chunkSequenceNumber, totalLength: chunk.totalLengthChars,
+                    totalSegmentCount: chunk.totalSegmentCount };
+            }
+        }
+        return { segments: chunk.segmentTexts, segmentCount: chunk.chunkSegmentCount, headerMetadata: md };
+    }
+    throw new Error(`Unsupported chunk version: ${chunk.version}`);
+}
+
+/**
+ * Parses a snapshot's blobs ({path: contents}) as SnapshotLoader.initialize does:
+ * header metadata, header segments, body chunks in orderedChunkMetadata order, and
+ * the catch-up ops blob (legacy format) if present (snapshotLoader.ts:39-92).
+ */
+function parseSnapshot(blobs) {
+    const head = latestChunk(JSON.parse(blobs.header), true);
+    const md = head.headerMetadata;
+    if (md === undefined) throw new Error("header metadata not available");
+    const out = { header: head.segments || [], body: [], seq: md.sequenceNumber,
+        minSeq: md.minSequenceNumber !== undefined ? md.minSequenceNumber : md.sequenceNumber, catchupOps: [] };
+    const ids = md.orderedChunkMetadata.map((c) => c.id);
+    if (head.segmentCount !== md.totalSegmentCount) {
+        for (const id of ids.slice(1)) {
+            if (blobs[id] === undefined) throw new Error(`missing chunk ${id}`);
+            for (const sp of latestChunk(JSON.parse(blobs[id]), false).segments || []) out.body.push(sp);
+        }
+    }
+    const rest = Object.keys(blobs).filter((k) => !ids.includes(k));
+    if (rest.length === 1) out.catchupOps = JSON.parse(blobs[rest[0]]);
+    else if (rest.length > 1) throw new Error("Unexpected blobs in snapshot");
+    return out;
+}
+
+/** Packs parsed snapshots into an mt_load_batch (32-byte mt_load_seg records). */
+class LoadBuilder {
+    constructor(props) {
+        this.props = props; this.docIds = []; this.offsets = [0]; this.nhdr = []; this.minSeq = []; this.seq = [];
+        this.recs = []; this.payload = [];
+    }
+    // SnapshotLoader.specToSegment (snapshotLoader.ts:93-124) over segmentFromSpec
+    // (sequenceFactory.ts:31-37); null where the reference would fail.
+    record(spec, names) {
+        const merge = spec !== null && typeof spec === "object" && "json" in spec;
+        const js = merge ? spec.json : spec;
+        let flags = 0, text = null, refType = 0, props;
+        if (typeof js === "string") text = js;
+        else if (js !== null && typeof js === "object" && "text" in js) {
+            if (typeof js.text !== "string") return null;
+            text = js.text; props = js.props;
+        } else if (js !== null && typeof js === "object" && "marker" in js) {
+            refType = js.marker && js.marker.refType;
+            if (!Number.isInteger(refType) || refType < 0) return null;
+            flags |= LS_MARKER; props = js.props;
+        } else return null;
+        let pid = -1;
+        if (props) {
+            if (typeof props !== "object") return null;
+            pid = this.props.intern(props);
+        }
+        const r = { flags, client: 0, seq: 0, rseq: 0, rclient: 0, pid, poff: 0, plen: refType };
+        if (text !== null) {
+            r.poff = this.payload.length; r.plen = text.length;
+            for (let i = 0; i < text.length; i++) this.payload.push(text.charCodeAt(i));
+        }
+        if (merge) {
+            if (spec.client !== undefined) { if (typeof spec.client !== "string") return null; r.flags |= LS_CLIENT; r.client = names.index(spec.client); }
+            if (spec.seq !== undefined) { if (!Number.isInteger(spec.seq)) return null; r.flags |= LS_SEQ; r.seq = spec.seq; }
+            if (spec.removedSeq !== undefined || spec.removedClient !== undefined) {
+                if (!Number.isInteger(spec.removedSeq) || typeof spec.removedClient !== "string") return null;
+                r.flags |= LS_REMOVED; r.rseq = spec.removedSeq; r.rclient = names.index(spec.removedClient);
+            }
+        }
+        return r;
+    }
+    /** Adds one document; false if rejected (it then loads as UNSUPPORTED). */
+    add(docId, snap, names) {
+        const p0 = this.payload.length, recs = [];
+        let ok = Number.isInteger(snap.seq) && Number.isInteger(snap.minSeq);
+        for (const spec of ok ? snap.header.concat(snap.body) : []) {
+            const r = this.record(spec, names);
+            if (r === null) { ok = false; break; }
+            recs.push(r);
+        }
+        if (!ok) { this.payload.length = p0; recs.length = 0; }
+        for (const r of recs) this.recs.push(r);
+        this.docIds.push(docId); this.offsets.push(this.recs.length);
+        this.nhdr.push(ok ? snap.header.length : 0);
+        this.minSeq.push(ok ? snap.minSeq : -1); this.seq.push(ok ? snap.seq : 0);
+        return ok;
+    }
+    build() {
+        const buf = new ArrayBuffer(32 * Math.max(1, this.recs.length)), dv = new DataView(buf);
+        this.recs.forEach((r, i) => {
+            const o = 32 * i;
+            dv.setUint8(o, r.flags); dv.setUint16(o + 2, r.client, true); dv.setInt32(o + 4, r.seq, true);
+            dv.setInt32(o + 8, r.rseq, true); dv.setUint16(o + 12, r.rclient, true); dv.setInt16(o + 14, r.pid, true);
+            dv.setUint32(o + 16, r.poff, true); dv.setUint32(o + 20, r.plen, true);
+        });
+        return { docIds: Uint32Array.from(this.docIds), segOffsets: Uint32Array.from(this.offsets),
+            headerSegments: Uint32Array.from(this.nhdr), minSeq: Int32Array.from(this.minSeq),
+            seq: Int32Array.from(this.seq), segs: new Uint8Array(buf),
+            payload: Uint16Array.from(this.payload.length ? this.payload : [0]) };
+    }
+}
+
 const DEFAULT_LIMITS = { rowsPerDoc: 8192, windowPerDoc: 4096, propsetsPerDoc: 8192, textPerDoc: 1 << 16 };
 
 /** One engine context (one GPU) and the documents it holds. */
@@ -203,6 +325,13 @@ class Engine {
         }
         addon.applyBatch(this.h, batch);
     }
+    uploadProps() {
+        if (this.uploadedSets !== this.props.sets.length) {
+            addon.setProps(this.h, this.props.toNative());
+            this.uploadedSets = this.props.sets.length;
+        }
+    }
+    loadSnapshot(batch) { this.uploadProps(); addon.loadSnapshot(this.h, batch); }
     sync() { addon.sync(this.h); }
     syncAsync() { return addon.syncAsync(this.h); }
     status(docs) { return addon.docStatus(this.h, Uint32Array.from(docs)); }
@@ -232,6 +361,25 @@ class MergeTreeClient {
         this.minSeq = msg.minimumSequenceNumber;
     }
     getCurrentSeq() { return this.currentSeq; }
+    /**
+     * Client.load (client.ts:958) through SnapshotLoader (snapshotLoader.ts:39-222):
+     * `blobs` maps blob paths (header, body_0.. / body, catch-up ops) to contents.
+     * Returns { catchupOps } for the caller to apply, as the reference's loader does.
+     */
+    load(blobs, longClientId = "snapshot") {
+        this.group.flush();
+        const snap = parseSnapshot(blobs);
+        const lb = new LoadBuilder(this.group.engine.props);
+        lb.add(this.docId, snap, this.names);
+        addon.setDocClientNames(this.group.engine.h, this.docId, this.names.names.map((n) => JSON.stringify(n)));
+        this.namesUploaded = this.names.names.length;
+        this.group.engine.loadSnapshot(lb.build());
+        this.group.engine.sync();
+        this.checkStatus();
+        this.longClientId = longClientId;
+        this.minSeq = snap.minSeq; this.currentSeq = snap.seq;
+        return { catchupOps: snap.catchupOps };
+    }
     checkStatus() {
         const st = this.group.engine.status([this.docId])[0];
         if (st) throw new Error(`document ${this.docId}: ${statusNames(st).join(", ")}`);
@@ -296,4 +444,5 @@ class ClientGroup {
     }
 }
 
-module.exports = { addon, Engine, ClientGroup, MergeTreeClient, BatchBuilder, PropTable, ClientNames, statusNames };
+module.exports = { addon, Engine, ClientGroup, MergeTreeClient, BatchBuilder, PropTable, ClientNames, statusNames,
+    LoadBuilder, parseSnapshot };

@@ -251,6 +251,32 @@ napi_value ApplyBatch(napi_env env, napi_callback_info info) {
     return rc ? throw_rc(env, c, rc, "mt_apply_batch") : undefined(env);
 }
 
+// loadSnapshot(ctx, batch): SnapshotLoader for every document of the batch
+// (segments already JSON-parsed by the JS host into 32-byte mt_load_seg records).
+napi_value LoadSnapshot(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
+    mt_load_batch B{};
+    const uint8_t* segs = nullptr;
+    size_t nd, no, nh, nm, ns, nb, np;
+    if (!field(env, argv[1], "docIds", napi_uint32_array, &B.doc_ids, &nd) ||
+        !field(env, argv[1], "segOffsets", napi_uint32_array, &B.seg_offsets, &no) ||
+        !field(env, argv[1], "headerSegments", napi_uint32_array, &B.header_segments, &nh) ||
+        !field(env, argv[1], "minSeq", napi_int32_array, &B.min_seq, &nm) ||
+        !field(env, argv[1], "seq", napi_int32_array, &B.seq, &ns) ||
+        !field(env, argv[1], "segs", napi_uint8_array, &segs, &nb) ||
+        !field(env, argv[1], "payload", napi_uint16_array, &B.payload, &np))
+        return nullptr;
+    if (no != nd + 1 || nh != nd || nm != nd || ns != nd) { napi_throw_range_error(env, nullptr, "per-document arrays disagree"); return nullptr; }
+    if (nb < 32ull * B.seg_offsets[nd]) { napi_throw_range_error(env, nullptr, "segs shorter than 32 * segOffsets[n]"); return nullptr; }
+    B.n_docs = (uint32_t)nd;
+    B.segs = (const mt_load_seg*)segs;
+    B.payload_units = np;
+    int rc = mt_load_snapshot(c, &B);
+    return rc ? throw_rc(env, c, rc, "mt_load_snapshot") : undefined(env);
+}
+
 napi_value Sync(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     if (!get_args(env, info, 1, argv)) return nullptr;
@@ -413,6 +439,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"setClientNames", nullptr, SetClientNames, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"setDocClientNames", nullptr, SetDocClientNames, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"applyBatch", nullptr, ApplyBatch, nullptr, nullptr, nullptr, kAttr, nullptr},
+        {"loadSnapshot", nullptr, LoadSnapshot, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"sync", nullptr, Sync, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"syncAsync", nullptr, SyncAsync, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"docStatus", nullptr, DocStatus, nullptr, nullptr, nullptr, kAttr, nullptr},

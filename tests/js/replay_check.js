@@ -2,7 +2,8 @@
 // Test driver for the Node host (fluidframework_amd/js): replays sequenced
 // message lists, one ClientGroup document per list, through MergeTreeClient
 // (the Client drop-in) and prints what the parity tests compare against the
-// oracle: text, length, SnapshotV1 ITree blobs and digests.
+// oracle: text, length, SnapshotV1 ITree blobs and digests (optionally after
+// loading a snapshot into each document).
 // usage: node replay_check.js IN.json OUT.json
 const fs = require("fs");
 const path = require("path");
@@ -17,6 +18,8 @@ const clients = spec.docs.map(() => {
     c.startOrUpdateCollaboration("observer");
     return c;
 });
+// optional: load a snapshot into each document first (Client.load / SnapshotLoader)
+if (spec.loads) spec.loads.forEach((blobs, d) => { if (blobs) clients[d].load(blobs); });
 spec.docs.forEach((msgs, d) => { for (const m of msgs) clients[d].applyMsg(m); });
 const out = { texts: [], lengths: [], blobs: [], digests: [] };
 for (const c of clients) {

@@ -54,3 +54,41 @@ def test_client_assert_seq_raises():
 @pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
 def test_client_group_on_gpu_matches_oracle(cfg):
     check(lambda n, **kw: Engine(n, device=0, **kw), cfg, 4)
+
+
+def check_load(factory):
+    """MergeTreeClient.load (Client.load / SnapshotLoader), then the rest of the stream."""
+    from test_snapshot_load import COLLAB_CASES, collab_case, golden_blobs, oracle_load, sub_batch
+    case = dict(COLLAB_CASES[1])
+    cut = case.pop("cut")
+    props, batch, snaps, blobs_l = collab_case(cut=cut, **case)
+    n = case["n_docs"]
+    eng = factory(n + 1, rows_per_doc=40000, window_per_doc=8192, propsets_per_doc=8192, text_per_doc=1 << 19,
+                  blocks_per_doc=16384)
+    eng.props = props
+    g = ClientGroup(eng)
+    clients = [g.new_client() for _ in range(n + 1)]
+    want, gblobs = golden_blobs("withAnnotations")
+    assert clients[n].load(want) == {"catchupOps": []}
+    od, _ = oracle_load(gblobs, props)
+    assert clients[n].getText() == od.get_text()
+    for d in range(n):
+        clients[d].load({("header" if i == 0 else f"body_{i - 1}"): b for i, b in enumerate(blobs_l[d])})
+        for m in batch_to_messages(batch, props, d)[cut:]:
+            clients[d].applyMsg(m)
+    for d in range(n):
+        od, st = oracle_load(blobs_l[d], props)
+        assert st == 0 and od.apply_run(sub_batch(batch, d, cut, case["ops"], 0), 0) == 0
+        assert clients[d].getText() == od.get_text()
+        o = int(batch.op_offsets[d + 1]) - 1
+        ob, _ = od.snapshot(int(batch.arrays["msn"][o]), int(batch.arrays["seq"][o]))
+        assert [e["value"]["contents"].encode() for e in clients[d].snapshot()["entries"]] == ob
+
+
+def test_client_load_on_emulation_matches_oracle():
+    check_load(emu_engine)
+
+
+@pytest.mark.gpu
+def test_client_load_on_gpu_matches_oracle():
+    check_load(lambda n, **kw: Engine(n, device=0, **kw))

@@ -19,7 +19,7 @@ from test_emu_parity import CONFIGS, ann_props
 pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 
 EXPORTS = ["applyBatch", "create", "destroy", "docStatus", "docsOpen", "getLength", "getText", "lastError",
-           "setClientNames", "setDocClientNames", "setProps", "setResidency", "snapshotV1", "sync", "syncAsync",
+           "loadSnapshot", "setClientNames", "setDocClientNames", "setProps", "setResidency", "snapshotV1", "sync", "syncAsync",
            "updateSeq"]
 
 
@@ -60,3 +60,47 @@ def test_node_host_on_emulation_matches_oracle(cfg):
 @pytest.mark.parametrize("cfg", ["cfg1", "cfg2", "cfg3"])
 def test_node_host_on_gpu_matches_oracle(cfg):
     check(cfg, 6, os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"))
+
+
+def check_load(addon):
+    """Client.load through the Node host: golden V1 files, and a collaborative
+    snapshot taken mid-stream followed by the rest of the stream."""
+    from test_snapshot_load import COLLAB_CASES, GOLDEN, collab_case, golden_blobs, oracle_load, sub_batch
+    loads, msgs, want_text, want_blobs = [], [], [], []
+    for name in GOLDEN:
+        want, blobs = golden_blobs(name)
+        loads.append(want)
+        msgs.append([])
+        od, st = oracle_load(blobs, ann_props())
+        assert st == 0
+        want_text.append(od.get_text())
+        want_blobs.append(None)
+    case = dict(COLLAB_CASES[0])
+    cut = case.pop("cut")
+    props, batch, snaps, blobs_l = collab_case(cut=cut, **case)
+    for d in range(case["n_docs"]):
+        loads.append({("header" if i == 0 else f"body_{i - 1}"): b for i, b in enumerate(blobs_l[d])})
+        msgs.append(batch_to_messages(batch, props, d)[cut:])
+        od, st = oracle_load(blobs_l[d], props)
+        assert st == 0
+        assert od.apply_run(sub_batch(batch, d, cut, case["ops"], 0), 0) == 0
+        want_text.append(od.get_text())
+        o = int(batch.op_offsets[d + 1]) - 1
+        ob, _ = od.snapshot(int(batch.arrays["msn"][o]), int(batch.arrays["seq"][o]))
+        want_blobs.append([("header" if i == 0 else f"body_{i - 1}", b.decode()) for i, b in enumerate(ob)])
+    got = run_node(msgs, addon=addon, loads=loads,
+                   limits=dict(rowsPerDoc=40000, windowPerDoc=8192, propsetsPerDoc=8192, textPerDoc=1 << 19,
+                               blocksPerDoc=16384))
+    for d in range(len(msgs)):
+        assert got["texts"][d] == want_text[d], f"doc {d} text"
+        if want_blobs[d] is not None:
+            assert [tuple(x) for x in got["blobs"][d]] == want_blobs[d], f"doc {d} snapshot"
+
+
+def test_node_host_load_on_emulation_matches_oracle():
+    check_load(build_emu_napi())
+
+
+@pytest.mark.gpu
+def test_node_host_load_on_gpu_matches_oracle():
+    check_load(os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"))
