@@ -501,8 +501,10 @@ static int mt_stage_docs(mt_ctx* c, uint32_t n, const uint32_t* docs, std::vecto
     return MT_OK;
 }
 
-int MT_FN(snapshot_v1)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t* msn, const int32_t* seq,
-                       uint64_t* digest, const char** arena, const uint64_t** blob_off, const uint32_t** blob_first) {
+// Client.snapshot (client.ts:923-956): SnapshotV1 or, with legacy set, SnapshotLegacy.
+static int mt_snapshot_blobs(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t* msn, const int32_t* seq,
+                             uint64_t* digest, const char** arena, const uint64_t** blob_off,
+                             const uint32_t** blob_first, bool legacy) {
     if (!c) return MT_E_INVALID;
     int rc = MT_FN(update_seq)(c, n, docs, msn, seq);       // Client.snapshot: updateSeqNumbers first (client.ts:936)
     if (rc) return rc;
@@ -511,8 +513,9 @@ int MT_FN(snapshot_v1)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_
     c->snap_arena.clear(); c->blob_off.assign(1, 0); c->blob_first.assign(1, 0);
     for (uint32_t i = 0; i < n; i++) {
         auto dn = c->doc_clients.find(docs[i]);
-        std::vector<std::string> blobs = mtsnap::snapshot_blobs(views[i], c->names,
-                                                                dn == c->doc_clients.end() ? nullptr : &dn->second);
+        std::vector<std::string> blobs = legacy ? mtsnap::snapshot_legacy_blobs(views[i], c->names)
+                                                : mtsnap::snapshot_blobs(views[i], c->names,
+                                                                         dn == c->doc_clients.end() ? nullptr : &dn->second);
         if (digest) digest[i] = mtsnap::blobs_digest(blobs);
         for (auto& b : blobs) { c->snap_arena += b; c->blob_off.push_back(c->snap_arena.size()); }
         c->blob_first.push_back((uint32_t)(c->blob_off.size() - 1));
@@ -521,6 +524,16 @@ int MT_FN(snapshot_v1)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_
     if (blob_off) *blob_off = c->blob_off.data();
     if (blob_first) *blob_first = c->blob_first.data();
     return MT_OK;
+}
+
+int MT_FN(snapshot_v1)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t* msn, const int32_t* seq,
+                       uint64_t* digest, const char** arena, const uint64_t** blob_off, const uint32_t** blob_first) {
+    return mt_snapshot_blobs(c, n, docs, msn, seq, digest, arena, blob_off, blob_first, false);
+}
+
+int MT_FN(snapshot_legacy)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t* msn, const int32_t* seq,
+                           uint64_t* digest, const char** arena, const uint64_t** blob_off, const uint32_t** blob_first) {
+    return mt_snapshot_blobs(c, n, docs, msn, seq, digest, arena, blob_off, blob_first, true);
 }
 
 // Digests only, serialized on `threads` host threads (no blob arena).

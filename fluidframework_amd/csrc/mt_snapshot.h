@@ -191,6 +191,85 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
     return blobs;
 }
 
+// Client.snapshot without newMergeTreeSnapshotFormat -> SnapshotLegacy.extractSync/emit
+// (MT/client.ts:950-954, MT/snapshotlegacy.ts:74-240, MT/snapshotChunks.ts:79-119,:161-180).
+// mergeTree.map at (minSeq, NonCollabClient) visits exactly the rows inserted at or
+// below the MSN and not removed at or below it (removes above the MSN keep their
+// text); all of them coalesce greedily (canAppend + matchProperties on clones).
+// Rows above the MSN are left to the catch-up ops blob, which the host appends.
+// Blob 0 is "header"; blob 1, if any, is "body".
+inline std::vector<std::string> snapshot_legacy_blobs(const MtSnapView& v, const MtNames& nm) {
+    const int minSeq = v.hdr.minSeq;
+    std::vector<std::string> segs; std::vector<long long> lens;
+    int prev = -1; std::vector<uint16_t> ptext; bool pcloned = false;
+    auto pushPrev = [&]() {
+        if (prev < 0) return;
+        std::string o;
+        const bool pm = (v.R[prev].meta & MT_M_MARKER) != 0;
+        if (pcloned) { seg_json(o, v, nm, prev, ptext.data(), ptext.size()); lens.push_back((long long)ptext.size()); }
+        else {
+            seg_json(o, v, nm, prev, pm ? nullptr : v.text + v.R[prev].toff, pm ? 0 : (size_t)v.R[prev].len);
+            lens.push_back(v.R[prev].len);
+        }
+        segs.push_back(std::move(o));
+    };
+    auto extract = [&](int s) {                                         // snapshotlegacy.ts:190-209
+        const bool removed = (v.R[s].meta & MT_M_REMOVED) != 0;
+        if (v.R[s].seq > minSeq || (removed && v.R[s].rseq <= minSeq)) return;
+        if (prev >= 0) {
+            const bool pm = (v.R[prev].meta & MT_M_MARKER) != 0, sm = (v.R[s].meta & MT_M_MARKER) != 0;
+            bool ok = !pm && !sm;
+            if (ok) {
+                const uint16_t* pt = pcloned ? ptext.data() : v.text + v.R[prev].toff;
+                const size_t pl = pcloned ? ptext.size() : (size_t)v.R[prev].len;
+                ok = !(pl > 0 && pt[pl - 1] == '\n') && ((long long)pl <= MT_GRAN || v.R[s].len <= MT_GRAN);
+            }
+            if (ok && props_match(v, nm, v.R[prev].props, v.R[s].props)) {
+                if (!pcloned) { ptext.assign(v.text + v.R[prev].toff, v.text + v.R[prev].toff + v.R[prev].len); pcloned = true; }
+                ptext.insert(ptext.end(), v.text + v.R[s].toff, v.text + v.R[s].toff + v.R[s].len);
+                return;
+            }
+            pushPrev();
+        }
+        prev = s; pcloned = false;
+    };
+    walk_all(v, v.hdr.root, extract);
+    pushPrev();
+    long long total = 0;
+    for (long long l : lens) total += l;                                // header.segmentsTotalLength (:181, :230-237)
+    struct Chunk { size_t start, count; long long length; };
+    auto take = [&](long long approx, size_t start) {                   // getSeqLengthSegs (:74-98)
+        Chunk c{start, 0, 0};
+        while (c.length < approx && c.start + c.count < segs.size()) { c.length += lens[c.start + c.count]; c.count++; }
+        return c;
+    };
+    auto chunkStr = [&](const Chunk& c, bool header) {
+        std::string o = "{\"chunkStartSegmentIndex\":"; put_int(o, (long long)c.start);
+        o += ",\"chunkSegmentCount\":"; put_int(o, (long long)c.count);
+        o += ",\"chunkLengthChars\":"; put_int(o, c.length);
+        o += ",\"totalLengthChars\":"; put_int(o, total);
+        o += ",\"totalSegmentCount\":"; put_int(o, (long long)segs.size());
+        o += ",\"chunkSequenceNumber\":"; put_int(o, minSeq);
+        o += ",\"segmentTexts\":[";
+        for (size_t i = 0; i < c.count; i++) { if (i) o.push_back(','); o += segs[c.start + i]; }
+        o += "]";
+        if (header) {                                                   // buildHeaderMetadataForLegecyChunk
+            o += ",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+            if (c.length < total) o += ",{\"id\":\"body\"}";
+            o += "],\"sequenceNumber\":"; put_int(o, minSeq);          // minSequenceNumber is undefined: omitted
+            o += ",\"totalLength\":"; put_int(o, total);
+            o += ",\"totalSegmentCount\":"; put_int(o, (long long)segs.size()); o += "}";
+        }
+        o += "}";
+        return o;
+    };
+    std::vector<std::string> blobs;
+    const Chunk c1 = take(10000, 0);                                   // SnapshotLegacy.sizeOfFirstChunk
+    blobs.push_back(chunkStr(c1, true));
+    if (c1.count < segs.size()) blobs.push_back(chunkStr(take(total, c1.count), false));
+    return blobs;
+}
+
 inline uint64_t xxh64(const uint8_t* p, size_t len, uint64_t seed) {
     const uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL, P3 = 1609587929392839161ULL,
                    P4 = 9650029242287828579ULL, P5 = 2870177450012600261ULL;

@@ -79,6 +79,8 @@ def _bind(lib, prefix: str):
         get_length=f("get_length", ctypes.c_int, [P, U32, P, P, P, P]),
         snapshot_v1=f("snapshot_v1", ctypes.c_int, [P, U32, P, P, P, P, ctypes.POINTER(P), ctypes.POINTER(P),
                                                     ctypes.POINTER(P)]),
+        snapshot_legacy=f("snapshot_legacy", ctypes.c_int, [P, U32, P, P, P, P, ctypes.POINTER(P),
+                                                            ctypes.POINTER(P), ctypes.POINTER(P)]),
         snapshot_digests=f("snapshot_digests", ctypes.c_int, [P, U32, P, P, P, P, ctypes.c_int]),
         get_text=f("get_text", ctypes.c_int, [P, U32, P, ctypes.POINTER(P), ctypes.POINTER(P)]),
         dump_segments=f("dump_segments", ctypes.c_int, [P, U32, ctypes.POINTER(P), ctypes.POINTER(U32)]),
@@ -314,14 +316,16 @@ class Engine:
                                           out.ctypes.data), "mt_get_length")
         return out
 
-    def snapshot(self, docs, msn, seq):
-        """SnapshotV1 blobs per document: list of (list[bytes], digest)."""
+    def snapshot(self, docs, msn, seq, legacy: bool = False):
+        """SnapshotV1 (or, with legacy, SnapshotLegacy header/body) blobs per document:
+        list of (list[bytes], digest)."""
         d, m, s = _u32(docs), _i32(msn), _i32(seq)
         dig = np.zeros(len(d), np.uint64)
         arena, boff, bfirst = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
-        self._check(self.fn["snapshot_v1"](self.h, len(d), d.ctypes.data, m.ctypes.data, s.ctypes.data,
-                                           dig.ctypes.data, ctypes.byref(arena), ctypes.byref(boff),
-                                           ctypes.byref(bfirst)), "mt_snapshot_v1")
+        fn = "snapshot_legacy" if legacy else "snapshot_v1"
+        self._check(self.fn[fn](self.h, len(d), d.ctypes.data, m.ctypes.data, s.ctypes.data,
+                                dig.ctypes.data, ctypes.byref(arena), ctypes.byref(boff),
+                                ctypes.byref(bfirst)), "mt_" + fn)
         first = np.ctypeslib.as_array(ctypes.cast(bfirst, ctypes.POINTER(ctypes.c_uint32)), (len(d) + 1,)).copy()
         nb = int(first[-1])
         offs = np.ctypeslib.as_array(ctypes.cast(boff, ctypes.POINTER(ctypes.c_uint64)), (nb + 1,)).copy()
@@ -386,8 +390,9 @@ class MergeTreeClient:
     queue of every client of the engine in one device batch.
     """
 
-    def __init__(self, engine: Engine, doc_id: int, group: "ClientGroup"):
+    def __init__(self, engine: Engine, doc_id: int, group: "ClientGroup", options: dict | None = None):
         self.engine, self.doc_id, self.group = engine, doc_id, group
+        self.options = options           # Client options (client.ts:82-84)
         self.pending: list = []
         self.names = ClientNames()       # per-document short client ids (client.ts:658-682)
         self.names_uploaded = 0
@@ -421,17 +426,30 @@ class MergeTreeClient:
         self._raise_status()
         return self.engine.get_text([self.doc_id])[0]
 
-    def snapshot(self, min_seq: int | None = None, seq: int | None = None) -> dict:
-        """ITree of the SnapshotV1 blobs (MT/snapshotV1.ts:98-163)."""
+    def snapshot(self, catchUpMsgs: list | None = None, min_seq: int | None = None, seq: int | None = None) -> dict:
+        """Client.snapshot (client.ts:923-956) as an ITree.  options
+        newMergeTreeSnapshotFormat True: SnapshotV1 (snapshotV1.ts:98-163), header,
+        body_0, ...; otherwise SnapshotLegacy (snapshotlegacy.ts:104-175), header,
+        body, then catchUpMsgs as JSON under catchUpBlobName (default "catchupOps")."""
+        import json as _json
         self.group.flush()
         self._raise_status()
+        opts = self.options or {}
+        v1 = opts.get("newMergeTreeSnapshotFormat") is True
+        if v1 and catchUpMsgs:
+            raise MergeTreeError("New format should not emit catchup ops")      # client.ts:945-947
         m = self.min_seq if min_seq is None else min_seq
         s = self.current_seq if seq is None else seq
-        blobs, _ = self.engine.snapshot([self.doc_id], [m], [s])[0]
-        entries = []
-        for i, b in enumerate(blobs):
-            entries.append({"mode": "100644", "path": "header" if i == 0 else f"body_{i - 1}", "type": "Blob",
-                            "value": {"contents": b.decode("utf-8"), "encoding": "utf-8"}})
+        blobs, _ = self.engine.snapshot([self.doc_id], [m], [s], legacy=not v1)[0]
+
+        def entry(path, contents):
+            return {"mode": "100644", "path": path, "type": "Blob", "value": {"contents": contents, "encoding": "utf-8"}}
+        entries = [entry("header" if i == 0 else (f"body_{i - 1}" if v1 else "body"), b.decode("utf-8"))
+                   for i, b in enumerate(blobs)]
+        if not v1 and catchUpMsgs:
+            name = opts.get("catchUpBlobName")
+            entries.append(entry("catchupOps" if name is None else name,
+                                 _json.dumps(catchUpMsgs, separators=(",", ":"), ensure_ascii=False)))
         return {"entries": entries}
 
     def getCurrentSeq(self) -> int:
@@ -464,12 +482,12 @@ class ClientGroup:
         self.engine = engine
         self.clients: list[MergeTreeClient] = []
 
-    def new_client(self) -> MergeTreeClient:
+    def new_client(self, options: dict | None = None) -> MergeTreeClient:
         d = len(self.clients)
         if d >= self.engine.max_docs:
             raise MergeTreeError("engine document capacity exhausted")
         self.engine.open_docs(d, 1)
-        c = MergeTreeClient(self.engine, d, self)
+        c = MergeTreeClient(self.engine, d, self, options)
         self.clients.append(c)
         return c
 

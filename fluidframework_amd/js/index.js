@@ -9,7 +9,7 @@
  *   MergeTreeClient.updateSeqNumbers(m, s)   Client.updateSeqNumbers  MT/client.ts:843
  *   MergeTreeClient.getLength()              Client.getLength         MT/client.ts:1071
  *   MergeTreeClient.getText()                createTextHelper().getText  MT/client.ts:917
- *   MergeTreeClient.snapshot()               Client.snapshot (SnapshotV1) MT/client.ts:923
+ *   MergeTreeClient.snapshot(catchUpMsgs)    Client.snapshot (SnapshotV1 / SnapshotLegacy) MT/client.ts:923
  *   MergeTreeClient.startOrUpdateCollaboration  MT/client.ts:1073
  * Messages are queued per document and applied in device batches: reads flush
  * every queued document of the group in one mt_apply_batch.  Protocol violations
@@ -337,7 +337,10 @@ class Engine {
     status(docs) { return addon.docStatus(this.h, Uint32Array.from(docs)); }
     getLength(docs, refSeq, client) { return addon.getLength(this.h, Uint32Array.from(docs), Int32Array.from(refSeq), Int32Array.from(client)); }
     updateSeq(docs, msn, seq) { addon.updateSeq(this.h, Uint32Array.from(docs), Int32Array.from(msn), Int32Array.from(seq)); }
-    snapshot(docs, msn, seq) { return addon.snapshotV1(this.h, Uint32Array.from(docs), Int32Array.from(msn), Int32Array.from(seq)); }
+    snapshot(docs, msn, seq, legacy = false) {
+        return (legacy ? addon.snapshotLegacy : addon.snapshotV1)(this.h, Uint32Array.from(docs), Int32Array.from(msn),
+            Int32Array.from(seq));
+    }
     getText(docs) { return addon.getText(this.h, Uint32Array.from(docs)); }
 }
 
@@ -347,8 +350,9 @@ class Engine {
  * one device batch, so thousands of documents replay together.
  */
 class MergeTreeClient {
-    constructor(group, docId) {
+    constructor(group, docId, options) {
         this.group = group; this.docId = docId;
+        this.options = options;                     // Client options (client.ts:82-84)
         this.pending = []; this.names = new ClientNames();
         this.currentSeq = 0; this.minSeq = 0; this.longClientId = undefined;
     }
@@ -400,28 +404,39 @@ class MergeTreeClient {
         this.checkStatus();
         return this.group.engine.getText([this.docId])[0];
     }
-    /** ITree of SnapshotV1 blobs (MT/snapshotV1.ts:98-163): header, body_0, ... */
-    snapshot() {
+    /**
+     * Client.snapshot (client.ts:923-956).  With options.newMergeTreeSnapshotFormat
+     * === true: SnapshotV1 (snapshotV1.ts:98-163), header, body_0, ...; otherwise
+     * SnapshotLegacy (snapshotlegacy.ts:104-175): header, body, then catchUpMsgs as
+     * the catch-up blob (options.catchUpBlobName ?? "catchupOps") when non-empty.
+     */
+    snapshot(catchUpMsgs) {
         this.group.flush();
         this.checkStatus();
-        const { blobs } = this.group.engine.snapshot([this.docId], [this.minSeq], [this.currentSeq])[0];
-        return {
-            entries: blobs.map((contents, i) => ({
-                mode: "100644", path: i === 0 ? "header" : `body_${i - 1}`, type: "Blob",
-                value: { contents, encoding: "utf-8" },
-            })),
-        };
+        const opts = this.options || {};
+        const v1 = opts.newMergeTreeSnapshotFormat === true;
+        if (v1 && catchUpMsgs !== undefined && catchUpMsgs.length !== 0) {
+            throw new Error("New format should not emit catchup ops");      // client.ts:945-947
+        }
+        const { blobs } = this.group.engine.snapshot([this.docId], [this.minSeq], [this.currentSeq], !v1)[0];
+        const entry = (path, contents) => ({ mode: "100644", path, type: "Blob", value: { contents, encoding: "utf-8" } });
+        const entries = blobs.map((contents, i) => entry(i === 0 ? "header" : (v1 ? `body_${i - 1}` : "body"), contents));
+        if (!v1 && catchUpMsgs !== undefined && catchUpMsgs.length > 0) {
+            const name = opts.catchUpBlobName !== undefined && opts.catchUpBlobName !== null ? opts.catchUpBlobName : "catchupOps";
+            entries.push(entry(name, JSON.stringify(catchUpMsgs)));
+        }
+        return { entries };
     }
 }
 
 /** Many documents on one engine: `newClient()` per document, `flush()` batches. */
 class ClientGroup {
     constructor(engine) { this.engine = engine; this.clients = []; }
-    newClient() {
+    newClient(options) {
         const d = this.clients.length;
         if (d >= this.engine.maxDocs) throw new Error("engine document capacity exhausted");
         this.engine.openDocs(d, 1);
-        const c = new MergeTreeClient(this, d);
+        const c = new MergeTreeClient(this, d, options);
         this.clients.push(c);
         return c;
     }

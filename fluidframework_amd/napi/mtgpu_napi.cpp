@@ -366,7 +366,8 @@ napi_value GetLength(napi_env env, napi_callback_info info) {
 }
 
 // snapshotV1(ctx, docs, msn, seq) -> [{blobs: [header, body_0, ...], digest: BigInt}]
-napi_value SnapshotV1(napi_env env, napi_callback_info info) {
+// snapshotLegacy(ctx, docs, msn, seq) -> [{blobs: [header(, body)], digest: BigInt}]
+static napi_value snapshot_blobs(napi_env env, napi_callback_info info, bool legacy) {
     napi_value argv[4];
     if (!get_args(env, info, 4, argv)) return nullptr;
     mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
@@ -376,8 +377,9 @@ napi_value SnapshotV1(napi_env env, napi_callback_info info) {
     if (n1 < n || n2 < n) { napi_throw_range_error(env, nullptr, "msn/seq shorter than docs"); return nullptr; }
     std::vector<uint64_t> dig(n + 1);
     const char* arena = nullptr; const uint64_t* boff = nullptr; const uint32_t* bfirst = nullptr;
-    int rc = mt_snapshot_v1(c, (uint32_t)n, docs, msn, seq, dig.data(), &arena, &boff, &bfirst);
-    if (rc) return throw_rc(env, c, rc, "mt_snapshot_v1");
+    int rc = legacy ? mt_snapshot_legacy(c, (uint32_t)n, docs, msn, seq, dig.data(), &arena, &boff, &bfirst)
+                    : mt_snapshot_v1(c, (uint32_t)n, docs, msn, seq, dig.data(), &arena, &boff, &bfirst);
+    if (rc) return throw_rc(env, c, rc, legacy ? "mt_snapshot_legacy" : "mt_snapshot_v1");
     napi_value out;
     NAPI_OK(napi_create_array_with_length(env, n, &out));
     for (size_t i = 0; i < n; i++) {
@@ -397,6 +399,8 @@ napi_value SnapshotV1(napi_env env, napi_callback_info info) {
     }
     return out;
 }
+napi_value SnapshotV1(napi_env env, napi_callback_info info) { return snapshot_blobs(env, info, false); }
+napi_value SnapshotLegacy(napi_env env, napi_callback_info info) { return snapshot_blobs(env, info, true); }
 
 // getText(ctx, docs) -> [string]: the observer's text (UTF-16 code units as-is)
 napi_value GetText(napi_env env, napi_callback_info info) {
@@ -446,6 +450,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"updateSeq", nullptr, UpdateSeq, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"getLength", nullptr, GetLength, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"snapshotV1", nullptr, SnapshotV1, nullptr, nullptr, nullptr, kAttr, nullptr},
+        {"snapshotLegacy", nullptr, SnapshotLegacy, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"getText", nullptr, GetText, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"lastError", nullptr, LastError, nullptr, nullptr, nullptr, kAttr, nullptr},
     };

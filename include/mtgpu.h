@@ -23,6 +23,9 @@
  *                               (MT/client.ts:923-956 → SnapshotV1.extractSync/emit,
  *                               MT/snapshotV1.ts:98-256): per-document header and
  *                               body_i blob strings + a 64-bit digest
+ *   mt_snapshot_legacy          `Client.snapshot(...)` without it (the default;
+ *                               MT/client.ts:950-954 → SnapshotLegacy,
+ *                               MT/snapshotlegacy.ts:104-240): header + body blobs
  *   mt_get_text                 `createTextHelper().getText(currentSeq, obs)`
  *                               MT/textSegment.ts:163-181
  *   mt_dump_segments            walkAllSegments (mergeTree.ts:2998) row dump, parity
@@ -284,6 +287,21 @@ int  mt_snapshot_v1(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
                     uint64_t* out_digest,
                     const char** arena, const uint64_t** blob_off,
                     const uint32_t** blob_first);
+/*
+ * SnapshotLegacy of each document, the reference's default format when
+ * options.newMergeTreeSnapshotFormat is unset (MT/client.ts:950-954 →
+ * SnapshotLegacy.extractSync/emit, MT/snapshotlegacy.ts:104-240): after
+ * updateSeqNumbers(msn[i], seq[i]), the segments at or below the MSN (removes
+ * above the MSN keep their text), coalesced, in a "header" chunk of ≥ 10,000
+ * characters and, if segments remain, one "body" chunk.  Same arena layout and
+ * digest as mt_snapshot_v1.  The catch-up ops blob (snapshotlegacy.ts:162-172)
+ * holds the caller's messages and is appended by the host.
+ */
+int  mt_snapshot_legacy(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
+                        const int32_t* msn, const int32_t* seq,
+                        uint64_t* out_digest,
+                        const char** arena, const uint64_t** blob_off,
+                        const uint32_t** blob_first);
 /* Digests only (same values as mt_snapshot_v1's), for many documents: one staged
  * download, serialization spread over `threads` host threads. */
 int  mt_snapshot_digests(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, const int32_t* msn,

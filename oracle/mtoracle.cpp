@@ -1035,6 +1035,76 @@ static std::vector<std::string> snapshot_v1(Doc& d, int msn, int seq) {
     return blobs;
 }
 
+// Client.snapshot without newMergeTreeSnapshotFormat -> SnapshotLegacy.extractSync/emit
+// (MT/client.ts:950-954, MT/snapshotlegacy.ts:74-240; serializeAsMinSupportedVersion and
+// buildHeaderMetadataForLegecyChunk, MT/snapshotChunks.ts:79-119, :161-180).  The catch-up
+// ops blob (:162-172) is the caller's and is not part of this restatement.
+static std::vector<std::string> snapshot_legacy(Doc& d, int msn, int seq) {
+    Tree& t = d.t;
+    if (t.collaborating) {                                                                        // updateSeqNumbers(minSeq, lastSeq)
+        if (t.currentSeq > seq) t.status |= MT_DS_ASSERT_SEQ;
+        t.currentSeq = seq; t.setMinSeq(msn);
+    }
+    const int snapSeq = t.minSeq;                                                                 // this.seq = collabWindow.minSeq (:179)
+    const int headerTotal = t.getLength(snapSeq, NonCollabClient);                                // :181-182
+    struct Out { std::string json; int len; };
+    std::vector<Out> segs;
+    Seg* prev = nullptr; u16s prevText; bool prevCloned = false;
+    auto pushPrev = [&]() {
+        if (!prev) return;
+        segs.push_back({seg_json(prev, prevCloned ? &prevText : nullptr), prevCloned ? (int)prevText.size() : prev->cachedLength});
+    };
+    auto extract = [&](Seg* s, int, int, int) {                                                   // :190-209
+        if (s->seq != UnassignedSeq && s->seq <= snapSeq &&
+            (!s->hasRemoved || s->removedSeq == UnassignedSeq || s->removedSeq > snapSeq)) {
+            bool ok = false;
+            if (prev && !prev->marker && !s->marker) {                                            // prev.canAppend(segment)
+                const u16s& pt = prevCloned ? prevText : prev->text;
+                ok = !(!pt.empty() && pt.back() == u'\n') &&
+                     ((int)pt.size() <= TextSegmentGranularity || s->cachedLength <= TextSegmentGranularity);
+            }
+            if (ok && match_properties(prev->hasProps ? &prev->props : nullptr, s->hasProps ? &s->props : nullptr)) {
+                if (!prevCloned) { prevText = prev->text; prevCloned = true; }                   // prev = prev.clone(); prev.append(..)
+                prevText += s->text;
+            } else { pushPrev(); prev = s; prevCloned = false; }
+        }
+    };
+    t.nodeMap(t.root, 0, snapSeq, NonCollabClient, 0, headerTotal, extract, nullptr, nullptr);   // mergeTree.map (:211)
+    pushPrev();
+    int total = 0; for (auto& o : segs) total += o.len;                                           // :216-237 (mismatch -> totalLength)
+    struct Chunk { int start, count, length; };
+    auto take = [&](int approx, int start) {                                                      // getSeqLengthSegs (:74-98)
+        Chunk c{start, 0, 0};
+        while (c.length < approx && c.start + c.count < (int)segs.size()) { c.length += segs[c.start + c.count].len; c.count++; }
+        return c;
+    };
+    auto chunkStr = [&](const Chunk& c, bool header) {
+        std::string o = "{\"chunkStartSegmentIndex\":"; num_to_js(o, c.start);
+        o += ",\"chunkSegmentCount\":"; num_to_js(o, c.count);
+        o += ",\"chunkLengthChars\":"; num_to_js(o, c.length);
+        o += ",\"totalLengthChars\":"; num_to_js(o, total);
+        o += ",\"totalSegmentCount\":"; num_to_js(o, (int)segs.size());
+        o += ",\"chunkSequenceNumber\":"; num_to_js(o, snapSeq);
+        o += ",\"segmentTexts\":[";
+        for (int i = 0; i < c.count; i++) { if (i) o.push_back(','); o += segs[c.start + i].json; }
+        o += "]";
+        if (header) {
+            o += ",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+            if (c.length < total) o += ",{\"id\":\"body\"}";
+            o += "],\"sequenceNumber\":"; num_to_js(o, snapSeq);
+            o += ",\"totalLength\":"; num_to_js(o, total);
+            o += ",\"totalSegmentCount\":"; num_to_js(o, (int)segs.size()); o += "}";
+        }
+        o += "}";
+        return o;
+    };
+    std::vector<std::string> blobs;
+    Chunk c1 = take(10000, 0);                                                                    // SnapshotLegacy.sizeOfFirstChunk (:57)
+    blobs.push_back(chunkStr(c1, true));
+    if (c1.count < (int)segs.size()) blobs.push_back(chunkStr(take(total, c1.count), false));    // :132-152
+    return blobs;
+}
+
 static uint64_t blobs_digest(const std::vector<std::string>& blobs) {
     std::string buf;
     for (auto& b : blobs) { uint64_t n = b.size(); buf.append((const char*)&n, 8); buf += b; }
@@ -1276,8 +1346,14 @@ int32_t ora_get_length(ora_doc* o, int32_t ref, int32_t client) {
     else cl = -1000 - client;
     return o->d.t.getLength(ref, cl);
 }
+static uint8_t* pack_blobs(const std::vector<std::string>& blobs, uint64_t* digest, uint64_t* total);
 uint8_t* ora_snapshot_v1(ora_doc* o, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total) {
-    std::vector<std::string> blobs = snapshot_v1(o->d, msn, seq);
+    return pack_blobs(snapshot_v1(o->d, msn, seq), digest, total);
+}
+uint8_t* ora_snapshot_legacy(ora_doc* o, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total) {
+    return pack_blobs(snapshot_legacy(o->d, msn, seq), digest, total);
+}
+static uint8_t* pack_blobs(const std::vector<std::string>& blobs, uint64_t* digest, uint64_t* total) {
     size_t n = 4; for (auto& b : blobs) n += 8 + b.size();
     uint8_t* buf = (uint8_t*)malloc(n); uint32_t nb = (uint32_t)blobs.size(); memcpy(buf, &nb, 4); size_t off = 4;
     for (auto& b : blobs) { uint64_t l = b.size(); memcpy(buf + off, &l, 8); off += 8; memcpy(buf + off, b.data(), l); off += l; }

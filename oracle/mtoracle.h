@@ -40,6 +40,8 @@ int      ora_load_snapshot(ora_doc* d, uint32_t n_blobs, const char* const* blob
 int32_t  ora_get_length(ora_doc* d, int32_t ref_seq, int32_t client); /* client -1: observer */
 /* Snapshot: returns a malloc'd buffer: u32 n_blobs, then per blob u64 len + bytes. */
 uint8_t* ora_snapshot_v1(ora_doc* d, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total_bytes);
+/* SnapshotLegacy (MT/snapshotlegacy.ts:104-240) blobs "header"[, "body"], same packing. */
+uint8_t* ora_snapshot_legacy(ora_doc* d, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total_bytes);
 uint16_t* ora_get_text(ora_doc* d, uint64_t* n_units);
 int32_t* ora_dump_segments(ora_doc* d, uint32_t* n_rows);  /* 12 int32 per row */
 void     ora_free_buf(void* p);

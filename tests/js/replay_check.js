@@ -2,7 +2,7 @@
 // Test driver for the Node host (fluidframework_amd/js): replays sequenced
 // message lists, one ClientGroup document per list, through MergeTreeClient
 // (the Client drop-in) and prints what the parity tests compare against the
-// oracle: text, length, SnapshotV1 ITree blobs and digests (optionally after
+// oracle: text, length, SnapshotV1 (and SnapshotLegacy) ITree blobs and digests (optionally after
 // loading a snapshot into each document).
 // usage: node replay_check.js IN.json OUT.json
 const fs = require("fs");
@@ -14,19 +14,26 @@ const spec = JSON.parse(fs.readFileSync(inPath, "utf8"));
 const eng = new mt.Engine(spec.docs.length, spec.limits || {});
 const group = new mt.ClientGroup(eng);
 const clients = spec.docs.map(() => {
-    const c = group.newClient();
+    const c = group.newClient(spec.options || { newMergeTreeSnapshotFormat: true });
     c.startOrUpdateCollaboration("observer");
     return c;
 });
 // optional: load a snapshot into each document first (Client.load / SnapshotLoader)
 if (spec.loads) spec.loads.forEach((blobs, d) => { if (blobs) clients[d].load(blobs); });
 spec.docs.forEach((msgs, d) => { for (const m of msgs) clients[d].applyMsg(m); });
-const out = { texts: [], lengths: [], blobs: [], digests: [] };
-for (const c of clients) {
+const out = { texts: [], lengths: [], blobs: [], digests: [], legacy: [] };
+clients.forEach((c, d) => {
     out.texts.push(c.getText());
     out.lengths.push(c.getLength());
     out.blobs.push(c.snapshot().entries.map((e) => [e.path, e.value.contents]));
-}
+    if (spec.legacy) {      // the reference's default format: a Client without newMergeTreeSnapshotFormat
+        const opts = c.options;
+        c.options = spec.legacy.options || {};
+        out.legacy.push(c.snapshot(spec.legacy.catchUp ? spec.legacy.catchUp[d] : undefined).entries
+            .map((e) => [e.path, e.value.contents]));
+        c.options = opts;
+    }
+});
 const snaps = eng.snapshot(clients.map((c) => c.docId), clients.map((c) => c.minSeq), clients.map((c) => c.getCurrentSeq()));
 out.digests = snaps.map((s) => s.digest.toString(16));
 fs.writeFileSync(outPath, JSON.stringify(out));

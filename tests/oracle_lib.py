@@ -50,6 +50,8 @@ def lib():
         L.ora_get_length.argtypes = [P, I32, I32]
         L.ora_snapshot_v1.restype = P
         L.ora_snapshot_v1.argtypes = [P, I32, I32, ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.ora_snapshot_legacy.restype = P
+        L.ora_snapshot_legacy.argtypes = [P, I32, I32, ctypes.POINTER(U64), ctypes.POINTER(U64)]
         L.ora_get_text.restype = P
         L.ora_get_text.argtypes = [P, ctypes.POINTER(U64)]
         L.ora_dump_segments.restype = P
@@ -142,9 +144,10 @@ class OracleDoc:
     def get_length(self, ref_seq: int = 0, client: int = -1) -> int:
         return int(self.L.ora_get_length(self.h, ref_seq, client))
 
-    def snapshot(self, msn: int = 0, seq: int = 0):
+    def snapshot(self, msn: int = 0, seq: int = 0, legacy: bool = False):
         dig, tot = ctypes.c_uint64(), ctypes.c_uint64()
-        buf = self.L.ora_snapshot_v1(self.h, msn, seq, ctypes.byref(dig), ctypes.byref(tot))
+        fn = self.L.ora_snapshot_legacy if legacy else self.L.ora_snapshot_v1
+        buf = fn(self.h, msn, seq, ctypes.byref(dig), ctypes.byref(tot))
         blobs = parse_blobs(buf, tot.value)
         self.L.ora_free_buf(buf)
         return blobs, dig.value

@@ -1,6 +1,8 @@
 """The Python Client drop-in (fluidframework_amd.engine.ClientGroup /
 MergeTreeClient, mirroring MT/client.ts) against the oracle, on the host
 emulation (CPU) and on the device (GPU)."""
+import json
+
 import pytest
 
 from emu_lib import emu_engine
@@ -17,7 +19,7 @@ def check(factory, cfg, n_docs):
     p = gen_params(seed=41, n_docs=n_docs, **CONFIGS[cfg])
     batch, st, kept = generate(p, props, keep=True)
     g = ClientGroup(factory(n_docs, **LIMITS))
-    clients = [g.new_client() for _ in range(n_docs)]
+    clients = [g.new_client({"newMergeTreeSnapshotFormat": True}) for _ in range(n_docs)]
     for d, c in enumerate(clients):
         c.startOrUpdateCollaboration("observer")
         for m in batch_to_messages(batch, props, d):
@@ -31,6 +33,15 @@ def check(factory, cfg, n_docs):
         tree = c.snapshot()
         assert [e["path"] for e in tree["entries"]] == ["header"] + [f"body_{i}" for i in range(len(blobs) - 1)]
         assert [e["value"]["contents"].encode() for e in tree["entries"]] == blobs
+        # The reference's default format (no newMergeTreeSnapshotFormat): SnapshotLegacy
+        # plus the caller's catch-up messages (client.ts:950-954, snapshotlegacy.ts:162-172).
+        c.options = None
+        catch_up = batch_to_messages(batch, props, d)[-2:]
+        lblobs, _ = od.snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]), legacy=True)
+        tree = c.snapshot(catch_up)
+        assert [e["path"] for e in tree["entries"]] == ["header", "body"][:len(lblobs)] + ["catchupOps"]
+        assert [e["value"]["contents"].encode() for e in tree["entries"][:-1]] == lblobs
+        assert json.loads(tree["entries"][-1]["value"]["contents"]) == catch_up
 
 
 @pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
@@ -58,20 +69,26 @@ def test_client_group_on_gpu_matches_oracle(cfg):
 
 def check_load(factory):
     """MergeTreeClient.load (Client.load / SnapshotLoader), then the rest of the stream."""
-    from test_snapshot_load import COLLAB_CASES, collab_case, golden_blobs, oracle_load, sub_batch
+    from test_snapshot_load import COLLAB_CASES, collab_case, golden_blobs, golden_legacy_blobs, oracle_load, sub_batch
     case = dict(COLLAB_CASES[1])
     cut = case.pop("cut")
     props, batch, snaps, blobs_l = collab_case(cut=cut, **case)
     n = case["n_docs"]
-    eng = factory(n + 1, rows_per_doc=40000, window_per_doc=8192, propsets_per_doc=8192, text_per_doc=1 << 19,
+    eng = factory(n + 2, rows_per_doc=40000, window_per_doc=8192, propsets_per_doc=8192, text_per_doc=1 << 19,
                   blocks_per_doc=16384)
     eng.props = props
     g = ClientGroup(eng)
-    clients = [g.new_client() for _ in range(n + 1)]
+    clients = [g.new_client({"newMergeTreeSnapshotFormat": True}) for _ in range(n + 1)]
     want, gblobs = golden_blobs("withAnnotations")
     assert clients[n].load(want) == {"catchupOps": []}
     od, _ = oracle_load(gblobs, props)
     assert clients[n].getText() == od.get_text()
+    # the reference's legacy file of the same string: loads, and re-emits byte-for-byte
+    lwant, lblobs = golden_legacy_blobs("withAnnotations")
+    lc = g.new_client()
+    assert lc.load(lwant) == {"catchupOps": []}
+    assert lc.getText() == od.get_text()
+    assert [e["value"]["contents"] for e in lc.snapshot()["entries"]] == lblobs
     for d in range(n):
         clients[d].load({("header" if i == 0 else f"body_{i - 1}"): b for i, b in enumerate(blobs_l[d])})
         for m in batch_to_messages(batch, props, d)[cut:]:

@@ -65,6 +65,14 @@ def compare(batch, props, n_docs, factory=None, **cap):
         assert eblobs == oblobs, f"doc {d} snapshot"
         assert edig == odig
         assert int(digs[d]) == odig, f"doc {d} mt_snapshot_digests"
+    # SnapshotLegacy at the same window: rows above the MSN are left out, rows
+    # removed above it keep their text (snapshotlegacy.ts:177-240).
+    legacy = eng.snapshot(range(n_docs), msn, seq, legacy=True)
+    for d in range(n_docs):
+        od, _ = oracle_docs[d]
+        oblobs, odig = od.snapshot(int(msn[d]), int(seq[d]), legacy=True)
+        assert legacy[d][0] == oblobs, f"doc {d} legacy snapshot"
+        assert legacy[d][1] == odig
     return eng
 
 

@@ -4,8 +4,8 @@ host emulation."""
 import pytest
 
 from test_gpu_parity import gpu_engine
-from test_snapshot_load import (COLLAB_CASES, GOLDEN, LOADBODY_CASES, check_collab, check_golden, check_loadbody,
-                                check_quiescent)
+from test_snapshot_load import (COLLAB_CASES, GOLDEN, LOADBODY_CASES, check_collab, check_golden,
+                                check_golden_legacy, check_loadbody, check_quiescent)
 
 pytestmark = pytest.mark.gpu
 
@@ -13,6 +13,11 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("name", GOLDEN)
 def test_gpu_loads_reference_snapshot(name):
     check_golden(name, gpu_engine)
+
+
+@pytest.mark.parametrize("name", GOLDEN)
+def test_gpu_legacy_snapshot_round_trip(name):
+    check_golden_legacy(name, gpu_engine)
 
 
 @pytest.mark.parametrize("case", COLLAB_CASES)

@@ -19,7 +19,8 @@ from test_emu_parity import CONFIGS, ann_props
 pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 
 EXPORTS = ["applyBatch", "create", "destroy", "docStatus", "docsOpen", "getLength", "getText", "lastError",
-           "loadSnapshot", "setClientNames", "setDocClientNames", "setProps", "setResidency", "snapshotV1", "sync", "syncAsync",
+           "loadSnapshot", "setClientNames", "setDocClientNames", "setProps", "setResidency", "snapshotLegacy", "snapshotV1", "sync",
+           "syncAsync",
            "updateSeq"]
 
 
@@ -29,8 +30,14 @@ def check(cfg, n_docs, addon, seed=31):
     batch, st, kept = generate(p, props, keep=True)
     assert st == [0] * n_docs
     msgs = [batch_to_messages(batch, props, d) for d in range(n_docs)]
+    # The reference's default (legacy) format too: even documents pass catch-up
+    # messages (their last 3), odd ones none; the blob is JSON.stringify(catchUpMsgs)
+    # under catchUpBlobName (snapshotlegacy.ts:162-172).
+    catch_up = [msgs[d][-3:] if d % 2 == 0 else [] for d in range(n_docs)]
+    blob_name = "randomNameForCatchUpOps"     # generateSharedStrings.ts:17 renames it the same way
     got = run_node(msgs, addon=addon, limits=dict(rowsPerDoc=20000, windowPerDoc=8192, propsetsPerDoc=8192,
-                                                  textPerDoc=1 << 18))
+                                                  textPerDoc=1 << 18),
+                   legacy={"options": {"catchUpBlobName": blob_name}, "catchUp": catch_up})
     last = batch.op_offsets[1:] - 1
     for d in range(n_docs):
         od = kept[d]
@@ -40,6 +47,11 @@ def check(cfg, n_docs, addon, seed=31):
         want = [("header" if i == 0 else f"body_{i - 1}", b.decode("utf-8")) for i, b in enumerate(blobs)]
         assert [tuple(x) for x in got["blobs"][d]] == want, f"doc {d} snapshot"
         assert int(got["digests"][d], 16) == dig
+        lblobs, _ = od.snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]), legacy=True)
+        want = [("header" if i == 0 else "body", b.decode("utf-8")) for i, b in enumerate(lblobs)]
+        if catch_up[d]:
+            want.append((blob_name, json.dumps(catch_up[d], separators=(",", ":"))))
+        assert [tuple(x) for x in got["legacy"][d]] == want, f"doc {d} legacy snapshot"
 
 
 def test_product_addon_loads_and_exports():

@@ -14,12 +14,15 @@ from fluidframework_amd.batch import PropTable
 from oracle_lib import OracleDoc
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "reference_snapshots_v1")
+# packages/dds/sequence/src/test/snapshots/legacy/*.json (legacyWithCatchUp/*.json are
+# byte-identical: these strings are detached, so no catch-up ops are recorded).
+GOLD_LEGACY = os.path.join(os.path.dirname(__file__), "golden", "reference_snapshots_legacy")
 SIZE_OF_FIRST_CHUNK = 10000  # SnapshotLegacy.sizeOfFirstChunk, snapshotlegacy.ts:57
 INSERT_TEXT = "text"
 
 
-def blobs_of(name):
-    d = json.load(open(os.path.join(GOLD, name + ".json")))
+def blobs_of(name, legacy=False):
+    d = json.load(open(os.path.join(GOLD_LEGACY if legacy else GOLD, name + ".json")))
     content = [e for e in d["entries"] if e["path"] == "content"][0]["value"]["entries"]
     return {e["path"]: e["value"]["contents"] for e in content}
 
@@ -58,3 +61,15 @@ def test_oracle_reproduces_reference_snapshot(name):
     assert list(got) == list(want)
     for k in want:
         assert got[k] == want[k], f"{name}/{k} differs"
+
+
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withMarkers", "withAnnotations"])
+def test_oracle_reproduces_reference_legacy_snapshot(name):
+    """SnapshotLegacy (the default format, snapshotlegacy.ts:104-240): header and body."""
+    want = blobs_of(name, legacy=True)
+    s = build(name)
+    blobs, _ = s.snapshot(0, 0, legacy=True)
+    got = {("header" if i == 0 else "body"): b.decode("utf-8") for i, b in enumerate(blobs)}
+    assert list(got) == list(want)
+    for k in want:
+        assert got[k] == want[k], f"legacy/{name}/{k} differs"

@@ -101,6 +101,39 @@ def check_golden(name, factory):
     assert [b.decode() for b in eb] == blobs
 
 
+def golden_legacy_blobs(name):
+    want = G.blobs_of(name, legacy=True)
+    return want, [want[k] for k in ("header", "body") if k in want]
+
+
+@pytest.mark.parametrize("name", GOLDEN)
+def test_oracle_legacy_snapshot_round_trip(name):
+    """Reference legacy files load (legacy chunk parsing) and re-serialize as
+    SnapshotLegacy byte-for-byte."""
+    want, blobs = golden_legacy_blobs(name)
+    d, st = oracle_load(blobs, PropTable())
+    assert st == 0
+    assert d.get_text() == G.build(name).get_text()
+    got, _ = d.snapshot(0, 0, legacy=True)
+    assert [b.decode() for b in got] == blobs
+
+
+@pytest.mark.parametrize("name", GOLDEN)
+def test_engine_legacy_snapshot_round_trip(name):
+    check_golden_legacy(name, emu_engine)
+
+
+def check_golden_legacy(name, factory):
+    want, blobs = golden_legacy_blobs(name)
+    props = PropTable()
+    eng = engine_load(factory, [parse_snapshot(want)], props)
+    assert int(eng.status([0])[0]) == 0
+    (eb, edig), = eng.snapshot([0], [0], [0], legacy=True)
+    assert [b.decode() for b in eb] == blobs
+    od, _ = oracle_load(blobs, props)
+    assert od.snapshot(0, 0, legacy=True)[1] == edig
+
+
 def test_parse_legacy_header_metadata():
     """Legacy chunks (version undefined) normalize as toLatestVersion does."""
     hdr = {"chunkStartSegmentIndex": 0, "chunkSegmentCount": 2, "chunkLengthChars": 5, "totalLengthChars": 5,
