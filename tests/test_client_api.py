@@ -109,3 +109,47 @@ def test_client_load_on_emulation_matches_oracle():
 @pytest.mark.gpu
 def test_client_load_on_gpu_matches_oracle():
     check_load(lambda n, **kw: Engine(n, device=0, **kw))
+
+
+def _msg(cid, seq, ref, msn, contents):
+    return dict(clientId=cid, sequenceNumber=seq, referenceSequenceNumber=ref, minimumSequenceNumber=msn, type="op",
+                contents=contents)
+
+
+def _legacy_header(texts, min_seq):
+    """Known-answer SnapshotLegacy header (snapshotlegacy.ts:74-98, snapshotChunks.ts:161-180)
+    for a document whose snapshot fits the first chunk."""
+    n = sum(len(t) for t in texts)
+    return json.dumps({"chunkStartSegmentIndex": 0, "chunkSegmentCount": len(texts), "chunkLengthChars": n,
+                       "totalLengthChars": n, "totalSegmentCount": len(texts), "chunkSequenceNumber": min_seq,
+                       "segmentTexts": texts,
+                       "headerMetadata": {"orderedChunkMetadata": [{"id": "header"}], "sequenceNumber": min_seq,
+                                          "totalLength": n, "totalSegmentCount": len(texts)}},
+                      separators=(",", ":"))
+
+
+def check_legacy_known_answers(factory):
+    """Hand-derived SnapshotLegacy bytes: an empty document; a remove above the MSN keeps its
+    text and coalesces; a segment inserted above the MSN is left to the catch-up ops; once the
+    MSN passes the remove, the removed text is gone and the survivors coalesce."""
+    g = ClientGroup(factory(2, **LIMITS))
+    empty, c = g.new_client(), g.new_client()
+    assert [e["value"]["contents"] for e in empty.snapshot()["entries"]] == [_legacy_header([], 0)]
+    c.applyMsg(_msg("a", 1, 0, 0, {"type": 0, "pos1": 0, "seg": "hello"}))
+    c.applyMsg(_msg("b", 2, 1, 0, {"type": 0, "pos1": 5, "seg": " world"}))
+    c.applyMsg(_msg("a", 3, 2, 1, {"type": 1, "pos1": 0, "pos2": 2}))
+    assert c.getText() == "llo world"
+    tree = c.snapshot()
+    assert [e["path"] for e in tree["entries"]] == ["header"]
+    assert tree["entries"][0]["value"]["contents"] == _legacy_header(["hello"], 1)
+    c.updateSeqNumbers(3, 3)
+    assert [e["value"]["contents"] for e in c.snapshot()["entries"]] == [_legacy_header(["llo world"], 3)]
+
+
+def test_legacy_known_answers_on_emulation():
+    check_legacy_known_answers(emu_engine)
+
+
+@pytest.mark.gpu
+def test_legacy_known_answers_on_gpu():
+    check_legacy_known_answers(lambda n, **kw: Engine(n, device=0, **kw))
