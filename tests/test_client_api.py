@@ -153,3 +153,29 @@ def test_legacy_known_answers_on_emulation():
 @pytest.mark.gpu
 def test_legacy_known_answers_on_gpu():
     check_legacy_known_answers(lambda n, **kw: Engine(n, device=0, **kw))
+
+
+def check_newline_blocks_append(factory):
+    """TextSegment.canAppend (textSegment.ts:63-68): a segment ending in "\\n" takes no
+    append, in zamboni's scour (mergeTree.ts:1278-1356) and in the snapshot's coalescing."""
+    g = ClientGroup(factory(1, **LIMITS))
+    c = g.new_client({"newMergeTreeSnapshotFormat": True})
+    c.applyMsg(_msg("a", 1, 0, 0, {"type": 0, "pos1": 0, "seg": "ab\n"}))
+    c.applyMsg(_msg("b", 2, 1, 0, {"type": 0, "pos1": 3, "seg": "cd"}))
+    c.applyMsg(_msg("a", 3, 2, 0, {"type": 0, "pos1": 5, "seg": "ef"}))
+    c.applyMsg(_msg("b", 4, 3, 0, {"type": 0, "pos1": 0, "seg": "x\n"}))
+    c.applyMsg(_msg("a", 5, 4, 0, {"type": 0, "pos1": 2, "seg": "y"}))
+    c.updateSeqNumbers(5, 5)
+    assert c.getText() == "x\nyab\ncdef"
+    assert [int(r[0]) for r in c.engine.dump(c.doc_id)] == [2, 4, 4]     # "x\n" | "yab\n" | "cdef"
+    hdr = json.loads(c.snapshot()["entries"][0]["value"]["contents"])
+    assert hdr["segments"] == ["x\n", "yab\n", "cdef"]
+
+
+def test_newline_blocks_append_on_emulation():
+    check_newline_blocks_append(emu_engine)
+
+
+@pytest.mark.gpu
+def test_newline_blocks_append_on_gpu():
+    check_newline_blocks_append(lambda n, **kw: Engine(n, device=0, **kw))
