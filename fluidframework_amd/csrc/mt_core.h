@@ -1016,19 +1016,12 @@ template <int RES> struct MtEngT {
     // prev restarts at every block, as each block is scoured separately.
     MT_HD int scourLeaves(const LaneArr<int>& blks, int nb, int nh) {
         // Lane t holds child slot t&7 of block t>>3; empty slots are masked out.
-        int bId[MT_MAXN], bN[MT_MAXN];
-#pragma unroll
-        for (int i = 0; i < MT_MAXN; i++) {
-            bId[i] = wave_at(blks, i < nb ? i : 0);
-            bN[i] = i < nb ? uni(bk(bId[i]).n) : 0;
-        }
+        // The block id comes by lane shuffle (no per-block scalar arrays: they spilled).
         const int span = 8 * nb;
+        const auto bsel = wave_gather8(blks);
         auto f = wave_map(span, [&](int t) MT_LAM {
-            const int bi = t >> 3;
-            int b = bId[0], n = bN[0];
-#pragma unroll
-            for (int i = 1; i < MT_MAXN; i++) if (bi == i) { b = bId[i]; n = bN[i]; }
-            return (t & 7) < n ? bk(b).c[t & 7] : -1;
+            const int b = own(bsel, t);
+            return (t & 7) < bk(b).n ? bk(b).c[t & 7] : -1;
         });
         uint64_t live = wave_ballot(wave_map(span, [&](int t) MT_LAM { return own(f, t) >= 0; }));
         auto fm = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? (int)row(g).meta : 0; });

@@ -113,6 +113,8 @@ template <int OFF> __device__ __forceinline__ int wave_from8(int a) {
     if constexpr (OFF < 0) return dpp0<0x110 | (-OFF)>(a);
     else return dpp0<0x100 | OFF>(a);
 }
+// lane t receives a[t / 8] (one value per group of 8 lanes); call from uniform control flow
+__device__ __forceinline__ int wave_gather8(int a) { return __shfl(a, __lane_id() >> 3); }
 // lane k's value replaced by v (k uniform)
 __device__ __forceinline__ int wave_set(int a, int k, int v) { return __lane_id() == k ? v : a; }
 // per-lane add into wave-private LDS (conflicting lanes serialize in hardware)
@@ -186,6 +188,11 @@ inline LaneArr<int> wave_from(const LaneArr<int>& a, int off) {
 template <int OFF> inline LaneArr<int> wave_from8(const LaneArr<int>& a) {
     LaneArr<int> r;
     for (int k = 0; k < MT_WAVE; k++) { const int s = (k & 15) + OFF; r.v[k] = (s >= 0 && s < 16) ? a.v[(k & ~15) + s] : 0; }
+    return r;
+}
+inline LaneArr<int> wave_gather8(const LaneArr<int>& a) {
+    LaneArr<int> r;
+    for (int t = 0; t < MT_WAVE; t++) r.v[t] = a.v[t >> 3];
     return r;
 }
 inline LaneArr<int> wave_set(LaneArr<int> a, int k, int v) { if (k >= 0 && k < MT_WAVE) a.v[k] = v; return a; }
