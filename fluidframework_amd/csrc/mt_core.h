@@ -59,6 +59,13 @@
 #define MT_B_HEAP 94
 #endif
 enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2 };
+// Diagnostic builds keep per-document phase/event counters (prof[]) across binds;
+// product builds never load or store them (8 SGPR pairs fewer live in the replay loop).
+#if defined(MT_PROFILE) || defined(MT_PROFILE2) || defined(MT_PROFILE3) || defined(MT_EVCOUNT) || defined(MT_EVCOUNT2)
+#define MT_KEEP_PROF 1
+#else
+#define MT_KEEP_PROF 0
+#endif
 
 // Phase profiling (diagnostic builds only, -DMT_PROFILE): shader-clock cycles
 // accumulated per phase into MtDocHdr.prof; never compiled into the product.
@@ -352,7 +359,9 @@ template <int RES> struct MtEngT {
     // uniform document state (MtDocHdr)
     int root, height, minSeq, curSeq, rowTop, blkTop, blkFree, heapN, winN, textTop, psetTop;
     uint32_t status;
-    unsigned long long c_ops, c_msgs, c_ins, c_rows, c_depth, c_scour;
+    // Counters of this bind (added into the header at store): 32-bit and zero-based, so
+    // they hold 6 SGPRs instead of 12 live across the replay loop.
+    uint32_t c_ops, c_msgs, c_ins, c_rows, c_depth, c_scour;
     unsigned long long prof[8];
     int textHalf; uint32_t blkCap;
     int nU; bool uValid; int uRef, uCli;
@@ -388,8 +397,10 @@ template <int RES> struct MtEngT {
         blkTop = uni(h.blkTop); blkFree = uni(h.blkFree); heapN = uni(h.heapN); winN = uni(h.winN); textTop = uni(h.textTop);
         psetTop = uni(h.psetTop); status = uni(h.status); textHalf = uni(h.textHalf);
         text = S.textBase + (size_t)textHalf * S.textCap;
+#if MT_KEEP_PROF
         for (int i = 0; i < 8; i++) prof[i] = h.prof[i];
-        c_ops = h.cnt[0]; c_msgs = h.cnt[1]; c_ins = h.cnt[2]; c_rows = h.cnt[3]; c_depth = h.cnt[4]; c_scour = h.cnt[5];
+#endif
+        c_ops = c_msgs = c_ins = c_rows = c_depth = c_scour = 0;
         nU = 0; uValid = false; uRef = -1; uCli = -1;
         heapTop = heapN > 0 ? uni(heap[1].maxSeq) : 0x7FFFFFFF;     // HBM home: bind precedes toLds
         lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0;
@@ -415,8 +426,11 @@ template <int RES> struct MtEngT {
               const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
               wave_for(m, [&](int k) MT_LAM { dst[base + k] = sc->rfree[base + k]; });
           } }
+#if MT_KEEP_PROF
         for (int i = 0; i < 8; i++) h.prof[i] = prof[i];
-        h.cnt[0] = c_ops; h.cnt[1] = c_msgs; h.cnt[2] = c_ins; h.cnt[3] = c_rows; h.cnt[4] = c_depth; h.cnt[5] = c_scour;
+#endif
+        h.cnt[0] += c_ops; h.cnt[1] += c_msgs; h.cnt[2] += c_ins; h.cnt[3] += c_rows; h.cnt[4] += c_depth;
+        h.cnt[5] += c_scour;
     }
     // Fresh empty collaborating document: root = empty block (MergeTree ctor :1105-1108,
     // startCollaboration :1243).
@@ -426,7 +440,11 @@ template <int RES> struct MtEngT {
         blkFreeN = 0; heapHW = 0; winHW = 0;
         text = S.textBase;
         c_ops = c_msgs = c_ins = c_rows = c_depth = c_scour = 0;
+        for (int i = 0; i < 6; i++) hdrp->cnt[i] = 0;               // store() adds this bind's counts
         for (int i = 0; i < 8; i++) prof[i] = 0;
+#if !MT_KEEP_PROF
+        for (int i = 0; i < 8; i++) hdrp->prof[i] = 0;
+#endif
         wave_for(8, [&](int i) MT_LAM { bk(0).c[i] = -1; });
         bk(0).len = 0; bk(0).parent = -1; bk(0).n = 0; bk(0).height = 0; bk(0).scour = -1;
     }
