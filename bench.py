@@ -55,6 +55,39 @@ CONFIGS = {
 }
 
 
+class Host:
+    """Where a bench run executes: the product (libmtgpu.so on the rank's GPU, RCCL for
+    config 5's exchange) unless a test driver substitutes the engine factory and the
+    backend (tests/bench_emu_driver.py runs the same code paths on the host emulation
+    with gloo to cover the multi-rank logic on CPU; its output is never a measurement)."""
+    factory = None          # (n_docs, device, **caps) -> Engine
+    backend = "nccl"        # config 5's collectives
+    device_type = "cuda"
+
+    @classmethod
+    def engine(cls, n, device, **kw):
+        if cls.factory is not None:
+            return cls.factory(n, device=device, **kw)
+        from fluidframework_amd.engine import Engine
+        return Engine(n, device=device, **kw)
+
+
+def launch(n, argv, script=None):
+    """`--gpus N` outside a torchrun environment: start N ranks, one process per GPU, with
+    torch.distributed.run on 127.0.0.1 (before anything here touches a GPU) and return
+    its exit code.  Every rank re-enters main() with RANK/LOCAL_RANK/WORLD_SIZE set."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(script or sys.argv[0])] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def ann_props():
     from fluidframework_amd.batch import PropTable
     pt = PropTable()
@@ -115,20 +148,32 @@ def cpu_baseline(eng, c, params_cls, seed, target_s, threads, ops_fn=None):
         eng.sync()
         b = eng.generated_download()
         st = np.zeros(n_docs, np.uint32)
-        secs = L.ora_replay_batch(ctypes.byref(b.to_c()), ctypes.byref(props.to_c()), threads, None,
+        dg = np.zeros(n_docs, np.uint64)
+        secs = L.ora_replay_batch(ctypes.byref(b.to_c()), ctypes.byref(props.to_c()), threads, dg.ctypes.data,
                                   st.ctypes.data)
-        return secs, int(b.op_offsets[-1])
+        return secs, int(b.op_offsets[-1]), dg, st
 
     pilot_docs = min(c["docs"], max(threads, 16))
-    t, n = run(pilot_docs)
+    t, n, dg, st = run(pilot_docs)
     docs = pilot_docs
     if t < target_s * 0.5:
         docs = int(min(c["docs"], max(pilot_docs, pilot_docs * target_s / max(t, 1e-3))))
         if docs > pilot_docs:
-            t, n = run(docs)
-    return {"value": n / t, "unit": "ops/s", "cores": threads, "kind": "port",
-            "sample": f"{docs} docs ({n} msgs) of the same workload, oracle (C++ restatement of "
-                      f"MT/mergeTree.ts + partialLengths.ts) on {threads} host threads, {t:.1f} s"}
+            t, n, dg, st = run(docs)
+    out = {"value": n / t, "unit": "ops/s", "cores": threads, "kind": "port",
+           "sample": f"{docs} docs ({n} msgs) of the same workload, oracle (C++ restatement of "
+                     f"MT/mergeTree.ts + partialLengths.ts) on {threads} host threads, {t:.1f} s"}
+    return out, dg, st
+
+
+def digest_parity(gpu_digests, oracle_digests, oracle_status):
+    """The bench line's parity field: SnapshotV1 digests of the timed replay's documents
+    against the oracle's replay of the same streams (the cpu_baseline sample)."""
+    k = len(oracle_digests)
+    same = int((np.asarray(gpu_digests[:k], np.uint64) == oracle_digests).sum())
+    if same == k and not np.asarray(oracle_status).any():
+        return f"SnapshotV1 digests == oracle on {k} docs (cpu_baseline sample) + status words clean"
+    return f"DIGEST MISMATCH: {k - same} of {k} sample docs differ from the oracle"
 
 
 def run_config4(args, c, world, rank, local):
@@ -138,7 +183,6 @@ def run_config4(args, c, world, rank, local):
     on top of it.  A step = restore the pre-built documents (device copy) +
     replay the measured stream."""
     from fluidframework_amd.batch import MtGenParams
-    from fluidframework_amd.engine import Engine
     dist = None
     if world > 1:
         import torch
@@ -147,7 +191,7 @@ def run_config4(args, c, world, rank, local):
         dist = (torch, tdist)
     n, pre, ops = c["docs"], c["prebuild"], c["ops"]
     rows = pre + 3 * ops + 64
-    eng = Engine(n, device=local, rows_per_doc=rows, blocks_per_doc=rows // 2 + 64, heap_per_doc=rows,
+    eng = Host.engine(n, local, rows_per_doc=rows, blocks_per_doc=rows // 2 + 64, heap_per_doc=rows,
                  window_per_doc=16384, text_per_doc=5 * pre + c["ins_len"] * ops + 4096,
                  propsets_per_doc=pre + ops + 64)
     eng.set_residency(RESIDENCY[args.residency])
@@ -232,7 +276,9 @@ def run_config4(args, c, world, rank, local):
         "gen_seconds": gen_s,
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_config4(eng, c, pa, pb, min(16, os.cpu_count() or 1))
+        out["cpu_baseline"], odg, ost = cpu_baseline_config4(eng, c, pa, pb, min(16, os.cpu_count() or 1))
+        if ok:
+            out["parity"] = digest_parity(digs, odg, ost)
     print(json.dumps(out), flush=True)
 
 
@@ -259,14 +305,16 @@ def cpu_baseline_config4(eng, c, pa, pb, threads):
     from fluidframework_amd.batch import concat_runs
     both = concat_runs(a, b)
     st = np.zeros(k, np.uint32)
+    dg = np.zeros(k, np.uint64)
     t_a = L.ora_replay_batch(ctypes.byref(a.to_c()), ctypes.byref(props.to_c()), threads, None, st.ctypes.data)
-    t_ab = L.ora_replay_batch(ctypes.byref(both.to_c()), ctypes.byref(props.to_c()), threads, None, st.ctypes.data)
+    t_ab = L.ora_replay_batch(ctypes.byref(both.to_c()), ctypes.byref(props.to_c()), threads, dg.ctypes.data,
+                              st.ctypes.data)
     n_b = int(b.op_offsets[-1])
     dt = max(t_ab - t_a, 1e-6)
     return {"value": n_b / dt, "unit": "ops/s", "cores": threads, "kind": "port",
             "sample": f"{k} pre-built docs ({int(a.op_offsets[-1])} prebuild + {n_b} measured msgs), oracle (C++ "
                       f"restatement of MT/mergeTree.ts + partialLengths.ts) on {threads} host threads; "
-                      f"measured-stream time = {t_ab:.1f} s - {t_a:.1f} s"}
+                      f"measured-stream time = {t_ab:.1f} s - {t_a:.1f} s"}, dg, st
 
 
 def run_config5(args, c, world, rank, local):
@@ -275,21 +323,23 @@ def run_config5(args, c, world, rank, local):
     rank, SnapshotV1 digests gathered to rank 0 (fluidframework_amd/shard.py)."""
     import torch
     from fluidframework_amd.batch import MtGenParams
-    from fluidframework_amd.engine import Engine
-    from fluidframework_amd.shard import SoloDist, build_sharded, clients_per_doc, zipf_op_counts
+    from fluidframework_amd.shard import SoloDist, build_sharded
+    device = torch.device(Host.device_type, local) if Host.device_type == "cuda" else torch.device("cpu")
     if world > 1:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if device.type == "cuda":
+            torch.cuda.set_device(local)
+            tdist.init_process_group(Host.backend, device_id=device)
+        else:
+            tdist.init_process_group(Host.backend)
         dist = tdist
     else:
         dist = SoloDist()
-    device = torch.device("cuda", local)
     total_docs = c["docs"] * world
     gen_kw = dict(lag_max=c["lag"], pct_insert=c["ins"], pct_remove=c["rem"], ins_len_max=c["ins_len"],
                   rem_len_max=c["rem_len"], n_ann_sets=c["ann_sets"], pct_rewrite=c["rewrite"])
     names = ['"c%d"' % i for i in range(64)]
-    fac = lambda n, caps: Engine(n, device=local, per_doc=caps)
+    fac = lambda n, caps: Host.engine(n, local, per_doc=caps)
     t0 = time.time()
     sh = build_sharded(dist, device, fac, total_docs, args.seed, MtGenParams, gen_kw, names=names)
     setup_s = time.time() - t0
@@ -346,30 +396,51 @@ def run_config5(args, c, world, rank, local):
     }
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline_config5(args, c, local)
+        if int(bad.item()) == 0:
+            out["parity"] = config5_parity(args, c, sh, digs)
     print(json.dumps(out), flush=True)
+
+
+def config5_parity(args, c, sh, digs, k=48):
+    """Oracle replay (its own generator, same seeds and per-document counts) of the
+    smallest-id documents, against the digests gathered to rank 0 (checker only)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fluidframework_amd.batch import MtGenParams
+    from oracle_lib import generate
+    k = min(k, len(sh.all_ops))
+    p = MtGenParams(args.seed, k, 0, 2, c["lag"], c["ins"], c["rem"], c["ins_len"], c["rem_len"], c["ann_sets"],
+                    c["rewrite"])
+    cl = sh.clients_all[:k] if getattr(sh, "clients_all", None) is not None else None
+    if cl is None:
+        return "status words clean on every rank (no client counts for an oracle check)"
+    batch, st, kept = generate(p, ann_props(), docs=range(k), keep=True, ops_per_doc=sh.all_ops[:k],
+                               clients_per_doc=cl)
+    last = batch.op_offsets[1:] - 1
+    odg = np.array([kept[d].snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]))[1]
+                    for d in range(k)], np.uint64)
+    return digest_parity(digs, odg, np.asarray(st)) + ", all ranks clean"
 
 
 def cpu_baseline_config5(args, c, local):
     """Oracle on a bounded sample of config-5 documents (same Zipf sizes)."""
     from fluidframework_amd.batch import MtGenParams
-    from fluidframework_amd.engine import Engine
     from fluidframework_amd.shard import clients_per_doc, generation_caps, zipf_op_counts
     threads = min(16, os.cpu_count() or 1)
     n = 4000
     ops = zipf_op_counts(n, args.seed ^ 0x5A)
     cl = clients_per_doc(n, args.seed ^ 0x5A)
-    eng = Engine(n, device=local, per_doc=generation_caps(ops, c["ins_len"]))
+    eng = Host.engine(n, local, per_doc=generation_caps(ops, c["ins_len"]))
     eng.upload_props(ann_props())
     eng.upload_names(['"c%d"' % i for i in range(64)])
     cc = dict(c)
     cc["docs"] = n
-    res = cpu_baseline(eng, cc, MtGenParams, args.seed ^ 0x5A, args.cpu_seconds, threads,
-                       ops_fn=lambda k: (ops[:k], cl[:k]))
+    res, _, _ = cpu_baseline(eng, cc, MtGenParams, args.seed ^ 0x5A, args.cpu_seconds, threads,
+                             ops_fn=lambda k: (ops[:k], cl[:k]))
     eng.close()
     return res
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -385,9 +456,14 @@ def main():
                     help="blk: blocks + heap in LDS, in-wave HBM continuation (default); hbm: every pool in HBM; "
                          "lds: rows/blocks/heap/window in LDS")
     ap.add_argument("--caps", default="", help="override pool caps, e.g. rows_per_doc=400,text_per_doc=16384")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: re-enter this script under torch.distributed.run
+        raise SystemExit(launch(args.gpus, sys.argv[1:] if argv is None else argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.config == "config4":
@@ -412,7 +488,6 @@ def main():
         dist = (torch, tdist)
 
     from fluidframework_amd.batch import MtGenParams
-    from fluidframework_amd.engine import Engine
 
     c = dict(CONFIGS[args.config])
     if args.docs:
@@ -423,7 +498,7 @@ def main():
     for kv in filter(None, args.caps.split(",")):
         k, v = kv.split("=")
         caps[k] = int(v)
-    eng = Engine(c["docs"], device=local, **caps)
+    eng = Host.engine(c["docs"], local, **caps)
     eng.set_residency(RESIDENCY[args.residency])
     eng.upload_props(ann_props())
     eng.upload_names(['"c%d"' % i for i in range(64)])
@@ -523,7 +598,9 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(eng, c, MtGenParams, seed, args.cpu_seconds, threads)
+        out["cpu_baseline"], odg, ost = cpu_baseline(eng, c, MtGenParams, seed, args.cpu_seconds, threads)
+        if ok:
+            out["parity"] = digest_parity(digs, odg, ost)
     print(json.dumps(out), flush=True)
 
 

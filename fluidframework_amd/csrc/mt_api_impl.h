@@ -208,7 +208,7 @@ static int mt_upload_ops(mt_ctx* c, const mt_op_batch* B) {
 #undef UP
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
-    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = B->n_runs;
+    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = B->n_runs; o.payload_units = B->payload_units;
     c->n_runs = B->n_runs;
     return MT_OK;
 }
@@ -501,6 +501,19 @@ static int mt_stage_docs(mt_ctx* c, uint32_t n, const uint32_t* docs, std::vecto
     return MT_OK;
 }
 
+// Client.snapshot asserts on the window it moves to (updateSeqNumbers, client.ts:843-850 ->
+// setMinSeq, mergeTree.ts:1712-1716): a document whose status word is set after that
+// (or before it) has no snapshot; the call fails instead of serializing it.
+static int mt_check_staged_status(mt_ctx* c, uint32_t n, const uint32_t* docs, const std::vector<MtSnapView>& v) {
+    for (uint32_t i = 0; i < n; i++)
+        if (v[i].hdr.status) {
+            char b[96];
+            snprintf(b, sizeof b, "document %u has status 0x%x (the reference would have thrown)", docs[i], v[i].hdr.status);
+            c->err = b;
+            return MT_E_DOC_STATUS;
+        }
+    return MT_OK;
+}
 // Client.snapshot (client.ts:923-956): SnapshotV1 or, with legacy set, SnapshotLegacy.
 static int mt_snapshot_blobs(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t* msn, const int32_t* seq,
                              uint64_t* digest, const char** arena, const uint64_t** blob_off,
@@ -510,6 +523,7 @@ static int mt_snapshot_blobs(mt_ctx* c, uint32_t n, const uint32_t* docs, const 
     if (rc) return rc;
     std::vector<uint8_t> host; std::vector<MtSnapView> views;
     if ((rc = mt_stage_docs(c, n, docs, host, views))) return rc;
+    if ((rc = mt_check_staged_status(c, n, docs, views))) return rc;
     c->snap_arena.clear(); c->blob_off.assign(1, 0); c->blob_first.assign(1, 0);
     for (uint32_t i = 0; i < n; i++) {
         auto dn = c->doc_clients.find(docs[i]);
@@ -544,6 +558,7 @@ int MT_FN(snapshot_digests)(mt_ctx* c, uint32_t n, const uint32_t* docs, const i
     if (rc) return rc;
     std::vector<uint8_t> host; std::vector<MtSnapView> views;
     if ((rc = mt_stage_docs(c, n, docs, host, views))) return rc;
+    if ((rc = mt_check_staged_status(c, n, docs, views))) return rc;
     if (threads < 1) threads = 1;
     if ((uint32_t)threads > n) threads = (int)(n ? n : 1);
     auto work = [&](int t) {
@@ -606,6 +621,8 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     if (!c || !P || P->n_docs == 0 || P->n_docs > c->S.maxDocs || P->ins_len_max == 0 || P->rem_len_max == 0 ||
         P->n_ann_sets == 0) return MT_E_INVALID;
     if (P->pct_insert + P->pct_remove < 100 && P->n_ann_sets > c->S.p_nsets) { c->err = "annotate prop sets not uploaded"; return MT_E_INVALID; }
+    if (P->ins_len_min > P->ins_len_max) { c->err = "ins_len_min > ins_len_max"; return MT_E_INVALID; }
+    if (P->seg_prop_sets > c->S.p_nsets) { c->err = "segment prop sets not uploaded"; return MT_E_INVALID; }
     std::vector<uint32_t> docs(P->n_docs), off(P->n_docs + 1), cl(P->n_docs);
     off[0] = 0;
     for (uint32_t i = 0; i < P->n_docs; i++) {
@@ -629,15 +646,13 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     mtb_h2d(c, c->b_gencl.p, cl.data(), 4ull * P->n_docs);
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
-    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs;
+    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs; o.payload_units = PU;
     c->n_runs = P->n_docs;
     c->gen_off.assign(off.begin(), off.end());
     if (!P->continue_docs) {
         rc = MT_FN(docs_open)(c, 0, P->n_docs);
         if (rc) return rc;
     }
-    if (P->ins_len_min > P->ins_len_max) { c->err = "ins_len_min > ins_len_max"; return MT_E_INVALID; }
-    if (P->seg_prop_sets > c->S.p_nsets) { c->err = "segment prop sets not uploaded"; return MT_E_INVALID; }
     MtGen g{};
     g.seed = P->seed; g.ops = P->ops_per_doc; g.clients = P->clients; g.lag_max = P->lag_max;
     g.pct_insert = P->pct_insert; g.pct_remove = P->pct_remove; g.ins_len_max = P->ins_len_max;
@@ -703,7 +718,7 @@ int MT_FN(upload_batch_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids,
     if (payload_units) mtb_d2d(c, c->b_pay.p, payload, 2 * payload_units);
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
-    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs;
+    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs; o.payload_units = payload_units;
     c->n_runs = n_runs;
     c->gen.enabled = 0;
     return mtb_sync(c);

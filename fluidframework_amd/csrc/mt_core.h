@@ -195,6 +195,7 @@ struct MtOps {                                // device copy of an mt_op_batch
     MtOpRec* rec;
     uint16_t* payload;
     uint32_t n_runs;
+    uint64_t payload_units;                   // records are bounds-checked against it on the device
 };
 
 // Snapshot load (mt_load_snapshot): the segments of each document (mt_load_seg)

@@ -104,6 +104,9 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
             if (c >= 64) e.status |= MT_DS_UNSUPPORTED;
             if (e.curSeq >= sq) e.status |= MT_DS_ASSERT_SEQ;       // completeAndLogOp, MT/client.ts:482
             if (e.minSeq > ms) e.status |= MT_DS_ASSERT_MSN;        // MT/client.ts:484
+            if (r < e.minSeq) e.status |= MT_DS_REFSEQ_BELOW_MSN;   // nacked by deli (deli/lambda.ts:302-318)
+            if (ty == MT_OP_INSERT && !(fl & MT_OPF_MARKER) && (uint64_t)poff + (uint64_t)plen > ops.payload_units)
+                e.status |= MT_DS_BAD_OP;
             if (e.status) break;
             if (!(e.uValid && e.uRef == r && e.uCli == c)) e.computeU(r, c, true);
             if (ty == MT_OP_INSERT) {

@@ -407,9 +407,13 @@ class MergeTreeClient:
         self.pending.append(msg)
 
     def updateSeqNumbers(self, min_seq: int, seq: int):
+        """Client.updateSeqNumbers (client.ts:843-850): the device window moves, and so
+        do the host copies that snapshot() passes back to mt_update_seq."""
         self.group.flush()
         self.engine.update_seq([self.doc_id], [min_seq], [seq])
+        self.engine.sync()
         self._raise_status()
+        self.min_seq, self.current_seq = int(min_seq), int(seq)
 
     def _raise_status(self):
         st = int(self.engine.status([self.doc_id])[0])

@@ -31,7 +31,7 @@ const F_END = 1, F_MARKER = 2, F_REWRITE = 4, F_SEG_PROPS = 8, F_COMBINE = 16;
 const STATUS = {
     0x01: "ASSERT_SEQ", 0x02: "ASSERT_MSN", 0x04: "INSERT_FAILED", 0x08: "UNSUPPORTED",
     0x10: "OOM_ROWS", 0x20: "OOM_BLOCKS", 0x40: "OOM_TEXT", 0x80: "OOM_PROPS",
-    0x100: "OOM_HEAP", 0x200: "OOM_WINDOW", 0x400: "PROPS_TOO_MANY",
+    0x100: "OOM_HEAP", 0x200: "OOM_WINDOW", 0x400: "PROPS_TOO_MANY", 0x800: "BAD_OP", 0x1000: "REFSEQ_BELOW_MSN",
 };
 function statusNames(st) {
     return Object.keys(STATUS).filter((b) => st & Number(b)).map((b) => STATUS[b]);

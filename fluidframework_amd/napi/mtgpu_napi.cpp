@@ -28,7 +28,11 @@ namespace {
         }                                                                          \
     } while (0)
 
-struct Ctx { mt_ctx* c = nullptr; };
+// One JS-visible engine context.  Single-caller contract: while a syncAsync is
+// pending (busy), every other call on the context throws, and destroy() is
+// deferred to the worker's completion; the pending work holds a reference to
+// the external, so it cannot be finalized under the worker.
+struct Ctx { mt_ctx* c = nullptr; int busy = 0; bool destroy_pending = false; };
 
 napi_value throw_rc(napi_env env, mt_ctx* c, int rc, const char* what) {
     std::string m = std::string(what) + " failed (" + std::to_string(rc) + "): " + (c ? mt_last_error(c) : "no context");
@@ -49,8 +53,12 @@ bool get_args(napi_env env, napi_callback_info info, size_t want, napi_value* ar
 
 mt_ctx* get_ctx(napi_env env, napi_value v) {
     void* p = nullptr;
-    if (napi_get_value_external(env, v, &p) != napi_ok || !p || !((Ctx*)p)->c) {
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p || !((Ctx*)p)->c || ((Ctx*)p)->destroy_pending) {
         napi_throw_type_error(env, nullptr, "expected an engine context (destroyed?)");
+        return nullptr;
+    }
+    if (((Ctx*)p)->busy) {
+        napi_throw_error(env, nullptr, "engine context busy: a syncAsync is pending (await it first)");
         return nullptr;
     }
     return ((Ctx*)p)->c;
@@ -136,8 +144,9 @@ napi_value Destroy(napi_env env, napi_callback_info info) {
     if (!get_args(env, info, 1, argv)) return nullptr;
     void* p = nullptr;
     if (napi_get_value_external(env, argv[0], &p) == napi_ok && p && ((Ctx*)p)->c) {
-        mt_destroy(((Ctx*)p)->c);
-        ((Ctx*)p)->c = nullptr;
+        Ctx* x = (Ctx*)p;
+        if (x->busy) x->destroy_pending = true;          // sync_done destroys it
+        else { mt_destroy(x->c); x->c = nullptr; }
     }
     return undefined(env);
 }
@@ -286,27 +295,34 @@ napi_value Sync(napi_env env, napi_callback_info info) {
 }
 
 // syncAsync(ctx) -> Promise: mt_sync on a libuv worker so the event loop is not blocked.
-struct SyncWork { mt_ctx* c; int rc; napi_deferred d; napi_async_work w; };
+struct SyncWork { Ctx* x; mt_ctx* c; int rc; napi_deferred d; napi_async_work w; napi_ref ref; };
 void sync_exec(napi_env, void* data) { SyncWork* s = (SyncWork*)data; s->rc = mt_sync(s->c); }
 void sync_done(napi_env env, napi_status, void* data) {
     SyncWork* s = (SyncWork*)data;
+    std::string m = s->rc ? "mt_sync failed (" + std::to_string(s->rc) + "): " + mt_last_error(s->c) : std::string();
+    s->x->busy = 0;
+    if (s->x->destroy_pending) { mt_destroy(s->x->c); s->x->c = nullptr; s->x->destroy_pending = false; }
     if (s->rc == 0) napi_resolve_deferred(env, s->d, undefined(env));
     else {
-        std::string m = "mt_sync failed (" + std::to_string(s->rc) + "): " + mt_last_error(s->c);
         napi_value msg, err;
         napi_create_string_utf8(env, m.c_str(), m.size(), &msg);
         napi_create_error(env, nullptr, msg, &err);
         napi_reject_deferred(env, s->d, err);
     }
     napi_delete_async_work(env, s->w);
+    napi_delete_reference(env, s->ref);
     delete s;
 }
 napi_value SyncAsync(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     if (!get_args(env, info, 1, argv)) return nullptr;
     mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
-    SyncWork* s = new SyncWork{c, 0, nullptr, nullptr};
+    void* xp = nullptr;
+    napi_get_value_external(env, argv[0], &xp);
+    SyncWork* s = new SyncWork{(Ctx*)xp, c, 0, nullptr, nullptr, nullptr};
     napi_value promise, name;
+    NAPI_OK(napi_create_reference(env, argv[0], 1, &s->ref));     // keeps the context alive until sync_done
+    s->x->busy = 1;
     NAPI_OK(napi_create_promise(env, &s->d, &promise));
     napi_create_string_utf8(env, "mt_sync", NAPI_AUTO_LENGTH, &name);
     NAPI_OK(napi_create_async_work(env, nullptr, name, sync_exec, sync_done, s, &s->w));

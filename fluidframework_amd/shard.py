@@ -99,6 +99,9 @@ class SoloDist:
     def all_gather(self, outs, t):
         outs[0].copy_(t)
 
+    def gather(self, t, gather_list=None, dst=0):
+        gather_list[0].copy_(t)
+
 
 CAP_KEYS = ("rows_per_doc", "blocks_per_doc", "heap_per_doc", "window_per_doc", "text_per_doc", "propsets_per_doc")
 
@@ -107,8 +110,10 @@ class ShardedReplay:
     """One rank's share of a sharded replay: an Engine holding its documents with
     their op streams resident, plus the plan (owner of every global document)."""
 
-    def __init__(self, engine, owned: np.ndarray, all_ops: np.ndarray, owner: np.ndarray, timings: dict):
+    def __init__(self, engine, owned: np.ndarray, all_ops: np.ndarray, owner: np.ndarray, timings: dict,
+                 clients_all: np.ndarray | None = None):
         self.engine, self.owned, self.all_ops, self.owner, self.timings = engine, owned, all_ops, owner, timings
+        self.clients_all = clients_all     # authoring clients of every global document
         self.ops = all_ops[owned]          # engine document slot i holds global document owned[i]
 
     @property
@@ -133,8 +138,9 @@ class ShardedReplay:
         buf = torch.zeros(mx, dtype=torch.int64, device=device)
         if n:
             buf[:n] = torch.from_numpy(dig.view(np.int64)).to(device)
-        out = [torch.zeros(mx, dtype=torch.int64, device=device) for _ in range(world)]
-        dist.all_gather(out, buf)
+        # a gather to rank 0 (the only consumer), not an all-gather
+        out = [torch.zeros(mx, dtype=torch.int64, device=device) for _ in range(world)] if rank == 0 else None
+        dist.gather(buf, gather_list=out, dst=0)
         self.timings["digest_ms"] = (time.perf_counter() - t0) * 1e3
         if rank != 0:
             return None
@@ -260,4 +266,4 @@ def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_
     eng.upload_batch_dev(np.arange(len(owned)), loc_off.astype(np.uint32),
                          rec_recv.data_ptr() if my_ops else 0, pay_recv.data_ptr() if my_ops else 0, my_ops * L)
     del rec_recv, pay_recv
-    return ShardedReplay(eng, owned, ops, owner, tm)
+    return ShardedReplay(eng, owned, ops, owner, tm, cli)

@@ -54,6 +54,8 @@ extern "C" {
 #define MT_E_INVALID        1  /* bad argument / shape                          */
 #define MT_E_HIP            2  /* a HIP runtime call failed                     */
 #define MT_E_OOM            3  /* a per-document pool (rows/blocks/text) is full */
+#define MT_E_DOC_STATUS     4  /* a snapshot was asked of a document whose status
+                                  word is set (the reference would have thrown)  */
 /* per-document status bits (mt_doc_status) */
 #define MT_DS_ASSERT_SEQ     0x01u /* currentSeq >= seq   (MT/client.ts:482, :846) */
 #define MT_DS_ASSERT_MSN     0x02u /* msn went backwards  (MT/client.ts:484, mergeTree.ts:1716) */
@@ -66,6 +68,11 @@ extern "C" {
 #define MT_DS_OOM_HEAP       0x100u
 #define MT_DS_OOM_WINDOW     0x200u
 #define MT_DS_PROPS_TOO_MANY 0x400u
+#define MT_DS_BAD_OP         0x800u /* an op record out of its batch's bounds (payload /
+                                       property table), checked on the device         */
+#define MT_DS_REFSEQ_BELOW_MSN 0x1000u /* refSeq < minSeq: deli nacks such ops
+                                       (deli/lambda.ts:302-318); the window aggregate
+                                       is exact only for refSeq >= minSeq             */
 
 /* ---- op records (IMergeTreeOp flattened; MT/ops.ts:6-110) --------------- */
 #define MT_OP_INSERT   0   /* MergeTreeDeltaType.INSERT   */

@@ -1,0 +1,48 @@
+"""bench.py's multi-GPU path on CPU: `--gpus 2` starts two ranks under
+torch.distributed.run, each replays its own documents (config 2: weak scaling, gloo
+barrier, max-over-ranks time) or its LPT share after rank 0's ingest (config 5:
+all_to_all redistribution + digest gather to rank 0), and rank 0 prints one JSON line
+with n_gpus 2.  At N=1 the line carries the digest parity check against the oracle.
+Runs bench's code on the host emulation (tests/bench_emu_driver.py)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "tests", "bench_emu_driver.py")
+
+
+def run(*args, timeout=300):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, DRIVER, *args], capture_output=True, text=True, timeout=timeout, env=env,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_launcher_config2_two_ranks():
+    out = run("--gpus", "2", "--config", "config2", "--docs", "3", "--ops", "400", "--steps", "2", "--warmup", "1",
+              "--no-cpu-baseline")
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
+    assert out["parity"] == "status words clean"
+    assert out["value"] > 0 and out["steps"] == 2
+
+
+def test_launcher_config5_two_ranks():
+    out = run("--gpus", "2", "--config", "config5", "--docs", "5", "--steps", "1", "--warmup", "0",
+              "--no-cpu-baseline")
+    assert out["n_gpus"] == 2
+    assert out["config"]["docs_total"] == 10
+    assert out["parity"].startswith("status words clean on every rank")
+
+
+def test_single_rank_digest_parity_against_oracle():
+    out = run("--config", "config2", "--docs", "20", "--ops", "300", "--steps", "1", "--warmup", "0",
+              "--cpu-seconds", "0.2")
+    assert out["n_gpus"] == 1
+    assert out["parity"].startswith("SnapshotV1 digests == oracle on"), out["parity"]
+    assert out["cpu_baseline"]["kind"] == "port"

@@ -143,7 +143,13 @@ def check_legacy_known_answers(factory):
     assert [e["path"] for e in tree["entries"]] == ["header"]
     assert tree["entries"][0]["value"]["contents"] == _legacy_header(["hello"], 1)
     c.updateSeqNumbers(3, 3)
+    assert (c.min_seq, c.current_seq) == (3, 3)
     assert [e["value"]["contents"] for e in c.snapshot()["entries"]] == [_legacy_header(["llo world"], 3)]
+    # the snapshot's own updateSeqNumbers(3, 3) must not move the MSN backwards (setMinSeq
+    # asserts, mergeTree.ts:1716): the document stays readable afterwards
+    assert int(c.engine.status([c.doc_id])[0]) == 0
+    assert c.getText() == "llo world"
+    assert c.snapshot()["entries"][0]["value"]["contents"] == _legacy_header(["llo world"], 3)
 
 
 def test_legacy_known_answers_on_emulation():
@@ -179,3 +185,31 @@ def test_newline_blocks_append_on_emulation():
 @pytest.mark.gpu
 def test_newline_blocks_append_on_gpu():
     check_newline_blocks_append(lambda n, **kw: Engine(n, device=0, **kw))
+
+
+def check_status_guards(factory):
+    """A refSeq below the MSN (deli nacks it, deli/lambda.ts:302-318) is flagged, not
+    replayed; a snapshot of a document with a status word fails (mt_snapshot_v1 returns
+    MT_E_DOC_STATUS) instead of serializing it."""
+    g = ClientGroup(factory(2, **LIMITS))
+    a, b = g.new_client({"newMergeTreeSnapshotFormat": True}), g.new_client({"newMergeTreeSnapshotFormat": True})
+    for c in (a, b):
+        c.applyMsg(_msg("x", 1, 0, 0, {"type": 0, "pos1": 0, "seg": "abc"}))
+        c.applyMsg(_msg("y", 2, 1, 1, {"type": 0, "pos1": 3, "seg": "def"}))
+    a.applyMsg(_msg("x", 3, 0, 1, {"type": 1, "pos1": 0, "pos2": 1}))       # refSeq 0 < minSeq 1
+    with pytest.raises(MergeTreeError, match="REFSEQ_BELOW_MSN"):
+        a.getText()
+    with pytest.raises(MergeTreeError):
+        a.snapshot()
+    assert b.getText() == "abcdef"                                         # other documents unaffected
+    with pytest.raises(MergeTreeError, match=r"\(4\)"):
+        g.engine.snapshot([a.doc_id], [1], [3])
+
+
+def test_status_guards_on_emulation():
+    check_status_guards(emu_engine)
+
+
+@pytest.mark.gpu
+def test_status_guards_on_gpu():
+    check_status_guards(lambda n, **kw: Engine(n, device=0, **kw))
