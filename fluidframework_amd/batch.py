@@ -195,6 +195,16 @@ class OpBatch:
                        arrs, np.ascontiguousarray(payload, np.uint16))
 
 
+def _group_members(op) -> list:
+    """applyRemoteOp's GROUP recursion (client.ts:804-812), flattened in order; every
+    member carries the message's seq."""
+    if not isinstance(op, dict):
+        return []
+    if op.get("type") == 3:
+        return [m for sub in (op.get("ops") or []) for m in _group_members(sub)]
+    return [op]
+
+
 class BatchBuilder:
     """Packs ISequencedDocumentMessage dicts (protocol.ts:126-166) per document."""
 
@@ -244,7 +254,9 @@ class BatchBuilder:
             else:
                 raise ValueError(f"Unrecognized IJSONSegment type: {seg!r}")
             pid = -1
-            if props:
+            if props is not None and jsjson.js_truthy(props):     # `if (props)` in TextSegment/Marker.make
+                if not isinstance(props, dict):
+                    raise ValueError(f"segment props must be an object: {props!r}")
                 pid = self.props.intern(props)
                 fl |= MT_OPF_SEG_PROPS
             units = jsjson.utf16_units(text) if text is not None else []
@@ -267,14 +279,17 @@ class BatchBuilder:
 
     def add_message(self, msg: dict):
         """One sequenced message (Client.applyMsg semantics, client.ts:819-841)."""
+        if not isinstance(msg.get("clientId"), str):
+            # getOrAddShortClientId keys a RedBlackTree with localeCompare (client.ts:73, :658):
+            # a null id cannot be registered once the tree holds ids
+            raise ValueError("clientId must be a string on the batch path")
         client = self.names.index(msg["clientId"])
         seq, ref, msn = int(msg["sequenceNumber"]), int(msg["referenceSequenceNumber"]), int(msg["minimumSequenceNumber"])
         if msg.get("type", "op") != "op":
             self._emit(type=MT_OP_NOOP, flags=MT_OPF_END_OF_MSG, client=client, seq=seq, ref_seq=ref, msn=msn, prop_id=-1)
             return
-        op = msg["contents"]
-        members = op["ops"] if op["type"] == 3 else [op]
-        members = [m for m in members if m["type"] in (MT_OP_INSERT, MT_OP_REMOVE, MT_OP_ANNOTATE)]
+        members = [m for m in _group_members(msg.get("contents"))
+                   if m.get("type") in (MT_OP_INSERT, MT_OP_REMOVE, MT_OP_ANNOTATE)]
         if not members:
             self._emit(type=MT_OP_NOOP, flags=MT_OPF_END_OF_MSG, client=client, seq=seq, ref_seq=ref, msn=msn, prop_id=-1)
             return

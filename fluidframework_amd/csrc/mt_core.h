@@ -30,7 +30,7 @@
 #include "../../include/mtgpu.h"
 
 #define MT_MAXH 16                    // max tree height (7^16 segments)
-#define MT_PSK 8                      // property keys per segment (more: PROPS_TOO_MANY)
+#define MT_PSK 16                     // property keys per segment, one per lane (more: PROPS_TOO_MANY)
 #define MT_MAXN 8                     // MaxNodesInBlock, MT/mergeTree.ts:350
 #define MT_GRAN 256                   // TextSegmentGranularity, MT/mergeTree.ts:1056
 #define MT_ZMAX 2                     // zamboniSegmentsMaxCount, MT/mergeTree.ts:1058
@@ -1241,17 +1241,17 @@ template <int RES> struct MtEngT {
             if (nv < 0) {
                 if (at >= 0) {
                     auto k1 = wave_from8<1>(kk), v1 = wave_from8<1>(vv);
-                    kk = wave_map(8, [&](int i) MT_LAM { const int a = own(kk, i), b = own(k1, i); return i < at ? a : b; });
-                    vv = wave_map(8, [&](int i) MT_LAM { const int a = own(vv, i), b = own(v1, i); return i < at ? a : b; });
+                    kk = wave_map(MT_PSK, [&](int i) MT_LAM { const int a = own(kk, i), b = own(k1, i); return i < at ? a : b; });
+                    vv = wave_map(MT_PSK, [&](int i) MT_LAM { const int a = own(vv, i), b = own(v1, i); return i < at ? a : b; });
                     n--;
                 }
             } else if (at >= 0) {
-                vv = wave_map(8, [&](int i) MT_LAM { return i == at ? nv : own(vv, i); });
+                vv = wave_map(MT_PSK, [&](int i) MT_LAM { return i == at ? nv : own(vv, i); });
             } else {
                 if (n >= MT_PSK) { status |= MT_DS_PROPS_TOO_MANY; psetTop--; return old; }
                 const int at2 = n;
-                kk = wave_map(8, [&](int i) MT_LAM { return i == at2 ? key : own(kk, i); });
-                vv = wave_map(8, [&](int i) MT_LAM { return i == at2 ? nv : own(vv, i); });
+                kk = wave_map(MT_PSK, [&](int i) MT_LAM { return i == at2 ? key : own(kk, i); });
+                vv = wave_map(MT_PSK, [&](int i) MT_LAM { return i == at2 ? nv : own(vv, i); });
                 n++;
             }
         }

@@ -145,7 +145,10 @@ class BatchBuilder {
             else if (seg.marker !== undefined) { props = seg.props; fl |= F_MARKER; pos2 = seg.marker.refType || 0; }
             else throw new Error("Unrecognized IJSONSegment type");
             let pid = -1;
-            if (props) { pid = this.props.intern(props); fl |= F_SEG_PROPS; }
+            if (props) {                                       // `if (props)` in TextSegment/Marker.make
+                if (typeof props !== "object") throw new Error("segment props must be an object");
+                pid = this.props.intern(props); fl |= F_SEG_PROPS;
+            }
             const off = this.payload.length;
             if (text !== null) for (let i = 0; i < text.length; i++) this.payload.push(text.charCodeAt(i));
             this.emit({ ...common, type: OP_INSERT, flags: fl, pos1: op.pos1, pos2, payloadOff: off,
@@ -164,14 +167,17 @@ class BatchBuilder {
     }
     /** One sequenced message (Client.applyMsg, client.ts:819-841). */
     addMessage(msg) {
+        // getOrAddShortClientId keys a RedBlackTree with localeCompare (client.ts:73, :658)
+        if (typeof msg.clientId !== "string") throw new Error("clientId must be a string on the batch path");
         const client = this.names.index(msg.clientId);
         const seq = msg.sequenceNumber, ref = msg.referenceSequenceNumber, msn = msg.minimumSequenceNumber;
         if ((msg.type === undefined ? "op" : msg.type) !== "op") {
             this.emit({ type: OP_NOOP, flags: F_END, client, seq, refSeq: ref, msn, propId: -1 });
             return;
         }
-        const op = msg.contents;
-        const members = (op.type === OP_GROUP ? op.ops : [op]).filter((m) => m.type === OP_INSERT || m.type === OP_REMOVE || m.type === OP_ANNOTATE);
+        // applyRemoteOp's GROUP recursion (client.ts:804-812), flattened; members share the seq
+        const flat = (op) => (op && typeof op === "object") ? (op.type === OP_GROUP ? (op.ops || []).flatMap(flat) : [op]) : [];
+        const members = flat(msg.contents).filter((m) => m.type === OP_INSERT || m.type === OP_REMOVE || m.type === OP_ANNOTATE);
         if (!members.length) { this.emit({ type: OP_NOOP, flags: F_END, client, seq, refSeq: ref, msn, propId: -1 }); return; }
         members.forEach((m, i) => this.member(m, client, seq, ref, msn, i === members.length - 1));
     }

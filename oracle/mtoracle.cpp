@@ -1289,6 +1289,96 @@ int ora_set_props(ora_doc* d, const mt_prop_table* p) { load_props(d->d.props, p
 int ora_set_client_names(ora_doc* d, uint32_t n, const char* const* cj) { d->d.names.clear(); for (uint32_t i = 0; i < n; i++) d->d.names.push_back(cj[i]); return 0; }
 uint32_t ora_apply_run(ora_doc* d, const mt_op_batch* b, uint32_t run) { return apply_run(d->d, b, run); }
 
+/* ---- Client.applyMsg on the message itself (MT/client.ts:790-850) ----
+ * Independent of the hosts' packers: the ISequencedDocumentMessage JSON is parsed
+ * here and dispatched as the reference does, with its own short-id registration,
+ * GROUP recursion and property interning. */
+// Interns an op's props object (Object.keys order, MT/segmentPropertiesManager.ts:91) as a set.
+static int intern_props_json(Doc& d, const JVal& props) {
+    std::vector<std::pair<u16s, int>> set;
+    for (int i : obj_order(props)) {
+        const JVal& v = props.ovals[i];
+        if (v.t == JVal::Null || v.t == JVal::Undef) set.push_back({props.okeys[i], -1});
+        else { d.props.values.push_back(v); set.push_back({props.okeys[i], (int)d.props.values.size() - 1}); }
+    }
+    d.props.sets.push_back(set);
+    return (int)d.props.sets.size() - 1;
+}
+static bool jnum(const JVal& o, const char16_t* k, int& out) {
+    const JVal* v = jget(o, k);
+    if (!v || v->t != JVal::Num) return false;
+    out = (int)v->n;
+    return true;
+}
+// completeAndLogOp's remote asserts (MT/client.ts:482-485), after the op as in the reference.
+static void complete_op(Tree& t, int seq, int msn) {
+    if (t.currentSeq >= seq) t.status |= MT_DS_ASSERT_SEQ;
+    if (t.minSeq > msn) t.status |= MT_DS_ASSERT_MSN;
+}
+static void apply_remote_json(Doc& d, const JVal& op, int cl, int ref, int seq, int msn) {       // applyRemoteOp :790-817
+    Tree& t = d.t;
+    int type;
+    if (op.t != JVal::Obj || !jnum(op, u"type", type)) return;                                  // default: ignored
+    if (type == MT_OP_INSERT) {                                                                   // applyInsertOp :412-462
+        int pos1;
+        const JVal* seg = jget(op, u"seg");
+        if (!jnum(op, u"pos1", pos1)) { if (jget(op, u"relativePos1")) t.status |= MT_DS_UNSUPPORTED; return; }
+        if (!seg || !truthy(seg)) { if (jget(op, u"register")) t.status |= MT_DS_UNSUPPORTED; return; }
+        Seg* s = segFromSpec(d, *seg);
+        if (!s) { t.status |= MT_DS_UNSUPPORTED; return; }
+        t.insertSegment(pos1, s, ref, cl, seq);
+        complete_op(t, seq, msn);
+    } else if (type == MT_OP_REMOVE || type == MT_OP_ANNOTATE) {                                   // :339-405
+        int p1, p2;
+        if (!jnum(op, u"pos1", p1) || !jnum(op, u"pos2", p2)) { t.status |= MT_DS_UNSUPPORTED; return; }
+        if (type == MT_OP_REMOVE) {
+            if (jget(op, u"register")) { t.status |= MT_DS_UNSUPPORTED; return; }                 // cut -> copy (:347-350)
+            t.markRangeRemoved(p1, p2, ref, cl, seq);
+        } else {
+            const JVal* props = jget(op, u"props");
+            const JVal* cop = jget(op, u"combiningOp");
+            bool rewrite = false;
+            if (cop && cop->t == JVal::Obj) {
+                const JVal* nm = jget(*cop, u"name");
+                if (nm && nm->t == JVal::Str && nm->s == u"rewrite") rewrite = true;
+                else { t.status |= MT_DS_UNSUPPORTED; return; }
+            }
+            if (!props || props->t != JVal::Obj) { t.status |= MT_DS_UNSUPPORTED; return; }
+            t.annotateRange(p1, p2, d.props, intern_props_json(d, *props), rewrite, ref, cl, seq);
+        }
+        complete_op(t, seq, msn);
+    } else if (type == 3) {                                                                       // GROUP :804-812
+        const JVal* ops = jget(op, u"ops");
+        if (ops && ops->t == JVal::Arr)
+            for (const JVal& m : ops->arr) { apply_remote_json(d, m, cl, ref, seq, msn); if (t.status & MT_DS_INSERT_FAILED) return; }
+    }
+}
+uint32_t ora_apply_msg_json(ora_doc* o, const char* json) {
+    Doc& d = o->d; Tree& t = d.t;
+    JVal m = json_parse(json);
+    const JVal* cid = jget(m, u"clientId");
+    int seq, ref, msn;
+    if (!cid || cid->t != JVal::Str || !jnum(m, u"sequenceNumber", seq) || !jnum(m, u"referenceSequenceNumber", ref) ||
+        !jnum(m, u"minimumSequenceNumber", msn)) { t.status |= MT_DS_UNSUPPORTED; return t.status; }
+    const int cl = load_short_id(d, cid->s);                                                     // getOrAddShortClientId :825
+    const JVal* ty = jget(m, u"type");
+    if (ty && ty->t == JVal::Str && ty->s == u"op") {
+        const JVal* c = jget(m, u"contents");
+        if (c) apply_remote_json(d, *c, cl, ref, seq, msn);
+    }
+    if (t.currentSeq > seq) t.status |= MT_DS_ASSERT_SEQ;                                        // updateSeqNumbers :843-850
+    t.currentSeq = seq;
+    if (msn > seq) t.status |= MT_DS_ASSERT_MSN;
+    t.setMinSeq(msn);
+    return t.status;
+}
+// getLength(refSeq, clientId) of the client with this long id (a JSON string literal);
+// an id not registered yet owns no segment, so any unused short id gives its view.
+int32_t ora_get_length_json(ora_doc* o, int32_t ref, const char* client_literal) {
+    auto it = o->d.nameToShort.find(jquote(parse_key(client_literal)));
+    return o->d.t.getLength(ref, it != o->d.nameToShort.end() ? it->second : -999999);
+}
+
 int ora_local_insert(ora_doc* o, int32_t pos, const uint16_t* text, uint32_t n, int32_t refType, int32_t ps) {
     Tree& t = o->d.t;
     Seg* s = specToSegment(o->d, text, n, refType, refType >= 0, ps);

@@ -25,6 +25,13 @@ int      ora_set_client_names(ora_doc* d, uint32_t n, const char* const* client_
 /* Apply run `run` of the batch (Client.applyMsg per message). Returns 0 or an
  * MT_DS_* status bitmask (the reference would have thrown). */
 uint32_t ora_apply_run(ora_doc* d, const mt_op_batch* b, uint32_t run);
+/* Client.applyMsg (MT/client.ts:790-850) on one ISequencedDocumentMessage given as
+ * JSON text: parsed and dispatched here (GROUP, non-"op" types, markers, props),
+ * independent of the hosts' batch packers.  Returns the MT_DS_* status. */
+uint32_t ora_apply_msg_json(ora_doc* d, const char* json);
+/* getLength(refSeq, client) for the client with long id `client_literal` (a JSON
+ * string literal, e.g. "\"alice\""). */
+int32_t  ora_get_length_json(ora_doc* d, int32_t ref_seq, const char* client_literal);
 /* Local (non-collaborating) ops, as SharedString.insertText/insertMarker/
  * annotateRange/removeText on a detached string (seq = UniversalSequenceNumber). */
 int      ora_local_insert(ora_doc* d, int32_t pos, const uint16_t* text, uint32_t n,

@@ -1,0 +1,176 @@
+"""TEST-ONLY: sequenced ISequencedDocumentMessage streams over the real message surface.
+
+The oracle acts as the sequencer's observer: for every message it gives the author's
+perspective length getLength(refSeq, author) (MT/mergeTree.ts:1569), so positions are
+valid, and it applies the message through its own JSON path (ora_apply_msg_json,
+restating Client.applyMsg, MT/client.ts:790-850).  The streams exercise what the
+synthetic device generator does not:
+
+* GROUP messages (MT/client.ts:804-812): 2-4 members, one seq, each member's positions
+  valid after the earlier members (the author sees its own inserts and removes);
+* non-"op" messages (noop/summarize/propose) that only move seq and MSN (:840);
+* remote marker inserts ({"marker":{"refType":n},"props":{...}}, MT/mergeTree.ts:640-662);
+* text segments with props, "props":{} (an empty but defined map), plain strings;
+* text with quotes, backslashes, control characters, non-ASCII, surrogate pairs and lone
+  surrogates (splits inside a pair make more of them), long inserts past the 256-unit
+  append granularity, and "\\n" (canAppend, MT/textSegment.ts:63-68);
+* property keys that are array indices ("0", "2", "10": enumerated first, ascending),
+  falsy values (0, "", false: the rewrite rule deletes them), null (delete), nested
+  objects and arrays (matchProperties recursion, MT/properties.ts:64-95), and
+  rewrite-to-empty annotates ({"name":"rewrite"} with {} or all-null props);
+* client churn: authors leave and new long ids join (non-ASCII ones included), so a
+  document sees many more distinct clients than are active at once.
+
+MSN follows deli (deli/lambda.ts:348-371): the minimum over connected clients' latest
+refSeq; refSeq >= MSN at send time.
+"""
+from __future__ import annotations
+
+import random
+
+from oracle_lib import OracleDoc
+
+SPECIAL = ['"', "\\", "\n", "\t", "\r", "\x01", "\x1f", "\x7f", "/", "é", "中", " ", "😀", "𝄞",
+           "\ud800", "\udfff", "\udc00", " ", "<", "&"]
+KEYS = ["0", "1", "2", "10", "k", "bold", "a b", "ключ", "x\"y", "4294967295", "01"]
+VALUES = ["s", "ü", "", 0, 1, -3, 1.5, 1e21, 0.25, True, False, {"a": 1}, [1, 2], {"0": "x", "b": [True]},
+          {"n": None}, "😀"]
+
+
+class StreamGen:
+    def __init__(self, seed: int, clients: int = 4, lag: int = 12, churn: float = 0.0, p_nonop: float = 0.06,
+                 p_group: float = 0.15, p_marker: float = 0.08, p_annotate: float = 0.2, p_remove: float = 0.3,
+                 p_special: float = 0.25, long_every: int = 40, max_ins: int = 9, id_prefix: str = "cli",
+                 max_total_clients: int | None = None):
+        self.rng = random.Random(seed)
+        self.lag, self.churn, self.p_nonop, self.p_group = lag, churn, p_nonop, p_group
+        self.p_marker, self.p_annotate, self.p_remove, self.p_special = p_marker, p_annotate, p_remove, p_special
+        self.long_every, self.max_ins = long_every, max_ins
+        self.id_prefix = id_prefix
+        self.max_total = max_total_clients
+        self.total = 0
+        self.active: dict[str, int] = {}          # long id -> latest refSeq
+        for _ in range(clients):
+            self._join(0)
+        self.cur = 0
+        self.msn = 0
+        self.obs = OracleDoc(True)
+        self.msgs: list[dict] = []
+
+    # -- clients ----------------------------------------------------------------
+    def _join(self, ref: int):
+        k = self.total
+        self.total += 1
+        nm = f"{self.id_prefix}-{k}" if k % 5 else f"ü{self.id_prefix}-{k}-😀"
+        self.active[nm] = ref
+        return nm
+
+    # -- content ----------------------------------------------------------------
+    def _text(self, n: int) -> str:
+        r = self.rng
+        out = []
+        for _ in range(n):
+            out.append(r.choice(SPECIAL) if r.random() < self.p_special else chr(97 + r.randrange(26)))
+        return "".join(out)
+
+    def _props(self, allow_null=True) -> dict:
+        r = self.rng
+        d = {}
+        for _ in range(r.randint(1, 3)):
+            k = r.choice(KEYS)
+            d[k] = None if (allow_null and r.random() < 0.2) else r.choice(VALUES)
+        return d
+
+    def _insert(self, L: int, k: int) -> tuple[dict, int]:
+        r = self.rng
+        pos = r.randint(0, L)
+        if r.random() < self.p_marker:
+            seg = {"marker": {"refType": r.choice([0, 1, 2, 4, 0x40])}}
+            if r.random() < 0.7:
+                seg["props"] = self._props(allow_null=False)
+            return {"type": 0, "pos1": pos, "seg": seg}, 1
+        n = r.randint(257, 300) if (self.long_every and k % self.long_every == self.long_every - 1) else \
+            r.randint(1, self.max_ins)
+        text = self._text(n)
+        if text and text[-1] == "\ud800" and r.random() < 0.5:
+            text = text[:-1] + "\n"
+        units = len(text.encode("utf-16-le", "surrogatepass")) // 2
+        x = r.random()
+        if x < 0.6:
+            seg = text
+        elif x < 0.7:
+            seg = {"text": text, "props": {}}
+        else:
+            seg = {"text": text, "props": self._props()}
+        return {"type": 0, "pos1": pos, "seg": seg}, units
+
+    def _range(self, L: int, ty: int) -> tuple[dict, int]:
+        r = self.rng
+        s = r.randrange(L)
+        e = min(L, s + 1 + r.randrange(12))
+        if ty == 1:
+            return {"type": 1, "pos1": s, "pos2": e}, -(e - s)
+        op = {"type": 2, "pos1": s, "pos2": e}
+        x = r.random()
+        if x < 0.1:
+            op["props"] = {}
+            op["combiningOp"] = {"name": "rewrite"}
+        elif x < 0.2:
+            op["props"] = {k: None for k in r.sample(KEYS, 2)}
+            op["combiningOp"] = {"name": "rewrite"}
+        else:
+            op["props"] = self._props()
+            if r.random() < 0.15:
+                op["combiningOp"] = {"name": "rewrite"}
+        return op, 0
+
+    def _member(self, L: int, k: int) -> tuple[dict, int]:
+        x = self.rng.random()
+        if L == 0 or x >= self.p_remove + self.p_annotate:
+            return self._insert(L, k)
+        return self._range(L, 1 if x < self.p_remove else 2)
+
+    # -- one sequenced message ----------------------------------------------------
+    def step(self) -> dict:
+        r = self.rng
+        k = len(self.msgs)
+        if self.churn and r.random() < self.churn and len(self.active) > 1 and \
+                (self.max_total is None or self.total < self.max_total):
+            del self.active[r.choice(sorted(self.active))]                # leave
+            self._join(self.cur)                                          # a new long id joins
+        a = r.choice(sorted(self.active))
+        ref = max(self.cur - r.randint(0, self.lag), self.active[a], self.msn)
+        self.active[a] = ref
+        msn = min(self.active.values())
+        seq = self.cur + 1
+        msg = dict(clientId=a, sequenceNumber=seq, referenceSequenceNumber=ref, minimumSequenceNumber=msn)
+        if r.random() < self.p_nonop:
+            msg["type"] = r.choice(["noop", "summarize", "propose"])
+            msg["contents"] = None
+        else:
+            L = self.obs.get_length_of(ref, a)
+            members = []
+            for _ in range(r.randint(2, 4) if r.random() < self.p_group else 1):
+                op, dl = self._member(L, k)
+                members.append(op)
+                L += dl
+            msg["type"] = "op"
+            msg["contents"] = members[0] if len(members) == 1 else {"type": 3, "ops": members}
+        st = self.obs.apply_msg(msg)
+        if st:
+            raise RuntimeError(f"oracle status {st:#x} at message {k}: {msg}")
+        self.cur, self.msn = seq, msn
+        self.msgs.append(msg)
+        return msg
+
+    def run(self, n: int) -> list[dict]:
+        for _ in range(n):
+            self.step()
+        return self.msgs
+
+
+def stream(seed: int, n: int, **kw):
+    """(messages, oracle observer after all of them)."""
+    g = StreamGen(seed, **kw)
+    g.run(n)
+    return g.msgs, g.obs

@@ -46,6 +46,10 @@ def lib():
         L.ora_local_annotate.argtypes = [P, I32, I32, I32, I32]
         L.ora_load_snapshot.restype = ctypes.c_int
         L.ora_load_snapshot.argtypes = [P, U32, P]
+        L.ora_apply_msg_json.restype = U32
+        L.ora_apply_msg_json.argtypes = [P, ctypes.c_char_p]
+        L.ora_get_length_json.restype = I32
+        L.ora_get_length_json.argtypes = [P, I32, ctypes.c_char_p]
         L.ora_get_length.restype = I32
         L.ora_get_length.argtypes = [P, I32, I32]
         L.ora_snapshot_v1.restype = P
@@ -107,6 +111,16 @@ class OracleDoc:
         arr = (ctypes.c_char_p * max(1, len(json_literals)))(*[s.encode() for s in json_literals])
         self._names = arr
         self.L.ora_set_client_names(self.h, len(json_literals), ctypes.cast(arr, ctypes.c_void_p))
+
+    def apply_msg(self, msg: dict) -> int:
+        """Client.applyMsg on the message itself (JSON; the oracle parses and dispatches it)."""
+        import json
+        return int(self.L.ora_apply_msg_json(self.h, json.dumps(msg, ensure_ascii=True).encode()))
+
+    def get_length_of(self, ref_seq: int, client_id: str) -> int:
+        """getLength(refSeq, shortId(client_id)) under the oracle's own registration."""
+        from fluidframework_amd.jsjson import quote
+        return int(self.L.ora_get_length_json(self.h, ref_seq, quote(client_id).encode("utf-8", "surrogatepass")))
 
     def apply_run(self, batch: OpBatch, run: int) -> int:
         return int(self.L.ora_apply_run(self.h, ctypes.byref(batch.to_c()), run))

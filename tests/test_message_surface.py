@@ -1,0 +1,118 @@
+"""The real message surface, end to end: ISequencedDocumentMessage streams (tests/msg_gen.py)
+with GROUP messages, non-"op" messages, remote marker inserts, text and props JSON edge
+cases and client churn go through the Python `Client` drop-in (ClientGroup, packing with
+batch.BatchBuilder) into the engine, and must match the oracle, which parses and applies
+the same messages itself (ora_apply_msg_json, MT/client.ts:790-850): observer text,
+segment structure, SnapshotV1 and SnapshotLegacy bytes and digests, perspective lengths.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from emu_lib import emu_engine
+from fluidframework_amd.engine import ClientGroup, Engine
+from msg_gen import stream
+
+LIMITS = dict(rows_per_doc=30000, window_per_doc=8192, propsets_per_doc=30000, text_per_doc=1 << 19,
+              blocks_per_doc=16384, heap_per_doc=30000)
+# dump columns that do not depend on how each side numbers clients (len, seq,
+# removedSeq, props hash, marker refType, tree depth and path)
+COLS = [0, 1, 3, 7, 8, 9, 10, 11]
+
+SURFACES = {
+    "mixed": dict(clients=4, lag=12),
+    "groups": dict(clients=3, lag=6, p_group=0.6, p_nonop=0.1),
+    "markers_props": dict(clients=5, lag=20, p_marker=0.3, p_annotate=0.35),
+    "unicode": dict(clients=2, lag=4, p_special=0.8, p_remove=0.4),
+    "churn": dict(clients=4, lag=10, churn=0.05, max_total_clients=60),
+}
+
+
+def check(factory, surface, seed=1, n_docs=3, n_msgs=1200):
+    streams = [stream(seed * 101 + d, n_msgs, **SURFACES[surface]) for d in range(n_docs)]
+    g = ClientGroup(factory(n_docs, **LIMITS))
+    clients = [g.new_client({"newMergeTreeSnapshotFormat": True}) for _ in range(n_docs)]
+    for c, (msgs, _) in zip(clients, streams):
+        c.startOrUpdateCollaboration("observer")
+        for m in msgs:
+            c.applyMsg(m)
+    g.flush()
+    eng = g.engine
+    assert (eng.status(range(n_docs)) == 0).all(), eng.status(range(n_docs))
+    texts = eng.get_text(range(n_docs))
+    for d, (msgs, obs) in enumerate(streams):
+        assert texts[d] == obs.get_text(), f"doc {d}: text"
+        ed, od = eng.dump(d), obs.dump()
+        assert ed.shape == od.shape, f"doc {d}: {ed.shape} vs {od.shape} rows"
+        bad = np.nonzero((ed[:, COLS] != od[:, COLS]).any(axis=1))[0]
+        assert len(bad) == 0, f"doc {d}: first differing row {bad[:3]}: {ed[bad[0]]} vs {od[bad[0]]}"
+        msn, seq = msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"]
+        for legacy in (False, True):
+            (eb, edig), = eng.snapshot([d], [msn], [seq], legacy=legacy)
+            ob, odig = obs.snapshot(msn, seq, legacy=legacy)
+            assert eb == ob, f"doc {d}: {'legacy' if legacy else 'v1'} snapshot bytes"
+            assert edig == odig
+    return streams, g
+
+
+@pytest.mark.parametrize("surface", list(SURFACES))
+def test_message_surface_on_emulation(surface):
+    check(emu_engine, surface)
+
+
+def test_stream_generator_covers_the_surface():
+    msgs, _ = stream(7, 1500, **SURFACES["mixed"])
+    kinds = {m["type"] for m in msgs}
+    assert {"op", "noop"} <= kinds or {"op", "summarize"} <= kinds
+    ops = [m["contents"] for m in msgs if m["type"] == "op"]
+    assert any(o["type"] == 3 for o in ops)
+    flat = [x for o in ops for x in (o["ops"] if o["type"] == 3 else [o])]
+    assert any(isinstance(o.get("seg"), dict) and "marker" in o["seg"] for o in flat)
+    assert any(o.get("combiningOp") for o in flat)
+    texts = "".join(o["seg"] if isinstance(o.get("seg"), str) else "" for o in flat)
+    assert "\ud800" in texts or "\udfff" in texts or "\udc00" in texts
+    assert "😀" in texts or "𝄞" in texts
+    msgs, _ = stream(8, 1500, **SURFACES["churn"])
+    assert len({m["clientId"] for m in msgs}) > 30
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("surface", list(SURFACES))
+def test_message_surface_on_gpu(surface):
+    check(lambda n, **kw: Engine(n, device=0, **kw), surface, n_docs=6)
+
+
+def check_node(addon, surface, seed=3, n_docs=3, n_msgs=800):
+    """The same streams through the Node host (js/index.js BatchBuilder + the N-API addon)."""
+    from js_lib import run_node
+    streams = [stream(seed * 101 + d, n_msgs, **SURFACES[surface]) for d in range(n_docs)]
+    got = run_node([m for m, _ in streams], addon=addon, limits=dict(rowsPerDoc=30000, windowPerDoc=8192,
+                                                                   propsetsPerDoc=30000, textPerDoc=1 << 19,
+                                                                   blocksPerDoc=16384, heapPerDoc=30000))
+    for d, (msgs, obs) in enumerate(streams):
+        assert got["texts"][d] == obs.get_text(), f"doc {d}: text"
+        assert got["lengths"][d] == obs.get_length()
+        blobs, dig = obs.snapshot(msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"])
+        want = [("header" if i == 0 else f"body_{i - 1}", b.decode("utf-8", "surrogatepass")) for i, b in
+                enumerate(blobs)]
+        assert [tuple(x) for x in got["blobs"][d]] == want, f"doc {d}: snapshot"
+        assert int(got["digests"][d], 16) == dig
+
+
+@pytest.mark.parametrize("surface", ["groups", "unicode", "churn"])
+def test_message_surface_node_host_on_emulation(surface):
+    from js_lib import NODE
+    from emu_lib import build_emu_napi
+    if NODE is None:
+        pytest.skip("node is not installed")
+    check_node(build_emu_napi(), surface)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("surface", ["groups", "markers_props", "unicode", "churn"])
+def test_message_surface_node_host_on_gpu(surface):
+    from js_lib import NODE, ROOT
+    if NODE is None:
+        pytest.skip("node is not installed")
+    check_node(os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"), surface, n_docs=6)
