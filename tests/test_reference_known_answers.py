@@ -1,0 +1,286 @@
+"""Known answers restated from the reference's own merge-tree specs, for the passive
+observer: each case is a short sequenced message list whose expected outcome (text and
+the exact SnapshotV1 header bytes, or the segment structure) is written out here by
+hand from the spec, and both the oracle (its own JSON path) and the engine (through the
+Python `Client` drop-in) must produce it.
+
+* properties.spec.ts:9-35 (matchProperties) — observed through coalescing: two adjacent
+  segments at or below the MSN serialize as one iff their properties match
+  (snapshotV1.ts:197-216, textSegment.ts:63-68).
+* mergeTree.annotate.spec.ts:15-66, :485-520 — the remote cases ("remote", "remote
+  only", "split remote"); and :644-677 ("sequenced local before remote") seen by an
+  observer: a rewrite annotate from one client, then a plain one from another.
+* snapshot.spec.ts:111-205 — MSN edge cases: segments below/above the MSN, removals above
+  the MSN of segments below/above it, inserts next to removed segments, bodies past
+  chunkSize; each snapshot loads back (Client.load) to the same text and length, and the
+  stream continues on the loaded document.
+* mergeTree.markRangeRemoved.deltaCallback.spec.ts:54-93 ("Event on Unlink") — a remove
+  splits twice; once the MSN passes it zamboni unlinks the removed segment and the
+  survivors on either side are not merged across it (scourNode resets prev,
+  mergeTree.ts:1296-1303).
+"""
+import json
+
+import pytest
+
+from emu_lib import emu_engine
+from fluidframework_amd.engine import ClientGroup, Engine
+from oracle_lib import OracleDoc
+
+LIMITS = dict(rows_per_doc=40000, window_per_doc=16384, propsets_per_doc=4096, text_per_doc=1 << 18,
+              blocks_per_doc=16384, heap_per_doc=40000)
+GPU = lambda n, **kw: Engine(n, device=0, **kw)  # noqa: E731
+
+
+def msg(cid, seq, ref, msn, contents, type="op"):
+    return dict(clientId=cid, sequenceNumber=seq, referenceSequenceNumber=ref, minimumSequenceNumber=msn,
+                type=type, contents=contents)
+
+
+def ins(pos, seg):
+    return {"type": 0, "pos1": pos, "seg": seg}
+
+
+def rem(a, b):
+    return {"type": 1, "pos1": a, "pos2": b}
+
+
+def ann(a, b, props, rewrite=False):
+    o = {"type": 2, "pos1": a, "pos2": b, "props": props}
+    if rewrite:
+        o["combiningOp"] = {"name": "rewrite"}
+    return o
+
+
+def v1_header(segments, min_seq, seq):
+    """SnapshotV1 header chunk bytes (snapshotV1.ts:98-163, snapshotChunks.ts:125-149) for a
+    document that fits one chunk; `segments` are already JSON-ready values."""
+    length = 0
+    for s in segments:
+        j = s["json"] if isinstance(s, dict) and "json" in s else s
+        length += len(j.encode("utf-16-le")) // 2 if isinstance(j, str) else \
+            (len(j["text"].encode("utf-16-le")) // 2 if "text" in j else 1)
+    hdr = {"version": "1", "segmentCount": len(segments), "length": length, "segments": segments, "startIndex": 0,
+           "headerMetadata": {"minSequenceNumber": min_seq, "sequenceNumber": seq,
+                              "orderedChunkMetadata": [{"id": "header"}], "totalLength": length,
+                              "totalSegmentCount": len(segments)}}
+    return json.dumps(hdr, separators=(",", ":"), ensure_ascii=False).encode()
+
+
+def run_both(factory, msgs, load_first=None):
+    """Apply `msgs` on the oracle (JSON path) and the engine; returns (oracle doc, client).
+    load_first: a {path: contents} snapshot loaded into both before the messages."""
+    od = OracleDoc(load_first is None)
+    if load_first is not None:
+        blobs = [load_first["header"]] + [load_first[k] for k in sorted(load_first) if k != "header"]
+        assert od.load_snapshot(blobs) == 0
+    g = ClientGroup(factory(1, **LIMITS))
+    c = g.new_client({"newMergeTreeSnapshotFormat": True})
+    if load_first is not None:
+        c.load(load_first)
+    for m in msgs:
+        assert od.apply_msg(m) == 0, m
+        c.applyMsg(m)
+    assert c.getText() == od.get_text()
+    return od, c
+
+
+def header_now(od, c):
+    """Both sides' SnapshotV1 header at the current window (no updateSeqNumbers)."""
+    (eb, _), = c.engine.snapshot([c.doc_id], [-1], [-1])
+    ob, _ = od.snapshot(c.min_seq, c.current_seq)
+    assert eb == ob
+    return eb[0]
+
+
+# ---- properties.spec.ts:9-35 -------------------------------------------------------
+MATCH = [
+    ({"a": "a"}, {"a": "a"}, True),
+    ({"a": "a"}, {"a": "b"}, False),
+    ({"a": "a", "1": 1}, {"a": "a", "1": 1}, True),
+    ({"a": "a", "1": 1}, {"a": "b", "1": 2}, False),
+    ({"a": "a"}, {"b": "a"}, False),
+    ({"a": "a"}, {"a": "a", "b": "b"}, False),
+    ({"c": {"a": "a"}}, {"c": {"a": "a"}}, True),
+    ({"c": {"a": "a"}}, {"c": {"a": "b"}}, False),
+]
+
+
+def check_match_properties(factory):
+    for pa, pb, same in MATCH:
+        msgs = [msg("x", 1, 0, 0, ins(0, {"text": "ab", "props": pa})),
+                msg("x", 2, 1, 1, ins(2, {"text": "cd", "props": pb})),
+                msg("x", 3, 2, 2, None, type="noop")]
+        od, c = run_both(factory, msgs)
+        js = lambda p: {k: p[k] for k in sorted(p, key=lambda k: (not k.isdigit(), int(k) if k.isdigit() else 0))}  # noqa
+        segs = [{"text": "abcd", "props": js(pa)}] if same else \
+            [{"text": "ab", "props": js(pa)}, {"text": "cd", "props": js(pb)}]
+        assert header_now(od, c) == v1_header(segs, 2, 3), (pa, pb)
+
+
+def test_match_properties_known_answers_on_emulation():
+    check_match_properties(emu_engine)
+
+
+@pytest.mark.gpu
+def test_match_properties_known_answers_on_gpu():
+    check_match_properties(GPU)
+
+
+# ---- mergeTree.annotate.spec.ts ------------------------------------------------------
+HELLO = {"header": v1_header(["hello world!"], 0, 0).decode()}
+
+
+def check_annotate_remote(factory):
+    # beforeEach (:27-45): "hello world!" (universal), a Tile marker inserted at
+    # markerPosition 3 by the remote client at seq 1; annotate [1, 5).
+    base = [msg("remote", 1, 0, 0, ins(3, {"marker": {"refType": 1}}))]
+    # "remote" (:49-66) / "remote only" (:485-510)
+    props = {"propertySource": "remote", "remoteProperty": 1}
+    od, c = run_both(factory, base + [msg("remote", 2, 1, 0, ann(1, 5, props))], load_first=HELLO)
+    marker = {"json": {"marker": {"refType": 1}, "props": props}, "seq": 1, "client": "remote"}
+    assert header_now(od, c) == v1_header(["h", {"text": "el", "props": props}, marker, {"text": "l", "props": props},
+                                           "o world!"], 0, 2)
+    # "split remote" (:512-520): a later insert inside the annotated "el" splits it; both
+    # halves keep the properties
+    od, c = run_both(factory, base + [msg("remote", 2, 1, 0, ann(1, 5, props)),
+                                      msg("other", 3, 2, 0, ins(2, "Z"))], load_first=HELLO)
+    zz = {"json": "Z", "seq": 3, "client": "other"}
+    assert header_now(od, c) == v1_header(["h", {"text": "e", "props": props}, zz, {"text": "l", "props": props}, marker,
+                                           {"text": "l", "props": props}, "o world!"], 0, 3)
+    # "sequenced local before remote" (:644-677) as an observer sees it: a rewrite
+    # annotate {propertySource: "local"} (seq 2) then the remote one (seq 3)
+    od, c = run_both(factory, base + [msg("local", 2, 1, 0, ann(1, 5, {"propertySource": "local"}, rewrite=True)),
+                                      msg("remote", 3, 2, 0, ann(1, 5, props))], load_first=HELLO)
+    marker = {"json": {"marker": {"refType": 1}, "props": props}, "seq": 1, "client": "remote"}
+    assert header_now(od, c) == v1_header(["h", {"text": "el", "props": props}, marker, {"text": "l", "props": props},
+                                           "o world!"], 0, 3)
+    # rewrite after the remote annotate drops every key it does not set (:581-642 rule)
+    od, c = run_both(factory, base + [msg("remote", 2, 1, 0, ann(1, 5, props)),
+                                      msg("local", 3, 2, 0, ann(1, 5, {"propertySource": "local"}, rewrite=True))],
+                     load_first=HELLO)
+    lp = {"propertySource": "local"}
+    marker = {"json": {"marker": {"refType": 1}, "props": lp}, "seq": 1, "client": "remote"}
+    assert header_now(od, c) == v1_header(["h", {"text": "el", "props": lp}, marker, {"text": "l", "props": lp},
+                                           "o world!"], 0, 3)
+
+
+def test_annotate_remote_known_answers_on_emulation():
+    check_annotate_remote(emu_engine)
+
+
+@pytest.mark.gpu
+def test_annotate_remote_known_answers_on_gpu():
+    check_annotate_remote(GPU)
+
+
+# ---- snapshot.spec.ts:111-205 ----------------------------------------------------------
+class Str:
+    """TestString (snapshot.spec.ts:30-109) from the observer's side: every op is a
+    sequenced message of client "fakeId" (refSeq = seq - 1); increaseMsn moves the MSN
+    to the op's own seq.  expect() snapshots both sides, loads each snapshot back
+    (Client.load / SnapshotLoader), checks text and length, and continues on the
+    loaded documents, as the spec does."""
+
+    def __init__(self, factory):
+        self.factory = factory
+        self.seq = self.min_seq = 0
+        self.od = OracleDoc(True)
+        self.g = ClientGroup(factory(8, **LIMITS))
+        self.c = self.g.new_client({"newMergeTreeSnapshotFormat": True})
+        self.len = 0
+
+    def _queue(self, op, inc):
+        ref = self.seq
+        self.seq += 1
+        if inc:
+            self.min_seq = self.seq
+        m = msg("fakeId", self.seq, ref, self.min_seq, op)
+        assert self.od.apply_msg(m) == 0
+        self.c.applyMsg(m)
+
+    def append(self, text, inc):
+        self.insert(self.len, text, inc)
+
+    def insert(self, pos, text, inc):
+        self._queue(ins(pos, text), inc)
+        self.len += len(text)
+
+    def remove(self, a, b, inc):
+        self._queue(rem(a, b), inc)
+        self.len -= b - a
+
+    def expect(self, text=None):
+        if text is not None:
+            assert self.c.getText() == text
+        assert self.od.get_text() == self.c.getText()
+        tree = self.c.snapshot()
+        blobs = {e["path"]: e["value"]["contents"] for e in tree["entries"]}
+        ob, _ = self.od.snapshot(self.c.min_seq, self.c.current_seq)
+        assert [e["value"]["contents"].encode() for e in tree["entries"]] == ob
+        od2 = OracleDoc(False)
+        assert od2.load_snapshot([blobs["header"]] + [blobs[f"body_{i}"] for i in range(len(blobs) - 1)]) == 0
+        c2 = self.g.new_client({"newMergeTreeSnapshotFormat": True})
+        c2.load(blobs)
+        assert c2.getText() == self.c.getText() == od2.get_text()
+        assert c2.getLength() == self.c.getLength() == od2.get_length()
+        self.od, self.c = od2, c2
+        return blobs
+
+
+def check_snapshot_spec(factory):
+    s = Str(factory); s.append("0", True); s.expect("0")                                  # below MSN
+    s = Str(factory); s.append("0", False); s.expect("0")                                 # ACKed above the MSN
+    s = Str(factory); s.append("0x", False); s.remove(1, 2, False); s.expect("0")         # removal above MSN
+    s = Str(factory); s.append("0x", True); s.remove(1, 2, False)                         # ... of a segment below it
+    b = s.expect("0")
+    assert json.loads(b["header"])["segments"] == ["0", {"json": "x", "removedSeq": 2, "removedClient": "fakeId"}]
+    s.append("1", False); s.expect("01")                                                  # insert after the load
+    s = Str(factory)                                                                      # relative to removed segment
+    s.append("0x", False); s.append("2", False); s.remove(1, 2, False); s.insert(1, "1", False); s.append("3", False)
+    s.expect("0123")
+    s = Str(factory)                                                                      # ... loaded from a snapshot
+    s.append("0x", False); s.append("2", False); s.remove(1, 2, False)
+    s.expect("02")
+    s.insert(1, "1", False); s.append("3", False); s.expect("0123")
+    for inc in (True, False):                                                             # bodies past chunkSize
+        s = Str(factory)
+        for i in range(10000 + 10):
+            s.append(str(i % 10), inc)
+        b = s.expect()
+        # below the MSN the appends coalesce into one segment (one chunk); above it every
+        # segment carries merge info and the chunks fill to 10,000 characters
+        assert len(b) == (1 if inc else 2)
+
+
+def test_snapshot_spec_known_answers_on_emulation():
+    check_snapshot_spec(emu_engine)
+
+
+@pytest.mark.gpu
+def test_snapshot_spec_known_answers_on_gpu():
+    check_snapshot_spec(GPU)
+
+
+# ---- mergeTree.markRangeRemoved.deltaCallback.spec.ts:54-93 --------------------------------
+def check_unlink(factory):
+    msgs = [msg("x", 1, 0, 0, rem(4, 6))]
+    od, c = run_both(factory, msgs, load_first=HELLO)
+    rows = c.engine.dump(c.doc_id)
+    assert [int(r[0]) for r in rows] == [4, 2, 6]            # "hell" | "o " (removed) | "world!": two splits
+    assert int(rows[1][3]) == 1
+    od.apply_msg(msg("x", 2, 1, 1, None, type="noop"))       # the MSN passes the removal
+    c.applyMsg(msg("x", 2, 1, 1, None, type="noop"))
+    assert c.getText() == od.get_text() == "hellworld!"
+    rows = c.engine.dump(c.doc_id)
+    assert [int(r[0]) for r in rows] == [4, 6]               # unlinked; no merge across it
+    assert (rows[:, [0, 1, 3, 9, 10, 11]] == od.dump()[:, [0, 1, 3, 9, 10, 11]]).all()
+
+
+def test_unlink_known_answer_on_emulation():
+    check_unlink(emu_engine)
+
+
+@pytest.mark.gpu
+def test_unlink_known_answer_on_gpu():
+    check_unlink(GPU)
