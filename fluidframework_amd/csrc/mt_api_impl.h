@@ -81,7 +81,7 @@ static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bo
     MT_ALLOC(blk, MtBlk, tot.blk) MT_ALLOC(heap, MtHeapE, tot.heap) MT_ALLOC(win, int, tot.win)
     MT_ALLOC(uid, int, tot.win) MT_ALLOC(udelta, int, tot.win) MT_ALLOC(uanc, int, tot.anc)
     MT_ALLOC(text, uint16_t, tot.text) MT_ALLOC(pset, MtPSet, tot.pset) MT_ALLOC(hdr, MtDocHdr, D)
-    MT_ALLOC(hold, int, D * MT_RFL)
+    MT_ALLOC(hold, int, D * MT_RFL) MT_ALLOC(ovx, MtOvx, D * MT_OVX_CAP)
 #undef MT_ALLOC
     if (mtb_malloc(&p, sizeof(MtDocLayout) * D) != 0) { c->err = "pool allocation failed: layout"; return MT_E_OOM; }
     S.layout = (const MtDocLayout*)p;
@@ -89,7 +89,8 @@ static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bo
     mtb_memset(S.hdr, 0, sizeof(MtDocHdr) * D);
     c->tot = tot;
     c->pool_bytes = sizeof(MtRow) * tot.row + sizeof(MtBlk) * tot.blk + sizeof(MtHeapE) * tot.heap + 12ull * tot.win +
-                    4ull * tot.anc + 2ull * tot.text + sizeof(MtPSet) * tot.pset + (sizeof(MtDocHdr) + 4ull * MT_RFL + sizeof(MtDocLayout)) * D;
+                    4ull * tot.anc + 2ull * tot.text + sizeof(MtPSet) * tot.pset +
+                    (sizeof(MtDocHdr) + 4ull * MT_RFL + sizeof(MtDocLayout) + sizeof(MtOvx) * MT_OVX_CAP) * D;
     return MT_OK;
 }
 
@@ -111,7 +112,8 @@ static std::vector<MtCkPart> mt_ck_parts(mt_ctx* c) {
     return {{&c->ck_rows, S.rows, sizeof(MtRow) * t.row}, {&c->ck_blk, S.blk, sizeof(MtBlk) * t.blk},
             {&c->ck_heap, S.heap, sizeof(MtHeapE) * t.heap}, {&c->ck_win, S.win, 4ull * t.win},
             {&c->ck_text, S.text, 2ull * t.text}, {&c->ck_pset, S.pset, sizeof(MtPSet) * t.pset},
-            {&c->ck_hdr, S.hdr, sizeof(MtDocHdr) * D}, {&c->ck_hold, S.hold, 4ull * MT_RFL * D}};
+            {&c->ck_hdr, S.hdr, sizeof(MtDocHdr) * D}, {&c->ck_hold, S.hold, 4ull * MT_RFL * D},
+            {&c->ck_ovx, S.ovx, sizeof(MtOvx) * MT_OVX_CAP * D}};
 }
 int MT_FN(checkpoint)(mt_ctx* c) {
     if (!c) return MT_E_INVALID;
@@ -141,7 +143,7 @@ void MT_FN(destroy)(mt_ctx* c) {
     if (!c) return;
     MtState& S = c->S;
     void* ps[] = {S.rows, S.blk, S.heap, S.win, S.uid, S.udelta, S.uanc, S.text, S.pset, S.hdr, S.hold, (void*)S.layout,
-                  c->ck_rows, c->ck_blk, c->ck_heap, c->ck_win, c->ck_text, c->ck_pset, c->ck_hdr, c->ck_hold};
+                  S.ovx, c->ck_rows, c->ck_blk, c->ck_heap, c->ck_win, c->ck_text, c->ck_pset, c->ck_hdr, c->ck_hold, c->ck_ovx};
     for (void* p : ps) if (p) mtb_free(p);
     mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_pset_off,
                             &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3,
@@ -257,13 +259,13 @@ int MT_FN(apply_batch)(mt_ctx* c, const mt_op_batch* B) {
 // becomes one REFLUSH step (a no-op where the reference's walk falls off the
 // tree, aliasing -> MT_DS_UNSUPPORTED where it would link a segment twice).
 static bool mt_load_seg_ok(const mt_load_seg& g, int ms, int cs) {
-    if ((g.flags & MT_LS_CLIENT) && g.client >= 64) return false;
+    if ((g.flags & MT_LS_CLIENT) && g.client >= MT_NONCOLLAB) return false;
     if (g.flags & MT_LS_SEQ) {
         if (g.seq < 0 || g.seq > cs) return false;
         if (g.seq != 0 && g.seq <= ms) return false;     // neither universal nor in the collab window
     }
     if (g.flags & MT_LS_REMOVED) {
-        if (g.removed_client >= 64 || g.removed_seq <= ms || g.removed_seq > cs) return false;
+        if (g.removed_client >= MT_NONCOLLAB || g.removed_seq <= ms || g.removed_seq > cs) return false;
     }
     return true;
 }

@@ -116,8 +116,7 @@ enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2 };
 #endif
 enum { MT_PH_U = 0, MT_PH_SPLIT, MT_PH_INSERT, MT_PH_RANGE, MT_PH_ZAMBONI, MT_PH_OP, MT_PH_GEN, MT_PH_TEXT };
 
-#define MT_M_CLIENT 0x000000FFu
-#define MT_M_RCLIENT 0x0000FF00u
+#define MT_M_CLIENT 0x0000FFFFu        // short client id (16 bits; MT/client.ts:658-682)
 #define MT_M_REMOVED 0x00010000u
 #define MT_M_MARKER 0x00020000u
 #define MT_M_INWIN 0x00040000u
@@ -133,8 +132,9 @@ struct __attribute__((aligned(16))) MtRow {   // one 48-byte record per segment 
     int props;       // property-set id, -1 = properties undefined
     int parent;      // leaf block, -1 = unlinked
     int tcap;        // owned text capacity at toff
-    unsigned long long ovl;  // removedClientOverlap bitmask
-    int pad[2];
+    unsigned long long ovl;  // removedClientOverlap: bit c for clients c < 63; bit 63 = more in the side list
+    uint32_t rcl;            // removedClientId (16 bits)
+    int pad1;
 };
 struct __attribute__((aligned(16))) MtBlk {   // one 64-byte record per B-tree block
     int c[8];        // children: segment rows (height 0) or blocks
@@ -152,6 +152,11 @@ struct __attribute__((aligned(16))) MtPSet {  // immutable property map (inserti
     int32_t pad[3];
 };
 struct MtHeapE { int seg; int maxSeq; };     // LRUSegment, MT/mergeTree.ts:915-923
+// removedClientOverlap entries of clients >= 63 (MT/mergeTree.ts:2563-2571), per document:
+// the overlap bitmask covers clients 0..62 and its bit 63 says "look here".  An entry is
+// live while its row still has the removedSeq it was written under.
+struct MtOvx { int row; int rseq; int client; int pad; };
+#define MT_OVX_CAP 512                         // side-list entries per document
 struct __attribute__((aligned(16))) MtDocHdr {
     int root, height, minSeq, curSeq, rowTop, blkTop, blkFree, heapN, winN, textTop, psetTop;
     uint32_t status;
@@ -160,7 +165,8 @@ struct __attribute__((aligned(16))) MtDocHdr {
     int rfN;                                 // recycled rows on the document's stack (hold pool)
     int blkFreeN;                            // blocks on the free list
     int heapHW, winHW;                       // high-water marks (pool sizing, mt_doc_pools)
-    int pad[3];
+    int ovxN;                                // overlap side-list entries
+    int pad[2];
     unsigned long long prof[8];              // MT_PROFILE builds: s_memtime cycles per phase
 };
 
@@ -177,6 +183,7 @@ struct MtState {                              // device pools, doc-major
     MtRow* rows;
     MtBlk* blk; MtHeapE* heap; int* win; int* uid; int* udelta; int* uanc;
     uint16_t* text; MtPSet* pset; MtDocHdr* hdr; int* hold;   // text: 2 halves of textCap per doc; hold: recycled-row stacks
+    MtOvx* ovx;                               // overlap side lists, MT_OVX_CAP per doc
     uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap, holdCap, maxDocs;   // largest per-doc caps
     const MtDocLayout* layout;                // [maxDocs]
     // interned op property sets (mt_prop_table)
@@ -221,7 +228,8 @@ struct MtLoad {
     const MtLoadSeg* segs; const uint16_t* payload;
     const uint32_t* plan_off; const MtLoadStep* plan;
 };
-#define MT_NONCOLLAB 254              // NonCollabClient (MT/constants.ts) in the 8-bit client field
+#define MT_NONCOLLAB 0xFFFE           // NonCollabClient (MT/constants.ts) in the 16-bit client field
+#define MT_NOBODY 0xFFFF              // a client id no row carries (getLength's "any other client")
 
 struct MtGen {                                // device stream generator parameters
     unsigned long long seed;
@@ -271,12 +279,24 @@ MT_INLINE int pick8(const int* c, int j) {
     for (int i = 1; i < 8; i++) v = (j == i) ? c[i] : v;
     return v;
 }
-MT_INLINE bool vis_rc(int seq, uint32_t meta, int rseq, unsigned long long ovl, int r, int c) {
+// Is client c in row s's removedClientOverlap?  Clients < 63 are bits of the mask; the
+// rest live in the document's side list (bit 63 set), scanned only in that rare case.
+MT_INLINE bool ovl_has(const MtOvx* ox, int n, unsigned long long ovl, int s, int rseq, int c) {
+    if (c < 63) return ((ovl >> c) & 1ull) != 0;
+    if (!(ovl >> 63)) return false;
+    for (int i = 0; i < n; i++) {
+        const MtOvx e = ox[i];
+        if (e.row == s && e.client == c && e.rseq == rseq) return true;
+    }
+    return false;
+}
+// nodeLength's visibility of segment row s under perspective (r, c), MT/mergeTree.ts:1652-1692.
+MT_INLINE bool vis_rc(int seq, uint32_t meta, int rseq, uint32_t rcl, unsigned long long ovl, int r, int c,
+                      const MtOvx* ox, int nox, int s) {
     const int cl = (int)(meta & MT_M_CLIENT);
     if (!(cl == c || seq <= r)) return false;
     if (meta & MT_M_REMOVED) {
-        const int rc = (int)((meta & MT_M_RCLIENT) >> 8);
-        if (rc == c || (c < 64 && ((ovl >> c) & 1ull)) || rseq <= r) return false;
+        if ((int)rcl == c || rseq <= r || ovl_has(ox, nox, ovl, s, rseq, c)) return false;
     }
     return true;
 }
@@ -324,6 +344,7 @@ template <int RES> struct MtEngT {
     MtRow* R;
     int *win, *uid, *udelta, *uanc;
     MtBlk* blk; MtHeapE* heap; uint16_t* text; MtPSet* pset;
+    MtOvx* ovx; int ovxN;
     MtScratch* sc;
     // pool accessors: LDS (MT_RES_LDS, MT_RES_BLK for blocks + heap) or HBM homes
     MT_HD MtRow& row(int s) const { if constexpr (LDS) return mt_lds().rows[s]; else return R[s]; }
@@ -392,6 +413,7 @@ template <int RES> struct MtEngT {
         const size_t wo = off(&Ly->win);
         win = st.win + wo; uid = st.uid + wo; udelta = st.udelta + wo; uanc = st.uanc + off(&Ly->anc);
         pset = st.pset + off(&Ly->pset);
+        ovx = st.ovx + (size_t)d * MT_OVX_CAP;
         sc = scratch;
         const MtDocHdr& h = *hdrp;
         root = uni(h.root); height = uni(h.height); minSeq = uni(h.minSeq); curSeq = uni(h.curSeq); rowTop = uni(h.rowTop);
@@ -406,7 +428,8 @@ template <int RES> struct MtEngT {
         heapTop = heapN > 0 ? uni(heap[1].maxSeq) : 0x7FFFFFFF;     // HBM home: bind precedes toLds
         lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0;
         rfHbm = st.hold + (size_t)d * MT_RFL; rfN = uni(h.rfN); blkFreeN = uni(h.blkFreeN);
-        heapHW = uni(h.heapHW); winHW = uni(h.winHW);
+        heapHW = uni(h.heapHW); winHW = uni(h.winHW); ovxN = uni(h.ovxN);
+        if (ovxN < 0 || ovxN > MT_OVX_CAP) ovxN = 0;
         lRows = lBlks = lHeap = 0; gRowCap = gBlkCap = gHeapCap = gWinCap = 0;
         if (rfN < 0 || rfN > MT_RFL) rfN = 0;
         { const int n = rfN; const int* src = rfHbm;
@@ -421,7 +444,7 @@ template <int RES> struct MtEngT {
         h.root = root; h.height = height; h.minSeq = minSeq; h.curSeq = curSeq; h.rowTop = rowTop;
         h.blkTop = blkTop; h.blkFree = blkFree; h.heapN = heapN; h.winN = winN; h.textTop = textTop;
         h.psetTop = psetTop; h.status = status; h.textHalf = textHalf; h.rfN = rfN; h.blkFreeN = blkFreeN;
-        h.heapHW = heapHW; h.winHW = winHW;
+        h.heapHW = heapHW; h.winHW = winHW; h.ovxN = ovxN;
         { const int n = rfN; int* dst = rfHbm;
           for (int base = 0; base < n; base += MT_WAVE) {
               const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
@@ -438,7 +461,7 @@ template <int RES> struct MtEngT {
     MT_HD void open() {
         root = 0; height = 0; minSeq = 0; curSeq = 0; rowTop = 0; blkTop = 1; blkFree = -1;
         heapN = 0; winN = 0; textTop = 0; psetTop = 0; status = 0; textHalf = 0; heapTop = 0x7FFFFFFF; rfN = 0;
-        blkFreeN = 0; heapHW = 0; winHW = 0;
+        blkFreeN = 0; heapHW = 0; winHW = 0; ovxN = 0;
         text = S.textBase;
         c_ops = c_msgs = c_ins = c_rows = c_depth = c_scour = 0;
         for (int i = 0; i < 6; i++) hdrp->cnt[i] = 0;               // store() adds this bind's counts
@@ -613,7 +636,7 @@ template <int RES> struct MtEngT {
                 const bool linked = row(s).parent >= 0;
                 w.live = linked && (sq > minSeq || (removed && rs > minSeq));
                 w.recycle = !linked && !(mt & MT_M_HREF);
-                const bool vr = vis_rc(sq, mt, rs, row(s).ovl, r, c);
+                const bool vr = vis_rc(sq, mt, rs, row(s).rcl, row(s).ovl, r, c, ovx, ovxN, s);
                 const bool vo = !removed;
                 w.delta = w.live ? ((vr ? row(s).len : 0) - (vo ? row(s).len : 0)) : 0;
                 return w;
@@ -686,7 +709,7 @@ template <int RES> struct MtEngT {
                 const uint32_t mt = row(s).meta;
                 const int rs = row(s).rseq;
                 ChildL o;
-                o.len = vis_rc(row(s).seq, mt, rs, row(s).ovl, r, c) ? row(s).len : 0;
+                o.len = vis_rc(row(s).seq, mt, rs, row(s).rcl, row(s).ovl, r, c, ovx, ovxN, s) ? row(s).len : 0;
                 // breakTie for a leaf at pos 0 (MT/mergeTree.ts:2270-2292): false if a
                 // removal the author has seen (removedSeq <= refSeq); true otherwise
                 // (every row has an assigned seq on the replay path).
@@ -718,6 +741,50 @@ template <int RES> struct MtEngT {
         });
     }
 
+    /* ---------------------------------- overlap side list (clients >= 63) -- */
+    // Drop entries whose row was unlinked, recycled or settled below the MSN (its
+    // overlap can no longer change any perspective's view); lane-parallel compaction.
+    MT_HD void ovxCompact() {
+        int w = 0;
+        for (int base = 0; base < ovxN; base += MT_WAVE) {
+            const int m = (ovxN - base) < MT_WAVE ? (ovxN - base) : MT_WAVE;
+            auto keep = wave_map(m, [&](int k) MT_LAM {
+                const MtOvx e = ovx[base + k];
+                return row(e.row).parent >= 0 && row(e.row).rseq == e.rseq && e.rseq > minSeq;
+            });
+            auto ent = wave_map(m, [&](int k) MT_LAM { return ovx[base + k]; });
+            auto rk = wave_rank(keep);
+            const int cnt = wave_count(keep);
+            wave_sync();
+            const int w0 = w;
+            wave_for(m, [&](int k) MT_LAM { if (own(keep, k)) ovx[w0 + own(rk, k)] = own(ent, k); });
+            wave_sync();
+            w += cnt;
+        }
+        ovxN = w;
+    }
+    MT_HD void ovxAdd(int s, int rseq, int c) {
+        if (ovxN >= MT_OVX_CAP) ovxCompact();
+        if (ovxN >= MT_OVX_CAP) { status |= MT_DS_OOM_OVERLAP; return; }
+        MtOvx e; e.row = s; e.rseq = rseq; e.client = c; e.pad = 0;
+        wave_for(1, [&](int) MT_LAM { ovx[ovxN] = e; });
+        ovxN++;
+    }
+    // A split's right half n inherits row s's side-list entries.
+    MT_HD void ovxCopy(int s, int n) {
+        const int rs = uni(row(s).rseq), n0 = ovxN;
+        for (int base = 0; base < n0; base += MT_WAVE) {
+            const int m = (n0 - base) < MT_WAVE ? (n0 - base) : MT_WAVE;
+            auto hit = wave_map(m, [&](int k) MT_LAM { const MtOvx e = ovx[base + k]; return e.row == s && e.rseq == rs; });
+            auto cl = wave_map(m, [&](int k) MT_LAM { return ovx[base + k].client; });
+            uint64_t b = wave_ballot(hit);
+            while (b) {
+                const int k = __builtin_ctzll(b); b &= b - 1;
+                ovxAdd(n, rs, wave_at(cl, k));
+            }
+        }
+    }
+
     /* ----------------------------------------------- structure edits -- */
     // Row split (BaseSegment.splitAt MT/mergeTree.ts:538-582; TextSegment
     // createSplitSegmentAt textSegment.ts:103-111): the right half copies every
@@ -729,7 +796,10 @@ template <int RES> struct MtEngT {
         const int ls = uni(row(s).len);
         const uint32_t mt = uni(row(s).meta);
         row(n).len = ls - pos; row(s).len = pos;
-        row(n).seq = row(s).seq; row(n).rseq = row(s).rseq; row(n).meta = mt & ~(MT_M_INWIN | MT_M_HREF); row(n).ovl = row(s).ovl;
+        const unsigned long long ov = uni64(row(s).ovl);
+        row(n).seq = row(s).seq; row(n).rseq = row(s).rseq; row(n).meta = mt & ~(MT_M_INWIN | MT_M_HREF); row(n).ovl = ov;
+        row(n).rcl = row(s).rcl;
+        if (ov >> 63) ovxCopy(s, n);
         row(n).toff = row(s).toff + pos; row(n).props = row(s).props; row(n).parent = row(s).parent;
         row(n).tcap = row(s).tcap - pos; row(s).tcap = pos;   // each row owns [toff, toff+tcap) of the arena
         if (mt & MT_M_INWIN) winAdd(n);
@@ -1301,15 +1371,25 @@ template <int RES> struct MtEngT {
                             const int s = own(ch, j);
                             const uint32_t mt = row(s).meta;
                             if (mt & MT_M_REMOVED) {                   // overlapping remove: keep first remover
-                                row(s).ovl = row(s).ovl | (1ull << c);
+                                row(s).ovl = row(s).ovl | (1ull << (c < 63 ? c : 63));
                                 return 0;
                             }
-                            row(s).meta = (mt & ~MT_M_RCLIENT) | MT_M_REMOVED | ((uint32_t)c << 8);
+                            row(s).meta = mt | MT_M_REMOVED;
+                            row(s).rcl = (uint32_t)c;
                             row(s).rseq = sq;
                             return row(s).len;
                         });
                         obsDelta = -wave_sum8(nd);
                         wave_sync();
+                        if (c >= 63) {                                 // removedClientOverlap beyond the mask
+                            const uint64_t ob = wave_ballot(wave_map(h.n, [&](int j) MT_LAM {
+                                return own(cond, j) && (row(own(ch, j)).rseq != sq);
+                            }));
+                            for (uint64_t b = ob; b; b &= b - 1) {
+                                const int j = __builtin_ctzll(b), s = wave_at(ch, j);
+                                ovxAdd(s, uni(row(s).rseq), c);
+                            }
+                        }
                         for (int j = 0; j < h.n; j++) if (wave_at(cond, j)) winAdd(wave_at(ch, j));
                     } else {
                         for (int j = 0; j < h.n; j++) {
@@ -1388,7 +1468,8 @@ template <int RES> struct MtEngT {
                 w.len = mk ? 1 : (int)g.plen;
                 w.seq = (g.flags & MT_LS_SEQ) ? g.seq : 0;
                 w.rseq = rm ? g.rseq : MT_NOREM;
-                w.meta = (uint32_t)cl | (rm ? (((uint32_t)g.rclient << 8) | MT_M_REMOVED) : 0u) | (mk ? MT_M_MARKER : 0u);
+                w.meta = (uint32_t)cl | (rm ? MT_M_REMOVED : 0u) | (mk ? MT_M_MARKER : 0u);
+                w.rcl = rm ? (uint32_t)g.rclient : 0u;
                 w.ovl = 0ull; w.props = -1; w.parent = -1;
                 w.toff = mk ? (int)g.plen : t0 + (int)(g.poff - pbase);
                 w.tcap = mk ? 0 : (int)g.plen;
@@ -1466,7 +1547,8 @@ template <int RES> struct MtEngT {
         const int n = allocRow();
         if (n < 0) return 0;
         row(n).len = L; row(n).seq = sq; row(n).rseq = rm ? uni(g->rseq) : MT_NOREM;
-        row(n).meta = (uint32_t)cli | (rm ? (((uint32_t)uni((int)g->rclient) << 8) | MT_M_REMOVED) : 0u) | (mk ? MT_M_MARKER : 0u);
+        row(n).meta = (uint32_t)cli | (rm ? MT_M_REMOVED : 0u) | (mk ? MT_M_MARKER : 0u);
+        row(n).rcl = rm ? (uint32_t)uni((int)g->rclient) : 0u;
         row(n).ovl = 0ull; row(n).parent = -1; row(n).props = -1;
         row(n).tcap = plen;
         if (mk) row(n).toff = uni((int)g->plen);
@@ -1505,7 +1587,7 @@ template <int RES> struct MtEngT {
             if (n < 0) return;
             row(n).len = L; row(n).seq = sq; row(n).rseq = MT_NOREM;
             row(n).meta = (uint32_t)c | (marker ? MT_M_MARKER : 0u);
-            row(n).ovl = 0ull; row(n).parent = -1;
+            row(n).ovl = 0ull; row(n).parent = -1; row(n).rcl = 0u;
             row(n).props = segProps >= 0 ? applyPropSet(-1, segProps, false) : -1;
             row(n).tcap = marker ? 0 : plen;
             if (marker) row(n).toff = refType;

@@ -101,7 +101,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
         const uint32_t w7 = (uint32_t)wave_at(w, 7);
         const int plen = (int)(w7 & 0xFFFF), pid = (int)(int16_t)(w7 >> 16);
         if (ty != MT_OP_NOOP) {
-            if (c >= 64) e.status |= MT_DS_UNSUPPORTED;
+            if (c >= MT_NONCOLLAB) e.status |= MT_DS_UNSUPPORTED;  // 0xFFFE/0xFFFF are reserved ids
             if (e.curSeq >= sq) e.status |= MT_DS_ASSERT_SEQ;       // completeAndLogOp, MT/client.ts:482
             if (e.minSeq > ms) e.status |= MT_DS_ASSERT_MSN;        // MT/client.ts:484
             if (r < e.minSeq) e.status |= MT_DS_REFSEQ_BELOW_MSN;   // nacked by deli (deli/lambda.ts:302-318)

@@ -158,7 +158,7 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
         const bool marker = (v.R[s].meta & MT_M_MARKER) != 0;
         seg_json(o, v, nm, s, marker ? nullptr : v.text + v.R[s].toff, marker ? 0 : (size_t)v.R[s].len);
         if (v.R[s].seq > minSeq) { o += ",\"seq\":"; put_int(o, v.R[s].seq); o += ",\"client\":"; o += client((int)(v.R[s].meta & MT_M_CLIENT)); }
-        if (removed) { o += ",\"removedSeq\":"; put_int(o, v.R[s].rseq); o += ",\"removedClient\":"; o += client((int)((v.R[s].meta & MT_M_RCLIENT) >> 8)); }
+        if (removed) { o += ",\"removedSeq\":"; put_int(o, v.R[s].rseq); o += ",\"removedClient\":"; o += client((int)v.R[s].rcl); }
         o += "}";
         segs.push_back(std::move(o)); lens.push_back(v.R[s].len);
     };
@@ -314,7 +314,7 @@ inline void dump_rows(const MtSnapView& v, const MtNames& nm, std::vector<int32_
         const uint32_t mt = v.R[s].meta;
         r[0] = v.R[s].len; r[1] = v.R[s].seq; r[2] = (mt & MT_M_CLIENT) == MT_NONCOLLAB ? -1 : (int32_t)(mt & MT_M_CLIENT);
         const bool removed = (mt & MT_M_REMOVED) != 0;
-        r[3] = removed ? v.R[s].rseq : INT32_MIN; r[4] = removed ? (int32_t)((mt & MT_M_RCLIENT) >> 8) : -1;
+        r[3] = removed ? v.R[s].rseq : INT32_MIN; r[4] = removed ? (int32_t)v.R[s].rcl : -1;
         r[5] = (int32_t)(v.R[s].ovl & 0xFFFFFFFFull); r[6] = (int32_t)(v.R[s].ovl >> 32);
         if (v.R[s].props >= 0) { std::string js; props_json(js, v.pset[v.R[s].props], nm); r[7] = (int32_t)(fnv1a(js) & 0x7FFFFFFF); }
         else r[7] = -1;

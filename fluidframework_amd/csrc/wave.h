@@ -44,6 +44,10 @@ template <class T> using LaneArr = T;
 // Mark a wave-uniform 32-bit value as such (moves it to an SGPR).
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ unsigned long long uni64(unsigned long long x) {
+    return (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x) |
+           ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32);
+}
 
 __device__ __forceinline__ int wave_lane() { return __lane_id(); }
 
@@ -132,6 +136,7 @@ template <class T> struct LaneArr {
 inline int wave_lane() { return 0; }
 inline int uni(int x) { return x; }
 inline uint32_t uni(uint32_t x) { return x; }
+inline unsigned long long uni64(unsigned long long x) { return x; }
 
 template <class F>
 inline auto wave_map(int n, F f) -> LaneArr<decltype(f(0))> {

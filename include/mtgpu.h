@@ -70,6 +70,7 @@ extern "C" {
 #define MT_DS_PROPS_TOO_MANY 0x400u
 #define MT_DS_BAD_OP         0x800u /* an op record out of its batch's bounds (payload /
                                        property table), checked on the device         */
+#define MT_DS_OOM_OVERLAP    0x2000u /* removedClientOverlap side list (clients >= 63) full */
 #define MT_DS_REFSEQ_BELOW_MSN 0x1000u /* refSeq < minSeq: deli nacks such ops
                                        (deli/lambda.ts:302-318); the window aggregate
                                        is exact only for refSeq >= minSeq             */
@@ -103,7 +104,7 @@ typedef struct mt_op_batch {
     uint32_t        n_ops;
     const uint8_t*  type;         /* [n_ops] MT_OP_*                           */
     const uint8_t*  flags;        /* [n_ops] MT_OPF_*                          */
-    const uint16_t* client;       /* [n_ops] per-document client index (< 64)   */
+    const uint16_t* client;       /* [n_ops] per-document client index (< 65534) */
     const int32_t*  seq;          /* [n_ops] sequenceNumber                     */
     const int32_t*  ref_seq;      /* [n_ops] referenceSequenceNumber            */
     const int32_t*  msn;          /* [n_ops] minimumSequenceNumber              */

@@ -353,6 +353,7 @@ struct Tree {
     std::vector<std::unique_ptr<Seg>> segs;
     std::vector<LRU> heap;               // Heap<LRUSegment>, L[0] sentinel
     uint32_t status = 0;
+    long long ovlHigh = 0;                 // overlap-list pushes by short ids >= 63 (test statistics)
 
     Tree() { root = makeBlock(0); heap.push_back({nullptr, -2}); }
     Block* makeBlock(int n) { blocks.emplace_back(new Block()); blocks.back()->childCount = n; return blocks.back().get(); }
@@ -758,7 +759,7 @@ struct Tree {
             if (s->hasRemoved) {
                 overwrite = true;
                 if (s->removedSeq == UnassignedSeq) { s->removedClientId = clientId; s->removedSeq = seq; }
-                else { if (!s->hasOverlap) { s->hasOverlap = true; s->overlap.clear(); } s->overlap.push_back(clientId); }
+                else { if (!s->hasOverlap) { s->hasOverlap = true; s->overlap.clear(); } s->overlap.push_back(clientId); if (clientId >= 63) ovlHigh++; }
             } else { s->hasRemoved = true; s->removedClientId = clientId; s->removedSeq = seq; }
             if (collaborating) { if (!(s->removedSeq == UnassignedSeq && clientId == cwClientId)) addToLRUSet(s, seq); }
         };
@@ -1465,7 +1466,7 @@ int32_t* ora_dump_segments(ora_doc* o, uint32_t* n_rows) {
         int32_t r[12];
         r[0] = s->cachedLength; r[1] = s->seq; r[2] = d.t.collaborating ? d.streamOf(s->clientId) : s->clientId;
         r[3] = s->hasRemoved ? s->removedSeq : INT32_MIN; r[4] = s->hasRemoved ? (d.t.collaborating ? d.streamOf(s->removedClientId) : s->removedClientId) : -1;
-        uint64_t m = 0; if (s->hasOverlap) for (int c : s->overlap) { int sc = d.streamOf(c); if (sc >= 0 && sc < 64) m |= 1ull << sc; }
+        uint64_t m = 0; if (s->hasOverlap) for (int c : s->overlap) { int sc = d.streamOf(c); if (sc >= 0) m |= 1ull << (sc < 63 ? sc : 63); }
         r[5] = (int32_t)(m & 0xFFFFFFFFu); r[6] = (int32_t)(m >> 32);
         if (s->hasProps) { std::string js; stringify(js, s->props); r[7] = (int32_t)(fnv1a(js) & 0x7FFFFFFF); } else r[7] = -1;
         r[8] = s->marker ? s->refType : -1;
@@ -1485,7 +1486,7 @@ int32_t* ora_dump_segments(ora_doc* o, uint32_t* n_rows) {
 void ora_stats(ora_doc* o, int32_t* out) {
     int h = 0; for (Node* x = o->d.t.root; x && !x->leaf; x = ((Block*)x)->childCount ? ((Block*)x)->children[0] : nullptr) h++;
     int nseg = 0; auto f = [&](Seg*) { nseg++; }; o->d.t.walkAll(o->d.t.root, f);
-    out[0] = h; out[1] = 0; out[2] = nseg; out[3] = (int)o->d.t.blocks.size();
+    out[0] = h; out[1] = (int)o->d.t.ovlHigh; out[2] = nseg; out[3] = (int)o->d.t.blocks.size();
 }
 
 uint32_t ora_generate_doc(const mt_gen_params* p, uint32_t doc, const mt_prop_table* props,

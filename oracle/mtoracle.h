@@ -52,7 +52,7 @@ uint8_t* ora_snapshot_legacy(ora_doc* d, int32_t msn, int32_t seq, uint64_t* dig
 uint16_t* ora_get_text(ora_doc* d, uint64_t* n_units);
 int32_t* ora_dump_segments(ora_doc* d, uint32_t* n_rows);  /* 12 int32 per row */
 void     ora_free_buf(void* p);
-/* Tree statistics: height, leaf blocks, segments, blocks. */
+/* Tree statistics: height, overlap-list pushes by short client ids >= 63, segments, blocks. */
 void     ora_stats(ora_doc* d, int32_t* out4);
 
 /* Stream generation (SURVEY.md §8(d) rules, same algorithm as mt_generate):

@@ -26,6 +26,10 @@ SURFACES = {
     "markers_props": dict(clients=5, lag=20, p_marker=0.3, p_annotate=0.35),
     "unicode": dict(clients=2, lag=4, p_special=0.8, p_remove=0.4),
     "churn": dict(clients=4, lag=10, churn=0.05, max_total_clients=60),
+    # > 300 distinct long ids over the document's life, overlapping removes by short ids >= 63
+    # (removedClientOverlap beyond the 63-bit mask: the per-document side list)
+    "churn300": dict(clients=6, lag=24, churn=0.42, p_remove=0.5, p_annotate=0.1, p_group=0.05, p_nonop=0.02,
+                     max_ins=4, long_every=0),
 }
 
 
@@ -75,6 +79,9 @@ def test_stream_generator_covers_the_surface():
     assert "😀" in texts or "𝄞" in texts
     msgs, _ = stream(8, 1500, **SURFACES["churn"])
     assert len({m["clientId"] for m in msgs}) > 30
+    msgs, obs = stream(101, 1200, **SURFACES["churn300"])
+    assert len({m["clientId"] for m in msgs}) > 300
+    assert obs.stats()[1] > 20          # overlapping removes by clients past the bitmask
 
 
 @pytest.mark.gpu
