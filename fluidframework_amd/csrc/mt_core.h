@@ -1024,21 +1024,6 @@ template <int RES> struct MtEngT {
         });
         return wave_count(ok) == na;
     }
-    // text[dst, dst+n1+n2) = text[src1, src1+n1) ++ text[src2, src2+n2), 64 units a pass.
-    MT_HD void copyText(int dst, int src1, int n1, int src2 = 0, int n2 = 0) {
-        const int n = n1 + n2;
-        MT_EV2(2, n); MT_EV2(3, 1);
-#ifdef MT_EXPERIMENT_NOCOPY
-        return;                            // timing experiment only: results are wrong
-#endif
-        for (int base = 0; base < n; base += MT_WAVE) {
-            const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
-            auto v = wave_map(m, [&](int k) MT_LAM { const int q = base + k; return (int)text[q < n1 ? src1 + q : src2 + (q - n1)]; });
-            wave_sync();
-            wave_for(m, [&](int k) MT_LAM { text[dst + base + k] = (uint16_t)own(v, k); });
-        }
-        wave_sync();
-    }
     // Text-arena compaction: copy the text of every linked row into the other
     // half of the document's arena (rows are immutable slices, so garbage from
     // relocated or unlinked rows accumulates until the half is full).
@@ -1075,44 +1060,98 @@ template <int RES> struct MtEngT {
         if (textTop + n > (int)S.textCap) { status |= MT_DS_OOM_TEXT; return -1; }
         const int o = textTop; textTop += n; return o;
     }
-    // TextSegment.append (textSegment.ts:74-85) on the arena.  A row owns
-    // [toff, toff + tcap); appends fill owned space, else the row moves to a new
-    // region of twice the size (amortized O(appended chars)).
-    // Returns the new (toff, tcap) of pv through references; lengths known by the caller.
-    MT_HD void appendText(int pv, int lp, int& tp, int& cp, int s, int ls, int ts, int cs) {
+    // text[dst, dst + Σ len) = the concatenation of up to 9 pieces: an optional head piece
+    // (hsrc, hlen), then the text of lanes [i0, i1) of (src, len), 64 units a pass (one
+    // load round trip per pass however many pieces).
+    MT_HD void gatherText(int dst, int hsrc, int hlen, const LaneArr<int>& src, const LaneArr<int>& len, int i0, int i1) {
+        int n = hlen;
+        for (int i = i0; i < i1; i++) n += wave_at(len, i);
+        MT_EV2(2, n); MT_EV2(3, 1);
+        for (int base = 0; base < n; base += MT_WAVE) {
+            const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
+            // piece of unit base+k: scan the (<= 9) piece prefixes, all scalar
+            auto from = wave_map(m, [&](int k) MT_LAM { const int q = base + k; return q < hlen ? hsrc + q : -1; });
+            int pre = hlen;
+            for (int i = i0; i < i1; i++) {
+                const int ps = wave_at(src, i), pl = wave_at(len, i), p0 = pre;
+                from = wave_map(m, [&](int k) MT_LAM {
+                    const int q = base + k, f0 = own(from, k);
+                    return (q >= p0 && q < p0 + pl) ? ps + (q - p0) : f0;
+                });
+                pre += pl;
+            }
+            auto v = wave_map(m, [&](int k) MT_LAM { return (int)text[own(from, k)]; });
+            wave_sync();
+            wave_for(m, [&](int k) MT_LAM { text[dst + base + k] = (uint16_t)own(v, k); });
+        }
+        wave_sync();
+    }
+    // One zamboni merge run (TextSegment.append, textSegment.ts:74-85, applied for each
+    // follower in order): head lane h takes the text of follower lanes [i0, i1).  The
+    // head owns [toff, toff + tcap) of the arena: followers whose text already sits right
+    // after the head's (split halves coming back together) extend it in place; the rest
+    // are copied into the head's slack, or head and rest move together to a new region
+    // of twice the size (amortized O(appended units)).  Returns the head's new length.
+    MT_HD int mergeRun(const LaneArr<int>& f, LaneArr<int>& ft, LaneArr<int>& fc, const LaneArr<int>& fl,
+                       int h, int i0, int i1) {
         MT_ZB(z2);
-        appendTextInner(pv, lp, tp, cp, s, ls, ts, cs);
+        const int hr = wave_at(f, h);
+        int tp = wave_at(ft, h), lp = wave_at(fl, h), cp = wave_at(fc, h);
+        int i = i0;
+        for (; i < i1; i++) {                              // in place: no copy
+            const int ts = wave_at(ft, i);
+            if (!(ts == tp + lp && cp == lp)) break;
+            cp = lp + wave_at(fc, i); lp += wave_at(fl, i);
+        }
+        if (i < i1) {
+            int rest = 0;
+            for (int j = i; j < i1; j++) rest += wave_at(fl, j);
+            if (lp + rest <= cp) {
+                gatherText(tp + lp, 0, 0, ft, fl, i, i1);
+            } else {
+                int nc = 2 * (lp + rest); if (nc < 16) nc = 16;
+                if (textTop + nc > (int)S.textCap) {
+                    // compaction moves every linked row's text (head and followers apart
+                    // again, slack gone): the whole run is copied, exactly sized
+                    textGC();
+                    ft = wave_map(8 * MT_MAXN, [&](int t) MT_LAM { const int g = own(f, t); return g >= 0 ? row(g).toff : 0; });
+                    fc = wave_map(8 * MT_MAXN, [&](int t) MT_LAM { const int g = own(f, t); return g >= 0 ? row(g).tcap : 0; });
+                    tp = wave_at(ft, h); lp = wave_at(fl, h); i = i0;
+                    rest = 0;
+                    for (int j = i; j < i1; j++) rest += wave_at(fl, j);
+                    nc = lp + rest;
+                }
+                const int o = textAlloc(nc);
+                if (o < 0) { MT_ZE(2, z2); return lp; }
+                gatherText(o, tp, lp, ft, fl, i, i1);
+                tp = o; cp = nc;
+            }
+            lp += rest;
+        }
+        row(hr).len = lp; row(hr).toff = tp; row(hr).tcap = cp;
         MT_ZE(2, z2);
+        return lp;
     }
-    MT_HD void appendTextInner(int pv, int lp, int& tp, int& cp, int s, int ls, int ts, int cs) {
-        if (ts == tp + lp && cp == lp) { row(pv).len = lp + ls; cp = lp + cs; row(pv).tcap = cp; return; }
-        if (lp + ls <= cp) { copyText(tp + lp, ts, ls); row(pv).len = lp + ls; return; }
-        int nc = 2 * (lp + ls); if (nc < 16) nc = 16;
-        if (textTop + nc > (int)S.textCap) { textGC(); nc = lp + ls; tp = uni(row(pv).toff); ts = uni(row(s).toff); }
-        const int o = textAlloc(nc);
-        if (o < 0) return;
-        copyText(o, tp, lp, ts, ls);
-        row(pv).toff = o; row(pv).tcap = nc; row(pv).len = lp + ls;
-        tp = o; cp = nc;
-    }
-    // scourNode for a block of rows (MT/mergeTree.ts:1278-1356); kept children
-    // are appended to sc->hold starting at nh; returns the new hold count.
-    // scourNode (MT/mergeTree.ts:1278-1356) for leaf blocks blks[0..nb) (a lane
-    // array, nb <= 7): kept children are appended to sc->hold from nh, with their
-    // observer lengths in sc->holdLen; returns the new hold count.  The rows of all
-    // the blocks (<= 49) are prefetched together (one row round trip plus one for
-    // the last text unit), then the merge chain runs sequentially on registers;
-    // prev restarts at every block, as each block is scoured separately.
+    // scourNode (MT/mergeTree.ts:1278-1356) for leaf blocks blks[0..nb) (a lane array,
+    // nb <= 7; lane t holds child slot t&7 of block t>>3): kept children are appended to
+    // sc->hold from nh, with their observer lengths in sc->holdLen; returns the new hold
+    // count.  Each block is scoured separately (prev restarts at every block).
+    //
+    // The reference walks the children with a `prev` cursor.  Here every decision that
+    // does not depend on the walk is made lane-parallel: unlink (removed at or below the
+    // MSN), held (removed above it, or inserted above it: prev resets), candidate
+    // (inserted at or below it), and whether candidate k may append to the run ending at
+    // k-1 (canAppend's marker / trailing "\n" / empty tests and matchProperties).  Only
+    // the 256-unit granularity rule depends on the run's accumulated length; a short
+    // scalar loop over the lanes in mergeable runs decides it.  Text then moves once per
+    // run (mergeRun), and unlinks, frees and the hold list are lane-parallel writes.
     MT_HD int scourLeaves(const LaneArr<int>& blks, int nb, int nh) {
-        // Lane t holds child slot t&7 of block t>>3; empty slots are masked out.
-        // The block id comes by lane shuffle (no per-block scalar arrays: they spilled).
         const int span = 8 * nb;
-        const auto bsel = wave_gather8(blks);
+        const auto bsel = wave_gather8(blks);       // block id by lane shuffle (per-block scalar arrays spilled)
         auto f = wave_map(span, [&](int t) MT_LAM {
             const int b = own(bsel, t);
             return (t & 7) < bk(b).n ? bk(b).c[t & 7] : -1;
         });
-        uint64_t live = wave_ballot(wave_map(span, [&](int t) MT_LAM { return own(f, t) >= 0; }));
         auto fm = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? (int)row(g).meta : 0; });
         auto fs = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).seq : 0; });
         auto fr = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).rseq : 0; });
@@ -1120,57 +1159,95 @@ template <int RES> struct MtEngT {
         auto fp = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).props : 0; });
         auto ft = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).toff : 0; });
         auto fc = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).tcap : 0; });
-        auto fe = wave_map(span, [&](int j) MT_LAM {
-            const int l = own(fl, j);
-            return (own(f, j) >= 0 && !(own(fm, j) & MT_M_MARKER) && l > 0) ? (int)text[own(ft, j) + l - 1] : 0;
+        const int ms = minSeq;
+        // class: 0 empty, 1 unlink, 2 held removed, 3 held above the MSN, 4 candidate
+        auto cls = wave_map(span, [&](int t) MT_LAM {
+            if (own(f, t) < 0) return 0;
+            const uint32_t mt = (uint32_t)own(fm, t);
+            if (mt & MT_M_REMOVED) return own(fr, t) <= ms ? 1 : 2;
+            return own(fs, t) <= ms ? 4 : 3;
         });
-        int prev = -1, prevLen = 0, prevToff = 0, prevCap = 0, prevProps = -1, prevLast = 0; bool prevMarker = false;
-        int epoch = gcEpoch;
-        int curB = 0;
-        while (live) {
-            const int k = __builtin_ctzll(live);
-            live &= live - 1;
-            if ((k >> 3) != curB) { prev = -1; curB = k >> 3; }      // each block is scoured separately
-            if (epoch != gcEpoch) {                                // text moved: refresh prefetched offsets
-                ft = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).toff : 0; });
-                fc = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).tcap : 0; });
-                if (prev >= 0) { prevToff = uni(row(prev).toff); prevCap = uni(row(prev).tcap); }
-                epoch = gcEpoch;
+        c_scour += (uint32_t)wave_count(wave_map(span, [&](int t) MT_LAM { return own(cls, t) != 0; }));
+        // k may append to k-1 (same block): both candidates, both non-empty, neither a marker
+        auto okPrev = wave_map(span, [&](int t) MT_LAM {
+            return (own(cls, t) == 4 && own(fl, t) > 0 && !((uint32_t)own(fm, t) & MT_M_MARKER)) ? 1 : 0;
+        });
+        const auto okPrev1 = wave_from8<-1>(okPrev), fp1 = wave_from8<-1>(fp);
+        auto pair = wave_map(span, [&](int t) MT_LAM { return ((t & 7) != 0 && own(okPrev, t) && own(okPrev1, t)) ? 1 : 0; });
+        uint64_t pm = wave_ballot(wave_map(span, [&](int t) MT_LAM { return own(pair, t) != 0; }));
+        uint64_t merged = 0;
+        auto runLen = fl;                                // a run head's final length
+        if (pm) {
+            // prev's last unit (canAppend: no trailing "\n") for lanes followed by a pair
+            const uint64_t needLast = pm >> 1;
+            auto lastNL = wave_map(span, [&](int t) MT_LAM {
+                return ((needLast >> t) & 1ull) ? (text[own(ft, t) + own(fl, t) - 1] == (uint16_t)'\n' ? 1 : 0) : 0;
+            });
+            const auto lastNL1 = wave_from8<-1>(lastNL);
+            // matchProperties: equal ids match; a missing map never matches a present one;
+            // two different maps compare key by key (propsMatch)
+            const uint64_t slow = wave_ballot(wave_map(span, [&](int t) MT_LAM {
+                const int a = own(fp1, t), b = own(fp, t);
+                return ((pm >> t) & 1ull) && a != b && a >= 0 && b >= 0;
+            }));
+            uint64_t propOk = wave_ballot(wave_map(span, [&](int t) MT_LAM {
+                const int a = own(fp1, t), b = own(fp, t);
+                return a == b;
+            }));
+            for (uint64_t sb = slow; sb; sb &= sb - 1) {
+                const int k = __builtin_ctzll(sb);
+                if (propsMatch(wave_at(fp1, k), wave_at(fp, k))) propOk |= 1ull << k;
             }
-            const int s = wave_at(f, k);
-            const uint32_t mt = (uint32_t)wave_at(fm, k);
-            c_scour++;
-            if (mt & MT_M_REMOVED) {
-                if (wave_at(fr, k) > minSeq) { sc->hold[nh] = s; sc->holdLen[nh] = 0; nh++; }
-                else {                                             // UNLINK
-                    row(s).parent = -1;
-                    if (!(mt & (MT_M_HREF | MT_M_INWIN))) freeRow(s);
+            pm &= propOk & ~wave_ballot(wave_map(span, [&](int t) MT_LAM { return own(lastNL1, t) != 0; }));
+            // the granularity rule: prev.len <= 256 || seg.len <= 256 on the accumulated run
+            uint64_t walk = pm | (pm >> 1);
+            int P = 0, head = -1;
+            while (walk) {
+                const int k = __builtin_ctzll(walk);
+                walk &= walk - 1;
+                const int lk = wave_at(fl, k);
+                if (((pm >> k) & 1ull) && (P <= MT_GRAN || lk <= MT_GRAN)) { merged |= 1ull << k; P += lk; }
+                else {
+                    if (head >= 0) runLen = wave_set(runLen, head, P);
+                    head = k; P = lk;
                 }
-                prev = -1;
-            } else if (wave_at(fs, k) <= minSeq) {
-                const int ls = wave_at(fl, k), ps = wave_at(fp, k);
-                bool can = prev >= 0 && !prevMarker && !(mt & MT_M_MARKER) && prevLast != (int)'\n' &&
-                           (prevLen <= MT_GRAN || ls <= MT_GRAN) && ls > 0;
-                if (can) can = propsMatch(prevProps, ps);
-                if (can) {
-                    appendText(prev, prevLen, prevToff, prevCap, s, ls, wave_at(ft, k), wave_at(fc, k));
-                    row(s).parent = -1;
-                    if (!(mt & (MT_M_HREF | MT_M_INWIN))) freeRow(s);
-                    prevLen += ls; prevLast = wave_at(fe, k);
-                    sc->holdLen[nh - 1] = prevLen;                 // prev is the last held row
-                } else {
-                    sc->hold[nh] = s; sc->holdLen[nh] = ls; nh++;
-                    prev = (ls > 0) ? s : -1;
-                    prevLen = ls; prevToff = wave_at(ft, k); prevCap = wave_at(fc, k); prevProps = ps;
-                    prevMarker = (mt & MT_M_MARKER) != 0; prevLast = wave_at(fe, k);
-                }
-            } else {
-                sc->hold[nh] = s; sc->holdLen[nh] = wave_at(fl, k); nh++;
-                prev = -1;
+            }
+            if (head >= 0) runLen = wave_set(runLen, head, P);
+            // move the text, one run at a time (followers still linked: compaction keeps their text)
+            for (uint64_t m = merged; m;) {
+                const int i0 = __builtin_ctzll(m);
+                int i1 = i0;
+                while ((m >> i1) & 1ull) i1++;
+                m &= ~((i1 >= 64 ? ~0ull : ((1ull << i1) - 1ull)));
+                mergeRun(f, ft, fc, fl, i0 - 1, i0, i1);
             }
         }
+        // unlinked and appended rows leave the tree; rows no heap entry or window refers
+        // to go back on the recycled-row stack (in lane order)
+        auto gone = wave_map(span, [&](int t) MT_LAM { return own(cls, t) == 1 || ((merged >> t) & 1ull); });
+        auto freeable = wave_map(span, [&](int t) MT_LAM {
+            return own(gone, t) && !((uint32_t)own(fm, t) & (MT_M_HREF | MT_M_INWIN));
+        });
+        const auto rkF = wave_rank(freeable);
+        const int nF = wave_count(freeable), f0 = rfN;
+        wave_for(span, [&](int t) MT_LAM {
+            if (!own(gone, t)) return;
+            row(own(f, t)).parent = -1;
+            if (own(freeable, t) && f0 + own(rkF, t) < MT_RFL) sc->rfree[f0 + own(rkF, t)] = own(f, t);
+        });
+        rfN = (f0 + nF) < MT_RFL ? (f0 + nF) : MT_RFL;
+        // kept children in order, with their observer lengths
+        auto keep = wave_map(span, [&](int t) MT_LAM { return own(cls, t) >= 2 && !((merged >> t) & 1ull); });
+        const auto rkK = wave_rank(keep);
+        const int nK = wave_count(keep), h0 = nh;
+        wave_for(span, [&](int t) MT_LAM {
+            if (!own(keep, t)) return;
+            const int c = own(cls, t);
+            sc->hold[h0 + own(rkK, t)] = own(f, t);
+            sc->holdLen[h0 + own(rkK, t)] = c == 2 ? 0 : (c == 4 ? own(runLen, t) : own(fl, t));
+        });
         wave_sync();
-        return nh;
+        return nh + nK;
     }
     // blockUpdatePathLengths(..., newStructure); firstLen >= 0: B's length is known.
     MT_HD void updatePathLens(int B, int firstLen = -1) {

@@ -238,3 +238,55 @@ def test_emu_generator_per_document_counts_matches_oracle():
     assert np.array_equal(gb.op_offsets, ob.op_offsets)
     for k in ("type", "flags", "client", "seq", "ref_seq", "msn", "pos1", "pos2", "payload_len", "prop_id"):
         assert np.array_equal(gb.arrays[k], ob.arrays[k]), k
+
+
+# Config-2 documents (bench seed) whose full 10k-message streams once exposed a text
+# compaction inside a multi-row zamboni merge run (caught by bench.py's digest parity).
+BENCH_DOCS = [240, 320, 459, 490]
+
+
+def bench_doc_batch(factory, docs):
+    import bench
+    from fluidframework_amd.batch import MtGenParams
+    c = dict(bench.CONFIGS["config2"])
+    props = bench.ann_props()
+    out = []
+    for d in docs:
+        c["docs"] = 1
+        g = factory(1, **bench.caps_for(c))
+        g.upload_props(props)
+        g.upload_names(NAMES)
+        p = MtGenParams(20241015, 1, c["ops"], c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"], c["rem_len"],
+                        c["ann_sets"], c["rewrite"])
+        p.doc_id_base = d
+        g.generate(p)
+        g.sync()
+        out.append(g.generated_download())
+        g.close()
+    return out, props
+
+
+def check_bench_docs(factory):
+    import bench
+    from oracle_lib import OracleDoc
+    c = dict(bench.CONFIGS["config2"])
+    batches, props = bench_doc_batch(factory, BENCH_DOCS)
+    for b in batches:
+        c["docs"] = 1
+        eng = factory(1, **bench.caps_for(c))
+        eng.upload_props(props)
+        eng.upload_names(NAMES)
+        eng.open_docs(0, 1)
+        eng.apply(b)
+        eng.sync()
+        assert eng.status([0])[0] == 0
+        od = OracleDoc(True, props, NAMES)
+        assert od.apply_run(b, 0) == 0
+        assert eng.get_text([0])[0] == od.get_text()
+        last = int(b.op_offsets[-1]) - 1
+        msn, seq = int(b.arrays["msn"][last]), int(b.arrays["seq"][last])
+        assert eng.snapshot([0], [msn], [seq])[0][1] == od.snapshot(msn, seq)[1]
+
+
+def test_emu_bench_docs_match_oracle():
+    check_bench_docs(emu_engine)

@@ -132,3 +132,8 @@ def test_gpu_per_document_capacities_and_generator_counts():
     for d in range(n):
         assert texts[d] == kept[d].get_text()
         assert int(digs[d]) == kept[d].snapshot(int(ob.arrays["msn"][last[d]]), int(ob.arrays["seq"][last[d]]))[1]
+
+
+def test_gpu_bench_docs_match_oracle():
+    from test_emu_parity import check_bench_docs
+    check_bench_docs(gpu_engine)

@@ -11,7 +11,7 @@ from fluidframework_amd.batch import MtGenParams
 import bench
 
 lib = "/tmp/libmtemu_ev2.so"
-subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wno-unknown-pragmas", "-DMT_EVCOUNT2",
+subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wno-unknown-pragmas", "-D" + os.environ.get("EVFLAG", "MT_EVCOUNT2"),
                        "-o", lib, os.path.join(ROOT, "tests", "emu", "mt_emu.cpp")])
 cfg = sys.argv[1] if len(sys.argv) > 1 else "config2"
 docs = int(sys.argv[2]) if len(sys.argv) > 2 else 4
