@@ -19,8 +19,10 @@ import numpy as np
 
 from . import jsjson
 
-MT_OP_INSERT, MT_OP_REMOVE, MT_OP_ANNOTATE, MT_OP_NOOP = 0, 1, 2, 3
+MT_OP_INSERT, MT_OP_REMOVE, MT_OP_ANNOTATE, MT_OP_NOOP, MT_OP_UNSUPPORTED = 0, 1, 2, 3, 4
 MT_OPF_END_OF_MSG, MT_OPF_MARKER, MT_OPF_REWRITE, MT_OPF_SEG_PROPS, MT_OPF_COMBINE = 1, 2, 4, 8, 16
+MT_OPF_REL1, MT_OPF_REL2, MT_OPF_MARKER_ID = 0x20, 0x40, 0x80
+MARKER_ID_KEY = "markerId"            # reservedMarkerIdKey, MT/mergeTree.ts:591
 
 MT_DS_NAMES = {
     0x01: "ASSERT_SEQ", 0x02: "ASSERT_MSN", 0x04: "INSERT_FAILED", 0x08: "UNSUPPORTED",
@@ -42,6 +44,7 @@ class MtOpBatch(ctypes.Structure):
         ("msn", ctypes.c_void_p), ("pos1", ctypes.c_void_p), ("pos2", ctypes.c_void_p),
         ("payload_off", ctypes.c_void_p), ("payload_len", ctypes.c_void_p), ("prop_id", ctypes.c_void_p),
         ("payload", ctypes.c_void_p), ("payload_units", ctypes.c_uint64),
+        ("n_rel", ctypes.c_uint32), ("rel", ctypes.c_void_p),
     ]
 
 
@@ -146,11 +149,27 @@ class PropTable:
 
 
 class ClientNames:
-    """Long client ids (strings) <-> per-document client index."""
+    """Per-document interning: long client ids (strings) <-> client index
+    (getOrAddShortClientId order, client.ts:658-682), and marker ids <-> the index of
+    the document's idToSegment table on the device (mergeTree.ts:1095, :1175)."""
 
     def __init__(self):
         self.ids: dict[str, int] = {}
         self.names: list[str] = []
+        self.marker_ids: dict[str, int] = {}
+
+    def marker_define(self, mid) -> int | None:
+        """A marker carrying id `mid` joins the document; None if the id is not a string
+        or is already in use (which marker the reference maps then depends on later block
+        updates, addNodeReferences mergeTree.ts:286-297: such documents stay off the path)."""
+        if not isinstance(mid, str) or mid in self.marker_ids:
+            return None
+        i = self.marker_ids[mid] = len(self.marker_ids)
+        return i
+
+    def marker_lookup(self, mid) -> int:
+        """getMarkerFromId: the index, or -1 when no marker with that id was mapped yet."""
+        return self.marker_ids.get(mid, -1) if isinstance(mid, str) else -1
 
     def index(self, long_id: str) -> int:
         i = self.ids.get(long_id)
@@ -168,6 +187,9 @@ _FIELDS = [("type", np.uint8), ("flags", np.uint8), ("client", np.uint16), ("seq
            ("payload_off", np.uint32), ("payload_len", np.uint32), ("prop_id", np.int32)]
 
 
+REL_DTYPE = np.dtype([("marker", np.int32), ("before", np.int32), ("offset", np.int32), ("pad", np.int32)])
+
+
 @dataclass
 class OpBatch:
     """Per-document runs of flattened op members (the mt_op_batch arrays)."""
@@ -175,6 +197,7 @@ class OpBatch:
     op_offsets: np.ndarray
     arrays: dict
     payload: np.ndarray
+    rel: np.ndarray = field(default_factory=lambda: np.zeros(0, REL_DTYPE))
     _c: Any = field(default=None, repr=False)
 
     @property
@@ -185,7 +208,8 @@ class OpBatch:
         if self._c is None:
             a = self.arrays
             self._c = MtOpBatch(len(self.doc_ids), _ptr(self.doc_ids), _ptr(self.op_offsets), self.n_ops,
-                                *(_ptr(a[n]) for n, _ in _FIELDS), _ptr(self.payload), int(self.payload.size))
+                                *(_ptr(a[n]) for n, _ in _FIELDS), _ptr(self.payload), int(self.payload.size),
+                                len(self.rel), _ptr(self.rel))
         return self._c
 
     @staticmethod
@@ -214,6 +238,7 @@ class BatchBuilder:
         self.payload: list[int] = []
         self.doc_ids: list[int] = []
         self.offsets: list[int] = [0]
+        self.rel: list[tuple] = []
 
     def begin_doc(self, doc_id: int):
         if len(self.doc_ids) and self.offsets[-1] == len(self.cols["type"]) and len(self.doc_ids) == len(self.offsets) - 1:
@@ -225,6 +250,23 @@ class BatchBuilder:
         for n, _ in _FIELDS:
             self.cols[n].append(kw.get(n, 0))
         self.offsets[-1] += 1
+
+    def _pos(self, op: dict, k: int):
+        """(value, flag) of op.pos{k}, or of op.relativePos{k} as an index into rel[]
+        (getValidOpRange, client.ts:506-523: pos wins; relativePos only when pos is
+        undefined).  (None, 0): neither."""
+        v = op.get(f"pos{k}")
+        if v is not None:
+            return int(v), 0
+        rp = op.get(f"relativePos{k}")
+        if not rp:
+            return None, 0
+        mid = rp.get("id") if isinstance(rp, dict) else None
+        idx = self.names.marker_lookup(mid) if jsjson.js_truthy(mid) else -1
+        off = rp.get("offset")
+        self.rel.append((idx, 1 if jsjson.js_truthy(rp.get("before")) else 0,
+                         int(off) if isinstance(off, (int, float)) and not isinstance(off, bool) else 0, 0))
+        return len(self.rel) - 1, (MT_OPF_REL1 if k == 1 else MT_OPF_REL2)
 
     def _member(self, op: dict, client: int, seq: int, ref: int, msn: int, last: bool):
         t = op["type"]
@@ -239,8 +281,11 @@ class BatchBuilder:
                 # touching the tree (client.ts:423-444); only seq/msn advance.
                 self._emit(type=MT_OP_NOOP, flags=fl, **common)
                 return
-            if "pos1" not in op:
-                raise NotImplementedError("relativePos1 inserts (mergeTree.ts:1949) are not on the batch path")
+            pos1, rf = self._pos(op, 1)
+            if pos1 is None:
+                self._emit(type=MT_OP_UNSUPPORTED, flags=fl, **common)
+                return
+            fl |= rf
             pos2 = 0
             if isinstance(seg, str):
                 text = seg
@@ -262,18 +307,34 @@ class BatchBuilder:
             units = jsjson.utf16_units(text) if text is not None else []
             off = len(self.payload)
             self.payload.extend(units)
-            self._emit(type=t, flags=fl, pos1=int(op["pos1"]), pos2=pos2, payload_off=off,
+            if text is None and pid >= 0 and jsjson.js_truthy(props.get(MARKER_ID_KEY)):   # Marker.getId
+                m = self.names.marker_define(props[MARKER_ID_KEY])
+                if m is None:
+                    self._emit(type=MT_OP_UNSUPPORTED, flags=fl, **common)
+                    return
+                fl |= MT_OPF_MARKER_ID
+                off = m
+            self._emit(type=t, flags=fl, pos1=pos1, pos2=pos2, payload_off=off,
                        payload_len=len(units), **{**common, "prop_id": pid})
         elif t in (MT_OP_REMOVE, MT_OP_ANNOTATE):
-            if "pos1" not in op or "pos2" not in op:
-                raise NotImplementedError("relative positions are not on the batch path")
+            if op.get("register") is not None:
+                raise NotImplementedError("cut into a register (client.ts:347-350) is not on the batch path")
+            pos1, f1 = self._pos(op, 1)
+            pos2, f2 = self._pos(op, 2)
+            if pos1 is None or pos2 is None:
+                self._emit(type=MT_OP_UNSUPPORTED, flags=fl, **common)
+                return
             pid = -1
             if t == MT_OP_ANNOTATE:
                 cop = op.get("combiningOp")
                 if cop is not None:
                     fl |= MT_OPF_REWRITE if cop.get("name") == "rewrite" else MT_OPF_COMBINE
+                if isinstance(op.get("props"), dict) and MARKER_ID_KEY in op["props"]:
+                    # re-keying a marker changes idToSegment only at later block updates
+                    self._emit(type=MT_OP_UNSUPPORTED, flags=fl, **common)
+                    return
                 pid = self.props.intern(op["props"])
-            self._emit(type=t, flags=fl, pos1=int(op["pos1"]), pos2=int(op["pos2"]), **{**common, "prop_id": pid})
+            self._emit(type=t, flags=fl | f1 | f2, pos1=pos1, pos2=pos2, **{**common, "prop_id": pid})
         else:
             self._emit(type=MT_OP_NOOP, flags=fl, **common)
 
@@ -299,7 +360,7 @@ class BatchBuilder:
     def build(self) -> OpBatch:
         arrays = {n: np.asarray(self.cols[n], dtype=t) for n, t in _FIELDS}
         return OpBatch(np.asarray(self.doc_ids, np.uint32), np.asarray(self.offsets, np.uint32), arrays,
-                       np.asarray(self.payload or [0], np.uint16))
+                       np.asarray(self.payload or [0], np.uint16), np.array(self.rel, dtype=REL_DTYPE))
 
 
 def concat_runs(a: OpBatch, b: OpBatch) -> OpBatch:

@@ -46,6 +46,7 @@ static void mt_caps_default(mt_limits& q) {
     if (!q.window_per_doc) q.window_per_doc = 4096;
     if (!q.text_per_doc) q.text_per_doc = q.rows_per_doc * 8;
     if (!q.propsets_per_doc) q.propsets_per_doc = 1024;
+    if (!q.markers_per_doc) q.markers_per_doc = 1024;
 }
 static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bool uniform, mt_ctx** out) {
     mt_ctx* c = new mt_ctx();
@@ -65,10 +66,12 @@ static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bo
         }
         MtDocLayout& y = c->layout_h[d];
         y.row = tot.row; y.blk = tot.blk; y.heap = tot.heap; y.win = tot.win; y.anc = tot.anc; y.text = tot.text; y.pset = tot.pset;
+        y.mid = tot.mid;
         y.rowCap = q.rows_per_doc; y.blkCap = q.blocks_per_doc; y.heapCap = q.heap_per_doc; y.winCap = q.window_per_doc;
-        y.textCap = q.text_per_doc; y.psetCap = q.propsets_per_doc;
+        y.textCap = q.text_per_doc; y.psetCap = q.propsets_per_doc; y.midCap = q.markers_per_doc;
         tot.row += y.rowCap; tot.blk += y.blkCap; tot.heap += y.heapCap + 1; tot.win += y.winCap;
         tot.anc += (unsigned long long)y.winCap * MT_MAXH; tot.text += 2ull * y.textCap; tot.pset += y.psetCap;
+        tot.mid += y.midCap;
         S.rowCap = std::max(S.rowCap, y.rowCap); S.blkCap = std::max(S.blkCap, y.blkCap); S.heapCap = std::max(S.heapCap, y.heapCap);
         S.winCap = std::max(S.winCap, y.winCap); S.textCap = std::max(S.textCap, y.textCap); S.psetCap = std::max(S.psetCap, y.psetCap);
     }
@@ -81,7 +84,7 @@ static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bo
     MT_ALLOC(blk, MtBlk, tot.blk) MT_ALLOC(heap, MtHeapE, tot.heap) MT_ALLOC(win, int, tot.win)
     MT_ALLOC(uid, int, tot.win) MT_ALLOC(udelta, int, tot.win) MT_ALLOC(uanc, int, tot.anc)
     MT_ALLOC(text, uint16_t, tot.text) MT_ALLOC(pset, MtPSet, tot.pset) MT_ALLOC(hdr, MtDocHdr, D)
-    MT_ALLOC(hold, int, D * MT_RFL) MT_ALLOC(ovx, MtOvx, D * MT_OVX_CAP)
+    MT_ALLOC(hold, int, D * MT_RFL) MT_ALLOC(ovx, MtOvx, D * MT_OVX_CAP) MT_ALLOC(mid, int, tot.mid)
 #undef MT_ALLOC
     if (mtb_malloc(&p, sizeof(MtDocLayout) * D) != 0) { c->err = "pool allocation failed: layout"; return MT_E_OOM; }
     S.layout = (const MtDocLayout*)p;
@@ -90,7 +93,7 @@ static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bo
     c->tot = tot;
     c->pool_bytes = sizeof(MtRow) * tot.row + sizeof(MtBlk) * tot.blk + sizeof(MtHeapE) * tot.heap + 12ull * tot.win +
                     4ull * tot.anc + 2ull * tot.text + sizeof(MtPSet) * tot.pset +
-                    (sizeof(MtDocHdr) + 4ull * MT_RFL + sizeof(MtDocLayout) + sizeof(MtOvx) * MT_OVX_CAP) * D;
+                    (sizeof(MtDocHdr) + 4ull * MT_RFL + sizeof(MtDocLayout) + sizeof(MtOvx) * MT_OVX_CAP) * D + 4ull * tot.mid;
     return MT_OK;
 }
 
@@ -113,7 +116,7 @@ static std::vector<MtCkPart> mt_ck_parts(mt_ctx* c) {
             {&c->ck_heap, S.heap, sizeof(MtHeapE) * t.heap}, {&c->ck_win, S.win, 4ull * t.win},
             {&c->ck_text, S.text, 2ull * t.text}, {&c->ck_pset, S.pset, sizeof(MtPSet) * t.pset},
             {&c->ck_hdr, S.hdr, sizeof(MtDocHdr) * D}, {&c->ck_hold, S.hold, 4ull * MT_RFL * D},
-            {&c->ck_ovx, S.ovx, sizeof(MtOvx) * MT_OVX_CAP * D}};
+            {&c->ck_ovx, S.ovx, sizeof(MtOvx) * MT_OVX_CAP * D}, {&c->ck_mid, S.mid, 4ull * t.mid}};
 }
 int MT_FN(checkpoint)(mt_ctx* c) {
     if (!c) return MT_E_INVALID;
@@ -143,9 +146,10 @@ void MT_FN(destroy)(mt_ctx* c) {
     if (!c) return;
     MtState& S = c->S;
     void* ps[] = {S.rows, S.blk, S.heap, S.win, S.uid, S.udelta, S.uanc, S.text, S.pset, S.hdr, S.hold, (void*)S.layout,
-                  S.ovx, c->ck_rows, c->ck_blk, c->ck_heap, c->ck_win, c->ck_text, c->ck_pset, c->ck_hdr, c->ck_hold, c->ck_ovx};
+                  S.ovx, S.mid, c->ck_rows, c->ck_blk, c->ck_heap, c->ck_win, c->ck_text, c->ck_pset, c->ck_hdr, c->ck_hold,
+                  c->ck_ovx, c->ck_mid};
     for (void* p : ps) if (p) mtb_free(p);
-    mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_pset_off,
+    mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_rel, &c->b_pset_off,
                             &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3,
                             &c->b_ld_meta, &c->b_ld_seg, &c->b_ld_pay, &c->b_ld_plan, &c->b_ld_poff};
     for (auto* b : bs) if (b->p) mtb_free(b->p);
@@ -207,10 +211,13 @@ static int mt_upload_ops(mt_ctx* c, const mt_op_batch* B) {
 #define UP(buf, src, bytes) if ((rc = mtb_ensure(c, c->buf, (bytes)))) return rc; if ((bytes) && (src)) mtb_h2d(c, c->buf.p, (src), (bytes));
     UP(b_doc, B->doc_ids, 4 * R) UP(b_off, B->op_offsets, 4 * (R + 1)) UP(b_rec, rec.data(), sizeof(MtOpRec) * N)
     UP(b_pay, B->payload, 2 * B->payload_units)
+    static_assert(sizeof(mt_rel_pos) == sizeof(MtRelPos), "relative position layout");
+    UP(b_rel, B->rel, sizeof(MtRelPos) * (size_t)B->n_rel)
 #undef UP
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = B->n_runs; o.payload_units = B->payload_units;
+    o.rel = (const MtRelPos*)c->b_rel.p; o.n_rel = B->rel ? B->n_rel : 0;
     c->n_runs = B->n_runs;
     return MT_OK;
 }
@@ -218,16 +225,20 @@ static int mt_upload_ops(mt_ctx* c, const mt_op_batch* B) {
 static int mt_check_batch(mt_ctx* c, const mt_op_batch* B) {
     if (!B || !B->op_offsets || (B->n_runs && !B->doc_ids)) { c->err = "null batch arrays"; return MT_E_INVALID; }
     if (B->op_offsets[B->n_runs] != B->n_ops) { c->err = "op_offsets[n_runs] != n_ops"; return MT_E_INVALID; }
+    if (B->n_rel && !B->rel) { c->err = "n_rel without rel"; return MT_E_INVALID; }
     for (uint32_t r = 0; r < B->n_runs; r++) {
         if (B->doc_ids[r] >= c->S.maxDocs) { c->err = "doc id out of range"; return MT_E_INVALID; }
         if (B->op_offsets[r] > B->op_offsets[r + 1]) { c->err = "op_offsets not monotone"; return MT_E_INVALID; }
     }
     for (uint32_t i = 0; i < B->n_ops; i++) {
+        if (B->type[i] > MT_OP_UNSUPPORTED) { c->err = "unknown op type"; return MT_E_INVALID; }
         if (B->type[i] == MT_OP_INSERT && !(B->flags[i] & MT_OPF_MARKER) &&
             (uint64_t)B->payload_off[i] + B->payload_len[i] > B->payload_units) { c->err = "payload out of range"; return MT_E_INVALID; }
         if (B->prop_id[i] >= 0 && (uint32_t)B->prop_id[i] >= c->S.p_nsets) { c->err = "prop_id out of range (mt_set_props first)"; return MT_E_INVALID; }
         if (B->prop_id[i] > 32767) { c->err = "more than 32767 property sets"; return MT_E_INVALID; }
         if (B->payload_len[i] > 65535) { c->err = "insert longer than 65535 UTF-16 units"; return MT_E_INVALID; }
+        if (((B->flags[i] & MT_OPF_REL1) && (uint32_t)B->pos1[i] >= B->n_rel) ||
+            ((B->flags[i] & MT_OPF_REL2) && (uint32_t)B->pos2[i] >= B->n_rel)) { c->err = "relative position index out of range"; return MT_E_INVALID; }
     }
     return MT_OK;
 }
@@ -649,6 +660,7 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs; o.payload_units = PU;
+    o.rel = nullptr; o.n_rel = 0;
     c->n_runs = P->n_docs;
     c->gen_off.assign(off.begin(), off.end());
     if (!P->continue_docs) {
@@ -721,6 +733,7 @@ int MT_FN(upload_batch_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids,
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs; o.payload_units = payload_units;
+    o.rel = nullptr; o.n_rel = 0;
     c->n_runs = n_runs;
     c->gen.enabled = 0;
     return mtb_sync(c);

@@ -134,7 +134,7 @@ struct __attribute__((aligned(16))) MtRow {   // one 48-byte record per segment 
     int tcap;        // owned text capacity at toff
     unsigned long long ovl;  // removedClientOverlap: bit c for clients c < 63; bit 63 = more in the side list
     uint32_t rcl;            // removedClientId (16 bits)
-    int pad1;
+    int mid;                 // marker: its markerId's per-document index + 1 (0: none)
 };
 struct __attribute__((aligned(16))) MtBlk {   // one 64-byte record per B-tree block
     int c[8];        // children: segment rows (height 0) or blocks
@@ -174,9 +174,9 @@ struct __attribute__((aligned(16))) MtDocHdr {
 // their capacities: documents of one context may be sized differently
 // (mt_create_docs), e.g. by their op counts.
 struct __attribute__((aligned(16))) MtDocLayout {
-    unsigned long long row, blk, heap, win, anc, text, pset;   // heap: cap+1 entries; text: 2 halves
-    uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap;
-    uint32_t pad[2];
+    unsigned long long row, blk, heap, win, anc, text, pset, mid;   // heap: cap+1 entries; text: 2 halves
+    uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap, midCap;
+    uint32_t pad[1];
 };
 
 struct MtState {                              // device pools, doc-major
@@ -184,6 +184,7 @@ struct MtState {                              // device pools, doc-major
     MtBlk* blk; MtHeapE* heap; int* win; int* uid; int* udelta; int* uanc;
     uint16_t* text; MtPSet* pset; MtDocHdr* hdr; int* hold;   // text: 2 halves of textCap per doc; hold: recycled-row stacks
     MtOvx* ovx;                               // overlap side lists, MT_OVX_CAP per doc
+    int* mid;                                 // marker-id tables (idToSegment): row per id, -1 unmapped
     uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap, holdCap, maxDocs;   // largest per-doc caps
     const MtDocLayout* layout;                // [maxDocs]
     // interned op property sets (mt_prop_table)
@@ -197,10 +198,12 @@ struct __attribute__((aligned(16))) MtOpRec {  // one 32-byte op record (mt_op_b
     uint32_t payload_off;
     uint16_t payload_len; int16_t prop_id;
 };
+struct MtRelPos { int marker, before, offset, pad; };   // mt_rel_pos
 struct MtOps {                                // device copy of an mt_op_batch
     const uint32_t* doc_ids; const uint32_t* op_off;
     MtOpRec* rec;
     uint16_t* payload;
+    const MtRelPos* rel; uint32_t n_rel;
     uint32_t n_runs;
     uint64_t payload_units;                   // records are bounds-checked against it on the device
 };
@@ -212,7 +215,7 @@ struct __attribute__((aligned(16))) MtLoadSeg {
     int32_t seq, rseq;
     uint16_t rclient; int16_t prop;
     uint32_t poff, plen;
-    uint32_t pad1[2];
+    uint32_t mid, pad1;                       // marker id index + 1 (0: none)
 };
 // One step of the body plan: START = first segment of an insertSegments call
 // (ensureIntervalBoundary at the observer's length, then insert), CONT = a later
@@ -345,6 +348,7 @@ template <int RES> struct MtEngT {
     int *win, *uid, *udelta, *uanc;
     MtBlk* blk; MtHeapE* heap; uint16_t* text; MtPSet* pset;
     MtOvx* ovx; int ovxN;
+    int* midt; int midCap;                    // idToSegment (MT/mergeTree.ts:1095, :1175)
     MtScratch* sc;
     // pool accessors: LDS (MT_RES_LDS, MT_RES_BLK for blocks + heap) or HBM homes
     MT_HD MtRow& row(int s) const { if constexpr (LDS) return mt_lds().rows[s]; else return R[s]; }
@@ -414,6 +418,7 @@ template <int RES> struct MtEngT {
         win = st.win + wo; uid = st.uid + wo; udelta = st.udelta + wo; uanc = st.uanc + off(&Ly->anc);
         pset = st.pset + off(&Ly->pset);
         ovx = st.ovx + (size_t)d * MT_OVX_CAP;
+        midt = st.mid + off(&Ly->mid); midCap = (int)uni(Ly->midCap);
         sc = scratch;
         const MtDocHdr& h = *hdrp;
         root = uni(h.root); height = uni(h.height); minSeq = uni(h.minSeq); curSeq = uni(h.curSeq); rowTop = uni(h.rowTop);
@@ -471,6 +476,9 @@ template <int RES> struct MtEngT {
 #endif
         wave_for(8, [&](int i) MT_LAM { bk(0).c[i] = -1; });
         bk(0).len = 0; bk(0).parent = -1; bk(0).n = 0; bk(0).height = 0; bk(0).scour = -1;
+        // idToSegment entries are not reset: an entry is read only for an id the host
+        // already saw mapped in this document (mt_rel_pos.marker >= 0), and relPos
+        // checks that the row still carries that id.
     }
 
     /* ---------------------------------------------------------- pools -- */
@@ -701,6 +709,39 @@ template <int RES> struct MtEngT {
         });
         return uni(bk(root).len) + s;
     }
+    // MergeTree.getPosition (MT/mergeTree.ts:1578-1596): the (r, c) perspective length
+    // of everything before row s; an unlinked row (parent undefined) is at 0.
+    MT_HD int getPosition(int s, int r, int c) {
+        int B = uni(row(s).parent);
+        if (B < 0) return 0;
+        if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
+        int node = s, pos = 0;
+        for (;;) {
+            BlkH h;
+            auto ch = blkLoad(B, h);
+            auto cl = childLens(B, h, ch, r, c);
+            const int nd = node;
+            const int j = wave_first(wave_map(h.n, [&](int i) MT_LAM { return own(ch, i) == nd; }));
+            pos += wave_sum8(wave_map(h.n, [&](int i) MT_LAM { return i < j ? own(cl, i).len : 0; }));
+            if (h.parent < 0) return pos;
+            node = B; B = h.parent;
+        }
+    }
+    // posFromRelativePos (MT/mergeTree.ts:1949-1972): the marker's position under (r, c),
+    // then past the marker (+ cachedLength 1 + offset) or before it (- offset).  -1: the
+    // id was never mapped (getMarkerFromId undefined).  A marker whose row was unlinked
+    // (or since recycled) sits at 0, as getPosition of a segment without parent does.
+    MT_HD int relPos(const MtRelPos& q, int r, int c) {
+        const int id = uni(q.marker);
+        if (id < 0 || id >= midCap) return -1;
+        const int s = uni(midt[id]);
+        if (s < 0 || s >= rowTop) return 0;
+        const bool live = uni(row(s).mid) == id + 1 && (uni(row(s).meta) & MT_M_MARKER);
+        int pos = live ? getPosition(s, r, c) : 0;
+        const int off = uni(q.offset);
+        if (!uni(q.before)) pos += 1 + off; else pos -= off;
+        return pos;
+    }
     // Perspective lengths of block B's children (nodeLength, MT/mergeTree.ts:1652-1692).
     MT_HD LaneArr<ChildL> childLens(int B, const BlkH& h, const LaneArr<int>& ch, int r, int c) {
         if (h.height == 0) {
@@ -798,7 +839,7 @@ template <int RES> struct MtEngT {
         row(n).len = ls - pos; row(s).len = pos;
         const unsigned long long ov = uni64(row(s).ovl);
         row(n).seq = row(s).seq; row(n).rseq = row(s).rseq; row(n).meta = mt & ~(MT_M_INWIN | MT_M_HREF); row(n).ovl = ov;
-        row(n).rcl = row(s).rcl;
+        row(n).rcl = row(s).rcl; row(n).mid = 0;
         if (ov >> 63) ovxCopy(s, n);
         row(n).toff = row(s).toff + pos; row(n).props = row(s).props; row(n).parent = row(s).parent;
         row(n).tcap = row(s).tcap - pos; row(s).tcap = pos;   // each row owns [toff, toff+tcap) of the arena
@@ -1548,6 +1589,10 @@ template <int RES> struct MtEngT {
                 w.meta = (uint32_t)cl | (rm ? MT_M_REMOVED : 0u) | (mk ? MT_M_MARKER : 0u);
                 w.rcl = rm ? (uint32_t)g.rclient : 0u;
                 w.ovl = 0ull; w.props = -1; w.parent = -1;
+                w.mid = mk ? (int)g.mid : 0;
+                // reloadFromSegments -> blockUpdate -> addNodeReferences maps the ids of
+                // markers with localNetLength > 0 (MT/mergeTree.ts:286-297)
+                if (mk && g.mid && !rm && (int)g.mid <= midCap) midt[g.mid - 1] = s;
                 w.toff = mk ? (int)g.plen : t0 + (int)(g.poff - pbase);
                 w.tcap = mk ? 0 : (int)g.plen;
             });
@@ -1627,6 +1672,11 @@ template <int RES> struct MtEngT {
         row(n).meta = (uint32_t)cli | (rm ? MT_M_REMOVED : 0u) | (mk ? MT_M_MARKER : 0u);
         row(n).rcl = rm ? (uint32_t)uni((int)g->rclient) : 0u;
         row(n).ovl = 0ull; row(n).parent = -1; row(n).props = -1;
+        {   // insertSegments maps a marker's id before its walk (MT/mergeTree.ts:2218-2222)
+            const int mi = mk ? uni((int)g->mid) : 0;
+            row(n).mid = mi;
+            if (mi) { if (mi > midCap) { status |= MT_DS_UNSUPPORTED; return 0; } midt[mi - 1] = n; }
+        }
         row(n).tcap = plen;
         if (mk) row(n).toff = uni((int)g->plen);
         else {
@@ -1651,7 +1701,8 @@ template <int RES> struct MtEngT {
         if (sq > minSeq) addToLRUSet(n, sq);
         return L;
     }
-    MT_HD void opInsert(int pos, int r, int c, int sq, const uint16_t* src, int plen, bool marker, int refType, int segProps) {
+    MT_HD void opInsert(int pos, int r, int c, int sq, const uint16_t* src, int plen, bool marker, int refType, int segProps,
+                        int markerId = -1) {
         // MergeTree.insertSegments (MT/mergeTree.ts:1974-2011)
         MT_PB(t0);
         int w = walk(MT_WALK_SPLIT, pos, r, c, -1, 0);
@@ -1665,6 +1716,11 @@ template <int RES> struct MtEngT {
             row(n).len = L; row(n).seq = sq; row(n).rseq = MT_NOREM;
             row(n).meta = (uint32_t)c | (marker ? MT_M_MARKER : 0u);
             row(n).ovl = 0ull; row(n).parent = -1; row(n).rcl = 0u;
+            row(n).mid = markerId >= 0 ? markerId + 1 : 0;
+            if (markerId >= 0) {                       // mapIdToSegment before the walk (MT/mergeTree.ts:2218-2222)
+                if (markerId >= midCap) { status |= MT_DS_UNSUPPORTED; return; }
+                midt[markerId] = n;
+            }
             row(n).props = segProps >= 0 ? applyPropSet(-1, segProps, false) : -1;
             row(n).tcap = marker ? 0 : plen;
             if (marker) row(n).toff = refType;

@@ -17,13 +17,13 @@ struct mt_ctx {
     MtDocLayout tot{};                                                     // pool element totals
     // mt_checkpoint shadows (device)
     void *ck_rows = nullptr, *ck_blk = nullptr, *ck_heap = nullptr, *ck_win = nullptr, *ck_text = nullptr,
-         *ck_pset = nullptr, *ck_hdr = nullptr, *ck_hold = nullptr, *ck_ovx = nullptr;
+         *ck_pset = nullptr, *ck_hdr = nullptr, *ck_hold = nullptr, *ck_ovx = nullptr, *ck_mid = nullptr;
     bool ck_valid = false;
     std::unordered_map<uint32_t, std::vector<std::string>> doc_clients;   // mt_set_doc_client_names
     std::string err;
     // device op batch (resident)
     struct DevBuf { void* p = nullptr; size_t cap = 0; };
-    DevBuf b_stage, b_pack_docs, b_pack_sz, b_pack_off, b_gencl, b_cursor, b_doc, b_off, b_rec, b_pay, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3,
+    DevBuf b_stage, b_pack_docs, b_pack_sz, b_pack_off, b_gencl, b_cursor, b_doc, b_off, b_rec, b_pay, b_rel, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3,
            b_ld_meta, b_ld_seg, b_ld_pay, b_ld_plan, b_ld_poff;
     MtOps ops{};
     uint32_t n_runs = 0;

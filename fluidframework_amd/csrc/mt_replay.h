@@ -100,6 +100,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
         const uint32_t poff = (uint32_t)wave_at(w, 6);
         const uint32_t w7 = (uint32_t)wave_at(w, 7);
         const int plen = (int)(w7 & 0xFFFF), pid = (int)(int16_t)(w7 >> 16);
+        if (ty == MT_OP_UNSUPPORTED) { e.status |= MT_DS_UNSUPPORTED; break; }
         if (ty != MT_OP_NOOP) {
             if (c >= MT_NONCOLLAB) e.status |= MT_DS_UNSUPPORTED;  // 0xFFFE/0xFFFF are reserved ids
             if (e.curSeq >= sq) e.status |= MT_DS_ASSERT_SEQ;       // completeAndLogOp, MT/client.ts:482
@@ -109,14 +110,23 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
                 e.status |= MT_DS_BAD_OP;
             if (e.status) break;
             if (!(e.uValid && e.uRef == r && e.uCli == c)) e.computeU(r, c, true);
+            int q1 = p1, q2 = p2;
+            if (fl & (MT_OPF_REL1 | MT_OPF_REL2)) {       // getValidOpRange (MT/client.ts:506-523)
+                if ((fl & MT_OPF_REL1) && (p1 < 0 || (uint32_t)p1 >= ops.n_rel)) { e.status |= MT_DS_BAD_OP; break; }
+                if ((fl & MT_OPF_REL2) && (p2 < 0 || (uint32_t)p2 >= ops.n_rel)) { e.status |= MT_DS_BAD_OP; break; }
+                if (fl & MT_OPF_REL1) q1 = e.relPos(ops.rel[p1], r, c);
+                if (fl & MT_OPF_REL2) q2 = e.relPos(ops.rel[p2], r, c);
+                if (q1 < 0 || ((fl & MT_OPF_REL2) && q2 < 0)) { e.status |= MT_DS_UNSUPPORTED; break; }
+            }
             if (ty == MT_OP_INSERT) {
                 const bool marker = (fl & MT_OPF_MARKER) != 0;
-                e.opInsert(p1, r, c, sq, ops.payload + poff, plen, marker, p2, (fl & MT_OPF_SEG_PROPS) ? pid : -1);
+                e.opInsert(q1, r, c, sq, ops.payload + poff, plen, marker, p2, (fl & MT_OPF_SEG_PROPS) ? pid : -1,
+                           (marker && (fl & MT_OPF_MARKER_ID)) ? (int)poff : -1);
             } else if (ty == MT_OP_REMOVE) {
-                e.opRange(MT_MAP_REMOVE, p1, p2, r, c, sq, -1, false);
+                e.opRange(MT_MAP_REMOVE, q1, q2, r, c, sq, -1, false);
             } else if (ty == MT_OP_ANNOTATE) {
                 if (fl & MT_OPF_COMBINE) { e.status |= MT_DS_UNSUPPORTED; break; }
-                e.opRange(MT_MAP_ANNOTATE, p1, p2, r, c, sq, pid, (fl & MT_OPF_REWRITE) != 0);
+                e.opRange(MT_MAP_ANNOTATE, q1, q2, r, c, sq, pid, (fl & MT_OPF_REWRITE) != 0);
             }
             e.uValid = false;
 #if defined(MT_PROFILE) && defined(__HIP_DEVICE_COMPILE__)

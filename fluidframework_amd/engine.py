@@ -35,7 +35,8 @@ class MergeTreeError(RuntimeError):
 
 class MtLimits(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint32) for n in ("max_docs", "rows_per_doc", "blocks_per_doc", "text_per_doc",
-                                               "propsets_per_doc", "heap_per_doc", "window_per_doc")]
+                                               "propsets_per_doc", "heap_per_doc", "window_per_doc",
+                                               "markers_per_doc")]
 
 
 class MtDocCounters(ctypes.Structure):
@@ -109,7 +110,8 @@ class Engine:
 
     def __init__(self, max_docs: int, rows_per_doc: int = 4096, blocks_per_doc: int = 0, text_per_doc: int = 0,
                  propsets_per_doc: int = 0, heap_per_doc: int = 0, window_per_doc: int = 0, device: int = 0,
-                 lib_path: str | None = None, prefix: str = "mt_", per_doc: dict | None = None):
+                 lib_path: str | None = None, prefix: str = "mt_", per_doc: dict | None = None,
+                 markers_per_doc: int = 0):
         """per_doc: optional dict of per-document capacity arrays (keys rows_per_doc,
         blocks_per_doc, text_per_doc, propsets_per_doc, heap_per_doc, window_per_doc;
         missing keys use the scalar arguments) -> mt_create_docs."""
@@ -121,12 +123,13 @@ class Engine:
         self.fn = _bind(self.lib, prefix)
         self.max_docs = max_docs
         lim = MtLimits(max_docs, rows_per_doc, blocks_per_doc, text_per_doc, propsets_per_doc, heap_per_doc,
-                       window_per_doc)
+                       window_per_doc, markers_per_doc)
         h = ctypes.c_void_p()
         if per_doc:
             arr = (MtLimits * max_docs)()
             scal = dict(rows_per_doc=rows_per_doc, blocks_per_doc=blocks_per_doc, text_per_doc=text_per_doc,
-                        propsets_per_doc=propsets_per_doc, heap_per_doc=heap_per_doc, window_per_doc=window_per_doc)
+                        propsets_per_doc=propsets_per_doc, heap_per_doc=heap_per_doc, window_per_doc=window_per_doc,
+                        markers_per_doc=markers_per_doc)
             cols = {k: (np.asarray(per_doc[k], np.uint32) if k in per_doc else None) for k in scal}
             for i in range(max_docs):
                 for k, v in scal.items():

@@ -26,8 +26,10 @@ const path = require("path");
 // MTGPU_NAPI: an alternate build of this addon (the tests' host-emulation build)
 const addon = require(process.env.MTGPU_NAPI || path.join(__dirname, "mtgpu.node"));
 
-const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_GROUP = 3;
-const F_END = 1, F_MARKER = 2, F_REWRITE = 4, F_SEG_PROPS = 8, F_COMBINE = 16;
+const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_GROUP = 3, OP_UNSUPPORTED = 4;
+const F_END = 1, F_MARKER = 2, F_REWRITE = 4, F_SEG_PROPS = 8, F_COMBINE = 16, F_REL1 = 0x20, F_REL2 = 0x40,
+    F_MARKER_ID = 0x80;
+const MARKER_ID_KEY = "markerId";   // reservedMarkerIdKey, MT/mergeTree.ts:591
 const STATUS = {
     0x01: "ASSERT_SEQ", 0x02: "ASSERT_MSN", 0x04: "INSERT_FAILED", 0x08: "UNSUPPORTED",
     0x10: "OOM_ROWS", 0x20: "OOM_BLOCKS", 0x40: "OOM_TEXT", 0x80: "OOM_PROPS",
@@ -106,13 +108,24 @@ class PropTable {
     }
 }
 
+/** Per-document interning: long client ids (getOrAddShortClientId order, client.ts:658-682)
+ * and marker ids -> the document's idToSegment table on the device (mergeTree.ts:1095). */
 class ClientNames {
-    constructor() { this.ids = new Map(); this.names = []; }
+    constructor() { this.ids = new Map(); this.names = []; this.markerIds = new Map(); }
     index(longId) {
         let i = this.ids.get(longId);
         if (i === undefined) { i = this.names.length; this.ids.set(longId, i); this.names.push(longId); }
         return i;
     }
+    /** A marker carrying this id joins the document; null for a non-string or reused id. */
+    markerDefine(id) {
+        if (typeof id !== "string" || this.markerIds.has(id)) return null;
+        const i = this.markerIds.size;
+        this.markerIds.set(id, i);
+        return i;
+    }
+    /** getMarkerFromId: the table index, -1 when never mapped. */
+    markerLookup(id) { return typeof id === "string" && this.markerIds.has(id) ? this.markerIds.get(id) : -1; }
 }
 
 const COLS = [["type", Uint8Array], ["flags", Uint8Array], ["client", Uint16Array], ["seq", Int32Array],
@@ -124,7 +137,17 @@ class BatchBuilder {
     constructor(props, names) {
         this.props = props; this.names = names;
         this.cols = {}; for (const [n] of COLS) this.cols[n] = [];
-        this.payload = []; this.docIds = []; this.offsets = [0];
+        this.payload = []; this.docIds = []; this.offsets = [0]; this.rel = [];
+    }
+    /** op.pos{k}, or op.relativePos{k} as an index into rel (getValidOpRange, client.ts:506-523). */
+    pos(op, k) {
+        const v = op["pos" + k];
+        if (v !== undefined) return [v, 0];
+        const rp = op["relativePos" + k];
+        if (!rp) return [undefined, 0];
+        const idx = rp.id ? this.names.markerLookup(rp.id) : -1;
+        this.rel.push([idx, rp.before ? 1 : 0, rp.offset !== undefined ? rp.offset : 0, 0]);
+        return [this.rel.length - 1, k === 1 ? F_REL1 : F_REL2];
     }
     beginDoc(docId) { this.docIds.push(docId); this.offsets.push(this.offsets[this.offsets.length - 1]); }
     emit(o) {
@@ -138,7 +161,9 @@ class BatchBuilder {
             const seg = op.seg;
             if (seg === undefined && op.register !== undefined) throw new Error("register-based insert (client.ts:425-440) is not on the batch path");
             if (!seg) { this.emit({ ...common, type: OP_NOOP, flags: fl }); return; }   // `if (op.seg)` falsy: no tree change
-            if (op.pos1 === undefined) throw new Error("relativePos1 inserts (mergeTree.ts:1949) are not on the batch path");
+            const [pos1, rf] = this.pos(op, 1);
+            if (pos1 === undefined) { this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return; }
+            fl |= rf;
             let text = null, props, pos2 = 0;
             if (typeof seg === "string") text = seg;
             else if (seg.text !== undefined) { text = seg.text; props = seg.props; }
@@ -149,18 +174,28 @@ class BatchBuilder {
                 if (typeof props !== "object") throw new Error("segment props must be an object");
                 pid = this.props.intern(props); fl |= F_SEG_PROPS;
             }
-            const off = this.payload.length;
+            let off = this.payload.length;
             if (text !== null) for (let i = 0; i < text.length; i++) this.payload.push(text.charCodeAt(i));
-            this.emit({ ...common, type: OP_INSERT, flags: fl, pos1: op.pos1, pos2, payloadOff: off,
+            if (text === null && pid >= 0 && props[MARKER_ID_KEY]) {           // Marker.getId
+                const m = this.names.markerDefine(props[MARKER_ID_KEY]);
+                if (m === null) { this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return; }
+                fl |= F_MARKER_ID; off = m;
+            }
+            this.emit({ ...common, type: OP_INSERT, flags: fl, pos1, pos2, payloadOff: off,
                 payloadLen: text !== null ? text.length : 0, propId: pid });
         } else if (op.type === OP_REMOVE || op.type === OP_ANNOTATE) {
-            if (op.pos1 === undefined || op.pos2 === undefined) throw new Error("relative positions are not on the batch path");
+            if (op.register !== undefined) throw new Error("cut into a register (client.ts:347-350) is not on the batch path");
+            const [pos1, f1] = this.pos(op, 1), [pos2, f2] = this.pos(op, 2);
+            if (pos1 === undefined || pos2 === undefined) { this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return; }
             let pid = -1;
             if (op.type === OP_ANNOTATE) {
                 if (op.combiningOp) fl |= op.combiningOp.name === "rewrite" ? F_REWRITE : F_COMBINE;
+                if (op.props && typeof op.props === "object" && MARKER_ID_KEY in op.props) {
+                    this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return;     // re-keyed marker ids
+                }
                 pid = this.props.intern(op.props);
             }
-            this.emit({ ...common, type: op.type, flags: fl, pos1: op.pos1, pos2: op.pos2, propId: pid });
+            this.emit({ ...common, type: op.type, flags: fl | f1 | f2, pos1, pos2, propId: pid });
         } else {
             this.emit({ ...common, type: OP_NOOP, flags: fl });
         }
@@ -183,7 +218,8 @@ class BatchBuilder {
     }
     build() {
         const b = { docIds: Uint32Array.from(this.docIds), opOffsets: Uint32Array.from(this.offsets),
-            payload: Uint16Array.from(this.payload.length ? this.payload : [0]) };
+            payload: Uint16Array.from(this.payload.length ? this.payload : [0]),
+            rel: Int32Array.from(this.rel.flat()) };
         for (const [n, T] of COLS) b[n] = T.from(this.cols[n]);
         return b;
     }
@@ -247,7 +283,7 @@ class LoadBuilder {
     }
     // SnapshotLoader.specToSegment (snapshotLoader.ts:93-124) over segmentFromSpec
     // (sequenceFactory.ts:31-37); null where the reference would fail.
-    record(spec, names) {
+    record(spec, names, header) {
         const merge = spec !== null && typeof spec === "object" && "json" in spec;
         const js = merge ? spec.json : spec;
         let flags = 0, text = null, refType = 0, props;
@@ -265,7 +301,15 @@ class LoadBuilder {
             if (typeof props !== "object") return null;
             pid = this.props.intern(props);
         }
-        const r = { flags, client: 0, seq: 0, rseq: 0, rclient: 0, pid, poff: 0, plen: refType };
+        let mid = 0;
+        // mapped: body markers (insertSegments), header markers not removed (addNodeReferences)
+        const mapped = !(merge && (spec.removedSeq !== undefined || spec.removedClient !== undefined)) || !header;
+        if ((flags & LS_MARKER) && props && props[MARKER_ID_KEY] && mapped) {          // Marker.getId
+            const m = names.markerDefine(props[MARKER_ID_KEY]);
+            if (m === null) return null;
+            mid = m + 1;
+        }
+        const r = { flags, client: 0, seq: 0, rseq: 0, rclient: 0, pid, poff: 0, plen: refType, mid };
         if (text !== null) {
             r.poff = this.payload.length; r.plen = text.length;
             for (let i = 0; i < text.length; i++) this.payload.push(text.charCodeAt(i));
@@ -284,8 +328,9 @@ class LoadBuilder {
     add(docId, snap, names) {
         const p0 = this.payload.length, recs = [];
         let ok = Number.isInteger(snap.seq) && Number.isInteger(snap.minSeq);
-        for (const spec of ok ? snap.header.concat(snap.body) : []) {
-            const r = this.record(spec, names);
+        const nh = snap.header.length;
+        for (const [i, spec] of (ok ? snap.header.concat(snap.body) : []).entries()) {
+            const r = this.record(spec, names, i < nh);
             if (r === null) { ok = false; break; }
             recs.push(r);
         }
@@ -302,7 +347,7 @@ class LoadBuilder {
             const o = 32 * i;
             dv.setUint8(o, r.flags); dv.setUint16(o + 2, r.client, true); dv.setInt32(o + 4, r.seq, true);
             dv.setInt32(o + 8, r.rseq, true); dv.setUint16(o + 12, r.rclient, true); dv.setInt16(o + 14, r.pid, true);
-            dv.setUint32(o + 16, r.poff, true); dv.setUint32(o + 20, r.plen, true);
+            dv.setUint32(o + 16, r.poff, true); dv.setUint32(o + 20, r.plen, true); dv.setUint32(o + 24, r.mid, true);
         });
         return { docIds: Uint32Array.from(this.docIds), segOffsets: Uint32Array.from(this.offsets),
             headerSegments: Uint32Array.from(this.nhdr), minSeq: Int32Array.from(this.minSeq),
@@ -311,7 +356,7 @@ class LoadBuilder {
     }
 }
 
-const DEFAULT_LIMITS = { rowsPerDoc: 8192, windowPerDoc: 4096, propsetsPerDoc: 8192, textPerDoc: 1 << 16 };
+const DEFAULT_LIMITS = { rowsPerDoc: 8192, windowPerDoc: 4096, propsetsPerDoc: 8192, textPerDoc: 1 << 16, markersPerDoc: 4096 };
 
 /** One engine context (one GPU) and the documents it holds. */
 class Engine {

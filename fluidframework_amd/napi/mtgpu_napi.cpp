@@ -130,6 +130,7 @@ napi_value Create(napi_env env, napi_callback_info info) {
     L.propsets_per_doc = u32_prop(env, argv[1], "propsetsPerDoc", 0);
     L.heap_per_doc = u32_prop(env, argv[1], "heapPerDoc", 0);
     L.window_per_doc = u32_prop(env, argv[1], "windowPerDoc", 0);
+    L.markers_per_doc = u32_prop(env, argv[1], "markersPerDoc", 0);
     mt_ctx* c = nullptr;
     int rc = mt_create(dev, &L, &c);
     if (rc) { napi_value r = throw_rc(env, c, rc, "mt_create"); if (c) mt_destroy(c); return r; }
@@ -256,6 +257,15 @@ napi_value ApplyBatch(napi_env env, napi_callback_info info) {
     for (int i = 0; i < 11; i++)
         if (n[i] < B.n_ops) { napi_throw_range_error(env, nullptr, "an op array is shorter than opOffsets[n]"); return nullptr; }
     B.payload_units = np;
+    {   // optional rel: Int32Array of (marker, before, offset, pad) quads (mt_rel_pos)
+        bool has = false;
+        napi_has_named_property(env, argv[1], "rel", &has);
+        if (has) {
+            const int32_t* rel = nullptr; size_t nr = 0;
+            if (!field(env, argv[1], "rel", napi_int32_array, &rel, &nr)) return nullptr;
+            B.n_rel = (uint32_t)(nr / 4); B.rel = (const mt_rel_pos*)rel;
+        }
+    }
     int rc = mt_apply_batch(c, &B);     // copies host arrays before returning
     return rc ? throw_rc(env, c, rc, "mt_apply_batch") : undefined(env);
 }

@@ -26,7 +26,8 @@ MT_LS_SEQ, MT_LS_CLIENT, MT_LS_REMOVED, MT_LS_MARKER = 0x01, 0x02, 0x04, 0x08
 
 LOAD_SEG_DTYPE = np.dtype([("flags", np.uint8), ("pad0", np.uint8), ("client", np.uint16), ("seq", np.int32),
                            ("removed_seq", np.int32), ("removed_client", np.uint16), ("prop_id", np.int16),
-                           ("payload_off", np.uint32), ("payload_len", np.uint32), ("pad1", np.uint32, (2,))])
+                           ("payload_off", np.uint32), ("payload_len", np.uint32), ("marker_id", np.uint32),
+                           ("pad1", np.uint32)])
 assert LOAD_SEG_DTYPE.itemsize == 32
 
 
@@ -103,7 +104,7 @@ def parse_snapshot(blobs: dict | list) -> ParsedSnapshot:
     return out
 
 
-def _seg_record(spec: Any, props: PropTable, names: ClientNames, payload: list) -> tuple | None:
+def _seg_record(spec: Any, props: PropTable, names: ClientNames, payload: list, header: bool = False) -> tuple | None:
     """SnapshotLoader.specToSegment (snapshotLoader.ts:93-124) over
     SharedStringFactory.segmentFromSpec (sequenceFactory.ts:31-37): the record
     fields, or None where the reference would fail."""
@@ -134,6 +135,16 @@ def _seg_record(spec: Any, props: PropTable, names: ClientNames, payload: list) 
         if not isinstance(p, dict):
             return None
         pid = props.intern(p)
+    mid = 0
+    # mapped ids: body markers (insertSegments, mergeTree.ts:2218-2222) and header markers not
+    # removed (reloadFromSegments -> addNodeReferences needs localNetLength > 0, :286-297)
+    removed = merge and (spec.get("removedSeq") is not None or spec.get("removedClient") is not None)
+    if flags & MT_LS_MARKER and isinstance(p, dict) and jsjson.js_truthy(p.get("markerId")) and \
+            not (header and removed):                                                    # Marker.getId
+        m = names.marker_define(p["markerId"])
+        if m is None:
+            return None                                   # duplicate or non-string id: off the batch path
+        mid = m + 1
     client, seq, rseq, rcl = 0, 0, 0, 0
     if merge:
         if "client" in spec and spec["client"] is not None:
@@ -153,7 +164,7 @@ def _seg_record(spec: Any, props: PropTable, names: ClientNames, payload: list) 
         for v in (seq, rseq):
             if not isinstance(v, int) or isinstance(v, bool):
                 return None
-    return (flags, 0, client, seq, rseq, rcl, pid, poff, plen, (0, 0))
+    return (flags, 0, client, seq, rseq, rcl, pid, poff, plen, mid, 0)
 
 
 @dataclass
@@ -189,8 +200,9 @@ class LoadBatchBuilder:
         """Adds one document; False if the host rejected it (it loads as MT_DS_UNSUPPORTED)."""
         p0, r0 = len(self.payload), len(self.recs)
         recs, ok = [], isinstance(snap.seq, int) and isinstance(snap.min_seq, int)
-        for spec in list(snap.header) + list(snap.body):
-            r = _seg_record(spec, self.props, names, self.payload) if ok else None
+        nh0 = len(snap.header)
+        for i, spec in enumerate(list(snap.header) + list(snap.body)):
+            r = _seg_record(spec, self.props, names, self.payload, header=i < nh0) if ok else None
             if r is None:
                 ok = False
                 break

@@ -81,6 +81,9 @@ extern "C" {
 #define MT_OP_ANNOTATE 2   /* MergeTreeDeltaType.ANNOTATE */
 #define MT_OP_NOOP     3   /* a sequenced message whose type !== "op" (or an empty
                               GROUP): only seq/msn advance (MT/client.ts:840)  */
+#define MT_OP_UNSUPPORTED 4 /* an op the host found off the batch path (e.g. a
+                              second marker with an id already in use): the
+                              document gets MT_DS_UNSUPPORTED                    */
 
 #define MT_OPF_END_OF_MSG 0x01u /* last member of one sequenced message: the
                                    engine runs updateSeqNumbers(msn, seq) after it.
@@ -90,6 +93,11 @@ extern "C" {
 #define MT_OPF_REWRITE    0x04u /* annotate with combiningOp {name:"rewrite"}      */
 #define MT_OPF_SEG_PROPS  0x08u /* insert seg has props (prop_id)                  */
 #define MT_OPF_COMBINE    0x10u /* annotate with another combiningOp: unsupported  */
+#define MT_OPF_REL1       0x20u /* pos1 is an index into rel[]: op.relativePos1
+                                   (posFromRelativePos, mergeTree.ts:1949-1972)    */
+#define MT_OPF_REL2       0x40u /* pos2 is an index into rel[]: op.relativePos2    */
+#define MT_OPF_MARKER_ID  0x80u /* marker insert whose props carry a markerId:
+                                   payload_off = the document's marker-id index   */
 
 /*
  * One batch = per-document runs of ops, concatenated by document.
@@ -97,6 +105,15 @@ extern "C" {
  * document slot doc_ids[d].  Text payloads are UTF-16 code units
  * (JS string semantics: lengths are .length of the JS string).
  */
+/* IRelativePosition (MT/ops.ts:46-61) with the marker id interned per document
+ * (marker = index, -1 for an id the document never mapped). */
+typedef struct mt_rel_pos {
+    int32_t marker;
+    int32_t before;               /* relativePos.before (truthy)                  */
+    int32_t offset;               /* relativePos.offset, 0 when undefined         */
+    int32_t pad;
+} mt_rel_pos;
+
 typedef struct mt_op_batch {
     uint32_t        n_runs;
     const uint32_t* doc_ids;      /* [n_runs]                                  */
@@ -115,6 +132,8 @@ typedef struct mt_op_batch {
     const int32_t*  prop_id;      /* [n_ops] index into the prop table, -1 none */
     const uint16_t* payload;      /* UTF-16 arena                               */
     uint64_t        payload_units;
+    uint32_t        n_rel;        /* relative positions referenced by REL1/REL2 */
+    const mt_rel_pos* rel;        /* [n_rel]                                    */
 } mt_op_batch;
 
 /* The packed 32-byte op record the device replays (one per op member), for
@@ -157,6 +176,7 @@ typedef struct mt_limits {
     uint32_t propsets_per_doc;  /* device property-set arena entries              */
     uint32_t heap_per_doc;      /* zamboni heap entries                           */
     uint32_t window_per_doc;    /* collab-window row list                         */
+    uint32_t markers_per_doc;   /* marker-id table (idToSegment); 0 = 1024        */
 } mt_limits;
 
 typedef struct mt_ctx mt_ctx;
@@ -180,7 +200,8 @@ typedef struct mt_load_seg {
     int16_t  prop_id;         /* mt_set_props set of spec.props, -1: none             */
     uint32_t payload_off;     /* text: UTF-16 offset into payload                      */
     uint32_t payload_len;     /* text: UTF-16 units; marker: refType                   */
-    uint32_t pad1[2];
+    uint32_t marker_id;       /* marker with a markerId prop: its per-document index + 1 */
+    uint32_t pad1;
 } mt_load_seg;
 /* Per document: segments [seg_offsets[i], seg_offsets[i+1]) in chunk order
  * (header chunk first, then body_0, body_1, ...), the first header_segments[i]

@@ -354,6 +354,7 @@ struct Tree {
     std::vector<LRU> heap;               // Heap<LRUSegment>, L[0] sentinel
     uint32_t status = 0;
     long long ovlHigh = 0;                 // overlap-list pushes by short ids >= 63 (test statistics)
+    std::map<u16s, Seg*> idToSegment;      // MT/mergeTree.ts:1095, mapIdToSegment :1175
 
     Tree() { root = makeBlock(0); heap.push_back({nullptr, -2}); }
     Block* makeBlock(int n) { blocks.emplace_back(new Block()); blocks.back()->childCount = n; return blocks.back().get(); }
@@ -364,9 +365,52 @@ struct Tree {
     /* ---- lengths ---- */
     int localNetLength(Seg* s) { return s->hasRemoved ? 0 : s->cachedLength; }           // :1151
     int nodeTotalLength(Node* n) { return n->leaf ? localNetLength((Seg*)n) : n->cachedLength; }
+    // Marker.getId (MT/mergeTree.ts:687-692): properties.markerId when truthy (string ids only here).
+    static const u16s* markerId(const Seg* s) {
+        if (!s->marker || !s->hasProps) return nullptr;
+        int i = obj_find(s->props, u"markerId");
+        if (i < 0 || s->props.ovals[i].t != JVal::Str || s->props.ovals[i].s.empty()) return nullptr;
+        return &s->props.ovals[i].s;
+    }
     void blockUpdate(Block* b) {                                                            // :2770
         int len = 0; for (int i = 0; i < b->childCount; i++) len += nodeTotalLength(b->children[i]);
         b->cachedLength = len;
+        for (int i = 0; i < b->childCount; i++) {                                           // addNodeReferences :286-297
+            Node* c = b->children[i];
+            if (!c->leaf || localNetLength((Seg*)c) <= 0) continue;
+            if (const u16s* id = markerId((Seg*)c)) idToSegment[*id] = (Seg*)c;
+        }
+    }
+    int getPosition(Node* node, int refSeq, int clientId) {                                 // :1578-1596
+        int total = 0; Block* parent = node->parent; Node* prev = node;
+        while (parent) {
+            for (int i = 0; i < parent->childCount; i++) {
+                Node* c = parent->children[i];
+                if (c == prev) break;
+                total += nodeLength(c, refSeq, clientId);
+            }
+            prev = parent; parent = parent->parent;
+        }
+        return total;
+    }
+    int posFromRelativePos(const JVal& rp, int refSeq, int clientId) {                      // :1949-1972
+        int pos = -1;
+        const JVal* id = nullptr;
+        for (int i = 0; i < (int)rp.okeys.size(); i++) if (rp.okeys[i] == u"id") id = &rp.ovals[i];
+        if (!id || id->t != JVal::Str || id->s.empty()) return pos;
+        auto it = idToSegment.find(id->s);
+        if (it == idToSegment.end()) return pos;
+        Seg* m = it->second;
+        pos = getPosition(m, refSeq, clientId);
+        const JVal* before = nullptr; const JVal* off = nullptr;
+        for (int i = 0; i < (int)rp.okeys.size(); i++) {
+            if (rp.okeys[i] == u"before") before = &rp.ovals[i];
+            if (rp.okeys[i] == u"offset") off = &rp.ovals[i];
+        }
+        const bool bf = before && truthy(before);
+        const int o = (off && off->t == JVal::Num) ? (int)off->n : 0;
+        if (!bf) pos += m->cachedLength + o; else pos -= o;
+        return pos;
     }
     int partialLength(Block* b, int refSeq, int clientId) {                                 // partialLengths.ts:466-496
         PSLs& P = *b->pl;
@@ -681,6 +725,7 @@ struct Tree {
         for (Seg* seg : in) {
             if (seg->cachedLength > 0) {
                 seg->seq = seq; seg->clientId = clientId;
+                if (const u16s* id = markerId(seg)) idToSegment[*id] = seg;                      // :2218-2222
                 if (seg->parent) {
                     if (insertPos <= getLength(refSeq, clientId)) { status |= MT_DS_UNSUPPORTED; return; }
                 } else {
@@ -717,6 +762,7 @@ struct Tree {
         ensureIntervalBoundary(pos, refSeq, clientId);
         if (seg->cachedLength > 0) {
             seg->seq = seq; seg->clientId = clientId;
+            if (const u16s* id = markerId(seg)) idToSegment[*id] = seg;                          // :2218-2222
             Block* sn = insertingWalk(root, pos, refSeq, clientId, seq, LEAF_INSERT, seg);
             if (!seg->parent) { status |= MT_DS_INSERT_FAILED; return; }
             updateRoot(sn);
@@ -1320,18 +1366,27 @@ static void apply_remote_json(Doc& d, const JVal& op, int cl, int ref, int seq, 
     Tree& t = d.t;
     int type;
     if (op.t != JVal::Obj || !jnum(op, u"type", type)) return;                                  // default: ignored
+    // getValidOpRange (MT/client.ts:506-523): pos, else posFromRelativePos when relativePos is set
+    auto opPos = [&](const char16_t* pk, const char16_t* rk, int& out) -> bool {
+        if (jnum(op, pk, out)) return true;
+        const JVal* rp = jget(op, rk);
+        if (!rp || !truthy(rp) || rp->t != JVal::Obj) return false;
+        out = t.posFromRelativePos(*rp, ref, cl);
+        if (out < 0) { t.status |= MT_DS_UNSUPPORTED; return false; }     // unknown marker id: off the path
+        return true;
+    };
     if (type == MT_OP_INSERT) {                                                                   // applyInsertOp :412-462
         int pos1;
         const JVal* seg = jget(op, u"seg");
-        if (!jnum(op, u"pos1", pos1)) { if (jget(op, u"relativePos1")) t.status |= MT_DS_UNSUPPORTED; return; }
         if (!seg || !truthy(seg)) { if (jget(op, u"register")) t.status |= MT_DS_UNSUPPORTED; return; }
+        if (!opPos(u"pos1", u"relativePos1", pos1)) { t.status |= MT_DS_UNSUPPORTED; return; }
         Seg* s = segFromSpec(d, *seg);
         if (!s) { t.status |= MT_DS_UNSUPPORTED; return; }
         t.insertSegment(pos1, s, ref, cl, seq);
         complete_op(t, seq, msn);
     } else if (type == MT_OP_REMOVE || type == MT_OP_ANNOTATE) {                                   // :339-405
         int p1, p2;
-        if (!jnum(op, u"pos1", p1) || !jnum(op, u"pos2", p2)) { t.status |= MT_DS_UNSUPPORTED; return; }
+        if (!opPos(u"pos1", u"relativePos1", p1) || !opPos(u"pos2", u"relativePos2", p2)) { t.status |= MT_DS_UNSUPPORTED; return; }
         if (type == MT_OP_REMOVE) {
             if (jget(op, u"register")) { t.status |= MT_DS_UNSUPPORTED; return; }                 // cut -> copy (:347-350)
             t.markRangeRemoved(p1, p2, ref, cl, seq);
@@ -1372,6 +1427,14 @@ uint32_t ora_apply_msg_json(ora_doc* o, const char* json) {
     if (msn > seq) t.status |= MT_DS_ASSERT_MSN;
     t.setMinSeq(msn);
     return t.status;
+}
+// posFromRelativePos (MT/mergeTree.ts:1949-1972) of an IRelativePosition given as JSON,
+// under the perspective of the client with this long id; -1: unknown marker id.
+int32_t ora_rel_pos_json(ora_doc* o, int32_t ref, const char* client_literal, const char* relpos_json) {
+    auto it = o->d.nameToShort.find(jquote(parse_key(client_literal)));
+    JVal rp = json_parse(relpos_json);
+    if (rp.t != JVal::Obj) return -1;
+    return o->d.t.posFromRelativePos(rp, ref, it != o->d.nameToShort.end() ? it->second : -999999);
 }
 // getLength(refSeq, clientId) of the client with this long id (a JSON string literal);
 // an id not registered yet owns no segment, so any unused short id gives its view.

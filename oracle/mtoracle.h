@@ -32,6 +32,9 @@ uint32_t ora_apply_msg_json(ora_doc* d, const char* json);
 /* getLength(refSeq, client) for the client with long id `client_literal` (a JSON
  * string literal, e.g. "\"alice\""). */
 int32_t  ora_get_length_json(ora_doc* d, int32_t ref_seq, const char* client_literal);
+/* posFromRelativePos of an IRelativePosition (JSON) under that client's perspective;
+ * -1 when no marker carries the id. */
+int32_t  ora_rel_pos_json(ora_doc* d, int32_t ref_seq, const char* client_literal, const char* relpos_json);
 /* Local (non-collaborating) ops, as SharedString.insertText/insertMarker/
  * annotateRange/removeText on a detached string (seq = UniversalSequenceNumber). */
 int      ora_local_insert(ora_doc* d, int32_t pos, const uint16_t* text, uint32_t n,

@@ -19,7 +19,9 @@ synthetic device generator does not:
   objects and arrays (matchProperties recursion, MT/properties.ts:64-95), and
   rewrite-to-empty annotates ({"name":"rewrite"} with {} or all-null props);
 * client churn: authors leave and new long ids join (non-ASCII ones included), so a
-  document sees many more distinct clients than are active at once.
+  document sees many more distinct clients than are active at once;
+* markers carrying a markerId and ops positioned relative to them (relativePos1,
+  posFromRelativePos MT/mergeTree.ts:1949-1972).
 
 MSN follows deli (deli/lambda.ts:348-371): the minimum over connected clients' latest
 refSeq; refSeq >= MSN at send time.
@@ -41,13 +43,15 @@ class StreamGen:
     def __init__(self, seed: int, clients: int = 4, lag: int = 12, churn: float = 0.0, p_nonop: float = 0.06,
                  p_group: float = 0.15, p_marker: float = 0.08, p_annotate: float = 0.2, p_remove: float = 0.3,
                  p_special: float = 0.25, long_every: int = 40, max_ins: int = 9, id_prefix: str = "cli",
-                 max_total_clients: int | None = None):
+                 max_total_clients: int | None = None, p_marker_id: float = 0.0, p_relative: float = 0.0):
         self.rng = random.Random(seed)
         self.lag, self.churn, self.p_nonop, self.p_group = lag, churn, p_nonop, p_group
         self.p_marker, self.p_annotate, self.p_remove, self.p_special = p_marker, p_annotate, p_remove, p_special
         self.long_every, self.max_ins = long_every, max_ins
         self.id_prefix = id_prefix
         self.max_total = max_total_clients
+        self.p_marker_id, self.p_relative = p_marker_id, p_relative
+        self.marker_ids: list[str] = []           # ids of markers inserted so far (idToSegment)
         self.total = 0
         self.active: dict[str, int] = {}          # long id -> latest refSeq
         for _ in range(clients):
@@ -88,6 +92,10 @@ class StreamGen:
             seg = {"marker": {"refType": r.choice([0, 1, 2, 4, 0x40])}}
             if r.random() < 0.7:
                 seg["props"] = self._props(allow_null=False)
+            if r.random() < self.p_marker_id:            # paragraph-marker style ids (Marker.getId)
+                mid = f"m{len(self.marker_ids) + len(self.pending_ids)}-ü"
+                seg["props"] = {**seg.get("props", {}), "markerId": mid}
+                self.pending_ids.append(mid)
             return {"type": 0, "pos1": pos, "seg": seg}, 1
         n = r.randint(257, 300) if (self.long_every and k % self.long_every == self.long_every - 1) else \
             r.randint(1, self.max_ins)
@@ -127,8 +135,33 @@ class StreamGen:
     def _member(self, L: int, k: int) -> tuple[dict, int]:
         x = self.rng.random()
         if L == 0 or x >= self.p_remove + self.p_annotate:
-            return self._insert(L, k)
-        return self._range(L, 1 if x < self.p_remove else 2)
+            op, dl = self._insert(L, k)
+        else:
+            op, dl = self._range(L, 1 if x < self.p_remove else 2)
+        if self.marker_ids and self._first_member and self.rng.random() < self.p_relative:
+            op, dl = self._relative(op, dl, L)
+        return op, dl
+
+    def _relative(self, op: dict, dl: int, L: int) -> tuple[dict, int]:
+        """Re-express the op's start relative to a marker id (IRelativePosition,
+        MT/ops.ts:46-61) when posFromRelativePos (computed by the oracle under the
+        author's perspective) gives a valid start; first member of a message only (later
+        GROUP members see the earlier members' edits)."""
+        r = self.rng
+        rp = {"id": r.choice(self.marker_ids)}
+        if r.random() < 0.5:
+            rp["before"] = True
+        if r.random() < 0.5:
+            rp["offset"] = r.randint(0, 3)
+        p = self.obs.rel_pos_of(self._ref, self._author, rp)
+        rest = {k: v for k, v in op.items() if k not in ("type", "pos1")}
+        if op["type"] == 0:
+            if 0 <= p <= L:
+                return {"type": 0, "relativePos1": rp, **rest}, dl
+            return op, dl
+        if 0 <= p < op["pos2"]:
+            return {"type": op["type"], "relativePos1": rp, **rest}, (-(op["pos2"] - p) if op["type"] == 1 else 0)
+        return op, dl
 
     # -- one sequenced message ----------------------------------------------------
     def step(self) -> dict:
@@ -144,13 +177,15 @@ class StreamGen:
         msn = min(self.active.values())
         seq = self.cur + 1
         msg = dict(clientId=a, sequenceNumber=seq, referenceSequenceNumber=ref, minimumSequenceNumber=msn)
+        self._author, self._ref, self.pending_ids = a, ref, []
         if r.random() < self.p_nonop:
             msg["type"] = r.choice(["noop", "summarize", "propose"])
             msg["contents"] = None
         else:
             L = self.obs.get_length_of(ref, a)
             members = []
-            for _ in range(r.randint(2, 4) if r.random() < self.p_group else 1):
+            for i in range(r.randint(2, 4) if r.random() < self.p_group else 1):
+                self._first_member = i == 0
                 op, dl = self._member(L, k)
                 members.append(op)
                 L += dl
@@ -160,6 +195,7 @@ class StreamGen:
         if st:
             raise RuntimeError(f"oracle status {st:#x} at message {k}: {msg}")
         self.cur, self.msn = seq, msn
+        self.marker_ids.extend(self.pending_ids)          # mapped once the insert applied
         self.msgs.append(msg)
         return msg
 

@@ -48,6 +48,8 @@ def lib():
         L.ora_load_snapshot.argtypes = [P, U32, P]
         L.ora_apply_msg_json.restype = U32
         L.ora_apply_msg_json.argtypes = [P, ctypes.c_char_p]
+        L.ora_rel_pos_json.restype = I32
+        L.ora_rel_pos_json.argtypes = [P, I32, ctypes.c_char_p, ctypes.c_char_p]
         L.ora_get_length_json.restype = I32
         L.ora_get_length_json.argtypes = [P, I32, ctypes.c_char_p]
         L.ora_get_length.restype = I32
@@ -121,6 +123,13 @@ class OracleDoc:
         """getLength(refSeq, shortId(client_id)) under the oracle's own registration."""
         from fluidframework_amd.jsjson import quote
         return int(self.L.ora_get_length_json(self.h, ref_seq, quote(client_id).encode("utf-8", "surrogatepass")))
+
+    def rel_pos_of(self, ref_seq: int, client_id: str, relpos: dict) -> int:
+        """posFromRelativePos under (ref_seq, client_id)'s perspective; -1: unknown id."""
+        import json
+        from fluidframework_amd.jsjson import quote
+        return int(self.L.ora_rel_pos_json(self.h, ref_seq, quote(client_id).encode("utf-8", "surrogatepass"),
+                                           json.dumps(relpos, ensure_ascii=True).encode()))
 
     def apply_run(self, batch: OpBatch, run: int) -> int:
         return int(self.L.ora_apply_run(self.h, ctypes.byref(batch.to_c()), run))

@@ -26,6 +26,8 @@ SURFACES = {
     "markers_props": dict(clients=5, lag=20, p_marker=0.3, p_annotate=0.35),
     "unicode": dict(clients=2, lag=4, p_special=0.8, p_remove=0.4),
     "churn": dict(clients=4, lag=10, churn=0.05, max_total_clients=60),
+    # markers with ids and ops positioned relative to them (MT/mergeTree.ts:1949-1972)
+    "relative": dict(clients=4, lag=16, p_marker=0.25, p_marker_id=0.7, p_relative=0.35, p_group=0.1),
     # > 300 distinct long ids over the document's life, overlapping removes by short ids >= 63
     # (removedClientOverlap beyond the 63-bit mask: the per-document side list)
     "churn300": dict(clients=6, lag=24, churn=0.42, p_remove=0.5, p_annotate=0.1, p_group=0.05, p_nonop=0.02,
@@ -79,6 +81,10 @@ def test_stream_generator_covers_the_surface():
     assert "😀" in texts or "𝄞" in texts
     msgs, _ = stream(8, 1500, **SURFACES["churn"])
     assert len({m["clientId"] for m in msgs}) > 30
+    msgs, _ = stream(9, 1200, **SURFACES["relative"])
+    rel = [x for m in msgs if m["type"] == "op" for x in (m["contents"]["ops"] if m["contents"]["type"] == 3
+                                                           else [m["contents"]]) if "relativePos1" in x]
+    assert len(rel) > 100 and {x["type"] for x in rel} == {0, 1, 2}
     msgs, obs = stream(101, 1200, **SURFACES["churn300"])
     assert len({m["clientId"] for m in msgs}) > 300
     assert obs.stats()[1] > 20          # overlapping removes by clients past the bitmask
@@ -107,7 +113,7 @@ def check_node(addon, surface, seed=3, n_docs=3, n_msgs=800):
         assert int(got["digests"][d], 16) == dig
 
 
-@pytest.mark.parametrize("surface", ["groups", "unicode", "churn"])
+@pytest.mark.parametrize("surface", ["groups", "unicode", "churn", "relative"])
 def test_message_surface_node_host_on_emulation(surface):
     from js_lib import NODE
     from emu_lib import build_emu_napi
@@ -117,7 +123,7 @@ def test_message_surface_node_host_on_emulation(surface):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("surface", ["groups", "markers_props", "unicode", "churn"])
+@pytest.mark.parametrize("surface", ["groups", "markers_props", "unicode", "churn", "relative"])
 def test_message_surface_node_host_on_gpu(surface):
     from js_lib import NODE, ROOT
     if NODE is None:
