@@ -149,7 +149,8 @@ void MT_FN(destroy)(mt_ctx* c) {
                   S.ovx, S.mid, c->ck_rows, c->ck_blk, c->ck_heap, c->ck_win, c->ck_text, c->ck_pset, c->ck_hdr, c->ck_hold,
                   c->ck_ovx, c->ck_mid};
     for (void* p : ps) if (p) mtb_free(p);
-    mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_rel, &c->b_pset_off,
+    mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_rel, &c->b_drec,
+                            &c->b_dcount, &c->b_pset_off,
                             &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3,
                             &c->b_ld_meta, &c->b_ld_seg, &c->b_ld_pay, &c->b_ld_plan, &c->b_ld_poff};
     for (auto* b : bs) if (b->p) mtb_free(b->p);
@@ -255,6 +256,12 @@ int MT_FN(replay_resident)(mt_ctx* c) {
     if (!c || !c->ops.op_off) return MT_E_INVALID;
     int rc = mtb_ensure(c, c->b_cursor, 4ull * c->n_runs + 4);
     if (rc) return rc;
+    if (c->delta_cap) {                                     // records of this batch only
+        const unsigned long long zero = 0;
+        mtb_h2d(c, c->b_dcount.p, &zero, 8);
+        c->ops.drec = (MtDeltaRec*)c->b_drec.p; c->ops.dcount = (unsigned long long*)c->b_dcount.p; c->ops.dcap = c->delta_cap;
+    } else { c->ops.drec = nullptr; c->ops.dcount = nullptr; c->ops.dcap = 0; }
+    c->delta_valid = false;
     MtGen g{}; g.enabled = 0;
     return mtb_launch_replay(c, g, c->n_runs);
 }
@@ -358,6 +365,52 @@ int MT_FN(load_snapshot)(mt_ctx* c, const mt_load_batch* B) {
     L.segs = (const MtLoadSeg*)c->b_ld_seg.p; L.payload = (const uint16_t*)c->b_ld_pay.p;
     L.plan_off = (const uint32_t*)c->b_ld_poff.p; L.plan = (const MtLoadStep*)c->b_ld_plan.p;
     return mtb_launch_load(c, L, n);
+}
+int MT_FN(delta_capture)(mt_ctx* c, uint64_t capacity) {
+    if (!c) return MT_E_INVALID;
+    c->delta_cap = 0;
+    if (capacity) {
+        int rc;
+        if ((rc = mtb_ensure(c, c->b_drec, sizeof(MtDeltaRec) * capacity))) return rc;
+        if ((rc = mtb_ensure(c, c->b_dcount, 16))) return rc;
+    }
+    c->delta_cap = capacity;
+    return MT_OK;
+}
+int MT_FN(delta_records)(mt_ctx* c, const mt_delta_rec** out, uint64_t* n) {
+    static_assert(sizeof(mt_delta_rec) == sizeof(MtDeltaRec), "delta record layout");
+    if (!c || !out || !n || !c->delta_cap) return MT_E_INVALID;
+    int rc = mtb_sync(c);
+    if (rc) return rc;
+    if (!c->delta_valid) {
+        unsigned long long cnt = 0;
+        mtb_d2h(c, &cnt, c->b_dcount.p, 8);
+        c->delta_over = cnt > c->delta_cap;
+        if (cnt > c->delta_cap) cnt = c->delta_cap;
+        c->delta_host.resize(cnt);
+        if (cnt) mtb_d2h(c, c->delta_host.data(), c->b_drec.p, sizeof(MtDeltaRec) * cnt);
+        // documents interleave in the buffer; one wave appends a document's records in
+        // program order, so a stable sort by op index restores callback order
+        std::stable_sort(c->delta_host.begin(), c->delta_host.end(),
+                         [](const MtDeltaRec& x, const MtDeltaRec& y) { return x.op < y.op; });
+        c->delta_valid = true;
+    }
+    *out = (const mt_delta_rec*)c->delta_host.data();
+    *n = c->delta_host.size();
+    if (c->delta_over) { c->err = "delta capture capacity exceeded"; return MT_E_OOM; }
+    return MT_OK;
+}
+int MT_FN(doc_pset)(mt_ctx* c, uint32_t doc, int32_t id, uint16_t* keys, int32_t* vals, uint32_t* n) {
+    if (!c || doc >= c->S.maxDocs || !keys || !vals || !n || id < 0) return MT_E_INVALID;
+    int rc = mtb_sync(c);
+    if (rc) return rc;
+    const MtDocLayout& y = c->layout_h[doc];
+    if ((uint32_t)id >= y.psetCap) return MT_E_INVALID;
+    MtPSet p;
+    mtb_d2h(c, &p, c->S.pset + y.pset + (size_t)id, sizeof(MtPSet));
+    *n = p.n < 0 ? 0u : (uint32_t)p.n;
+    for (uint32_t i = 0; i < *n && i < MT_PSK; i++) { keys[i] = p.key[i]; vals[i] = p.val[i]; }
+    return MT_OK;
 }
 int MT_FN(set_residency)(mt_ctx* c, int use_lds, int rows, int blocks, int heap) {
     if (!c || use_lds < 0 || use_lds > 2 || rows < 0 || blocks < 0 || heap < 0 || rows > MT_L_ROWS ||
@@ -660,7 +713,7 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs; o.payload_units = PU;
-    o.rel = nullptr; o.n_rel = 0;
+    o.rel = nullptr; o.n_rel = 0; o.drec = nullptr; o.dcount = nullptr; o.dcap = 0;
     c->n_runs = P->n_docs;
     c->gen_off.assign(off.begin(), off.end());
     if (!P->continue_docs) {

@@ -199,11 +199,16 @@ struct __attribute__((aligned(16))) MtOpRec {  // one 32-byte op record (mt_op_b
     uint16_t payload_len; int16_t prop_id;
 };
 struct MtRelPos { int marker, before, offset, pad; };   // mt_rel_pos
+// One delta / maintenance callback entry (mt_delta_rec): kind, the observer-view position
+// of the segment when the callback fires, its cachedLength, its row and two
+// kind-specific fields (see include/mtgpu.h).
+struct __attribute__((aligned(16))) MtDeltaRec { uint32_t op; int kind, pos, len, seg, a, b, pad; };
 struct MtOps {                                // device copy of an mt_op_batch
     const uint32_t* doc_ids; const uint32_t* op_off;
     MtOpRec* rec;
     uint16_t* payload;
     const MtRelPos* rel; uint32_t n_rel;
+    MtDeltaRec* drec; unsigned long long* dcount; unsigned long long dcap;   // delta capture (null: off)
     uint32_t n_runs;
     uint64_t payload_units;                   // records are bounds-checked against it on the device
 };
@@ -267,11 +272,9 @@ struct __attribute__((aligned(16))) MtLdsBlk {
 // per-wave scratch (LDS on the device)
 struct MtScratch {
     int pathB[MT_MAXH + 2], pathJ[MT_MAXH + 2];
-    int fB[MT_MAXH + 2], fJ[MT_MAXH + 2], fS[MT_MAXH + 2], fE[MT_MAXH + 2], fL[MT_MAXH + 2], fD[MT_MAXH + 2];
     int hold[64];
     int holdLen[64];                  // observer length of each held child (scourLeaves)
     int pk[MT_PSK], pv[MT_PSK];
-    int lastOld, lastNew;
     int rfree[MT_RFL];                // recycled rows (unlinked, out of the window, no heap entry)
     int corr[MT_MAXN];                // per-child perspective corrections (childLens)
 };
@@ -349,6 +352,7 @@ template <int RES> struct MtEngT {
     MtBlk* blk; MtHeapE* heap; uint16_t* text; MtPSet* pset;
     MtOvx* ovx; int ovxN;
     int* midt; int midCap;                    // idToSegment (MT/mergeTree.ts:1095, :1175)
+    MtDeltaRec* drec; unsigned long long* dcount; unsigned long long dcap; uint32_t curOp;   // delta capture
     MtScratch* sc;
     // pool accessors: LDS (MT_RES_LDS, MT_RES_BLK for blocks + heap) or HBM homes
     MT_HD MtRow& row(int s) const { if constexpr (LDS) return mt_lds().rows[s]; else return R[s]; }
@@ -419,6 +423,7 @@ template <int RES> struct MtEngT {
         pset = st.pset + off(&Ly->pset);
         ovx = st.ovx + (size_t)d * MT_OVX_CAP;
         midt = st.mid + off(&Ly->mid); midCap = (int)uni(Ly->midCap);
+        drec = nullptr; dcount = nullptr; dcap = 0; curOp = 0;
         sc = scratch;
         const MtDocHdr& h = *hdrp;
         root = uni(h.root); height = uni(h.height); minSeq = uni(h.minSeq); curSeq = uni(h.curSeq); rowTop = uni(h.rowTop);
@@ -597,6 +602,26 @@ template <int RES> struct MtEngT {
         if (winN > winHW) winHW = winN;
         row(s).meta = mt | MT_M_INWIN;
     }
+    // winAdd for the rows of lanes [0, n) where sel: one meta load for all, the rows not yet
+    // in the window appended in lane order (one round trip instead of one per row).
+    MT_HD void winAddLanes(const LaneArr<int>& ids, const LaneArr<bool>& sel, int n) {
+        auto add = wave_map(n, [&](int j) MT_LAM {
+            return own(sel, j) && !(row(own(ids, j)).meta & MT_M_INWIN);
+        });
+        const int cnt = wave_count(add);
+        if (!cnt) return;
+        if (winN + cnt > (int)S.winCap) { status |= MT_DS_OOM_WINDOW; return; }
+        const auto rk = wave_rank(add);
+        const int w0 = winN;
+        wave_for(n, [&](int j) MT_LAM {
+            if (!own(add, j)) return;
+            const int s = own(ids, j);
+            wn(w0 + own(rk, j)) = s;
+            row(s).meta = row(s).meta | MT_M_INWIN;
+        });
+        winN += cnt;
+        if (winN > winHW) winHW = winN;
+    }
     // Scalar fields of a block (SGPRs) and its children (one per lane).
     MT_HD BlkH head(int B) const {
         BlkH h;
@@ -741,6 +766,38 @@ template <int RES> struct MtEngT {
         const int off = uni(q.offset);
         if (!uni(q.before)) pos += 1 + off; else pos -= off;
         return pos;
+    }
+    /* ------------------------------------------- delta / maintenance records -- */
+    // Appends one record at the batch's global cursor (documents interleave; every record
+    // carries its op index, and one wave appends a document's records in program order).
+    MT_HD void emitDelta(int kind, int pos, int len, int seg, int a, int b) {
+        const unsigned long long idx = wave_atomic_next(dcount);
+        if (idx >= dcap) return;
+        MtDeltaRec q; q.op = curOp; q.kind = kind; q.pos = pos; q.len = len; q.seg = seg; q.a = a; q.b = b; q.pad = 0;
+        const MtDeltaRec* qp = &q;
+        wave_for(8, [&](int k) MT_LAM { ((int*)&drec[idx])[k] = ((const int*)qp)[k]; });
+    }
+    // Observer-view position of row s (MergeTree.getPosition for the local client, whose
+    // view is every sequenced op: removed rows count 0); 0 when unlinked.
+    MT_HD int obsPosition(int s) {
+        int B = uni(row(s).parent);
+        if (B < 0) return 0;
+        int node = s, pos = 0;
+        bool leaf = true;
+        for (;;) {
+            BlkH h;
+            auto ch = blkLoad(B, h);
+            const bool lf = leaf;
+            auto ol = wave_map(h.n, [&](int j) MT_LAM {
+                const int g = own(ch, j);
+                return lf ? ((row(g).meta & MT_M_REMOVED) ? 0 : row(g).len) : bk(g).len;
+            });
+            const int nd = node;
+            const int j = wave_first(wave_map(h.n, [&](int i) MT_LAM { return own(ch, i) == nd; }));
+            pos += wave_sum8(wave_map(h.n, [&](int i) MT_LAM { return i < j ? own(ol, i) : 0; }));
+            if (h.parent < 0) return pos;
+            node = B; B = h.parent; leaf = false;
+        }
     }
     // Perspective lengths of block B's children (nodeLength, MT/mergeTree.ts:1652-1692).
     MT_HD LaneArr<ChildL> childLens(int B, const BlkH& h, const LaneArr<int>& ch, int r, int c) {
@@ -933,6 +990,12 @@ template <int RES> struct MtEngT {
                         const int n = splitRow(s, pj);
                         if (n < 0) return MT_W_FAIL;
                         insertAtPath(L, j + 1, n, 0);
+                        if (drec) {                            // SPLIT, splitLeafSegment (mergeTree.ts:2243-2258)
+                            const int ps = obsPosition(s);
+                            const bool rm = (uni(row(s).meta) & MT_M_REMOVED) != 0;
+                            emitDelta(MT_DK_SPLIT, ps, pj, s, n, uni(row(n).len));
+                            (void)rm;
+                        }
                         lastIdx = j + 1;                      // an insert at pos lands before the new right half
                         // A row split keeps every row under the same ancestors unless a
                         // block split moved some: U's per-ancestor delta sums stay exact
@@ -1263,6 +1326,19 @@ template <int RES> struct MtEngT {
                 mergeRun(f, ft, fc, fl, i0 - 1, i0, i1);
             }
         }
+        if (drec) {        // maintenance callbacks in child order: UNLINK (:1299-1305), APPEND (:1325-1331)
+            const uint64_t unl = wave_ballot(wave_map(span, [&](int t) MT_LAM { return own(cls, t) == 1; }));
+            int head = -1, acc = 0;
+            for (uint64_t b = unl | merged | (merged >> 1); b; b &= b - 1) {
+                const int k = __builtin_ctzll(b);
+                if ((unl >> k) & 1ull) { const int g = wave_at(f, k); emitDelta(MT_DK_UNLINK, obsPosition(g), wave_at(fl, k), g, -1, -1); }
+                else if ((merged >> k) & 1ull) {                   // prevSegment's length after this append
+                    const int hg = wave_at(f, head), g = wave_at(f, k), lk = wave_at(fl, k);
+                    acc += lk;
+                    emitDelta(MT_DK_APPEND, obsPosition(hg), acc, hg, g, lk);
+                } else { head = k; acc = wave_at(fl, k); }
+            }
+        }
         // unlinked and appended rows leave the tree; rows no heap entry or window refers
         // to go back on the recycled-row stack (in lane order)
         auto gone = wave_map(span, [&](int t) MT_LAM { return own(cls, t) == 1 || ((merged >> t) & 1ull); });
@@ -1456,22 +1532,27 @@ template <int RES> struct MtEngT {
     // nodeMap over [start, end) under (r, c) with the remove / annotate leaf
     // action and post-order length maintenance (MT/mergeTree.ts:2626-2739,
     // :2584-2624, :2927-2994).  Child lengths are evaluated before the child is
-    // touched, as in the reference's in-order traversal.
+    // touched, as in the reference's in-order traversal.  The frame stack lives in
+    // lanes (lane L = level L: readlane/writelane, no LDS round trips): block, next
+    // child, start/end relative to the block, the child's length, the observer-length
+    // delta under the block and (delta capture) the block's observer-view position.
     MT_HD void rangeMap(int mode, int start, int end, int r, int c, int sq, int opset, bool rewrite) {
         if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
+        const bool rec = drec != nullptr;
+        LaneArr<int> fB{}, fJ{}, fS{}, fE{}, fL{}, fD{}, fO{};
+        fB = wave_set(fB, 0, root); fS = wave_set(fS, 0, start); fE = wave_set(fE, 0, end);
+        int lastOld = -2, lastNew = -1;
         int L = 0;
-        sc->fB[0] = root; sc->fJ[0] = 0; sc->fS[0] = start; sc->fE[0] = end; sc->fD[0] = 0;
-        sc->lastOld = -2; sc->lastNew = -1;
         while (L >= 0) {
-            const int B = uni(sc->fB[L]);
+            const int B = wave_at(fB, L);
             BlkH h;
             auto ch = blkLoad(B, h);
             auto cl = childLens(B, h, ch, r, c);
             auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
-            const int j0 = uni(sc->fJ[L]);
+            const int j0 = wave_at(fJ, L);
             auto lensFrom = wave_map(h.n, [&](int j) MT_LAM { return j >= j0 ? own(lens, j) : 0; });
             auto pre = wave_excl_scan8(lensFrom);
-            const int st = uni(sc->fS[L]), en = uni(sc->fE[L]);
+            const int st = wave_at(fS, L), en = wave_at(fE, L);
             auto cond = wave_map(h.n, [&](int j) MT_LAM {
                 const int lj = own(lens, j), pj = own(pre, j);
                 return j >= j0 && (en - pj) > 0 && lj > 0 && (st - pj) < lj;
@@ -1508,44 +1589,71 @@ template <int RES> struct MtEngT {
                                 ovxAdd(s, uni(row(s).rseq), c);
                             }
                         }
-                        for (int j = 0; j < h.n; j++) if (wave_at(cond, j)) winAdd(wave_at(ch, j));
+                        winAddLanes(ch, cond, h.n);
+                        if (rec) {                                     // removedSegments: newly removed only
+                            const int base = wave_at(fO, L);
+                            auto ol = wave_map(h.n, [&](int j) MT_LAM {
+                                const int g = own(ch, j); return (row(g).meta & MT_M_REMOVED) ? 0 : row(g).len;
+                            });
+                            auto opre = wave_excl_scan8(ol);
+                            for (uint64_t b = wave_ballot(wave_map(h.n, [&](int j) MT_LAM { return own(nd, j) > 0; })); b; b &= b - 1) {
+                                const int j = __builtin_ctzll(b);
+                                emitDelta(MT_DK_REMOVE, base + wave_at(opre, j), wave_at(nd, j), wave_at(ch, j), -1, -1);
+                            }
+                        }
                     } else {
+                        LaneArr<int> opre{};
+                        int base = 0;
+                        if (rec) {
+                            base = wave_at(fO, L);
+                            auto ol = wave_map(h.n, [&](int j) MT_LAM {
+                                const int g = own(ch, j); return (row(g).meta & MT_M_REMOVED) ? 0 : row(g).len;
+                            });
+                            opre = wave_excl_scan8(ol);
+                        }
                         for (int j = 0; j < h.n; j++) {
                             if (!wave_at(cond, j)) continue;
                             const int s = wave_at(ch, j);
                             const int old = uni(row(s).props);
                             int nw;
-                            if (old == uni(sc->lastOld)) nw = uni(sc->lastNew);
-                            else { nw = applyPropSet(old, opset, rewrite); sc->lastOld = old; sc->lastNew = nw; }
+                            if (old == lastOld) nw = lastNew;
+                            else { nw = applyPropSet(old, opset, rewrite); lastOld = old; lastNew = nw; }
                             row(s).props = nw;
+                            if (rec) emitDelta(MT_DK_ANNOTATE, base + wave_at(opre, j), uni(row(s).len), s, old, nw);
                         }
                     }
                     addToLRUSet(wave_at(ch, first), sq);
                 }
                 if (mode == MT_MAP_REMOVE) bk(B).len = h.len + obsDelta;
-                const int d = uni(sc->fD[L]) + obsDelta;
+                const int d = wave_at(fD, L) + obsDelta;
                 L--;
                 if (L >= 0) {
-                    sc->fD[L] = uni(sc->fD[L]) + d; sc->fS[L] = uni(sc->fS[L]) - uni(sc->fL[L]);
-                    sc->fE[L] = uni(sc->fE[L]) - uni(sc->fL[L]); sc->fJ[L] = uni(sc->fJ[L]) + 1;
+                    const int fl = wave_at(fL, L);
+                    fD = wave_set(fD, L, wave_at(fD, L) + d); fS = wave_set(fS, L, wave_at(fS, L) - fl);
+                    fE = wave_set(fE, L, wave_at(fE, L) - fl); fJ = wave_set(fJ, L, wave_at(fJ, L) + 1);
                 }
                 continue;
             }
             const int jj = wave_first(cond);
             if (jj >= 0) {
                 const int pj = wave_at(pre, jj);
-                sc->fS[L] = st - pj; sc->fE[L] = en - pj; sc->fJ[L] = jj; sc->fL[L] = wave_at(lens, jj);
+                fS = wave_set(fS, L, st - pj); fE = wave_set(fE, L, en - pj); fJ = wave_set(fJ, L, jj);
+                fL = wave_set(fL, L, wave_at(lens, jj));
+                int ob = 0;
+                if (rec) ob = wave_at(fO, L) + wave_sum8(wave_map(h.n, [&](int i) MT_LAM { return i < jj ? bk(own(ch, i)).len : 0; }));
                 const int child = wave_at(ch, jj);
                 L++;
-                sc->fB[L] = child; sc->fJ[L] = 0; sc->fS[L] = st - pj; sc->fE[L] = en - pj; sc->fD[L] = 0;
+                fB = wave_set(fB, L, child); fJ = wave_set(fJ, L, 0); fS = wave_set(fS, L, st - pj);
+                fE = wave_set(fE, L, en - pj); fD = wave_set(fD, L, 0); fO = wave_set(fO, L, ob);
                 continue;
             }
-            const int d = uni(sc->fD[L]);
+            const int d = wave_at(fD, L);
             if (d != 0) bk(B).len = h.len + d;
             L--;
             if (L >= 0) {
-                sc->fD[L] = uni(sc->fD[L]) + d; sc->fS[L] = uni(sc->fS[L]) - uni(sc->fL[L]);
-                sc->fE[L] = uni(sc->fE[L]) - uni(sc->fL[L]); sc->fJ[L] = uni(sc->fJ[L]) + 1;
+                const int fl = wave_at(fL, L);
+                fD = wave_set(fD, L, wave_at(fD, L) + d); fS = wave_set(fS, L, wave_at(fS, L) - fl);
+                fE = wave_set(fE, L, wave_at(fE, L) - fl); fJ = wave_set(fJ, L, wave_at(fJ, L) + 1);
             }
         }
         uValid = false;
@@ -1753,6 +1861,7 @@ template <int RES> struct MtEngT {
             c_rows += 2;
             winAdd(n);
             if (sq > minSeq) addToLRUSet(n, sq);
+            if (drec) emitDelta(MT_DK_INSERT, obsPosition(n), L, n, uni(row(n).props), -1);   // insertSegments callback
         }
         zamboni();
     }

@@ -23,7 +23,7 @@ struct mt_ctx {
     std::string err;
     // device op batch (resident)
     struct DevBuf { void* p = nullptr; size_t cap = 0; };
-    DevBuf b_stage, b_pack_docs, b_pack_sz, b_pack_off, b_gencl, b_cursor, b_doc, b_off, b_rec, b_pay, b_rel, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3,
+    DevBuf b_stage, b_pack_docs, b_pack_sz, b_pack_off, b_gencl, b_cursor, b_doc, b_off, b_rec, b_pay, b_rel, b_drec, b_dcount, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3,
            b_ld_meta, b_ld_seg, b_ld_pay, b_ld_plan, b_ld_poff;
     MtOps ops{};
     uint32_t n_runs = 0;
@@ -43,4 +43,8 @@ struct mt_ctx {
     std::vector<uint32_t> blob_first;
     std::vector<uint16_t> text_arena;
     std::vector<uint64_t> text_off;
+    // delta capture (mt_delta_capture / mt_delta_records)
+    uint64_t delta_cap = 0;
+    bool delta_valid = false, delta_over = false;
+    std::vector<MtDeltaRec> delta_host;
 };

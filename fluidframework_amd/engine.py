@@ -94,7 +94,15 @@ def _bind(lib, prefix: str):
         generated_copy_dev=f("generated_copy_dev", ctypes.c_int, [P, U32, U32, P, P]),
         upload_batch_dev=f("upload_batch_dev", ctypes.c_int, [P, U32, P, P, P, P, ctypes.c_uint64]),
         load_snapshot=f("load_snapshot", ctypes.c_int, [P, P]),
+        delta_capture=f("delta_capture", ctypes.c_int, [P, ctypes.c_uint64]),
+        delta_records=f("delta_records", ctypes.c_int, [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_uint64)]),
+        doc_pset=f("doc_pset", ctypes.c_int, [P, U32, I32, P, P, ctypes.POINTER(U32)]),
     )
+
+
+DELTA_DTYPE = np.dtype([("op", np.uint32), ("kind", np.int32), ("pos", np.int32), ("len", np.int32),
+                        ("seg", np.int32), ("a", np.int32), ("b", np.int32), ("pad", np.int32)])
+DELTA_KINDS = {0: "INSERT", 1: "REMOVE", 2: "ANNOTATE", -1: "APPEND", -2: "SPLIT", -3: "UNLINK"}
 
 
 def _u32(a) -> np.ndarray:
@@ -307,6 +315,34 @@ class Engine:
         self.upload_props()
         self._check(self.fn["load_snapshot"](self.h, ctypes.byref(batch.to_c())), "mt_load_snapshot")
 
+    # ---- delta callbacks as records (include/mtgpu.h mt_delta_rec) ----
+    def delta_capture(self, capacity: int):
+        """Record the delta / maintenance callbacks of the following batches (0: off)."""
+        self._check(self.fn["delta_capture"](self.h, int(capacity)), "mt_delta_capture")
+
+    def delta_records(self) -> np.ndarray:
+        """The last batch's records (DELTA_DTYPE), sorted by op index, callback order within an op."""
+        ptr, n = ctypes.c_void_p(), ctypes.c_uint64()
+        self._check(self.fn["delta_records"](self.h, ctypes.byref(ptr), ctypes.byref(n)), "mt_delta_records")
+        if not n.value:
+            return np.zeros(0, DELTA_DTYPE)
+        return np.frombuffer(ctypes.string_at(ptr, n.value * DELTA_DTYPE.itemsize), DELTA_DTYPE).copy()
+
+    def doc_pset(self, doc: int, pset_id: int):
+        """(key ids, value ids) of a document's device property set, insertion order."""
+        k, v, n = np.zeros(16, np.uint16), np.zeros(16, np.int32), ctypes.c_uint32()
+        self._check(self.fn["doc_pset"](self.h, doc, pset_id, k.ctypes.data, v.ctypes.data, ctypes.byref(n)),
+                    "mt_doc_pset")
+        return k[:n.value].copy(), v[:n.value].copy()
+
+    def pset_dict(self, doc: int, pset_id: int):
+        """A device property set as a Python dict (None for -1: properties undefined)."""
+        import json as _json
+        if pset_id < 0:
+            return None
+        keys, vals = self.doc_pset(doc, pset_id)
+        return {self.props.keys[int(k)]: _json.loads(self.props.values_json[int(v)]) for k, v in zip(keys, vals)}
+
     def update_seq(self, docs, msn, seq):
         d, m, s = _u32(docs), _i32(msn), _i32(seq)
         self._check(self.fn["update_seq"](self.h, len(d), d.ctypes.data, m.ctypes.data, s.ctypes.data),
@@ -515,5 +551,6 @@ class ClientGroup:
                 self.engine.upload_doc_names(c.doc_id, c.names.json_literals())
                 c.names_uploaded = len(c.names.names)
         batch = bb.build()
+        self.last_batch = batch          # op indexing of delta records (Engine.delta_records)
         self.engine.apply(batch)
         self.engine.sync()

@@ -181,6 +181,34 @@ typedef struct mt_limits {
 
 typedef struct mt_ctx mt_ctx;
 
+/* ---- delta callbacks as packed records (MT/mergeTreeDeltaCallback.ts) --- */
+/* kind: MergeTreeDeltaType for the delta callback (MT/ops.ts:17-22), MergeTreeMaintenanceType
+ * for the maintenance callback (MT/mergeTreeDeltaCallback.ts:11-23). */
+#define MT_DK_INSERT     0
+#define MT_DK_REMOVE     1
+#define MT_DK_ANNOTATE   2
+#define MT_DK_APPEND   (-1)
+#define MT_DK_SPLIT    (-2)
+#define MT_DK_UNLINK   (-3)
+/*
+ * One entry of a callback's deltaSegments, in callback order (the delta callback of an op
+ * fires after its ensureIntervalBoundary SPLITs and before the zamboni APPEND/UNLINKs it
+ * triggers).  pos is SequenceEvent.ranges[].position: the segment's position in the
+ * observer's view (client.getPosition) evaluated when the callback fires.
+ *   INSERT   seg = the new segment, len = cachedLength, a = its property set (mt_doc_pset)
+ *   REMOVE   seg = a newly removed segment (overlapping removes are not reported)
+ *   ANNOTATE seg = an annotated segment, a / b = its property set before / after
+ *   SPLIT    seg = the left part (len = its new length), a = the right part, b = its length
+ *   APPEND   seg = prevSegment (len = its new length), a = the appended segment, b = its length
+ *   UNLINK   seg = the unlinked segment
+ * Segments are engine row ids, stable while the segment is linked.
+ */
+typedef struct mt_delta_rec {
+    uint32_t op;        /* index of the op member in the batch (mt_op_batch order) */
+    int32_t  kind;
+    int32_t  pos, len, seg, a, b, pad;
+} mt_delta_rec;
+
 /* ---- snapshot load (MT/snapshotLoader.ts) ------------------------------- */
 /* One snapshot segment, i.e. one element of a chunk's `segments` array after
  * the host's JSON.parse (IJSONSegment or IJSONSegmentWithMergeInfo,
@@ -353,6 +381,17 @@ int  mt_get_text(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
  * segment object twice the document gets MT_DS_UNSUPPORTED.  Stream-ordered;
  * status words after mt_sync. */
 int  mt_load_snapshot(mt_ctx* ctx, const mt_load_batch* batch);
+/* Delta capture for the following batches (mt_apply_batch / mt_replay_resident):
+ * capacity records per batch; 0 turns capture off (the default: the replay kernels
+ * then never touch the record buffer). */
+int  mt_delta_capture(mt_ctx* ctx, uint64_t capacity);
+/* The records of the last batch in callback order per document and op (sorted by op
+ * index, program order within an op): a library-owned array valid until the next
+ * batch.  MT_E_OOM if the batch produced more than the capacity. */
+int  mt_delta_records(mt_ctx* ctx, const mt_delta_rec** out, uint64_t* n);
+/* The keys and values (host-interned ids, value -1 never occurs) of property set
+ * pset_id of document doc, in insertion order; returns the count in *n (<= 16). */
+int  mt_doc_pset(mt_ctx* ctx, uint32_t doc, int32_t pset_id, uint16_t* keys, int32_t* values, uint32_t* n);
 int  mt_dump_segments(mt_ctx* ctx, uint32_t doc_id, int32_t** rows, uint32_t* n_rows);
 void mt_free(void* p);
 

@@ -355,6 +355,17 @@ struct Tree {
     uint32_t status = 0;
     long long ovlHigh = 0;                 // overlap-list pushes by short ids >= 63 (test statistics)
     std::map<u16s, Seg*> idToSegment;      // MT/mergeTree.ts:1095, mapIdToSegment :1175
+    // Delta / maintenance callbacks (MT/mergeTreeDeltaCallback.ts) as records: op member
+    // index, kind (MergeTreeDeltaType / MergeTreeMaintenanceType), the segment's local
+    // position when the callback fires, its cachedLength, a kind-specific length, and
+    // for inserts / annotates the property maps as JSON.
+    struct DRec { int op, kind, pos, len, b; std::string pa, pb; };
+    std::vector<DRec>* capture = nullptr;
+    int curOp = 0;
+    static std::string propsJson(const Seg* s);
+    void drec(int kind, Seg* s, int len, int b, const std::string& pa = "null", const std::string& pb = "null") {
+        if (capture) capture->push_back({curOp, kind, getPosition(s, currentSeq, cwClientId), len, b, pa, pb});
+    }
 
     Tree() { root = makeBlock(0); heap.push_back({nullptr, -2}); }
     Block* makeBlock(int n) { blocks.emplace_back(new Block()); blocks.back()->childCount = n; return blocks.back().get(); }
@@ -671,7 +682,10 @@ struct Tree {
                     newNode = sn; childIndex++;
                 } else {
                     Seg* s = (Seg*)child; Node* next = nullptr;
-                    if (kind == LEAF_SPLIT) next = splitAt(s, _pos);
+                    if (kind == LEAF_SPLIT) {
+                        next = splitAt(s, _pos);
+                        if (next) drec(-2, s, s->cachedLength, next->cachedLength);             // SPLIT :2249-2255
+                    }
                     else { assignChild(block, cand, childIndex); next = s; }
                     if (next) { newNode = next; childIndex++; }
                     else return nullptr;
@@ -767,6 +781,7 @@ struct Tree {
             if (!seg->parent) { status |= MT_DS_INSERT_FAILED; return; }
             updateRoot(sn);
             if (collaborating && !(seg->seq == UnassignedSeq && clientId == cwClientId) && seg->seq > minSeq) addToLRUSet(seg, seg->seq);
+            drec(0, seg, seg->cachedLength, 0, "null", propsJson(seg));                          // INSERT callback :1992-2000
         }
         if (collaborating && seq != UnassignedSeq) zamboni();
     }
@@ -801,7 +816,9 @@ struct Tree {
         ensureIntervalBoundary(start, refSeq, clientId);
         ensureIntervalBoundary(end, refSeq, clientId);
         bool overwrite = false;
+        std::vector<Seg*> removed;
         auto leaf = [&](Seg* s, int, int, int) {
+            if (!s->hasRemoved) removed.push_back(s);                                            // removedSegments :2654-2659
             if (s->hasRemoved) {
                 overwrite = true;
                 if (s->removedSeq == UnassignedSeq) { s->removedClientId = clientId; s->removedSeq = seq; }
@@ -811,6 +828,7 @@ struct Tree {
         };
         auto post = [&](Block* b) { if (overwrite) nodeUpdateLengthNewStructure(b); else blockUpdateLength(b, seq, clientId); };
         nodeMapPost(root, 0, refSeq, clientId, start, end, leaf, post);
+        for (Seg* x : removed) drec(1, x, x->cachedLength, 0);                                    // REMOVE callback :2725-2733
         if (collaborating && seq != UnassignedSeq) zamboni();
     }
     void addProperties(Seg* s, const PropTable& pt, int set, bool rewrite, int seq, bool collab) {
@@ -835,11 +853,15 @@ struct Tree {
     void annotateRange(int start, int end, const PropTable& pt, int set, bool rewrite, int refSeq, int clientId, int seq) { // :2584
         ensureIntervalBoundary(start, refSeq, clientId);
         ensureIntervalBoundary(end, refSeq, clientId);
+        std::vector<std::pair<Seg*, std::string>> ann;
         auto leaf = [&](Seg* s, int, int, int) {
+            std::string before = capture ? propsJson(s) : std::string();
             addProperties(s, pt, set, rewrite, seq, collaborating);
+            if (capture) ann.push_back({s, before});
             if (collaborating && seq != UnassignedSeq) addToLRUSet(s, seq);
         };
         nodeMap(root, 0, refSeq, clientId, start, end, leaf, nullptr, nullptr);
+        for (auto& x : ann) drec(2, x.first, x.first->cachedLength, 0, x.second, propsJson(x.first));   // ANNOTATE :2609-2617
         if (collaborating && seq != UnassignedSeq) zamboni();
     }
     /* ---- zamboni ---- */
@@ -856,11 +878,15 @@ struct Tree {
                 Seg* s = (Seg*)c;
                 if (s->hasRemoved) {
                     if (s->removedSeq > minSeq) hold.push_back(s);
-                    else s->parent = nullptr;                       // UNLINK
+                    else { drec(-3, s, s->cachedLength, 0); s->parent = nullptr; }   // UNLINK :1298-1306
                     prev = nullptr;
                 } else if (s->seq <= minSeq) {
                     bool ca = prev && canAppend(prev, s) && match_properties(prev->hasProps ? &prev->props : nullptr, s->hasProps ? &s->props : nullptr) && localNetLength(s) > 0;
-                    if (ca) { prev->text += s->text; prev->cachedLength = (int)prev->text.size(); s->parent = nullptr; }
+                    if (ca) {
+                        prev->text += s->text; prev->cachedLength = (int)prev->text.size();
+                        drec(-1, prev, prev->cachedLength, s->cachedLength);              // APPEND :1323-1331
+                        s->parent = nullptr;
+                    }
                     else { hold.push_back(s); prev = localNetLength(s) > 0 ? s : nullptr; }
                 } else { hold.push_back(s); prev = nullptr; }
             } else { hold.push_back(c); prev = nullptr; }
@@ -934,6 +960,11 @@ struct Tree {
     template <class F> void walkAll(Block* b, F& f) { for (int i = 0; i < b->childCount; i++) { Node* c = b->children[i]; if (c->leaf) f((Seg*)c); else walkAll((Block*)c, f); } }
 };
 
+std::string Tree::propsJson(const Seg* s) {
+    if (!s->hasProps) return "null";
+    std::string o; stringify(o, s->props); return o;
+}
+
 /* ======================================================================== */
 /* Client (MT/client.ts) + snapshot                                          */
 /* ======================================================================== */
@@ -946,6 +977,7 @@ struct Doc {
     std::vector<std::string> shortToName;    // shortClientIdMap (JSON literal)
     std::vector<int> shortToStream;          // short id -> stream client index (-1 observer)
     std::vector<int> streamToShort;
+    int opCounter = 0;                       // op members applied (mt_op_batch indexing of the message stream)
 
     int shortId(int streamIdx) {             // getOrAddShortClientId, MT/client.ts:658-682
         if (streamIdx < (int)streamToShort.size() && streamToShort[streamIdx] >= 0) return streamToShort[streamIdx];
@@ -1366,6 +1398,7 @@ static void apply_remote_json(Doc& d, const JVal& op, int cl, int ref, int seq, 
     Tree& t = d.t;
     int type;
     if (op.t != JVal::Obj || !jnum(op, u"type", type)) return;                                  // default: ignored
+    if (type == MT_OP_INSERT || type == MT_OP_REMOVE || type == MT_OP_ANNOTATE) t.curOp = d.opCounter++;
     // getValidOpRange (MT/client.ts:506-523): pos, else posFromRelativePos when relativePos is set
     auto opPos = [&](const char16_t* pk, const char16_t* rk, int& out) -> bool {
         if (jnum(op, pk, out)) return true;
@@ -1418,10 +1451,12 @@ uint32_t ora_apply_msg_json(ora_doc* o, const char* json) {
         !jnum(m, u"minimumSequenceNumber", msn)) { t.status |= MT_DS_UNSUPPORTED; return t.status; }
     const int cl = load_short_id(d, cid->s);                                                     // getOrAddShortClientId :825
     const JVal* ty = jget(m, u"type");
+    const int op0 = d.opCounter;
     if (ty && ty->t == JVal::Str && ty->s == u"op") {
         const JVal* c = jget(m, u"contents");
         if (c) apply_remote_json(d, *c, cl, ref, seq, msn);
     }
+    if (d.opCounter == op0) t.curOp = d.opCounter++;            // a message with no member op: one record slot
     if (t.currentSeq > seq) t.status |= MT_DS_ASSERT_SEQ;                                        // updateSeqNumbers :843-850
     t.currentSeq = seq;
     if (msn > seq) t.status |= MT_DS_ASSERT_MSN;
@@ -1438,6 +1473,26 @@ int32_t ora_rel_pos_json(ora_doc* o, int32_t ref, const char* client_literal, co
 }
 // getLength(refSeq, clientId) of the client with this long id (a JSON string literal);
 // an id not registered yet owns no segment, so any unused short id gives its view.
+// Delta capture: on/off; the records as a JSON array of
+// [op, kind, pos, len, b, propsBefore|null, propsAfter|null] (malloc'd, NUL-terminated).
+void ora_delta_capture(ora_doc* o, int on) {
+    if (on && !o->d.t.capture) o->d.t.capture = new std::vector<Tree::DRec>();
+    if (!on) { delete o->d.t.capture; o->d.t.capture = nullptr; }
+}
+char* ora_delta_json(ora_doc* o) {
+    std::string j = "[";
+    if (o->d.t.capture)
+        for (size_t i = 0; i < o->d.t.capture->size(); i++) {
+            const Tree::DRec& r = (*o->d.t.capture)[i];
+            if (i) j += ",";
+            j += "[" + std::to_string(r.op) + "," + std::to_string(r.kind) + "," + std::to_string(r.pos) + "," +
+                 std::to_string(r.len) + "," + std::to_string(r.b) + "," + (r.kind == 2 ? r.pa : std::string("null")) + "," +
+                 (r.kind == 0 || r.kind == 2 ? r.pb : std::string("null")) + "]";
+        }
+    j += "]";
+    char* out = (char*)malloc(j.size() + 1); memcpy(out, j.c_str(), j.size() + 1);
+    return out;
+}
 int32_t ora_get_length_json(ora_doc* o, int32_t ref, const char* client_literal) {
     auto it = o->d.nameToShort.find(jquote(parse_key(client_literal)));
     return o->d.t.getLength(ref, it != o->d.nameToShort.end() ? it->second : -999999);

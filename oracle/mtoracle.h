@@ -35,6 +35,10 @@ int32_t  ora_get_length_json(ora_doc* d, int32_t ref_seq, const char* client_lit
 /* posFromRelativePos of an IRelativePosition (JSON) under that client's perspective;
  * -1 when no marker carries the id. */
 int32_t  ora_rel_pos_json(ora_doc* d, int32_t ref_seq, const char* client_literal, const char* relpos_json);
+/* Delta / maintenance callbacks as records (on != 0), and the records so far as a JSON
+ * array [op, kind, pos, len, b, propsBefore|null, propsAfter|null] (free with ora_free_buf). */
+void     ora_delta_capture(ora_doc* d, int on);
+char*    ora_delta_json(ora_doc* d);
 /* Local (non-collaborating) ops, as SharedString.insertText/insertMarker/
  * annotateRange/removeText on a detached string (seq = UniversalSequenceNumber). */
 int      ora_local_insert(ora_doc* d, int32_t pos, const uint16_t* text, uint32_t n,

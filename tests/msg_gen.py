@@ -43,7 +43,8 @@ class StreamGen:
     def __init__(self, seed: int, clients: int = 4, lag: int = 12, churn: float = 0.0, p_nonop: float = 0.06,
                  p_group: float = 0.15, p_marker: float = 0.08, p_annotate: float = 0.2, p_remove: float = 0.3,
                  p_special: float = 0.25, long_every: int = 40, max_ins: int = 9, id_prefix: str = "cli",
-                 max_total_clients: int | None = None, p_marker_id: float = 0.0, p_relative: float = 0.0):
+                 max_total_clients: int | None = None, p_marker_id: float = 0.0, p_relative: float = 0.0,
+                 capture: bool = False):
         self.rng = random.Random(seed)
         self.lag, self.churn, self.p_nonop, self.p_group = lag, churn, p_nonop, p_group
         self.p_marker, self.p_annotate, self.p_remove, self.p_special = p_marker, p_annotate, p_remove, p_special
@@ -59,6 +60,8 @@ class StreamGen:
         self.cur = 0
         self.msn = 0
         self.obs = OracleDoc(True)
+        if capture:
+            self.obs.delta_capture(True)
         self.msgs: list[dict] = []
 
     # -- clients ----------------------------------------------------------------

@@ -50,6 +50,9 @@ def lib():
         L.ora_apply_msg_json.argtypes = [P, ctypes.c_char_p]
         L.ora_rel_pos_json.restype = I32
         L.ora_rel_pos_json.argtypes = [P, I32, ctypes.c_char_p, ctypes.c_char_p]
+        L.ora_delta_capture.argtypes = [P, ctypes.c_int]
+        L.ora_delta_json.restype = P
+        L.ora_delta_json.argtypes = [P]
         L.ora_get_length_json.restype = I32
         L.ora_get_length_json.argtypes = [P, I32, ctypes.c_char_p]
         L.ora_get_length.restype = I32
@@ -123,6 +126,17 @@ class OracleDoc:
         """getLength(refSeq, shortId(client_id)) under the oracle's own registration."""
         from fluidframework_amd.jsjson import quote
         return int(self.L.ora_get_length_json(self.h, ref_seq, quote(client_id).encode("utf-8", "surrogatepass")))
+
+    def delta_capture(self, on: bool = True):
+        self.L.ora_delta_capture(self.h, 1 if on else 0)
+
+    def delta_records(self) -> list:
+        """[[op, kind, pos, len, b, propsBefore, propsAfter], ...] (props as parsed JSON)."""
+        import json
+        buf = self.L.ora_delta_json(self.h)
+        out = json.loads(ctypes.string_at(buf).decode("utf-8", "surrogatepass"))
+        self.L.ora_free_buf(buf)
+        return out
 
     def rel_pos_of(self, ref_seq: int, client_id: str, relpos: dict) -> int:
         """posFromRelativePos under (ref_seq, client_id)'s perspective; -1: unknown id."""

@@ -129,3 +129,51 @@ def test_message_surface_node_host_on_gpu(surface):
     if NODE is None:
         pytest.skip("node is not installed")
     check_node(os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"), surface, n_docs=6)
+
+
+def check_delta_records(factory, surface, seed=5, n_docs=3, n_msgs=900):
+    """§8(f4): the engine's delta / maintenance records (mt_delta_records) equal the oracle's
+    callbacks (MT/mergeTreeDeltaCallback.ts: INSERT / REMOVE / ANNOTATE deltaSegments, SPLIT /
+    APPEND / UNLINK maintenance) record for record: op, kind, observer position, lengths,
+    and the property maps before / after an annotate."""
+    streams = [stream(seed * 31 + d, n_msgs, capture=True, **SURFACES[surface]) for d in range(n_docs)]
+    eng = factory(n_docs, **LIMITS)
+    eng.delta_capture(1 << 20)
+    g = ClientGroup(eng)
+    clients = [g.new_client({"newMergeTreeSnapshotFormat": True}) for _ in range(n_docs)]
+    for c, (msgs, _) in zip(clients, streams):
+        for m in msgs:
+            c.applyMsg(m)
+    g.flush()
+    assert (eng.status(range(n_docs)) == 0).all()
+    recs = eng.delta_records()
+    offs = g.last_batch.op_offsets
+    kinds = set()
+    for d, (msgs, obs) in enumerate(streams):
+        mine = recs[(recs["op"] >= offs[d]) & (recs["op"] < offs[d + 1])]
+        want = obs.delta_records()
+        assert len(mine) == len(want), f"doc {d}: {len(mine)} vs {len(want)} records"
+        for i, (x, w) in enumerate(zip(mine, want)):
+            op, kind, pos, ln, b, pa, pb = w
+            got = (int(x["op"]) - int(offs[d]), int(x["kind"]), int(x["pos"]), int(x["len"]))
+            assert got == (op, kind, pos, ln), f"doc {d} record {i}: {got} vs {w[:4]}"
+            if kind in (-1, -2):
+                assert int(x["b"]) == b, (d, i)
+            if kind == 0:
+                assert eng.pset_dict(d, int(x["a"])) == pb, (d, i)
+            if kind == 2:
+                assert (eng.pset_dict(d, int(x["a"])), eng.pset_dict(d, int(x["b"]))) == (pa, pb), (d, i)
+            kinds.add(kind)
+    return kinds
+
+
+@pytest.mark.parametrize("surface", ["mixed", "groups", "markers_props"])
+def test_delta_records_on_emulation(surface):
+    kinds = check_delta_records(emu_engine, surface)
+    assert {0, 1, 2, -1, -2, -3} <= kinds
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("surface", ["mixed", "groups", "markers_props", "churn300"])
+def test_delta_records_on_gpu(surface):
+    check_delta_records(lambda n, **kw: Engine(n, device=0, **kw), surface, n_docs=6)
