@@ -338,8 +338,9 @@ class BatchBuilder:
         else:
             self._emit(type=MT_OP_NOOP, flags=fl, **common)
 
-    def add_message(self, msg: dict):
-        """One sequenced message (Client.applyMsg semantics, client.ts:819-841)."""
+    def add_message(self, msg: dict) -> list:
+        """One sequenced message (Client.applyMsg semantics, client.ts:819-841).  Returns
+        the batch op index of each merge-tree member (GROUP order; [] for none)."""
         if not isinstance(msg.get("clientId"), str):
             # getOrAddShortClientId keys a RedBlackTree with localeCompare (client.ts:73, :658):
             # a null id cannot be registered once the tree holds ids
@@ -348,14 +349,16 @@ class BatchBuilder:
         seq, ref, msn = int(msg["sequenceNumber"]), int(msg["referenceSequenceNumber"]), int(msg["minimumSequenceNumber"])
         if msg.get("type", "op") != "op":
             self._emit(type=MT_OP_NOOP, flags=MT_OPF_END_OF_MSG, client=client, seq=seq, ref_seq=ref, msn=msn, prop_id=-1)
-            return
+            return []
         members = [m for m in _group_members(msg.get("contents"))
                    if m.get("type") in (MT_OP_INSERT, MT_OP_REMOVE, MT_OP_ANNOTATE)]
         if not members:
             self._emit(type=MT_OP_NOOP, flags=MT_OPF_END_OF_MSG, client=client, seq=seq, ref_seq=ref, msn=msn, prop_id=-1)
-            return
+            return []
+        first = len(self.cols["type"])
         for i, m in enumerate(members):
             self._member(m, client, seq, ref, msn, i == len(members) - 1)
+        return list(range(first, first + len(members)))
 
     def build(self) -> OpBatch:
         arrays = {n: np.asarray(self.cols[n], dtype=t) for n, t in _FIELDS}

@@ -438,6 +438,7 @@ class MergeTreeClient:
         self.current_seq = 0
         self.min_seq = 0
         self.longClientId = None
+        self.delta_listener = None       # SequenceDoc's sequenceDelta subscription (sequence.py)
 
     def startOrUpdateCollaboration(self, longClientId, minSeq=0, currentSeq=0, branchId=0):
         self.longClientId = longClientId
@@ -474,7 +475,6 @@ class MergeTreeClient:
         newMergeTreeSnapshotFormat True: SnapshotV1 (snapshotV1.ts:98-163), header,
         body_0, ...; otherwise SnapshotLegacy (snapshotlegacy.ts:104-175), header,
         body, then catchUpMsgs as JSON under catchUpBlobName (default "catchupOps")."""
-        import json as _json
         self.group.flush()
         self._raise_status()
         opts = self.options or {}
@@ -491,8 +491,8 @@ class MergeTreeClient:
                    for i, b in enumerate(blobs)]
         if not v1 and catchUpMsgs:
             name = opts.get("catchUpBlobName")
-            entries.append(entry("catchupOps" if name is None else name,
-                                 _json.dumps(catchUpMsgs, separators=(",", ":"), ensure_ascii=False)))
+            # serializer.stringify: JSON.stringify key order and number forms
+            entries.append(entry("catchupOps" if name is None else name, jsjson.stringify(catchUpMsgs)))
         return {"entries": entries}
 
     def getCurrentSeq(self) -> int:
@@ -539,18 +539,56 @@ class ClientGroup:
         if not busy:
             return
         bb = BatchBuilder(self.engine.props, None)
+        listen = []
         for c in busy:
             bb.names = c.names
             bb.begin_doc(c.doc_id)
+            entries = []
             for m in c.pending:
-                bb.add_message(m)
+                entries.append((m, bb.add_message(m)))
                 c.current_seq = int(m["sequenceNumber"])
                 c.min_seq = max(c.min_seq, int(m["minimumSequenceNumber"]))
             c.pending = []
+            if c.delta_listener is not None:
+                listen.append((c, entries))
             if c.names_uploaded != len(c.names.names):
                 self.engine.upload_doc_names(c.doc_id, c.names.json_literals())
                 c.names_uploaded = len(c.names.names)
         batch = bb.build()
         self.last_batch = batch          # op indexing of delta records (Engine.delta_records)
+        if listen:
+            self.engine.delta_capture(max(4096, 64 * batch.n_ops))
         self.engine.apply(batch)
         self.engine.sync()
+        if listen:
+            self._deliver(listen)
+
+    def _deliver(self, listen):
+        """Hand each listening client its messages' sequenceDelta events: per op member,
+        the INSERT/REMOVE/ANNOTATE records as ranges with their property maps."""
+        recs = self.engine.delta_records()
+        by_op: dict = {}
+        for r in recs:
+            if 0 <= int(r["kind"]) <= 2:
+                by_op.setdefault(int(r["op"]), []).append(r)
+        for c, entries in listen:
+            st = int(self.engine.status([c.doc_id])[0])
+            if st:
+                raise MergeTreeError(f"document {c.doc_id}: {', '.join(status_names(st))}")
+            cache: dict = {}
+
+            def pset(i, doc=c.doc_id, cache=cache):
+                if i not in cache:
+                    cache[i] = self.engine.pset_dict(doc, i)
+                return cache[i]
+
+            def events_of(op, pset=pset):
+                out = []
+                for r in by_op.get(op, ()):
+                    k = int(r["kind"])
+                    a, b = int(r["a"]), int(r["b"])
+                    out.append({"kind": k, "pos": int(r["pos"]), "len": int(r["len"]),
+                                "before": pset(a) if k == 2 else None,
+                                "after": pset(b) if k == 2 else (pset(a) if k == 0 else None)})
+                return out
+            c.delta_listener(entries, events_of)

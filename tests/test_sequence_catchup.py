@@ -1,0 +1,216 @@
+"""§8(f2): SharedSegmentSequence's legacy catch-up path (sequence.ts:592-658) on the engine.
+
+For a channel's op stream (the other channels' messages leave seq gaps, so many messages
+have refSeq != seq - 1), fluidframework_amd.sequence.SequenceDoc stashes every message,
+transforming the ones that need it from the engine's sequenceDelta records
+(createOpsFromDelta, sequence.ts:58-105), and writes SnapshotLegacy + catch-up blob.
+
+* The whole tree equals the one computed from the ORACLE's records of the same stream
+  (ora_delta_json: the oracle's own callback restatement) with the same stash rules, and
+  its header/body blobs equal the oracle's SnapshotLegacy bytes.
+* The property the transformation exists for (sequence.ts:612-631): loading the legacy
+  snapshot and applying the catch-up messages on the oracle (SnapshotLoader +
+  Client.applyMsg, its own JSON path) reproduces the document: same text and the same
+  properties per character.
+* createOpsFromDelta known answers written out from sequence.ts:58-105 and
+  segmentPropertiesManager.ts:67-112 (remove/annotate coalescing, rewrite delta keys).
+"""
+import json
+
+import pytest
+
+from emu_lib import emu_engine
+from fluidframework_amd import jsjson
+from fluidframework_amd import sequence as sq
+from fluidframework_amd.batch import _group_members
+from fluidframework_amd.engine import ClientGroup, Engine
+from msg_gen import stream
+from oracle_lib import OracleDoc
+from test_message_surface import LIMITS, SURFACES
+
+GPU = lambda n, **kw: Engine(n, device=0, **kw)  # noqa: E731
+
+
+def channel_stream(seed: int, n: int, surface: str) -> list:
+    """The sequenced ops of one channel: the stream's non-op messages stand for other
+    channels' traffic (they reach the delta manager, not the DDS)."""
+    msgs, _ = stream(seed, n, **SURFACES[surface])
+    return [m for m in msgs if m["type"] == "op"]
+
+
+def oracle_tree(msgs: list):
+    """(oracle doc, expected stash) from the oracle's delta records and the stash rules."""
+    od = OracleDoc(True)
+    od.delta_capture(True)
+    for m in msgs:
+        assert od.apply_msg(m) == 0, m
+    by_op: dict = {}
+    for op, kind, pos, ln, _b, pa, pb in od.delta_records():
+        if 0 <= kind <= 2:
+            by_op.setdefault(op, []).append({"kind": kind, "pos": pos, "len": ln,
+                                             "before": pa if kind == 2 else None, "after": pb})
+    stash, op = [], 0
+    for m in msgs:
+        n = len([x for x in _group_members(m.get("contents")) if x.get("type") in (0, 1, 2)])
+        ids = list(range(op, op + n))
+        op += max(n, 1)
+        e = json.loads(json.dumps(m))
+        if e["referenceSequenceNumber"] != e["sequenceNumber"] - 1:
+            e = sq.transform_message(e, [by_op.get(i, []) for i in ids])
+        stash.append(e)
+        if len(stash) > 20 and stash[20]["sequenceNumber"] < m["minimumSequenceNumber"]:
+            stash = [x for x in stash if x["sequenceNumber"] > m["minimumSequenceNumber"]]
+    msn, seq = msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"]
+    stash = [x for x in stash if x["sequenceNumber"] > msn]
+    for x in stash:
+        x["minimumSequenceNumber"] = msn
+    return od, stash, msn, seq
+
+
+def annotated_units(blobs: list) -> list:
+    """(code unit, properties) per character of a SnapshotV1 (removed segments dropped)."""
+    out = []
+    for b in blobs:
+        for s in json.loads(b)["segments"]:
+            if isinstance(s, dict) and "json" in s:
+                if "removedSeq" in s:
+                    continue
+                s = s["json"]
+            if isinstance(s, str):
+                out += [(u, None) for u in jsjson.utf16_units(s)]
+            elif "text" in s:
+                out += [(u, s.get("props")) for u in jsjson.utf16_units(s["text"])]
+            else:
+                out.append(("marker", s["marker"].get("refType"), s.get("props")))
+    return out
+
+
+def run_channels(factory, surface: str, n_docs: int = 3, n_msgs: int = 700, flush_every: int = 97):
+    """Stash/blob parity on every surface; the load + catch-up replay property on those
+    without relative positions: a live document resolves a relativePos against a marker
+    that was removed (idToSegment keeps it), but SnapshotLegacy writes only the segments
+    live at the MSN, so in the reference too an untransformed catch-up op naming a marker
+    removed at or below the MSN no longer resolves after a load."""
+    replay = not SURFACES[surface].get("p_relative")
+    chans = [channel_stream(17 * d + 3, n_msgs, surface) for d in range(n_docs)]
+    eng = factory(n_docs, **LIMITS)
+    g = ClientGroup(eng)
+    docs = [sq.SequenceDoc(g) for _ in range(n_docs)]
+    for k in range(max(len(c) for c in chans)):
+        for d, c in zip(docs, chans):
+            if k < len(c):
+                d.process(c[k])
+        if k % flush_every == flush_every - 1:
+            g.flush()                                  # several device batches per stream
+    transformed, in_stash = 0, 0
+    for d, msgs in zip(docs, chans):
+        tree = d.snapshot()
+        blobs = {e["path"]: e["value"]["contents"] for e in tree["entries"]}
+        od, want, msn, seq = oracle_tree(msgs)
+        moved = [m["sequenceNumber"] for m in msgs if m["referenceSequenceNumber"] != m["sequenceNumber"] - 1]
+        transformed += len(moved)
+        in_stash += sum(s > msn for s in moved)
+        # the stash, byte for byte (JSON.stringify order), and the legacy blobs
+        assert blobs.get("catchupOps") == (jsjson.stringify(want) if want else None)
+        ob, _ = od.snapshot(msn, seq, legacy=True)
+        assert [blobs["header"].encode()] + ([blobs["body"].encode()] if "body" in blobs else []) == ob
+        assert od.get_text() == d.getText()
+        if not replay:
+            continue
+        # load + catch-up reproduces the document
+        ld = OracleDoc(False)
+        assert ld.load_snapshot([blobs["header"]] + ([blobs["body"]] if "body" in blobs else [])) == 0
+        for m in json.loads(blobs.get("catchupOps", "[]")):
+            assert ld.apply_msg(m) == 0, m
+        assert ld.get_text() == od.get_text() == d.getText()
+        assert annotated_units(ld.snapshot(seq, seq)[0]) == annotated_units(od.snapshot(seq, seq)[0])
+    return transformed, in_stash
+
+
+@pytest.mark.parametrize("surface", ["mixed", "groups", "markers_props", "unicode", "relative"])
+def test_catchup_on_emulation(surface):
+    moved, in_stash = run_channels(emu_engine, surface)
+    assert moved > 300 and in_stash > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("surface", ["mixed", "groups", "markers_props", "unicode", "relative", "churn"])
+def test_catchup_on_gpu(surface):
+    moved, in_stash = run_channels(GPU, surface, n_docs=6)
+    assert moved > 600 and in_stash > 0
+
+
+def test_new_format_keeps_no_stash():
+    eng = emu_engine(1, **LIMITS)
+    d = sq.SequenceDoc(ClientGroup(eng), {"newMergeTreeSnapshotFormat": True})
+    for m in channel_stream(5, 200, "mixed"):
+        d.process(m)
+    tree = d.snapshot()
+    assert d.messagesSinceMSNChange == []
+    assert [e["path"] for e in tree["entries"]][0] == "header"
+    assert all(not e["path"].startswith("catchup") for e in tree["entries"])
+
+
+def test_non_op_message_rejected():
+    d = sq.SequenceDoc(ClientGroup(emu_engine(1, **LIMITS)))
+    with pytest.raises(ValueError):
+        d.process(dict(clientId="a", sequenceNumber=1, referenceSequenceNumber=0, minimumSequenceNumber=0,
+                       type="noop", contents=None))
+
+
+# ---- createOpsFromDelta known answers (sequence.ts:58-105) -----------------------------
+def R(kind, pos, ln, before=None, after=None):
+    return {"kind": kind, "pos": pos, "len": ln, "before": before, "after": after}
+
+
+def test_remove_ranges_coalesce_on_equal_start():
+    # removed segments collapse to the position of the first: each later range starts there
+    ops = sq.ops_from_delta({"type": 1, "pos1": 3, "pos2": 9}, [R(1, 3, 2), R(1, 3, 4), R(1, 5, 1)])
+    assert ops == [{"pos1": 3, "pos2": 9, "type": 1}, {"pos1": 5, "pos2": 6, "type": 1}]
+
+
+def test_annotate_ranges_coalesce_when_adjacent_and_matching():
+    m = {"type": 2, "pos1": 0, "pos2": 9, "props": {"b": 1}}
+    ops = sq.ops_from_delta(m, [R(2, 0, 2, None, {"b": 1}), R(2, 2, 3, {"x": 1}, {"x": 1, "b": 1}),
+                                R(2, 6, 1, None, {"b": 1}), R(2, 7, 2, {"b": 2}, {"b": 2})])
+    # values come from the segment after the op (b=2 on the last one: no match, no merge)
+    assert ops == [{"pos1": 0, "pos2": 5, "props": {"b": 1}, "type": 2},
+                   {"pos1": 6, "pos2": 7, "props": {"b": 1}, "type": 2},
+                   {"pos1": 7, "pos2": 9, "props": {"b": 2}, "type": 2}]
+
+
+def test_rewrite_delta_keys_and_values():
+    # rewrite: keys the op drops (falsy in the op) first, in the segment's key order, then
+    # the op's keys; integer-like keys enumerate first; dropped keys map to null
+    m = {"type": 2, "pos1": 0, "pos2": 1, "props": {"z": 1, "k": 0, "5": "v"}, "combiningOp": {"name": "rewrite"}}
+    ops = sq.ops_from_delta(m, [R(2, 0, 1, {"q": 1, "k": 3, "2": True, "z": 2}, {"z": 1, "k": 0, "5": "v"})])
+    assert list(ops[0]["props"]) == ["2", "5", "q", "k", "z"]
+    assert ops[0]["props"] == {"2": None, "5": "v", "q": None, "k": 0, "z": 1}
+
+
+def test_insert_segment_json():
+    assert sq.ops_from_delta({"type": 0, "pos1": 1, "seg": "ab"}, [R(0, 1, 2)]) == \
+        [{"pos1": 1, "seg": "ab", "type": 0}]
+    assert sq.ops_from_delta({"type": 0, "seg": {"text": "ab", "props": {}}}, [R(0, 4, 2, None, {})]) == \
+        [{"pos1": 4, "seg": {"text": "ab", "props": {}}, "type": 0}]
+    assert sq.ops_from_delta({"type": 0, "seg": {"marker": {"refType": 1}, "props": {"a": 1}}},
+                             [R(0, 0, 1, None, {"a": 1})]) == \
+        [{"pos1": 0, "seg": {"marker": {"refType": 1}, "props": {"a": 1}}, "type": 0}]
+
+
+def test_transform_message_group_and_empty():
+    msg = dict(clientId="a", sequenceNumber=9, referenceSequenceNumber=4, minimumSequenceNumber=2, type="op",
+               contents={"type": 3, "ops": [{"type": 1, "pos1": 0, "pos2": 2}, {"type": 0, "pos1": 0, "seg": "x"}]})
+    out = sq.transform_message(msg, [[], [R(0, 0, 1)]])
+    assert list(out) == list(msg) and out["referenceSequenceNumber"] == 8
+    assert out["contents"] == {"pos1": 0, "seg": "x", "type": 0}        # one op: not a group
+    out = sq.transform_message(msg, [[], []])
+    assert jsjson.stringify(out["contents"]) == '{"ops":[],"type":3}'   # createGroupOp() of nothing
+
+
+def test_match_properties_restatement():
+    assert sq.match_properties({"a": {"b": [1, 2]}}, {"a": {"b": [1, 2]}})
+    assert not sq.match_properties({"a": {"b": [1, 2]}}, {"a": {"b": [1, 3]}})
+    assert not sq.match_properties({"a": 1}, {"a": 1, "b": None})
+    assert sq.match_properties(None, {}) is False and sq.match_properties({}, {}) is True
+    assert sq.match_properties({"a": None}, {"a": None})
