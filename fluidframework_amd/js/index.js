@@ -128,6 +128,12 @@ class ClientNames {
     markerLookup(id) { return typeof id === "string" && this.markerIds.has(id) ? this.markerIds.get(id) : -1; }
 }
 
+// applyRemoteOp's GROUP recursion (client.ts:804-812), flattened; members share the seq
+function mergeTreeMembers(contents) {
+    const flat = (op) => (op && typeof op === "object") ? (op.type === OP_GROUP ? (op.ops || []).flatMap(flat) : [op]) : [];
+    return flat(contents).filter((m) => m.type === OP_INSERT || m.type === OP_REMOVE || m.type === OP_ANNOTATE);
+}
+
 const COLS = [["type", Uint8Array], ["flags", Uint8Array], ["client", Uint16Array], ["seq", Int32Array],
     ["refSeq", Int32Array], ["msn", Int32Array], ["pos1", Int32Array], ["pos2", Int32Array],
     ["payloadOff", Uint32Array], ["payloadLen", Uint32Array], ["propId", Int32Array]];
@@ -200,7 +206,8 @@ class BatchBuilder {
             this.emit({ ...common, type: OP_NOOP, flags: fl });
         }
     }
-    /** One sequenced message (Client.applyMsg, client.ts:819-841). */
+    /** One sequenced message (Client.applyMsg, client.ts:819-841); returns the batch op
+     * index of each merge-tree member (GROUP order; [] for none). */
     addMessage(msg) {
         // getOrAddShortClientId keys a RedBlackTree with localeCompare (client.ts:73, :658)
         if (typeof msg.clientId !== "string") throw new Error("clientId must be a string on the batch path");
@@ -208,13 +215,13 @@ class BatchBuilder {
         const seq = msg.sequenceNumber, ref = msg.referenceSequenceNumber, msn = msg.minimumSequenceNumber;
         if ((msg.type === undefined ? "op" : msg.type) !== "op") {
             this.emit({ type: OP_NOOP, flags: F_END, client, seq, refSeq: ref, msn, propId: -1 });
-            return;
+            return [];
         }
-        // applyRemoteOp's GROUP recursion (client.ts:804-812), flattened; members share the seq
-        const flat = (op) => (op && typeof op === "object") ? (op.type === OP_GROUP ? (op.ops || []).flatMap(flat) : [op]) : [];
-        const members = flat(msg.contents).filter((m) => m.type === OP_INSERT || m.type === OP_REMOVE || m.type === OP_ANNOTATE);
-        if (!members.length) { this.emit({ type: OP_NOOP, flags: F_END, client, seq, refSeq: ref, msn, propId: -1 }); return; }
+        const members = mergeTreeMembers(msg.contents);
+        if (!members.length) { this.emit({ type: OP_NOOP, flags: F_END, client, seq, refSeq: ref, msn, propId: -1 }); return []; }
+        const first = this.cols.type.length;
         members.forEach((m, i) => this.member(m, client, seq, ref, msn, i === members.length - 1));
+        return members.map((_, i) => first + i);
     }
     build() {
         const b = { docIds: Uint32Array.from(this.docIds), opOffsets: Uint32Array.from(this.offsets),
@@ -393,6 +400,18 @@ class Engine {
             Int32Array.from(seq));
     }
     getText(docs) { return addon.getText(this.h, Uint32Array.from(docs)); }
+    /** Record the delta / maintenance callbacks of later batches (mt_delta_capture; 0: off). */
+    deltaCapture(capacity) { addon.deltaCapture(this.h, capacity); }
+    /** The last batch's records: Int32Array, 8 per record (op, kind, pos, len, seg, a, b, pad). */
+    deltaRecords() { return addon.deltaRecords(this.h); }
+    /** A document's device property set as a plain object (undefined for -1). */
+    psetObject(doc, id) {
+        if (id < 0) return undefined;
+        const { keys, values } = addon.docPset(this.h, doc, id);
+        const o = {};
+        keys.forEach((k, i) => { o[this.props.keys[k]] = JSON.parse(this.props.valueJson[values[i]]); });
+        return o;
+    }
 }
 
 /**
@@ -406,6 +425,7 @@ class MergeTreeClient {
         this.options = options;                     // Client options (client.ts:82-84)
         this.pending = []; this.names = new ClientNames();
         this.currentSeq = 0; this.minSeq = 0; this.longClientId = undefined;
+        this.deltaListener = null;                  // SequenceChannel's sequenceDelta subscription
     }
     startOrUpdateCollaboration(longClientId, minSeq = 0, currentSeq = 0) {
         this.longClientId = longClientId;
@@ -417,11 +437,30 @@ class MergeTreeClient {
     }
     getCurrentSeq() { return this.currentSeq; }
     /**
-     * Client.load (client.ts:958) through SnapshotLoader (snapshotLoader.ts:39-222):
-     * `blobs` maps blob paths (header, body_0.. / body, catch-up ops) to contents.
-     * Returns { catchupOps } for the caller to apply, as the reference's loader does.
+     * Client.load (client.ts:958-965) with the reference's signature: reads the snapshot
+     * through an IChannelStorageService (readBlob / list, as SnapshotLoader.initialize
+     * and loadBodyAndCatchupOps do, snapshotLoader.ts:39-84) and resolves to
+     * { catchupOpsP }, the catch-up messages for the caller to apply.
      */
-    load(blobs, longClientId = "snapshot") {
+    async load(runtime, storage, serializer) {
+        const text = (b) => {
+            if (typeof b === "string") return b;
+            if (b instanceof ArrayBuffer) return Buffer.from(b).toString("utf8");
+            return Buffer.from(b.buffer, b.byteOffset, b.byteLength).toString("utf8");   // bufferToString(b, "utf8")
+        };
+        const blobs = { header: text(await storage.readBlob("header")) };
+        for (const p of await storage.list("")) {
+            if (blobs[p] === undefined) blobs[p] = text(await storage.readBlob(p));
+        }
+        const id = runtime && runtime.clientId !== undefined ? runtime.clientId : "snapshot";
+        const { catchupOps } = this.loadBlobs(blobs, id);
+        return { catchupOpsP: Promise.resolve(catchupOps) };
+    }
+    /**
+     * SnapshotLoader over already-read blobs: `blobs` maps blob paths (header, body_0.. /
+     * body, catch-up ops) to contents.  Returns { catchupOps } for the caller to apply.
+     */
+    loadBlobs(blobs, longClientId = "snapshot") {
         this.group.flush();
         const snap = parseSnapshot(blobs);
         const lb = new LoadBuilder(this.group.engine.props);
@@ -456,12 +495,22 @@ class MergeTreeClient {
         return this.group.engine.getText([this.docId])[0];
     }
     /**
-     * Client.snapshot (client.ts:923-956).  With options.newMergeTreeSnapshotFormat
+     * Client.snapshot (client.ts:923-956) with the reference's signature: the delta
+     * manager's MSN and last seq move the window (updateSeqNumbers), then the tree.
+     */
+    snapshot(runtime, handle, serializer, catchUpMsgs) {
+        const dm = runtime.deltaManager;
+        this.updateSeqNumbers(dm.minimumSequenceNumber, dm.lastSequenceNumber);
+        return this.snapshotTree(catchUpMsgs, serializer, handle);
+    }
+    /**
+     * The tree at the client's current window.  With options.newMergeTreeSnapshotFormat
      * === true: SnapshotV1 (snapshotV1.ts:98-163), header, body_0, ...; otherwise
      * SnapshotLegacy (snapshotlegacy.ts:104-175): header, body, then catchUpMsgs as
-     * the catch-up blob (options.catchUpBlobName ?? "catchupOps") when non-empty.
+     * the catch-up blob (options.catchUpBlobName ?? "catchupOps", serializer.stringify)
+     * when non-empty.
      */
-    snapshot(catchUpMsgs) {
+    snapshotTree(catchUpMsgs, serializer, handle) {
         this.group.flush();
         this.checkStatus();
         const opts = this.options || {};
@@ -474,7 +523,7 @@ class MergeTreeClient {
         const entries = blobs.map((contents, i) => entry(i === 0 ? "header" : (v1 ? `body_${i - 1}` : "body"), contents));
         if (!v1 && catchUpMsgs !== undefined && catchUpMsgs.length > 0) {
             const name = opts.catchUpBlobName !== undefined && opts.catchUpBlobName !== null ? opts.catchUpBlobName : "catchupOps";
-            entries.push(entry(name, JSON.stringify(catchUpMsgs)));
+            entries.push(entry(name, serializer ? serializer.stringify(catchUpMsgs, handle) : JSON.stringify(catchUpMsgs)));
         }
         return { entries };
     }
@@ -495,20 +544,186 @@ class ClientGroup {
         const busy = this.clients.filter((c) => c.pending.length);
         if (!busy.length) return;
         const bb = new BatchBuilder(this.engine.props, null);
+        const listen = [];
         for (const c of busy) {
             bb.names = c.names;
             bb.beginDoc(c.docId);
-            for (const m of c.pending) bb.addMessage(m);
+            const entries = c.pending.map((m) => [m, bb.addMessage(m)]);
             c.pending = [];
+            if (c.deltaListener) listen.push([c, entries]);
             if (c.namesUploaded !== c.names.names.length) {     // snapshot "client" fields use long ids
                 addon.setDocClientNames(this.engine.h, c.docId, c.names.names.map((n) => JSON.stringify(n)));
                 c.namesUploaded = c.names.names.length;
             }
         }
-        this.engine.apply(bb.build());
+        const batch = bb.build();
+        if (listen.length) this.engine.deltaCapture(Math.max(4096, 64 * batch.type.length));
+        this.engine.apply(batch);
         this.engine.sync();
+        if (listen.length) this.deliver(listen);
+    }
+    /** Each listening client's messages with their sequenceDelta events: per op member, the
+     * INSERT / REMOVE / ANNOTATE records as ranges with their property maps. */
+    deliver(listen) {
+        const r = this.engine.deltaRecords();
+        const byOp = new Map();
+        for (let i = 0; i < r.length; i += 8) {
+            if (r[i + 1] < 0 || r[i + 1] > 2) continue;
+            if (!byOp.has(r[i])) byOp.set(r[i], []);
+            byOp.get(r[i]).push(i);
+        }
+        for (const [c, entries] of listen) {
+            c.checkStatus();
+            const cache = new Map();
+            const pset = (id) => {
+                if (!cache.has(id)) cache.set(id, this.engine.psetObject(c.docId, id));
+                return cache.get(id);
+            };
+            const eventsOf = (op) => (byOp.get(op) || []).map((i) => {
+                const kind = r[i + 1], a = r[i + 5], b = r[i + 6];
+                return { kind, pos: r[i + 2], len: r[i + 3],
+                    before: kind === OP_ANNOTATE ? pset(a) : undefined,
+                    after: kind === OP_ANNOTATE ? pset(b) : (kind === OP_INSERT ? pset(a) : undefined) };
+            });
+            c.deltaListener(entries, eventsOf);
+        }
     }
 }
 
+// ---- SharedSegmentSequence's merge-tree plumbing (packages/dds/sequence/src/sequence.ts) ----
+
+/** matchProperties (MT/properties.ts:64-95). */
+function matchProperties(a, b) {
+    if (a) {
+        if (!b) return false;
+        for (const key in a) {             // eslint-disable-line guard-for-in
+            if (b[key] === undefined) return false;
+            else if (typeof b[key] === "object") { if (!matchProperties(a[key], b[key])) return false; }
+            else if (b[key] !== a[key]) return false;
+        }
+        for (const key in b) if (a[key] === undefined) return false;     // eslint-disable-line guard-for-in
+    } else if (b) return false;
+    return true;
+}
+
+/** Object.keys of SegmentPropertiesManager.addProperties' deltas for a sequenced annotate on an
+ * observer (segmentPropertiesManager.ts:67-112): under "rewrite", the keys it deletes (falsy
+ * in the op) in the segment's key order, then every key of the op's props. */
+function annotateDeltaKeys(op, before) {
+    const deltas = {};
+    const newProps = op.props || {};
+    if (op.combiningOp && op.combiningOp.name === "rewrite" && before) {
+        for (const key of Object.keys(before)) if (!newProps[key]) deltas[key] = null;
+    }
+    for (const key of Object.keys(newProps)) deltas[key] = null;
+    return Object.keys(deltas);
+}
+
+/** segment.clone().toJSONObject() of an inserted segment (textSegment.ts:48-54, mergeTree.ts:649-653). */
+function segmentJson(opSeg, props) {
+    if (typeof opSeg === "string" || opSeg.text !== undefined) {
+        const text = typeof opSeg === "string" ? opSeg : opSeg.text;
+        return props ? { text, props } : text;
+    }
+    const o = { marker: { refType: opSeg.marker.refType } };
+    if (props) o.props = props;
+    return o;
+}
+
+/** createOpsFromDelta (sequence.ts:58-105) for one op's sequenceDelta event (ranges in order). */
+function opsFromDelta(member, ranges) {
+    const ops = [];
+    for (const r of ranges) {
+        if (r.kind === OP_ANNOTATE) {
+            const last = ops[ops.length - 1];
+            const after = r.after || {};
+            const props = {};
+            for (const key of annotateDeltaKeys(member, r.before)) props[key] = after[key] === undefined ? null : after[key];
+            if (last && last.pos2 === r.pos && matchProperties(last.props, props)) last.pos2 += r.len;
+            else ops.push({ pos1: r.pos, pos2: r.pos + r.len, props, type: OP_ANNOTATE });
+        } else if (r.kind === OP_INSERT) {
+            ops.push({ pos1: r.pos, seg: segmentJson(member.seg, r.after), type: OP_INSERT });
+        } else if (r.kind === OP_REMOVE) {
+            const last = ops[ops.length - 1];
+            if (last && last.pos1 === r.pos) last.pos2 += r.len;
+            else ops.push({ pos1: r.pos, pos2: r.pos + r.len, type: OP_REMOVE });
+        }
+    }
+    return ops;
+}
+
+/**
+ * One SharedString channel's merge-tree plumbing on a ClientGroup document (the part of
+ * SharedSegmentSequence on the replay path):
+ *   processCore(message)   -> processMergeTreeMsg (sequence.ts:604-642): Client.applyMsg, and
+ *                             for the legacy format the stash of sequenced ops, the ones with
+ *                             refSeq !== seq - 1 rebuilt from their sequenceDelta events
+ *                             (the engine's delta records) with refSeq = seq - 1
+ *   snapshotMergeTree(serializer) (sequence.ts:592-602) -> Client.snapshot with the stash
+ *   loadCore(storage)      -> Client.load, then the catch-up ops through processMergeTreeMsg
+ * `runtime` supplies options and deltaManager {minimumSequenceNumber, lastSequenceNumber}.
+ * The stash's transformations resolve when the group flushes (any read).
+ */
+class SequenceChannel {
+    constructor(group, runtime) {
+        this.runtime = runtime;
+        const options = (runtime && runtime.options) || {};
+        this.client = group.newClient(options);
+        this.client.startOrUpdateCollaboration(runtime && runtime.clientId);
+        this.legacy = options.newMergeTreeSnapshotFormat !== true;
+        this.messagesSinceMSNChange = [];
+        if (this.legacy) this.client.deltaListener = (entries, eventsOf) => this.stash(entries, eventsOf);
+    }
+    processCore(message, local) {
+        if (message.type !== "op") throw new Error("Sequence message not operation");     // sequence.ts:559
+        this.client.applyMsg(JSON.parse(JSON.stringify(message)));      // parseHandles: the channel's own copy
+    }
+    stash(entries, eventsOf) {
+        for (const [message, opIds] of entries) {
+            let stashMessage = message;
+            if (message.referenceSequenceNumber !== message.sequenceNumber - 1) {
+                const ops = [];
+                mergeTreeMembers(message.contents).forEach((m, i) => { ops.push(...opsFromDelta(m, eventsOf(opIds[i]))); });
+                stashMessage = { ...message, referenceSequenceNumber: message.sequenceNumber - 1,
+                    contents: ops.length !== 1 ? { ops, type: OP_GROUP } : ops[0] };
+            }
+            this.messagesSinceMSNChange.push(stashMessage);
+            if (this.messagesSinceMSNChange.length > 20
+                && this.messagesSinceMSNChange[20].sequenceNumber < message.minimumSequenceNumber) {
+                this.processMinSequenceNumberChanged(message.minimumSequenceNumber);
+            }
+        }
+    }
+    processMinSequenceNumberChanged(minSeq) {           // sequence.ts:648-658
+        let index = 0;
+        for (; index < this.messagesSinceMSNChange.length; index++) {
+            if (this.messagesSinceMSNChange[index].sequenceNumber > minSeq) break;
+        }
+        if (index !== 0) this.messagesSinceMSNChange = this.messagesSinceMSNChange.slice(index);
+    }
+    snapshotMergeTree(serializer, handle) {
+        this.client.group.flush();
+        const minSeq = this.runtime.deltaManager.minimumSequenceNumber;
+        this.processMinSequenceNumberChanged(minSeq);
+        this.messagesSinceMSNChange.forEach((m) => { m.minimumSequenceNumber = minSeq; });
+        return this.client.snapshot(this.runtime, handle, serializer, this.messagesSinceMSNChange);
+    }
+    /** loadCore (sequence.ts:496-541) for the merge-tree part of the channel's storage. */
+    async loadCore(storage, serializer) {
+        const { catchupOpsP } = await this.client.load(this.runtime, storage, serializer);
+        for (const m of await catchupOpsP) {
+            const w = { minSeq: this.client.minSeq, currentSeq: this.client.currentSeq };
+            if (m.minimumSequenceNumber < w.minSeq || m.referenceSequenceNumber < w.minSeq
+                || m.sequenceNumber <= w.minSeq || m.sequenceNumber <= w.currentSeq) {
+                throw new Error(`Invalid catchup operations in snapshot: ${JSON.stringify({
+                    op: { seq: m.sequenceNumber, minSeq: m.minimumSequenceNumber, refSeq: m.referenceSequenceNumber },
+                    collabWindow: { seq: w.currentSeq, minSeq: w.minSeq } })}`);
+            }
+            this.processCore(m, false);
+        }
+    }
+    getText() { return this.client.getText(); }
+}
+
 module.exports = { addon, Engine, ClientGroup, MergeTreeClient, BatchBuilder, PropTable, ClientNames, statusNames,
-    LoadBuilder, parseSnapshot };
+    LoadBuilder, parseSnapshot, SequenceChannel, opsFromDelta, matchProperties };

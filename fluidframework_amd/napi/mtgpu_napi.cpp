@@ -448,6 +448,46 @@ napi_value GetText(napi_env env, napi_callback_info info) {
     return out;
 }
 
+// deltaCapture(ctx, capacity): record the delta / maintenance callbacks of later batches
+napi_value DeltaCapture(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
+    int64_t cap = 0; napi_get_value_int64(env, argv[1], &cap);
+    int rc = mt_delta_capture(c, cap > 0 ? (uint64_t)cap : 0);
+    return rc ? throw_rc(env, c, rc, "mt_delta_capture") : undefined(env);
+}
+
+// deltaRecords(ctx) -> Int32Array of 8 per record (mt_delta_rec: op, kind, pos, len, seg, a, b, pad)
+napi_value DeltaRecords(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
+    const mt_delta_rec* r = nullptr; uint64_t n = 0;
+    int rc = mt_delta_records(c, &r, &n);
+    if (rc) return throw_rc(env, c, rc, "mt_delta_records");
+    return make_i32(env, (const int32_t*)r, (size_t)n * 8);
+}
+
+// docPset(ctx, doc, id) -> {keys: Uint32Array, values: Int32Array} (interned ids, insertion order)
+napi_value DocPset(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return nullptr;
+    mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
+    uint32_t doc = 0; int32_t id = -1;
+    napi_get_value_uint32(env, argv[1], &doc); napi_get_value_int32(env, argv[2], &id);
+    uint16_t k[16]; int32_t v[16]; uint32_t n = 0;
+    int rc = mt_doc_pset(c, doc, id, k, v, &n);
+    if (rc) return throw_rc(env, c, rc, "mt_doc_pset");
+    uint32_t k32[16];
+    for (uint32_t i = 0; i < n; i++) k32[i] = k[i];
+    napi_value o;
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "keys", make_u32(env, k32, n));
+    napi_set_named_property(env, o, "values", make_i32(env, v, n));
+    return o;
+}
+
 napi_value LastError(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     if (!get_args(env, info, 1, argv)) return nullptr;
@@ -478,6 +518,9 @@ napi_value Init(napi_env env, napi_value exports) {
         {"snapshotV1", nullptr, SnapshotV1, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"snapshotLegacy", nullptr, SnapshotLegacy, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"getText", nullptr, GetText, nullptr, nullptr, nullptr, kAttr, nullptr},
+        {"deltaCapture", nullptr, DeltaCapture, nullptr, nullptr, nullptr, kAttr, nullptr},
+        {"deltaRecords", nullptr, DeltaRecords, nullptr, nullptr, nullptr, kAttr, nullptr},
+        {"docPset", nullptr, DocPset, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"lastError", nullptr, LastError, nullptr, nullptr, nullptr, kAttr, nullptr},
     };
     napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);

@@ -218,5 +218,21 @@ class SequenceDoc:
         self.client.updateSeqNumbers(m, s)
         return self.client.snapshot(self.messagesSinceMSNChange if self.legacy else None, min_seq=m, seq=s)
 
+    def load(self, blobs: dict):
+        """loadCore (sequence.ts:496-541) for the merge-tree blobs: Client.load, then the
+        catch-up messages through processMergeTreeMsg after the window checks."""
+        out = self.client.load(blobs)
+        self.last_msn, self.last_seq = self.client.min_seq, self.client.current_seq
+        for m in out["catchupOps"]:
+            lo, cur = self.client.min_seq, self.client.current_seq
+            if m["minimumSequenceNumber"] < lo or m["referenceSequenceNumber"] < lo or \
+                    m["sequenceNumber"] <= lo or m["sequenceNumber"] <= cur:
+                raise ValueError("Invalid catchup operations in snapshot: " + jsjson.stringify(
+                    {"op": {"seq": m["sequenceNumber"], "minSeq": m["minimumSequenceNumber"],
+                            "refSeq": m["referenceSequenceNumber"]},
+                     "collabWindow": {"seq": cur, "minSeq": lo}}))
+            self.process(m)
+            self.client.current_seq = int(m["sequenceNumber"])
+
     def getText(self) -> str:
         return self.client.getText()

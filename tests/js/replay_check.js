@@ -19,17 +19,17 @@ const clients = spec.docs.map(() => {
     return c;
 });
 // optional: load a snapshot into each document first (Client.load / SnapshotLoader)
-if (spec.loads) spec.loads.forEach((blobs, d) => { if (blobs) clients[d].load(blobs); });
+if (spec.loads) spec.loads.forEach((blobs, d) => { if (blobs) clients[d].loadBlobs(blobs); });
 spec.docs.forEach((msgs, d) => { for (const m of msgs) clients[d].applyMsg(m); });
 const out = { texts: [], lengths: [], blobs: [], digests: [], legacy: [] };
 clients.forEach((c, d) => {
     out.texts.push(c.getText());
     out.lengths.push(c.getLength());
-    out.blobs.push(c.snapshot().entries.map((e) => [e.path, e.value.contents]));
+    out.blobs.push(c.snapshotTree().entries.map((e) => [e.path, e.value.contents]));
     if (spec.legacy) {      // the reference's default format: a Client without newMergeTreeSnapshotFormat
         const opts = c.options;
         c.options = spec.legacy.options || {};
-        out.legacy.push(c.snapshot(spec.legacy.catchUp ? spec.legacy.catchUp[d] : undefined).entries
+        out.legacy.push(c.snapshotTree(spec.legacy.catchUp ? spec.legacy.catchUp[d] : undefined).entries
             .map((e) => [e.path, e.value.contents]));
         c.options = opts;
     }

@@ -43,6 +43,18 @@ def batch_to_messages(batch, props, run):
     return out
 
 
+def run_driver(name, spec, addon=None, timeout=240):
+    """Run tests/js/<name> on a JSON spec; returns its JSON output."""
+    env = dict(os.environ)
+    if addon:
+        env["MTGPU_NAPI"] = addon
+    with tempfile.TemporaryDirectory() as td:
+        ip, op = os.path.join(td, "in.json"), os.path.join(td, "out.json")
+        json.dump(spec, open(ip, "w"))
+        subprocess.run([NODE, os.path.join(ROOT, "tests", "js", name), ip, op], check=True, env=env, timeout=timeout)
+        return json.load(open(op))
+
+
 def run_node(doc_msgs, addon=None, limits=None, timeout=240, loads=None, legacy=None):
     env = dict(os.environ)
     if addon:
