@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 from emu_lib import emu_engine
+from fluidframework_amd.engine import Engine
 from fluidframework_amd.batch import concat_runs as concat
 from oracle_lib import gen_params, generate, replay
 from test_emu_parity import NAMES, ann_props
@@ -38,25 +39,23 @@ def test_prebuild_generator_matches_oracle():
         assert np.array_equal(eng.dump(d), kept[d].dump())
 
 
-@pytest.mark.parametrize("lag", [64, 512])
-def test_deep_window_on_checkpoint_matches_oracle(lag):
+def check_deep_window(factory, n, pre, ops, lag, rows, window, text, psets=8192):
     props = ann_props()
-    n = 2
-    eng = emu_engine(n, rows_per_doc=12000, window_per_doc=8192, propsets_per_doc=8192, text_per_doc=1 << 16)
+    eng = factory(n, rows_per_doc=rows, window_per_doc=window, propsets_per_doc=psets, text_per_doc=text)
     eng.upload_props(props)
     eng.upload_names(NAMES)
-    pa = prebuild_params(n, 3000)
+    pa = prebuild_params(n, pre)
     eng.generate(pa)
     eng.sync()
     a = eng.generated_download()
     eng.checkpoint()
-    pb = gen_params(seed=505, n_docs=n, ops=1500, clients=8, lag=lag, ins=60, rem=40, ins_len=8, rem_len=8)
+    pb = gen_params(seed=505, n_docs=n, ops=ops, clients=8, lag=lag, ins=60, rem=40, ins_len=8, rem_len=8)
     pb.continue_docs = 1
     eng.generate(pb)
     eng.sync()
     assert (eng.status(range(n)) == 0).all()
     b = eng.generated_download()
-    assert (b.arrays["seq"][b.op_offsets[:-1]] == 3001).all()        # continues the pre-built documents
+    assert (b.arrays["seq"][b.op_offsets[:-1]] == pre + 1).all()     # continues the pre-built documents
     neg = np.full(n, -1, np.int32)
     dig_gen = eng.snapshot_digests(range(n), neg, neg, threads=2)
     eng.restore()
@@ -73,3 +72,18 @@ def test_deep_window_on_checkpoint_matches_oracle(lag):
         assert eng.get_text([d])[0] == od.get_text()
         assert np.array_equal(eng.dump(d), od.dump())
         assert int(dig_replay[d]) == od.snapshot(int(both.arrays["msn"][last[d]]), int(both.arrays["seq"][last[d]]))[1]
+
+
+@pytest.mark.parametrize("lag", [64, 512])
+def test_deep_window_on_checkpoint_matches_oracle(lag):
+    check_deep_window(emu_engine, 2, 3000, 1500, lag, rows=12000, window=8192, text=1 << 16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lag", [512, 1024])
+def test_gpu_config4_downscaled_matches_oracle(lag):
+    """SURVEY §8(c)'s config-4 down-scale on the device: 2 documents pre-built to 20k
+    segments, checkpointed, then a deep-window stream (lag up to 1,024, tree height 5+)
+    generated on top and replayed from the restored checkpoint."""
+    check_deep_window(lambda n, **kw: Engine(n, device=0, **kw), 2, 20000, 4000, lag,
+                      rows=40000, window=16384, text=1 << 18, psets=40000)
