@@ -113,7 +113,8 @@ __global__ __launch_bounds__(64) void mt_get_length_kernel(MtState S, const uint
     const uint32_t doc = docs[blockIdx.x];
     MtEng e;
     e.bind(S, doc, &sc);
-    const int l = e.perspectiveLength(ref[blockIdx.x], cli[blockIdx.x] < 0 ? MT_NOBODY : cli[blockIdx.x]);
+    // read-only: queries of one document run in parallel workgroups
+    const int l = e.perspectiveLengthRO(ref[blockIdx.x], cli[blockIdx.x] < 0 ? MT_NOBODY : cli[blockIdx.x]);
     if (__lane_id() == 0) out[blockIdx.x] = l;
 }
 

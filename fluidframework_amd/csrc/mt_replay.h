@@ -111,6 +111,8 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
             if (ty == MT_OP_INSERT && !(fl & MT_OPF_MARKER) && (uint64_t)poff + (uint64_t)plen > ops.payload_units)
                 e.status |= MT_DS_BAD_OP;
             if (e.status) break;
+            const bool pre = ty == MT_OP_INSERT && !(fl & MT_OPF_MARKER) && plen <= MT_WAVE;
+            const auto pay = wave_map(pre ? plen : 0, [&](int k) MT_LAM { return (int)ops.payload[poff + (uint32_t)k]; });
             if (!(e.uValid && e.uRef == r && e.uCli == c)) e.computeU(r, c, true);
             int q1 = p1, q2 = p2;
             if (fl & (MT_OPF_REL1 | MT_OPF_REL2)) {       // getValidOpRange (MT/client.ts:506-523)
@@ -123,7 +125,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
             if (ty == MT_OP_INSERT) {
                 const bool marker = (fl & MT_OPF_MARKER) != 0;
                 e.opInsert(q1, r, c, sq, ops.payload + poff, plen, marker, p2, (fl & MT_OPF_SEG_PROPS) ? pid : -1,
-                           (marker && (fl & MT_OPF_MARKER_ID)) ? (int)poff : -1);
+                           (marker && (fl & MT_OPF_MARKER_ID)) ? (int)poff : -1, pay);
             } else if (ty == MT_OP_REMOVE) {
                 e.opRange(MT_MAP_REMOVE, q1, q2, r, c, sq, -1, false);
             } else if (ty == MT_OP_ANNOTATE) {

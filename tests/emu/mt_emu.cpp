@@ -91,7 +91,7 @@ static int mtb_launch_update_seq(mt_ctx* c, const uint32_t* docs, const int32_t*
 static int mtb_launch_get_length(mt_ctx* c, const uint32_t* docs, const int32_t* ref, const int32_t* cli, int32_t* out, uint32_t n) {
     for (uint32_t i = 0; i < n; i++) {
         MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc);
-        out[i] = e.perspectiveLength(ref[i], cli[i] < 0 ? MT_NOBODY : cli[i]);
+        out[i] = e.perspectiveLengthRO(ref[i], cli[i] < 0 ? MT_NOBODY : cli[i]);
     }
     return MT_OK;
 }

@@ -95,6 +95,11 @@ def test_gpu_get_length_matches_oracle():
             got = eng.get_length(range(4), refs, [c] * 4)
             want = [kept[d].get_length(int(refs[d]), c) for d in range(4)]
             assert list(got) == want
+    # many perspectives of the same documents in one call (one workgroup per query)
+    q = [(d, int(max(seqs[d] - lag, batch.arrays["msn"][batch.op_offsets[d + 1] - 1])), c)
+         for d in range(4) for lag in range(0, 33, 4) for c in range(8)]
+    got = eng.get_length([x[0] for x in q], [x[1] for x in q], [x[2] for x in q])
+    assert list(got) == [kept[d].get_length(r, c) for d, r, c in q]
 
 
 def test_gpu_per_document_capacities_and_generator_counts():
