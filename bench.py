@@ -440,6 +440,82 @@ def cpu_baseline_config5(args, c, local):
     return res
 
 
+def batch_messages(batch, run):
+    """ISequencedDocumentMessage dicts (protocol.ts:126-166) of one generated run; client i
+    is "c{i}" (the ingest leg's input, built untimed)."""
+    a = batch.arrays
+    o0, o1 = int(batch.op_offsets[run]), int(batch.op_offsets[run + 1])
+    pay = batch.payload
+    out = []
+    for i in range(o0, o1):
+        t = int(a["type"][i])
+        m = {"clientId": f"c{int(a['client'][i])}", "sequenceNumber": int(a["seq"][i]),
+             "referenceSequenceNumber": int(a["ref_seq"][i]), "minimumSequenceNumber": int(a["msn"][i]), "type": "op"}
+        if t == 0:
+            po, pl = int(a["payload_off"][i]), int(a["payload_len"][i])
+            m["contents"] = {"type": 0, "pos1": int(a["pos1"][i]), "seg": pay[po:po + pl].tobytes().decode("utf-16-le")}
+        else:
+            m["contents"] = {"type": t, "pos1": int(a["pos1"][i]), "pos2": int(a["pos2"][i])}
+            if t == 2:
+                m["contents"]["props"] = {"k0": "v"}
+        out.append(m)
+    return out
+
+
+def ingest_leg(local, c, seed, sample_docs=64):
+    """Host ingest (host packing and H2D reported, not hidden): the
+    messages of `sample_docs` documents of the workload packed by the Python host
+    (fluidframework_amd.batch.BatchBuilder) and by the Node host (js/index.js
+    BatchBuilder), and the packed batch's upload to HBM (mt_upload_batch + sync)."""
+    import shutil
+    import subprocess
+    import tempfile
+    from fluidframework_amd.batch import BatchBuilder, ClientNames, MtGenParams, PropTable
+    n = min(sample_docs, c["docs"])
+    eng = Host.engine(n, local, **caps_for(dict(c, docs=n)))
+    eng.upload_props(ann_props())
+    eng.upload_names(['"c%d"' % i for i in range(64)])
+    eng.generate(MtGenParams(seed, n, c["ops"], c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"],
+                             c["rem_len"], c["ann_sets"], c["rewrite"]))
+    eng.sync()
+    docs = [batch_messages(eng.generated_download(), d) for d in range(n)]
+    msgs = sum(len(d) for d in docs)
+    t0 = time.perf_counter()
+    bb = BatchBuilder(PropTable(), None)
+    for d, lst in enumerate(docs):
+        bb.names = ClientNames()
+        bb.begin_doc(d)
+        for m in lst:
+            bb.add_message(m)
+    batch = bb.build()
+    py_s = time.perf_counter() - t0
+    eng.open_docs(0, n)
+    eng.sync()
+    t0 = time.perf_counter()
+    eng.upload(batch)
+    eng.sync()
+    h2d_s = time.perf_counter() - t0
+    h2d_bytes = int(batch.n_ops) * 32 + int(batch.payload.nbytes)
+    node = None
+    exe = shutil.which("node")
+    if exe:
+        with tempfile.TemporaryDirectory() as td:
+            fp = os.path.join(td, "msgs.json")
+            with open(fp, "w") as f:
+                json.dump(docs, f)
+            r = subprocess.run([exe, os.path.join(ROOT, "fluidframework_amd", "js", "pack_bench.js"), fp],
+                               capture_output=True, text=True, timeout=600)
+            if r.returncode == 0:
+                node = json.loads(r.stdout.strip().splitlines()[-1])
+    eng.close()
+    return {"sample": f"{n} docs x {c['ops']} msgs of the workload ({msgs} messages, one op each)",
+            "python_pack_msgs_per_s": msgs / py_s,
+            "node_pack_msgs_per_s": (node["msgs"] / (node["ms"] / 1e3)) if node else None,
+            "h2d_msgs_per_s": msgs / h2d_s, "h2d_GBps": h2d_bytes / h2d_s / 1e9, "h2d_bytes": h2d_bytes,
+            "note": "single host thread per packer; H2D = mt_upload_batch (pageable host arrays -> HBM) + sync; "
+                    "the timed replay starts from resident streams, these rates bound a live ingest path"}
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -451,6 +527,7 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=20241015)
     ap.add_argument("--prebuild", type=int, default=0, help="config4: override pre-build appends per document")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the host ingest leg (packers, H2D)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--residency", default="blk", choices=["lds", "hbm", "blk"],
                     help="blk: blocks + heap in LDS, in-wave HBM continuation (default); hbm: every pool in HBM; "
@@ -601,6 +678,8 @@ def main(argv=None):
         out["cpu_baseline"], odg, ost = cpu_baseline(eng, c, MtGenParams, seed, args.cpu_seconds, threads)
         if ok:
             out["parity"] = digest_parity(digs, odg, ost)
+    if world == 1 and not args.no_ingest:
+        out["ingest"] = ingest_leg(local, c, seed)
     print(json.dumps(out), flush=True)
 
 

@@ -12,5 +12,3 @@ for flag in MT_PROFILE MT_PROFILE2; do
   MT_PROF_FLAG=$flag timeout -k 10 400 python tools/phase_config4.py 256 200000 5000 > $O/c4_${flag}.log 2>&1 || { echo FAIL c4 $flag; tail -20 $O/c4_${flag}.log; exit 1; }
   cat $O/c4_${flag}.log
 done
-bash tools/gpu_sq_counters.sh > $O/sq.log 2>&1 || { tail -20 $O/sq.log; exit 1; }
-cat $O/sq.log
