@@ -11,10 +11,18 @@ DEPS = [SRC, os.path.join(ROOT, "include", "mtgpu.h")] + [os.path.join(ROOT, "fl
                 ("mt_core.h", "mt_replay.h", "mt_snapshot.h", "mt_pack.h", "mt_api_impl.h", "mt_ctx.h", "wave.h")]
 
 
+def _atomic_build(cmd, out):
+    """Compile to a private temporary name and rename over `out`, so parallel test
+    workers (pytest -n) never load a half-written library."""
+    tmp = f"{out}.{os.getpid()}.tmp"
+    subprocess.check_call([tmp if a is None else a for a in cmd])
+    os.replace(tmp, out)
+
+
 def build_emu(force=False):
     if force or not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(d) for d in DEPS):
-        subprocess.check_call(["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wno-unknown-pragmas",
-                               "-o", LIB, SRC])
+        _atomic_build(["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wno-unknown-pragmas",
+                       "-o", None, SRC], LIB)
     return LIB
 
 
@@ -39,9 +47,11 @@ def build_emu_napi():
     names = sorted(set(re.findall(r"\b(mt_[a-z0-9_]+)\s*\(", open(hdr).read())))
     text = "".join(f"#define {n} emu_{n[3:]}\n" for n in names)
     if not os.path.exists(ren) or open(ren).read() != text:
-        open(ren, "w").write(text)
+        tmp = f"{ren}.{os.getpid()}.tmp"
+        open(tmp, "w").write(text)
+        os.replace(tmp, ren)
     deps = [src, hdr, lib, ren]
     if not os.path.exists(NAPI_EMU) or any(os.path.getmtime(NAPI_EMU) < os.path.getmtime(d) for d in deps):
-        subprocess.check_call(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-I/usr/include/node", "-include", ren,
-                               "-o", NAPI_EMU, src, lib, "-Wl,-rpath," + os.path.dirname(lib)])
+        _atomic_build(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-I/usr/include/node", "-include", ren,
+                       "-o", None, src, lib, "-Wl,-rpath," + os.path.dirname(lib)], NAPI_EMU)
     return NAPI_EMU

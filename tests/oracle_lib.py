@@ -21,7 +21,9 @@ LIB = os.path.join(ROOT, "oracle", "_build", "libmtoracle.so")
 def build_oracle(force: bool = False) -> str:
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
         os.makedirs(os.path.dirname(LIB), exist_ok=True)
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", LIB, SRC])
+        tmp = f"{LIB}.{os.getpid()}.tmp"  # rename into place: parallel workers never load a partial file
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", tmp, SRC])
+        os.replace(tmp, LIB)
     return LIB
 
 
