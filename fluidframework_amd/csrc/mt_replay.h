@@ -77,7 +77,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
     // Replay prefetches op i+1's record while op i runs (generation writes the
     // record at the top of each iteration, so it loads in place).
     auto wn = wave_map(8, [&](int q) MT_LAM { return (!g && o0 < o1) ? ((const int*)&ops.rec[o0])[q] : 0; });
-    if (!g) { e.drec = ops.drec; e.dcount = ops.dcount; e.dcap = ops.dcap; }
+    if (!g && Eng::kRec) { e.drec = ops.drec; e.dcount = ops.dcount; e.dcap = ops.dcap; }
     for (uint32_t i = o0; i < o1; i++) {
         e.curOp = i;
         if (Eng::kLds && !e.ldsHeadroom()) return i;

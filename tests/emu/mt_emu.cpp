@@ -19,6 +19,44 @@ static void mtb_h2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n)
 static void mtb_d2h(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static void mtb_d2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static int mtb_sync(mt_ctx*) { return MT_OK; }
+// REC as on the device: the capture instantiation only while a delta buffer is armed.
+template <bool REC>
+static void replay_runs(mt_ctx* c, uint32_t n_runs) {
+    uint32_t* cursor = (uint32_t*)c->b_cursor.p;
+    for (uint32_t run = 0; run < n_runs; run++) {
+        const uint32_t doc = c->ops.doc_ids[run], o0 = c->ops.op_off[run];
+        uint32_t cur = o0;
+        if (c->use_lds == 2) {
+            MtScratch sc; MtEngT<MT_RES_BLK, REC> e; e.bind(c->S, doc, &sc);
+            if (e.toLds(0, c->lds_blks, c->lds_heap)) {
+                cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
+                e.fromLds();
+            }
+            e.store(doc);
+            if (cur < c->ops.op_off[run + 1]) {               // continues in HBM within the same "wave"
+                MtEngT<MT_RES_HBM, REC> h; h.bind(c->S, doc, &sc);
+                mt_replay_run(h, c->ops, run, doc, nullptr, nullptr, cur);
+                h.store(doc);
+                // cursor keeps the hand-over point (diagnostic); the HBM pass below skips it
+            }
+        } else if (c->use_lds) {
+            MtScratch sc; MtEngT<MT_RES_LDS, REC> e; e.bind(c->S, doc, &sc);
+            if (e.toLds(c->lds_rows, c->lds_blks, c->lds_heap)) {
+                cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
+                e.fromLds();
+            }
+            e.store(doc);
+        }
+        cursor[run] = cur;
+    }
+    for (uint32_t run = 0; run < n_runs && c->use_lds != 2; run++) {
+        if (cursor[run] >= c->ops.op_off[run + 1]) continue;
+        const uint32_t doc = c->ops.doc_ids[run];
+        MtScratch sc; MtEngT<MT_RES_HBM, REC> e; e.bind(c->S, doc, &sc);
+        mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, cursor[run]);
+        e.store(doc);
+    }
+}
 // Same two launches as the device (mt_engine.hip): LDS-resident pass, then the
 // HBM pass resuming at each run's cursor.
 static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
@@ -32,40 +70,8 @@ static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
         }
         return MT_OK;
     }
-    uint32_t* cursor = (uint32_t*)c->b_cursor.p;
-    for (uint32_t run = 0; run < n_runs; run++) {
-        const uint32_t doc = c->ops.doc_ids[run], o0 = c->ops.op_off[run];
-        uint32_t cur = o0;
-        if (c->use_lds == 2) {
-            MtScratch sc; MtEngT<MT_RES_BLK> e; e.bind(c->S, doc, &sc);
-            if (e.toLds(0, c->lds_blks, c->lds_heap)) {
-                cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
-                e.fromLds();
-            }
-            e.store(doc);
-            if (cur < c->ops.op_off[run + 1]) {               // continues in HBM within the same "wave"
-                MtEng h; h.bind(c->S, doc, &sc);
-                mt_replay_run(h, c->ops, run, doc, nullptr, nullptr, cur);
-                h.store(doc);
-                // cursor keeps the hand-over point (diagnostic); the HBM pass below skips it
-            }
-        } else if (c->use_lds) {
-            MtScratch sc; MtEngT<MT_RES_LDS> e; e.bind(c->S, doc, &sc);
-            if (e.toLds(c->lds_rows, c->lds_blks, c->lds_heap)) {
-                cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
-                e.fromLds();
-            }
-            e.store(doc);
-        }
-        cursor[run] = cur;
-    }
-    for (uint32_t run = 0; run < n_runs && c->use_lds != 2; run++) {
-        if (cursor[run] >= c->ops.op_off[run + 1]) continue;
-        const uint32_t doc = c->ops.doc_ids[run];
-        MtScratch sc; MtEng e; e.bind(c->S, doc, &sc);
-        mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, cursor[run]);
-        e.store(doc);
-    }
+    if (c->ops.drec) replay_runs<true>(c, n_runs);
+    else replay_runs<false>(c, n_runs);
     return MT_OK;
 }
 static int mtb_launch_open(mt_ctx* c, uint32_t first, uint32_t n) {
