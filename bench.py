@@ -31,9 +31,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0
-RESIDENCY = {"hbm": 0, "lds": 1, "blk": 2}
+RESIDENCY = {"hbm": 0, "lds": 1, "blk": 2, "big": 3}
 REPLAY_KERNEL = {"hbm": "mt_replay_kernel", "lds": "mt_replay_lds_kernel + mt_replay_kernel",
-                 "blk": "mt_replay_blk_kernel"}  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+                 "blk": "mt_replay_blk_kernel", "big": "mt_replay_big_kernel"}  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 
 CONFIGS = {
     # name: (docs, ops, clients, lag, ins%, rem%, ins_len, rem_len, ann_sets, rewrite%)
@@ -529,11 +529,14 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the host ingest leg (packers, H2D)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--residency", default="blk", choices=["lds", "hbm", "blk"],
-                    help="blk: blocks + heap in LDS, in-wave HBM continuation (default); hbm: every pool in HBM; "
-                         "lds: rows/blocks/heap/window in LDS")
+    ap.add_argument("--residency", default="auto", choices=["auto", "lds", "hbm", "blk", "big"],
+                    help="blk: blocks + heap in LDS, in-wave HBM continuation; big: heap + window + U set in LDS "
+                         "for long documents; hbm: every pool in HBM; lds: rows/blocks/heap/window in LDS; "
+                         "auto (default): big for config4, blk otherwise")
     ap.add_argument("--caps", default="", help="override pool caps, e.g. rows_per_doc=400,text_per_doc=16384")
     args = ap.parse_args(argv)
+    if args.residency == "auto":
+        args.residency = "big" if args.config == "config4" else "blk"
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU: re-enter this script under torch.distributed.run

@@ -413,13 +413,15 @@ int MT_FN(doc_pset)(mt_ctx* c, uint32_t doc, int32_t id, uint16_t* keys, int32_t
     return MT_OK;
 }
 int MT_FN(set_residency)(mt_ctx* c, int use_lds, int rows, int blocks, int heap) {
-    if (!c || use_lds < 0 || use_lds > 2 || rows < 0 || blocks < 0 || heap < 0 || rows > MT_L_ROWS ||
-        blocks > (use_lds == 2 ? MT_B_BLKS : MT_L_BLKS) || heap > (use_lds == 2 ? MT_B_HEAP : MT_L_HEAP))
+    const int maxHeap = use_lds == 3 ? MT_G_HEAP : (use_lds == 2 ? MT_B_HEAP : MT_L_HEAP);
+    if (!c || use_lds < 0 || use_lds > 3 || rows < 0 || blocks < 0 || heap < 0 ||
+        rows > (use_lds == 3 ? MT_G_WIN : MT_L_ROWS) ||
+        blocks > (use_lds == 2 ? MT_B_BLKS : MT_L_BLKS) || heap > maxHeap)
         return MT_E_INVALID;
     c->use_lds = use_lds;
-    c->lds_rows = rows ? rows : MT_L_ROWS;
+    c->lds_rows = rows ? rows : (use_lds == 3 ? MT_G_WIN : MT_L_ROWS);   // 3: window entries in LDS
     c->lds_blks = blocks ? blocks : (use_lds == 2 ? MT_B_BLKS : MT_L_BLKS);
-    c->lds_heap = heap ? heap : (use_lds == 2 ? MT_B_HEAP : MT_L_HEAP);
+    c->lds_heap = heap ? heap : maxHeap;
     return MT_OK;
 }
 // Where each run of the last LDS-resident replay handed over to the HBM kernel

@@ -58,7 +58,21 @@
 #ifndef MT_B_HEAP
 #define MT_B_HEAP 94
 #endif
-enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2 };
+// Long-document residency (mt_replay_big_kernel): a document whose blocks cannot fit
+// LDS (config 4: ~50k blocks) keeps its zamboni heap, collab window and the first
+// MT_G_U U-set entries with their ancestor chains in LDS (~68 KB: two documents per CU),
+// rows and blocks in HBM.  Meant for launches with few documents per CU.
+#ifndef MT_G_U
+#define MT_G_U 768
+#endif
+#ifndef MT_G_HEAP
+#define MT_G_HEAP 2046
+#endif
+#ifndef MT_G_WIN
+#define MT_G_WIN 2048
+#endif
+#define MT_G_H 12                     // ancestor-chain levels kept per U entry (tree height < MT_G_H - 2)
+enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2, MT_RES_BIG = 3 };
 // Diagnostic builds keep per-document phase/event counters (prof[]) across binds;
 // product builds never load or store them (8 SGPR pairs fewer live in the replay loop).
 #if defined(MT_PROFILE) || defined(MT_PROFILE2) || defined(MT_PROFILE3) || defined(MT_EVCOUNT) || defined(MT_EVCOUNT2)
@@ -269,6 +283,15 @@ struct __attribute__((aligned(16))) MtLdsBlk {
     uint8_t uanc[MT_B_U * MT_L_H];    // block ids < MT_B_BLKS < 255; 255 = none
 };
 
+// LDS home of a long document's heap, window and U set while mt_replay_big_kernel runs it.
+struct __attribute__((aligned(16))) MtLdsBig {
+    MtHeapE heap[MT_G_HEAP + 2];
+    int win[MT_G_WIN];
+    int uid[MT_G_U], udelta[MT_G_U];
+    int uanc[MT_G_U * MT_G_H];        // block ids (-1 = none)
+    uint16_t ulist[MT_G_U];           // a descent's U entries under the current block (walk)
+};
+
 // per-wave scratch (LDS on the device)
 struct MtScratch {
     int pathB[MT_MAXH + 2], pathJ[MT_MAXH + 2];
@@ -338,12 +361,22 @@ __shared__ MtLdsBlk mt_ldsb_v;
 static MtLdsBlk mt_ldsb_v;
 #endif
 MT_INLINE MtLdsBlk& mt_ldsb() { return mt_ldsb_v; }
+#if defined(__HIP_DEVICE_COMPILE__)
+__shared__ MtLdsBig mt_ldsg_v;
+#else
+static MtLdsBig mt_ldsg_v;
+#endif
+MT_INLINE MtLdsBig& mt_ldsg() { return mt_ldsg_v; }
 
 // RES: MT_RES_HBM (every pool in HBM), MT_RES_LDS (rows, blocks, heap, window,
-// U set in LDS) or MT_RES_BLK (blocks and heap in LDS).
-template <int RES> struct MtEngT {
+// U set in LDS) or MT_RES_BLK (blocks and heap in LDS).  REC: the instantiation can
+// capture delta records (mt_set_delta_capture); the replay kernels launch REC=false
+// unless a capture buffer is armed, so the hot path carries none of that code.
+template <int RES, bool REC = true> struct MtEngT {
+    static constexpr bool kRec = REC;
     static constexpr bool LDS = RES == MT_RES_LDS;      // all hot pools in LDS
-    static constexpr bool BLKL = RES != MT_RES_HBM;     // blocks + heap in LDS
+    static constexpr bool BIG = RES == MT_RES_BIG;      // heap, window, U set in LDS; blocks in HBM
+    static constexpr bool BLKL = RES == MT_RES_LDS || RES == MT_RES_BLK;   // blocks + heap in LDS
     MtEngParams S;
     MtDocHdr* hdrp;
     // doc-local views
@@ -360,29 +393,59 @@ template <int RES> struct MtEngT {
         if constexpr (LDS) return mt_lds().blk[b]; else if constexpr (BLKL) return mt_ldsb().blk[b]; else return blk[b];
     }
     MT_HD MtHeapE& hp(int k) const {
-        if constexpr (LDS) return mt_lds().heap[k]; else if constexpr (BLKL) return mt_ldsb().heap[k]; else return heap[k];
+        if constexpr (LDS) return mt_lds().heap[k]; else if constexpr (BLKL) return mt_ldsb().heap[k];
+        else if constexpr (BIG) return mt_ldsg().heap[k]; else return heap[k];
     }
-    MT_HD int& wn(int k) const { if constexpr (LDS) return mt_lds().win[k]; else return win[k]; }
+    MT_HD int& wn(int k) const {
+        if constexpr (LDS) return mt_lds().win[k];
+        else if constexpr (BIG) { if (k < lRows) return mt_ldsg().win[k]; return win[k]; }   // beyond lRows: HBM home
+        else return win[k];
+    }
     MT_HD int& ui(int k) const { if constexpr (LDS) return mt_lds().uid[k]; else return uid[k]; }
     MT_HD int& ud(int k) const { if constexpr (LDS) return mt_lds().udelta[k]; else return udelta[k]; }
-    // MT_RES_BLK keeps the first MT_B_U U-set entries in LDS.  U loops run per
-    // 64-entry chunk (chunks never straddle MT_B_U), so each chunk picks its home
-    // at compile time: forU calls f(std::bool_constant<inLds>, base, m).
-    static constexpr bool UL = RES == MT_RES_BLK;
-    template <bool L> MT_HD int uiAt(int k) const { if constexpr (UL && L) return mt_ldsb().uid[k]; else return ui(k); }
-    template <bool L> MT_HD int udAt(int k) const { if constexpr (UL && L) return mt_ldsb().udelta[k]; else return ud(k); }
+    // MT_RES_BLK keeps the first MT_B_U U-set entries in LDS, MT_RES_BIG the first
+    // MT_G_U.  U loops run per 64-entry chunk (chunks never straddle the cap), so each
+    // chunk picks its home at compile time: forU calls f(std::bool_constant<inLds>, base, m).
+    static constexpr bool UL = RES == MT_RES_BLK || RES == MT_RES_BIG;
+    static constexpr int UCAP = RES == MT_RES_BLK ? MT_B_U : (RES == MT_RES_BIG ? MT_G_U : 0);
+    template <bool L> MT_HD int uiAt(int k) const {
+        if constexpr (UL && L) { if constexpr (BIG) return mt_ldsg().uid[k]; else return mt_ldsb().uid[k]; }
+        else return ui(k);
+    }
+    template <bool L> MT_HD int udAt(int k) const {
+        if constexpr (UL && L) { if constexpr (BIG) return mt_ldsg().udelta[k]; else return mt_ldsb().udelta[k]; }
+        else return ud(k);
+    }
+    template <bool L> MT_HD void uPutAt(int k, int id, int delta) {
+        if constexpr (UL && L) {
+            if constexpr (BIG) { mt_ldsg().uid[k] = id; mt_ldsg().udelta[k] = delta; }
+            else { mt_ldsb().uid[k] = id; mt_ldsb().udelta[k] = delta; }
+        } else { ui(k) = id; ud(k) = delta; }
+    }
     template <bool L> MT_HD void ancPutAt(int u, int h, int a) {
-        if constexpr (UL && L) mt_ldsb().uanc[u * MT_L_H + h] = (uint8_t)(a < 0 ? 255 : a);
-        else ancPut(u, h, a);
+        if constexpr (UL && L) {
+            if constexpr (BIG) mt_ldsg().uanc[u * MT_G_H + h] = a;
+            else mt_ldsb().uanc[u * MT_L_H + h] = (uint8_t)(a < 0 ? 255 : a);
+        } else ancPut(u, h, a);
     }
     template <bool L> MT_HD int ancGetAt(int u, int h) const {
-        if constexpr (UL && L) { const int a = mt_ldsb().uanc[u * MT_L_H + h]; return a == 255 ? -1 : a; }
+        if constexpr (UL && L) {
+            if constexpr (BIG) return mt_ldsg().uanc[u * MT_G_H + h];
+            else { const int a = mt_ldsb().uanc[u * MT_L_H + h]; return a == 255 ? -1 : a; }
+        } else return ancGet(u, h);
+    }
+    MT_HD void ancPutAny(int u, int h, int a) {
+        if constexpr (UL) { if (u < UCAP) ancPutAt<true>(u, h, a); else ancPutAt<false>(u, h, a); }
+        else ancPut(u, h, a);
+    }
+    MT_HD int ancGetAny(int u, int h) const {
+        if constexpr (UL) { if (u < UCAP) return ancGetAt<true>(u, h); return ancGetAt<false>(u, h); }
         else return ancGet(u, h);
     }
     template <class F> MT_HD void forU(F f) const {
         for (int base = 0; base < nU; base += MT_WAVE) {
             const int m = (nU - base) < MT_WAVE ? (nU - base) : MT_WAVE;
-            if (UL && base < MT_B_U) f(std::true_type{}, base, m);
+            if (UL && base < UCAP) f(std::true_type{}, base, m);
             else f(std::false_type{}, base, m);
         }
     }
@@ -403,7 +466,7 @@ template <int RES> struct MtEngT {
     int blkFreeN;                       // blocks on the free list
     int heapHW, winHW;                  // high-water marks of heapN / winN
     // LDS residency (toLds/fromLds): LDS caps, and the HBM caps they stand in for
-    static constexpr bool kLds = BLKL;                  // runs check ldsHeadroom before each op
+    static constexpr bool kLds = BLKL || BIG;           // runs check ldsHeadroom before each op
     int lRows, lBlks, lHeap;
     uint32_t gRowCap, gBlkCap, gHeapCap, gWinCap;
 
@@ -521,7 +584,21 @@ template <int RES> struct MtEngT {
     // the LDS pools (caps lr/lb/lh <= the MT_L_* array sizes).  False (nothing
     // moved) if they do not fit.  R/blk/heap/win keep pointing at the HBM homes.
     MT_HD bool toLds(int lr, int lb, int lh) {
-        static_assert(BLKL, "LDS residency needs MtEngT<MT_RES_LDS or MT_RES_BLK>");
+        static_assert(BLKL || BIG, "LDS residency needs MtEngT<MT_RES_LDS, MT_RES_BLK or MT_RES_BIG>");
+        if constexpr (BIG) {                                    // heap + window (U set is per op)
+            if (lh <= 0 || lh > MT_G_HEAP) lh = MT_G_HEAP;
+            if (lr <= 0 || lr > MT_G_WIN) lr = MT_G_WIN;       // window entries kept in LDS (the rest in HBM)
+            if (heapN > lh || height + 3 > MT_G_H) return false;
+            MtLdsBig& G = mt_ldsg();
+            copyI((int*)G.heap, (const int*)heap, 2 * (heapN + 1));
+            copyI(G.win, win, winN < lr ? winN : lr);
+            wave_sync();
+            gRowCap = S.rowCap; gBlkCap = blkCap; gHeapCap = S.heapCap; gWinCap = S.winCap;
+            S.heapCap = gHeapCap < (uint32_t)lh ? gHeapCap : (uint32_t)lh;
+            lRows = lr; lBlks = 0x7FFFFFFF; lHeap = lh;
+            nU = 0; uValid = false;
+            return true;
+        }
         if constexpr (!LDS) {                                   // MT_RES_BLK: blocks + heap only
             if (lb > MT_B_BLKS) lb = MT_B_BLKS;
             if (lh > MT_B_HEAP) lh = MT_B_HEAP;
@@ -554,6 +631,15 @@ template <int RES> struct MtEngT {
         return true;
     }
     MT_HD void fromLds() {
+        if constexpr (BIG) {
+            MtLdsBig& G = mt_ldsg();
+            copyI((int*)heap, (const int*)G.heap, 2 * (heapN + 1));
+            copyI(win, G.win, winN < lRows ? winN : lRows);
+            wave_sync();
+            S.heapCap = gHeapCap;
+            nU = 0; uValid = false;
+            return;
+        }
         if constexpr (!LDS) {
             MtLdsBlk& B = mt_ldsb();
             copyQ((MtQ16*)blk, (const MtQ16*)B.blk, blkTop * (int)(sizeof(MtBlk) / 16));
@@ -576,6 +662,7 @@ template <int RES> struct MtEngT {
     // row splits + 1 new row, 2 split cascades of height+2 blocks and packParent
     // regrowth; one heap entry per op plus one per message.
     MT_HD bool ldsHeadroom() const {
+        if constexpr (BIG) return (lHeap - heapN) >= 4 && height + 3 <= MT_G_H;
         if constexpr (!BLKL) return true;
         // Block budget per message: the split + insert cascades allocate at most
         // 2*height + 5 blocks; packParent regrowth (+2 per level at most, and rare)
@@ -647,6 +734,29 @@ template <int RES> struct MtEngT {
         const int n = h.n;
         return wave_map(8, [&](int j) MT_LAM { return j < n ? own(w, j) : -1; });
     }
+    // Blocks in HBM: the records of all children of an interior block in one round trip
+    // (lane t holds dword t&15 of child t>>4 in r0 and of child (t>>4)+4 in r1), so the
+    // descent needs no separate loads for the children's lengths or the next level's block.
+    MT_HD void kidsLoad(const LaneArr<int>& ch, int n, LaneArr<int>& r0, LaneArr<int>& r1) const {
+        const auto c0 = wave_shfl(ch, [](int t) MT_LAM { return t >> 4; });
+        const auto c1 = wave_shfl(ch, [](int t) MT_LAM { return (t >> 4) + 4; });
+        r0 = wave_map(MT_WAVE, [&](int t) MT_LAM { return (t >> 4) < n ? ((const int*)&bk(own(c0, t)))[t & 15] : 0; });
+        r1 = wave_map(MT_WAVE, [&](int t) MT_LAM { return (t >> 4) + 4 < n ? ((const int*)&bk(own(c1, t)))[t & 15] : 0; });
+    }
+    // lanes 0..7: child j's observer length (dword 8 of its record)
+    MT_HD static LaneArr<int> kidsLen(const LaneArr<int>& r0, const LaneArr<int>& r1) {
+        const auto a = wave_shfl(r0, [](int t) MT_LAM { return ((t & 3) << 4) + 8; });
+        const auto b = wave_shfl(r1, [](int t) MT_LAM { return ((t & 3) << 4) + 8; });
+        return wave_map(8, [&](int j) MT_LAM { return j < 4 ? own(a, j) : own(b, j); });
+    }
+    // child j's record as blkLoad returns it (j uniform)
+    MT_HD static LaneArr<int> kidRec(const LaneArr<int>& r0, const LaneArr<int>& r1, int j, BlkH& h) {
+        const int o = (j & 3) << 4;
+        const auto w = wave_shfl(j < 4 ? r0 : r1, [o](int t) MT_LAM { return o + (t & 15); });
+        h.len = wave_at(w, 8); h.parent = wave_at(w, 9); h.n = wave_at(w, 10); h.height = wave_at(w, 11); h.scour = wave_at(w, 12);
+        const int n = h.n;
+        return wave_map(8, [&](int i) MT_LAM { return i < n ? own(w, i) : -1; });
+    }
     MT_HD int childObsLen(int h, int id) const {
         if (h == 0) return (row(id).meta & MT_M_REMOVED) ? 0 : row(id).len;
         return bk(id).len;
@@ -691,9 +801,11 @@ template <int RES> struct MtEngT {
                 auto rc = wave_map(m, [&](int k) MT_LAM { return own(wi, k).recycle; });
                 auto rkr = wave_rank(rc);
                 const int cntR = wave_count(rc), f0 = rfN;
+                const int nw0 = newWin;
                 wave_for(m, [&](int k) MT_LAM {
                     const WinI w = own(wi, k);
-                    if (w.live) wn(newWin + own(rk, k)) = w.id;
+                    // compaction writes only entries that move (none until the first pruned one)
+                    if (w.live) { if (nw0 + own(rk, k) != base + k) wn(nw0 + own(rk, k)) = w.id; }
                     else row(w.id).meta = row(w.id).meta & ~MT_M_INWIN;
                     if (w.recycle && f0 + own(rkr, k) < MT_RFL) sc->rfree[f0 + own(rkr, k)] = w.id;
                 });
@@ -705,25 +817,49 @@ template <int RES> struct MtEngT {
             const int cntU = wave_count(du);
             const int nu0 = nU;
             const int H = height;
-            wave_for(m, [&](int k) MT_LAM {
-                if (own(du, k)) {
-                    const int pos = nu0 + own(rk2, k);
-                    int a = own(wi, k).parent;
-                    if constexpr (UL) {
-                        if (pos < MT_B_U) {
-                            mt_ldsb().uid[pos] = own(wi, k).id; mt_ldsb().udelta[pos] = own(wi, k).delta;
-                            for (int h = 0; h <= H; h++) { ancPutAt<true>(pos, h, a); a = (a >= 0) ? bk(a).parent : -1; }
-                        } else {
-                            ui(pos) = own(wi, k).id; ud(pos) = own(wi, k).delta;
-                            for (int h = 0; h <= H; h++) { ancPutAt<false>(pos, h, a); a = (a >= 0) ? bk(a).parent : -1; }
-                        }
+            wave_for(m, [&](int k) MT_LAM {          // U entry: row, delta, ancestor chain
+                if (!own(du, k)) return;
+                const int pos = nu0 + own(rk2, k);
+                const WinI w = own(wi, k);
+                // blocks in LDS: the chain is walked here; in HBM: level 0 only, the rest below
+                const int HH = BLKL ? H : 0;
+                int a = w.parent;
+                if constexpr (UL) {
+                    if (pos < UCAP) {
+                        uPutAt<true>(pos, w.id, w.delta);
+                        for (int h = 0; h <= HH; h++) { ancPutAt<true>(pos, h, a); a = (a >= 0) ? bk(a).parent : -1; }
                     } else {
-                        ui(pos) = own(wi, k).id; ud(pos) = own(wi, k).delta;
-                        for (int h = 0; h <= H; h++) { ancPut(pos, h, a); a = (a >= 0) ? bk(a).parent : -1; }
+                        uPutAt<false>(pos, w.id, w.delta);
+                        for (int h = 0; h <= HH; h++) { ancPutAt<false>(pos, h, a); a = (a >= 0) ? bk(a).parent : -1; }
                     }
+                } else {
+                    ui(pos) = w.id; ud(pos) = w.delta;
+                    for (int h = 0; h <= HH; h++) { ancPut(pos, h, a); a = (a >= 0) ? bk(a).parent : -1; }
                 }
             });
             nU += cntU;
+        }
+        wave_sync();
+        // Blocks in HBM: ancestor chains level by level for up to four 64-entry chunks at
+        // once; the parent loads of one level are independent, so a level costs one round
+        // trip for 256 entries instead of one per chunk.
+        const int H = height;
+        for (int g0 = 0; !BLKL && g0 < nU; g0 += 4 * MT_WAVE) {
+            const int nu = nU;
+            wave_for(MT_WAVE, [&](int k) MT_LAM {
+                int a[4]; int pos[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    pos[q] = g0 + q * MT_WAVE + k;
+                    a[q] = pos[q] < nu ? ancGetAny(pos[q], 0) : -1;
+                }
+                for (int h = 1; h <= H; h++) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) a[q] = a[q] >= 0 ? bk(a[q]).parent : -1;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) if (pos[q] < nu) ancPutAny(pos[q], h, a[q]);
+                }
+            });
         }
         if (prune) winN = newWin;
         MT_EV(1, nU);
@@ -826,7 +962,9 @@ template <int RES> struct MtEngT {
         }
     }
     // Perspective lengths of block B's children (nodeLength, MT/mergeTree.ts:1652-1692).
-    MT_HD LaneArr<ChildL> childLens(int B, const BlkH& h, const LaneArr<int>& ch, int r, int c) {
+    // lsN >= 0 (MT_RES_BIG descents): only the lsN U entries listed in ulist lie under B.
+    MT_HD LaneArr<ChildL> childLens(int B, const BlkH& h, const LaneArr<int>& ch, int r, int c,
+                                    bool haveLen = false, const LaneArr<int>& kl = LaneArr<int>{}, int lsN = -1) {
         if (h.height == 0) {
             return wave_map(h.n, [&](int j) MT_LAM {
                 const int s = own(ch, j);
@@ -849,20 +987,59 @@ template <int RES> struct MtEngT {
         for (int j = 0; j < MT_MAXN; j++) cid[j] = j < n ? wave_at(ch, j) : -2;
         wave_for(MT_MAXN, [&](int j) MT_LAM { sc->corr[j] = 0; });
         wave_sync();
-        forU([&](auto inL, int base, int m) MT_LAM {
-            constexpr bool L = decltype(inL)::value;
-            wave_for(m, [&](int k) MT_LAM {
-                const int a = ancGetAt<L>(base + k, hc);
-                int jk = -1;
+        bool listed = false;
+        if constexpr (BIG) {
+            if (lsN >= 0) {
+                listed = true;
+                for (int base = 0; base < lsN; base += MT_WAVE) {
+                    const int m = (lsN - base) < MT_WAVE ? (lsN - base) : MT_WAVE;
+                    wave_for(m, [&](int k) MT_LAM {
+                        const int u = mt_ldsg().ulist[base + k];
+                        const int a = mt_ldsg().uanc[u * MT_G_H + hc];
+                        int jk = -1;
 #pragma unroll
-                for (int j = 0; j < MT_MAXN; j++) if (cid[j] == a) jk = j;
-                if (jk >= 0) lds_add(&sc->corr[jk], udAt<L>(base + k));
+                        for (int j = 0; j < MT_MAXN; j++) if (cid[j] == a) jk = j;
+                        if (jk >= 0) lds_add(&sc->corr[jk], mt_ldsg().udelta[u]);
+                    });
+                }
+            }
+        }
+        if (!listed) {
+            forU([&](auto inL, int base, int m) MT_LAM {
+                constexpr bool L = decltype(inL)::value;
+                wave_for(m, [&](int k) MT_LAM {
+                    const int a = ancGetAt<L>(base + k, hc);
+                    int jk = -1;
+#pragma unroll
+                    for (int j = 0; j < MT_MAXN; j++) if (cid[j] == a) jk = j;
+                    if (jk >= 0) lds_add(&sc->corr[jk], udAt<L>(base + k));
+                });
             });
-        });
+        }
         wave_sync();
         return wave_map(n, [&](int j) MT_LAM {
-            ChildL o; o.len = bk(own(ch, j)).len + sc->corr[j]; o.tie = true; return o;
+            ChildL o; o.len = (haveLen ? own(kl, j) : bk(own(ch, j)).len) + sc->corr[j]; o.tie = true; return o;
         });
+    }
+
+    // MT_RES_BIG descents: the U entries (of the list, or all when lsN < 0) whose ancestor
+    // at level hc is `child`, compacted into ulist; returns their count.  A walk then
+    // scans only the U rows under its current block instead of all of U at every level.
+    MT_HD int narrowU(int lsN, int hc, int child) {
+        const int n0 = lsN < 0 ? nU : lsN;
+        int w = 0;
+        for (int base = 0; base < n0; base += MT_WAVE) {
+            const int m = (n0 - base) < MT_WAVE ? (n0 - base) : MT_WAVE;
+            auto u = wave_map(m, [&](int k) MT_LAM { return lsN < 0 ? base + k : (int)mt_ldsg().ulist[base + k]; });
+            auto keep = wave_map(m, [&](int k) MT_LAM { return mt_ldsg().uanc[own(u, k) * MT_G_H + hc] == child; });
+            const auto rk = wave_rank(keep);
+            const int cnt = wave_count(keep), w0 = w;
+            wave_sync();                                  // in place: the chunk is read before it is rewritten
+            wave_for(m, [&](int k) MT_LAM { if (own(keep, k)) mt_ldsg().ulist[w0 + own(rk, k)] = (uint16_t)own(u, k); });
+            w += cnt;
+        }
+        wave_sync();
+        return w;
     }
 
     /* ---------------------------------- overlap side list (clients >= 63) -- */
@@ -990,15 +1167,21 @@ template <int RES> struct MtEngT {
     MT_HD int walk(int kind, int pos, int r, int c, int cand, int candLen) {
         if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
         int B = root, L = 0, p = pos;
+        const bool narrow = BIG && nU <= UCAP;   // U entries all in LDS: narrow them per level
+        int lsN = -1;
+        BlkH h;
+        MT_QB(q0); MT_QC(2);
+        auto ch = blkLoad(B, h);
+        MT_QE(0, q0);
         for (;;) {
-            BlkH h;
-            MT_QB(q0); MT_QC(2);
-            auto ch = blkLoad(B, h);
-            MT_QE(0, q0);
             MT_EV(5, 1);
             sc->pathB[L] = B;
             MT_QB(q1);
-            auto cl = childLens(B, h, ch, r, c);
+            // blocks in HBM: children's records (lengths + the next level's block) in one trip
+            const bool kpre = !BLKL && h.height > 0;
+            LaneArr<int> r0{}, r1{};
+            if (kpre) kidsLoad(ch, h.n, r0, r1);
+            auto cl = kpre ? childLens(B, h, ch, r, c, true, kidsLen(r0, r1), lsN) : childLens(B, h, ch, r, c);
             MT_QE(1, q1);
             auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
             auto pre = wave_excl_scan8(lens);
@@ -1012,7 +1195,12 @@ template <int RES> struct MtEngT {
             const int j = wave_first(cond);
             if (j >= 0) {
                 const int pj = p - wave_at(pre, j);
-                if (interior) { sc->pathJ[L] = j; L++; B = wave_at(ch, j); p = pj; continue; }
+                if (interior) {
+                    sc->pathJ[L] = j; L++; B = wave_at(ch, j); p = pj;
+                    if (narrow && h.height > 1) lsN = narrowU(lsN, h.height - 1, B);
+                    if (kpre) ch = kidRec(r0, r1, j, h); else ch = blkLoad(B, h);
+                    continue;
+                }
                 const int s = wave_at(ch, j);
                 lastL = L; lastSplit = false;
                 if (kind == MT_WALK_SPLIT) {
@@ -1020,7 +1208,7 @@ template <int RES> struct MtEngT {
                         const int n = splitRow(s, pj);
                         if (n < 0) return MT_W_FAIL;
                         insertAtPath(L, j + 1, n, 0);
-                        if (drec) {                            // SPLIT, splitLeafSegment (mergeTree.ts:2243-2258)
+                        if (REC && drec) {                     // SPLIT, splitLeafSegment (mergeTree.ts:2243-2258)
                             const int ps = obsPosition(s);
                             const bool rm = (uni(row(s).meta) & MT_M_REMOVED) != 0;
                             emitDelta(MT_DK_SPLIT, ps, pj, s, n, uni(row(n).len));
@@ -1364,7 +1552,7 @@ template <int RES> struct MtEngT {
                 mergeRun(f, ft, fc, fl, i0 - 1, i0, i1);
             }
         }
-        if (drec) {        // maintenance callbacks in child order: UNLINK (:1299-1305), APPEND (:1325-1331)
+        if (REC && drec) { // maintenance callbacks in child order: UNLINK (:1299-1305), APPEND (:1325-1331)
             const uint64_t unl = wave_ballot(wave_map(span, [&](int t) MT_LAM { return own(cls, t) == 1; }));
             int head = -1, acc = 0;
             for (uint64_t b = unl | merged | (merged >> 1); b; b &= b - 1) {
@@ -1576,7 +1764,7 @@ template <int RES> struct MtEngT {
     // delta under the block and (delta capture) the block's observer-view position.
     MT_HD void rangeMap(int mode, int start, int end, int r, int c, int sq, int opset, bool rewrite) {
         if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
-        const bool rec = drec != nullptr;
+        const bool rec = REC && drec != nullptr;
         LaneArr<int> fB{}, fJ{}, fS{}, fE{}, fL{}, fD{}, fO{};
         fB = wave_set(fB, 0, root); fS = wave_set(fS, 0, start); fE = wave_set(fE, 0, end);
         int lastOld = -2, lastNew = -1;
@@ -1903,7 +2091,7 @@ template <int RES> struct MtEngT {
             c_rows += 2;
             const uint32_t m1 = winAddKnown(n, (uint32_t)c | (marker ? MT_M_MARKER : 0u));
             if (sq > minSeq) addToLRUSetKnown(n, sq, landB, m1);
-            if (drec) emitDelta(MT_DK_INSERT, obsPosition(n), L, n, uni(row(n).props), -1);   // insertSegments callback
+            if (REC && drec) emitDelta(MT_DK_INSERT, obsPosition(n), L, n, uni(row(n).props), -1);   // insertSegments callback
         }
         zamboni();
     }
@@ -1924,6 +2112,7 @@ template <int RES> struct MtEngT {
     }
 };
 using MtEng = MtEngT<MT_RES_HBM>;
+using MtEngFast = MtEngT<MT_RES_HBM, false>;
 
 // SnapshotLoader for document i of a load batch (MT/snapshotLoader.ts:39-222) on
 // a freshly opened engine document: header, collaboration start, body plan.

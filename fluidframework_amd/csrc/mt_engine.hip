@@ -62,6 +62,31 @@ __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(Mt
         h.store(doc);
     }
 }
+// Long documents (MT_RES_BIG): heap, window and U set in LDS (~68 KB, two workgroups per
+// CU), blocks and rows in HBM; one wave per SIMD at most, so the register budget is 256
+// VGPRs and nothing spills.  A document whose heap or height outgrows LDS continues in HBM.
+template <bool REC>
+__global__ __launch_bounds__(64, 1) void mt_replay_big_kernel(MtState S, MtOps ops, uint32_t* cursor, int lw, int lh) {
+    __shared__ MtScratch sc;
+    const uint32_t run = blockIdx.x;
+    const uint32_t doc = ops.doc_ids[run];
+    const uint32_t o0 = ops.op_off[run];
+    MtEngT<MT_RES_BIG, REC> e;
+    e.bind(S, doc, &sc);
+    uint32_t cur = o0;
+    if (e.toLds(lw, 0, lh)) {
+        cur = mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0);
+        e.fromLds();
+    }
+    cursor[run] = cur;
+    e.store(doc);
+    if (cur < ops.op_off[run + 1]) {
+        MtEngT<MT_RES_HBM, REC> h;
+        h.bind(S, doc, &sc);
+        mt_replay_run(h, ops, run, doc, nullptr, nullptr, cur);
+        h.store(doc);
+    }
+}
 template <bool REC>
 __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_kernel(MtState S, MtOps ops, const uint32_t* cursor) {
     __shared__ MtScratch sc;
@@ -175,7 +200,10 @@ static int mtb_check(mt_ctx* c) {
 }
 template <bool REC>
 static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs) {
-    if (c->use_lds == 2) {
+    if (c->use_lds == 3) {
+        hipLaunchKernelGGL(mt_replay_big_kernel<REC>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
+                           c->lds_rows, c->lds_heap);
+    } else if (c->use_lds == 2) {
         hipLaunchKernelGGL(mt_replay_blk_kernel<REC>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
                            c->lds_blks, c->lds_heap);
     } else if (c->use_lds) {

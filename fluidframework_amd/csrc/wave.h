@@ -119,6 +119,8 @@ template <int OFF> __device__ __forceinline__ int wave_from8(int a) {
 }
 // lane t receives a[t / 8] (one value per group of 8 lanes); call from uniform control flow
 __device__ __forceinline__ int wave_gather8(int a) { return __shfl(a, __lane_id() >> 3); }
+// lane t receives a[src(t)] (src in [0, 64)); call from uniform control flow
+template <class F> __device__ __forceinline__ int wave_shfl(int a, F src) { return __shfl(a, src(__lane_id())); }
 // lane k's value replaced by v (k uniform)
 __device__ __forceinline__ int wave_set(int a, int k, int v) { return __lane_id() == k ? v : a; }
 // per-lane add into wave-private LDS (conflicting lanes serialize in hardware)
@@ -205,6 +207,11 @@ template <int OFF> inline LaneArr<int> wave_from8(const LaneArr<int>& a) {
 inline LaneArr<int> wave_gather8(const LaneArr<int>& a) {
     LaneArr<int> r;
     for (int t = 0; t < MT_WAVE; t++) r.v[t] = a.v[t >> 3];
+    return r;
+}
+template <class F> inline LaneArr<int> wave_shfl(const LaneArr<int>& a, F src) {
+    LaneArr<int> r;
+    for (int t = 0; t < MT_WAVE; t++) r.v[t] = a.v[src(t) & 63];
     return r;
 }
 inline LaneArr<int> wave_set(LaneArr<int> a, int k, int v) { if (k >= 0 && k < MT_WAVE) a.v[k] = v; return a; }

@@ -291,7 +291,10 @@ int  mt_replay_resident(mt_ctx* ctx);
  * to LDS (9.6 KB per document, 4 waves per SIMD), rows/window/text stay in HBM,
  * and a document that outgrows the LDS blocks continues from HBM in the same
  * wave at the exact op it reached; 0: every pool in HBM; 1: rows, blocks, heap
- * and window all in LDS (finished by a second HBM launch when outgrown).
+ * and window all in LDS (finished by a second HBM launch when outgrown); 3: long
+ * documents (blocks beyond LDS): zamboni heap, collab window and U set in LDS
+ * (~68 KB, two documents per CU), blocks/rows/text in HBM, same in-wave hand-over
+ * (rows = window entries kept in LDS, the rest stay in HBM).
  * rows/blocks/heap (0 = compiled maximum) may only lower the caps; tests use
  * small caps to force the hand-over. */
 int  mt_set_residency(mt_ctx* ctx, int use_lds, int rows, int blocks, int heap);

@@ -26,7 +26,19 @@ static void replay_runs(mt_ctx* c, uint32_t n_runs) {
     for (uint32_t run = 0; run < n_runs; run++) {
         const uint32_t doc = c->ops.doc_ids[run], o0 = c->ops.op_off[run];
         uint32_t cur = o0;
-        if (c->use_lds == 2) {
+        if (c->use_lds == 3) {
+            MtScratch sc; MtEngT<MT_RES_BIG, REC> e; e.bind(c->S, doc, &sc);
+            if (e.toLds(c->lds_rows, 0, c->lds_heap)) {
+                cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
+                e.fromLds();
+            }
+            e.store(doc);
+            if (cur < c->ops.op_off[run + 1]) {
+                MtEngT<MT_RES_HBM, REC> h; h.bind(c->S, doc, &sc);
+                mt_replay_run(h, c->ops, run, doc, nullptr, nullptr, cur);
+                h.store(doc);
+            }
+        } else if (c->use_lds == 2) {
             MtScratch sc; MtEngT<MT_RES_BLK, REC> e; e.bind(c->S, doc, &sc);
             if (e.toLds(0, c->lds_blks, c->lds_heap)) {
                 cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
@@ -49,7 +61,7 @@ static void replay_runs(mt_ctx* c, uint32_t n_runs) {
         }
         cursor[run] = cur;
     }
-    for (uint32_t run = 0; run < n_runs && c->use_lds != 2; run++) {
+    for (uint32_t run = 0; run < n_runs && c->use_lds < 2; run++) {
         if (cursor[run] >= c->ops.op_off[run + 1]) continue;
         const uint32_t doc = c->ops.doc_ids[run];
         MtScratch sc; MtEngT<MT_RES_HBM, REC> e; e.bind(c->S, doc, &sc);

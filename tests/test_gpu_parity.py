@@ -24,7 +24,8 @@ def test_gpu_matches_oracle(cfg):
     compare(batch, props, 8, factory=gpu_engine)
 
 
-@pytest.mark.parametrize("res", [(1, 40, 40, 12), (1, 90, 48, 24), (0, 0, 0, 0), (2, 0, 40, 12), (2, 0, 0, 0)])
+@pytest.mark.parametrize("res", [(1, 40, 40, 12), (1, 90, 48, 24), (0, 0, 0, 0), (2, 0, 40, 12), (2, 0, 0, 0),
+                                 (3, 0, 0, 0), (3, 16, 0, 12)])
 def test_gpu_residency_handover_matches_oracle(res):
     # Small LDS caps: documents leave LDS mid-run and mt_replay_kernel finishes
     # them from HBM at the exact op reached; (0, ...) is the HBM kernel alone.

@@ -39,7 +39,7 @@ def test_prebuild_generator_matches_oracle():
         assert np.array_equal(eng.dump(d), kept[d].dump())
 
 
-def check_deep_window(factory, n, pre, ops, lag, rows, window, text, psets=8192):
+def check_deep_window(factory, n, pre, ops, lag, rows, window, text, psets=8192, residency=None):
     props = ann_props()
     eng = factory(n, rows_per_doc=rows, window_per_doc=window, propsets_per_doc=psets, text_per_doc=text)
     eng.upload_props(props)
@@ -59,6 +59,8 @@ def check_deep_window(factory, n, pre, ops, lag, rows, window, text, psets=8192)
     neg = np.full(n, -1, np.int32)
     dig_gen = eng.snapshot_digests(range(n), neg, neg, threads=2)
     eng.restore()
+    if residency is not None:
+        eng.set_residency(*residency)
     eng.generated_to_resident()
     eng.replay_resident()
     eng.sync()
@@ -74,16 +76,21 @@ def check_deep_window(factory, n, pre, ops, lag, rows, window, text, psets=8192)
         assert int(dig_replay[d]) == od.snapshot(int(both.arrays["msn"][last[d]]), int(both.arrays["seq"][last[d]]))[1]
 
 
+# residency: (2) blk (blocks outgrow LDS: HBM continuation), (3) long-document mode with
+# the compiled LDS caps, and with a 64-entry LDS window (the rest in HBM) and an 8-entry
+# heap cap that forces the in-wave hand-over.
+@pytest.mark.parametrize("res", [(2, 0, 0, 0), (3, 0, 0, 0), (3, 64, 0, 8)])
 @pytest.mark.parametrize("lag", [64, 512])
-def test_deep_window_on_checkpoint_matches_oracle(lag):
-    check_deep_window(emu_engine, 2, 3000, 1500, lag, rows=12000, window=8192, text=1 << 16)
+def test_deep_window_on_checkpoint_matches_oracle(lag, res):
+    check_deep_window(emu_engine, 2, 3000, 1500, lag, rows=12000, window=8192, text=1 << 16, residency=res)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("res", [(2, 0, 0, 0), (3, 0, 0, 0), (3, 64, 0, 8)])
 @pytest.mark.parametrize("lag", [512, 1024])
-def test_gpu_config4_downscaled_matches_oracle(lag):
+def test_gpu_config4_downscaled_matches_oracle(lag, res):
     """SURVEY §8(c)'s config-4 down-scale on the device: 2 documents pre-built to 20k
     segments, checkpointed, then a deep-window stream (lag up to 1,024, tree height 5+)
     generated on top and replayed from the restored checkpoint."""
     check_deep_window(lambda n, **kw: Engine(n, device=0, **kw), 2, 20000, 4000, lag,
-                      rows=40000, window=16384, text=1 << 18, psets=40000)
+                      rows=40000, window=16384, text=1 << 18, psets=40000, residency=res)

@@ -15,6 +15,7 @@ if not os.path.exists(lib):
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 pre = int(sys.argv[2]) if len(sys.argv) > 2 else 200000
 ops = int(sys.argv[3]) if len(sys.argv) > 3 else 20000
+res = sys.argv[4] if len(sys.argv) > 4 else "blk"
 c = bench.CONFIGS["config4"]
 rows = pre + 3 * ops + 64
 eng = Engine(n, lib_path=lib, rows_per_doc=rows, blocks_per_doc=rows // 2 + 64, heap_per_doc=rows, window_per_doc=16384,
@@ -24,6 +25,7 @@ pa = MtGenParams(1, n, pre, 1, 0, 100, 0, 5, 1, 1, 0); pa.ins_len_min, pa.seg_pr
 eng.generate(pa); eng.sync(); eng.checkpoint()
 pb = MtGenParams(2, n, ops, 8, 1024, 60, 40, 8, 8, 2, 0); pb.continue_docs = 1
 eng.generate(pb); eng.sync(); eng.generated_to_resident(); eng.restore()
+eng.set_residency(bench.RESIDENCY[res])
 fn = eng.lib.mt_prof_get; fn.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
 base = np.zeros((n, 8), np.uint64); fn(eng.h, n, base.ctypes.data)
 t = time.time(); eng.replay_resident(); eng.sync(); dt = time.time() - t
@@ -32,6 +34,6 @@ tot = (raw - base).sum(axis=0).astype(float)
 names = ["computeU", "split-walks", "insert-walk", "rangeMap", "zamboni", "op-total", "gen", "textGC"]
 if flag == "MT_PROFILE2":
     names = ["walk blkLoad", "walk childLens", "walk levels(n)", "computeU", "computeU(n)", "heapGet", "heapGet(n)", "scourLeaf"]
-print(f"{flag} config4 docs={n} prebuild={pre} ops={ops} replay wall {dt*1e3:.1f} ms; per-doc mean cycles per msg:")
+print(f"{flag} residency={res} config4 docs={n} prebuild={pre} ops={ops} replay wall {dt*1e3:.1f} ms; per-doc mean cycles per msg:")
 for i, nm in enumerate(names):
     print(f"  {nm:16s} {tot[i]/n/ops:10.0f}")
