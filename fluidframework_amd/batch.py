@@ -21,6 +21,7 @@ from . import jsjson
 
 MT_OP_INSERT, MT_OP_REMOVE, MT_OP_ANNOTATE, MT_OP_NOOP, MT_OP_UNSUPPORTED = 0, 1, 2, 3, 4
 MT_OPF_END_OF_MSG, MT_OPF_MARKER, MT_OPF_REWRITE, MT_OPF_SEG_PROPS, MT_OPF_COMBINE = 1, 2, 4, 8, 16
+MT_OP_CUT, MT_OP_COPY, MT_OP_PASTE = 5, 6, 7      # register ops (include/mtgpu.h)
 MT_OPF_REL1, MT_OPF_REL2, MT_OPF_MARKER_ID = 0x20, 0x40, 0x80
 MARKER_ID_KEY = "markerId"            # reservedMarkerIdKey, MT/mergeTree.ts:591
 
@@ -157,6 +158,14 @@ class ClientNames:
         self.ids: dict[str, int] = {}
         self.names: list[str] = []
         self.marker_ids: dict[str, int] = {}
+        self.register_ids: dict[str, int] = {}
+
+    def register_index(self, name: str) -> int:
+        """The document's index of a register name (RegisterCollection key, with the author)."""
+        i = self.register_ids.get(name)
+        if i is None:
+            i = self.register_ids[name] = len(self.register_ids)
+        return i
 
     def marker_define(self, mid) -> int | None:
         """A marker carrying id `mid` joins the document; None if the id is not a string
@@ -274,8 +283,20 @@ class BatchBuilder:
         common = dict(client=client, seq=seq, ref_seq=ref, msn=msn, prop_id=-1)
         if t == MT_OP_INSERT:
             seg = op.get("seg")
-            if seg is None and op.get("register") is not None:
-                raise NotImplementedError("register-based insert (client.ts:425-440) is not on the batch path")
+            reg = op.get("register")
+            if not seg and jsjson.js_truthy(reg):
+                # applyInsertOp's register branch (client.ts:425-444): with a truthy range end
+                # the op copies [pos1, pos2) into the register, else it pastes the register
+                pos1, rf = self._pos(op, 1)
+                if pos1 is None or not isinstance(reg, str) or rf or \
+                        (op.get("pos2") is None and op.get("relativePos2")):
+                    self._emit(type=MT_OP_UNSUPPORTED, flags=fl, **common)
+                    return
+                p2 = op.get("pos2")
+                ty = MT_OP_COPY if (p2 is not None and p2 != 0) else MT_OP_PASTE
+                self._emit(type=ty, flags=fl, pos1=pos1, pos2=int(p2) if ty == MT_OP_COPY else 0,
+                           payload_off=self.names.register_index(reg), **common)
+                return
             if not seg:
                 # `if (op.seg)` is falsy for "" / missing: applyInsertOp returns without
                 # touching the tree (client.ts:423-444); only seq/msn advance.
@@ -317,8 +338,7 @@ class BatchBuilder:
             self._emit(type=t, flags=fl, pos1=pos1, pos2=pos2, payload_off=off,
                        payload_len=len(units), **{**common, "prop_id": pid})
         elif t in (MT_OP_REMOVE, MT_OP_ANNOTATE):
-            if op.get("register") is not None:
-                raise NotImplementedError("cut into a register (client.ts:347-350) is not on the batch path")
+            reg = op.get("register") if t == MT_OP_REMOVE else None
             pos1, f1 = self._pos(op, 1)
             pos2, f2 = self._pos(op, 2)
             if pos1 is None or pos2 is None:
@@ -334,6 +354,13 @@ class BatchBuilder:
                     self._emit(type=MT_OP_UNSUPPORTED, flags=fl, **common)
                     return
                 pid = self.props.intern(op["props"])
+            if jsjson.js_truthy(reg):                   # cut: Client.copy, then markRangeRemoved (:347-350)
+                if not isinstance(reg, str):
+                    self._emit(type=MT_OP_UNSUPPORTED, flags=fl, **common)
+                    return
+                self._emit(type=MT_OP_CUT, flags=fl | f1 | f2, pos1=pos1, pos2=pos2,
+                           payload_off=self.names.register_index(reg), **common)
+                return
             self._emit(type=t, flags=fl | f1 | f2, pos1=pos1, pos2=pos2, **{**common, "prop_id": pid})
         else:
             self._emit(type=MT_OP_NOOP, flags=fl, **common)

@@ -85,6 +85,7 @@ static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bo
     MT_ALLOC(uid, int, tot.win) MT_ALLOC(udelta, int, tot.win) MT_ALLOC(uanc, int, tot.anc)
     MT_ALLOC(text, uint16_t, tot.text) MT_ALLOC(pset, MtPSet, tot.pset) MT_ALLOC(hdr, MtDocHdr, D)
     MT_ALLOC(hold, int, D * MT_RFL) MT_ALLOC(ovx, MtOvx, D * MT_OVX_CAP) MT_ALLOC(mid, int, tot.mid)
+    MT_ALLOC(reg, MtReg, D * MT_REG_CAP)
 #undef MT_ALLOC
     if (mtb_malloc(&p, sizeof(MtDocLayout) * D) != 0) { c->err = "pool allocation failed: layout"; return MT_E_OOM; }
     S.layout = (const MtDocLayout*)p;
@@ -93,7 +94,8 @@ static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bo
     c->tot = tot;
     c->pool_bytes = sizeof(MtRow) * tot.row + sizeof(MtBlk) * tot.blk + sizeof(MtHeapE) * tot.heap + 12ull * tot.win +
                     4ull * tot.anc + 2ull * tot.text + sizeof(MtPSet) * tot.pset +
-                    (sizeof(MtDocHdr) + 4ull * MT_RFL + sizeof(MtDocLayout) + sizeof(MtOvx) * MT_OVX_CAP) * D + 4ull * tot.mid;
+                    (sizeof(MtDocHdr) + 4ull * MT_RFL + sizeof(MtDocLayout) + sizeof(MtOvx) * MT_OVX_CAP +
+                     sizeof(MtReg) * MT_REG_CAP) * D + 4ull * tot.mid;
     return MT_OK;
 }
 
@@ -116,7 +118,8 @@ static std::vector<MtCkPart> mt_ck_parts(mt_ctx* c) {
             {&c->ck_heap, S.heap, sizeof(MtHeapE) * t.heap}, {&c->ck_win, S.win, 4ull * t.win},
             {&c->ck_text, S.text, 2ull * t.text}, {&c->ck_pset, S.pset, sizeof(MtPSet) * t.pset},
             {&c->ck_hdr, S.hdr, sizeof(MtDocHdr) * D}, {&c->ck_hold, S.hold, 4ull * MT_RFL * D},
-            {&c->ck_ovx, S.ovx, sizeof(MtOvx) * MT_OVX_CAP * D}, {&c->ck_mid, S.mid, 4ull * t.mid}};
+            {&c->ck_ovx, S.ovx, sizeof(MtOvx) * MT_OVX_CAP * D}, {&c->ck_mid, S.mid, 4ull * t.mid},
+            {&c->ck_reg, S.reg, sizeof(MtReg) * MT_REG_CAP * D}};
 }
 int MT_FN(checkpoint)(mt_ctx* c) {
     if (!c) return MT_E_INVALID;
@@ -146,8 +149,8 @@ void MT_FN(destroy)(mt_ctx* c) {
     if (!c) return;
     MtState& S = c->S;
     void* ps[] = {S.rows, S.blk, S.heap, S.win, S.uid, S.udelta, S.uanc, S.text, S.pset, S.hdr, S.hold, (void*)S.layout,
-                  S.ovx, S.mid, c->ck_rows, c->ck_blk, c->ck_heap, c->ck_win, c->ck_text, c->ck_pset, c->ck_hdr, c->ck_hold,
-                  c->ck_ovx, c->ck_mid};
+                  S.ovx, S.mid, S.reg, c->ck_rows, c->ck_blk, c->ck_heap, c->ck_win, c->ck_text, c->ck_pset, c->ck_hdr,
+                  c->ck_hold, c->ck_ovx, c->ck_mid, c->ck_reg};
     for (void* p : ps) if (p) mtb_free(p);
     mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_rel, &c->b_drec,
                             &c->b_dcount, &c->b_pset_off,
@@ -220,6 +223,8 @@ static int mt_upload_ops(mt_ctx* c, const mt_op_batch* B) {
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = B->n_runs; o.payload_units = B->payload_units;
     o.rel = (const MtRelPos*)c->b_rel.p; o.n_rel = B->rel ? B->n_rel : 0;
     c->n_runs = B->n_runs;
+    c->batch_reg = false;
+    for (size_t i = 0; i < N && !c->batch_reg; i++) c->batch_reg = B->type[i] >= MT_OP_CUT && B->type[i] <= MT_OP_PASTE;
     return MT_OK;
 }
 
@@ -232,7 +237,7 @@ static int mt_check_batch(mt_ctx* c, const mt_op_batch* B) {
         if (B->op_offsets[r] > B->op_offsets[r + 1]) { c->err = "op_offsets not monotone"; return MT_E_INVALID; }
     }
     for (uint32_t i = 0; i < B->n_ops; i++) {
-        if (B->type[i] > MT_OP_UNSUPPORTED) { c->err = "unknown op type"; return MT_E_INVALID; }
+        if (B->type[i] > MT_OP_PASTE) { c->err = "unknown op type"; return MT_E_INVALID; }
         if (B->type[i] == MT_OP_INSERT && !(B->flags[i] & MT_OPF_MARKER) &&
             (uint64_t)B->payload_off[i] + B->payload_len[i] > B->payload_units) { c->err = "payload out of range"; return MT_E_INVALID; }
         if (B->prop_id[i] >= 0 && (uint32_t)B->prop_id[i] >= c->S.p_nsets) { c->err = "prop_id out of range (mt_set_props first)"; return MT_E_INVALID; }
@@ -717,6 +722,7 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs; o.payload_units = PU;
     o.rel = nullptr; o.n_rel = 0; o.drec = nullptr; o.dcount = nullptr; o.dcap = 0;
     c->n_runs = P->n_docs;
+    c->batch_reg = false;                     // generated streams hold no register ops
     c->gen_off.assign(off.begin(), off.end());
     if (!P->continue_docs) {
         rc = MT_FN(docs_open)(c, 0, P->n_docs);
@@ -790,6 +796,7 @@ int MT_FN(upload_batch_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids,
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs; o.payload_units = payload_units;
     o.rel = nullptr; o.n_rel = 0;
     c->n_runs = n_runs;
+    c->batch_reg = false;                     // device-built streams (shard.py) hold no register ops
     c->gen.enabled = 0;
     return mtb_sync(c);
 }

@@ -134,6 +134,7 @@ enum { MT_PH_U = 0, MT_PH_SPLIT, MT_PH_INSERT, MT_PH_RANGE, MT_PH_ZAMBONI, MT_PH
 #define MT_M_REMOVED 0x00010000u
 #define MT_M_MARKER 0x00020000u
 #define MT_M_INWIN 0x00040000u
+#define MT_M_REG 0x00080000u          // a clone held by a register (not linked; its text survives compaction)
 #define MT_M_HREF1 0x01000000u        // heap-entry reference count, bits 24..31 (saturating)
 #define MT_M_HREF 0xFF000000u
 
@@ -171,6 +172,12 @@ struct MtHeapE { int seg; int maxSeq; };     // LRUSegment, MT/mergeTree.ts:915-
 // live while its row still has the removedSeq it was written under.
 struct MtOvx { int row; int rseq; int client; int pad; };
 #define MT_OVX_CAP 512                         // side-list entries per document
+// RegisterCollection entries (MT/mergeTree.ts:864-896) per document: the cloned segments
+// of one (client, register name), as unlinked rows.  flags: 1 = holds a clone of a
+// removed segment, 2 = pasted (its rows are in the tree now).
+#define MT_REG_CAP 8
+#define MT_REG_SEGS 28
+struct MtReg { int client, name, n, flags; int rows[MT_REG_SEGS]; };
 struct __attribute__((aligned(16))) MtDocHdr {
     int root, height, minSeq, curSeq, rowTop, blkTop, blkFree, heapN, winN, textTop, psetTop;
     uint32_t status;
@@ -199,6 +206,7 @@ struct MtState {                              // device pools, doc-major
     uint16_t* text; MtPSet* pset; MtDocHdr* hdr; int* hold;   // text: 2 halves of textCap per doc; hold: recycled-row stacks
     MtOvx* ovx;                               // overlap side lists, MT_OVX_CAP per doc
     int* mid;                                 // marker-id tables (idToSegment): row per id, -1 unmapped
+    MtReg* reg;                               // register collections, MT_REG_CAP per doc
     uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap, holdCap, maxDocs;   // largest per-doc caps
     const MtDocLayout* layout;                // [maxDocs]
     // interned op property sets (mt_prop_table)
@@ -336,7 +344,7 @@ struct WinI { int id; int delta; int parent; bool live; bool recycle; };
 
 enum { MT_WALK_SPLIT = 0, MT_WALK_INSERT = 1 };
 enum { MT_W_OK = 0, MT_W_NOCHANGE = 1, MT_W_FAIL = 2 };
-enum { MT_MAP_REMOVE = 0, MT_MAP_ANNOTATE = 1 };
+enum { MT_MAP_REMOVE = 0, MT_MAP_ANNOTATE = 1, MT_MAP_COLLECT = 2 };
 
 // The wave's view of one document: doc-local pool pointers and the few global
 // parameters it needs (kept small: every field is wave-uniform and lives in SGPRs).
@@ -369,11 +377,12 @@ static MtLdsBig mt_ldsg_v;
 MT_INLINE MtLdsBig& mt_ldsg() { return mt_ldsg_v; }
 
 // RES: MT_RES_HBM (every pool in HBM), MT_RES_LDS (rows, blocks, heap, window,
-// U set in LDS) or MT_RES_BLK (blocks and heap in LDS).  REC: the instantiation can
-// capture delta records (mt_set_delta_capture); the replay kernels launch REC=false
-// unless a capture buffer is armed, so the hot path carries none of that code.
-template <int RES, bool REC = true> struct MtEngT {
-    static constexpr bool kRec = REC;
+// U set in LDS) or MT_RES_BLK (blocks and heap in LDS).  FULL: the instantiation can
+// capture delta records (mt_set_delta_capture) and apply register ops (MT_OP_CUT / COPY /
+// PASTE); the replay kernels launch FULL=false unless a capture buffer is armed or the
+// batch holds register ops, so the hot path carries none of that code.
+template <int RES, bool FULL = true> struct MtEngT {
+    static constexpr bool kFull = FULL;
     static constexpr bool LDS = RES == MT_RES_LDS;      // all hot pools in LDS
     static constexpr bool BIG = RES == MT_RES_BIG;      // heap, window, U set in LDS; blocks in HBM
     static constexpr bool BLKL = RES == MT_RES_LDS || RES == MT_RES_BLK;   // blocks + heap in LDS
@@ -385,6 +394,7 @@ template <int RES, bool REC = true> struct MtEngT {
     MtBlk* blk; MtHeapE* heap; uint16_t* text; MtPSet* pset;
     MtOvx* ovx; int ovxN;
     int* midt; int midCap;                    // idToSegment (MT/mergeTree.ts:1095, :1175)
+    MtReg* regs;                              // RegisterCollection (MT_REG_CAP entries)
     MtDeltaRec* drec; unsigned long long* dcount; unsigned long long dcap; uint32_t curOp;   // delta capture
     MtScratch* sc;
     // pool accessors: LDS (MT_RES_LDS, MT_RES_BLK for blocks + heap) or HBM homes
@@ -461,6 +471,7 @@ template <int RES, bool REC = true> struct MtEngT {
     int heapTop;                        // hp(1).maxSeq cached (INT_MAX when empty)
     int gcEpoch;                        // bumped by every text compaction
     int lastL, lastIdx; bool lastSplit; // landing spot of the last walk; did it split a block
+    int nCol;                           // rows gathered by rangeMap(MT_MAP_COLLECT) into sc->hold
     int landB;                          // leaf block the last insertAtPath linked its node under
     int rfN; int* rfHbm;                // recycled-row stack: depth, HBM home between runs
     int blkFreeN;                       // blocks on the free list
@@ -486,6 +497,7 @@ template <int RES, bool REC = true> struct MtEngT {
         win = st.win + wo; uid = st.uid + wo; udelta = st.udelta + wo; uanc = st.uanc + off(&Ly->anc);
         pset = st.pset + off(&Ly->pset);
         ovx = st.ovx + (size_t)d * MT_OVX_CAP;
+        regs = st.reg + (size_t)d * MT_REG_CAP;
         midt = st.mid + off(&Ly->mid); midCap = (int)uni(Ly->midCap);
         drec = nullptr; dcount = nullptr; dcap = 0; curOp = 0;
         sc = scratch;
@@ -545,6 +557,7 @@ template <int RES, bool REC = true> struct MtEngT {
 #endif
         wave_for(8, [&](int i) MT_LAM { bk(0).c[i] = -1; });
         bk(0).len = 0; bk(0).parent = -1; bk(0).n = 0; bk(0).height = 0; bk(0).scour = -1;
+        wave_for(MT_REG_CAP, [&](int i) MT_LAM { regs[i].client = -1; regs[i].n = 0; regs[i].flags = 0; });
         // idToSegment entries are not reset: an entry is read only for an id the host
         // already saw mapped in this document (mt_rel_pos.marker >= 0), and relPos
         // checks that the row still carries that id.
@@ -1208,7 +1221,7 @@ template <int RES, bool REC = true> struct MtEngT {
                         const int n = splitRow(s, pj);
                         if (n < 0) return MT_W_FAIL;
                         insertAtPath(L, j + 1, n, 0);
-                        if (REC && drec) {                     // SPLIT, splitLeafSegment (mergeTree.ts:2243-2258)
+                        if (FULL && drec) {                     // SPLIT, splitLeafSegment (mergeTree.ts:2243-2258)
                             const int ps = obsPosition(s);
                             const bool rm = (uni(row(s).meta) & MT_M_REMOVED) != 0;
                             emitDelta(MT_DK_SPLIT, ps, pj, s, n, uni(row(n).len));
@@ -1367,7 +1380,7 @@ template <int RES, bool REC = true> struct MtEngT {
             const int m = (rowTop - base) < MT_WAVE ? (rowTop - base) : MT_WAVE;
             auto ln = wave_map(m, [&](int k) MT_LAM {
                 const int s = base + k;
-                return (row(s).parent >= 0 && !(row(s).meta & MT_M_MARKER)) ? row(s).len : 0;
+                return ((row(s).parent >= 0 || (row(s).meta & MT_M_REG)) && !(row(s).meta & MT_M_MARKER)) ? row(s).len : 0;
             });
             auto pre = wave_excl_scan(ln);
             const int tot = wave_sum(ln);
@@ -1552,7 +1565,7 @@ template <int RES, bool REC = true> struct MtEngT {
                 mergeRun(f, ft, fc, fl, i0 - 1, i0, i1);
             }
         }
-        if (REC && drec) { // maintenance callbacks in child order: UNLINK (:1299-1305), APPEND (:1325-1331)
+        if (FULL && drec) { // maintenance callbacks in child order: UNLINK (:1299-1305), APPEND (:1325-1331)
             const uint64_t unl = wave_ballot(wave_map(span, [&](int t) MT_LAM { return own(cls, t) == 1; }));
             int head = -1, acc = 0;
             for (uint64_t b = unl | merged | (merged >> 1); b; b &= b - 1) {
@@ -1764,7 +1777,7 @@ template <int RES, bool REC = true> struct MtEngT {
     // delta under the block and (delta capture) the block's observer-view position.
     MT_HD void rangeMap(int mode, int start, int end, int r, int c, int sq, int opset, bool rewrite) {
         if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
-        const bool rec = REC && drec != nullptr;
+        const bool rec = FULL && drec != nullptr;
         LaneArr<int> fB{}, fJ{}, fS{}, fE{}, fL{}, fD{}, fO{};
         fB = wave_set(fB, 0, root); fS = wave_set(fS, 0, start); fE = wave_set(fE, 0, end);
         int lastOld = -2, lastNew = -1;
@@ -1790,7 +1803,14 @@ template <int RES, bool REC = true> struct MtEngT {
                 if (first >= 0) {
                     const int nact = wave_count(cond);
                     c_rows += 2ull * (uint64_t)nact;
-                    if (mode == MT_MAP_REMOVE) {
+                    if (mode == MT_MAP_COLLECT) {                      // cloneSegments' gatherSegment (:1599-1604)
+                        const auto rk = wave_rank(cond);
+                        const int k0 = nCol;
+                        wave_for(h.n, [&](int j) MT_LAM {
+                            if (own(cond, j) && k0 + own(rk, j) < MT_REG_SEGS) sc->hold[k0 + own(rk, j)] = own(ch, j);
+                        });
+                        nCol += nact;
+                    } else if (mode == MT_MAP_REMOVE) {
                         auto nd = wave_map(h.n, [&](int j) MT_LAM {
                             if (!own(cond, j)) return 0;
                             const int s = own(ch, j);
@@ -1848,7 +1868,7 @@ template <int RES, bool REC = true> struct MtEngT {
                             if (rec) emitDelta(MT_DK_ANNOTATE, base + wave_at(opre, j), uni(row(s).len), s, old, nw);
                         }
                     }
-                    addToLRUSet(wave_at(ch, first), sq);
+                    if (mode != MT_MAP_COLLECT) addToLRUSet(wave_at(ch, first), sq);
                 }
                 if (mode == MT_MAP_REMOVE) bk(B).len = h.len + obsDelta;
                 const int d = wave_at(fD, L) + obsDelta;
@@ -2091,8 +2111,91 @@ template <int RES, bool REC = true> struct MtEngT {
             c_rows += 2;
             const uint32_t m1 = winAddKnown(n, (uint32_t)c | (marker ? MT_M_MARKER : 0u));
             if (sq > minSeq) addToLRUSetKnown(n, sq, landB, m1);
-            if (REC && drec) emitDelta(MT_DK_INSERT, obsPosition(n), L, n, uni(row(n).props), -1);   // insertSegments callback
+            if (FULL && drec) emitDelta(MT_DK_INSERT, obsPosition(n), L, n, uni(row(n).props), -1);   // insertSegments callback
         }
+        zamboni();
+    }
+    /* ------------------------------------------------ register copy/paste -- */
+    // The (client, name) entry of the RegisterCollection, or a free one when `alloc`;
+    // -1 if absent (or the table is full).
+    MT_HD int regFind(int c, int name, bool alloc) {
+        auto cl = wave_map(MT_REG_CAP, [&](int i) MT_LAM { return regs[i].client; });
+        auto nm = wave_map(MT_REG_CAP, [&](int i) MT_LAM { return regs[i].name; });
+        const int hit = wave_first(wave_map(MT_REG_CAP, [&](int i) MT_LAM { return own(cl, i) == c && own(nm, i) == name; }));
+        if (hit >= 0 || !alloc) return hit;
+        return wave_first(wave_map(MT_REG_CAP, [&](int i) MT_LAM { return own(cl, i) < 0; }));
+    }
+    // Client.copy (MT/client.ts:600-608): cloneSegments(refSeq, client, start, end)
+    // (MT/mergeTree.ts:1597-1614: every segment the range touches, whole, cloned with
+    // clientId, seq, removedSeq, removedClientId and a copy of its properties,
+    // MT/mergeTree.ts:476-483) replaces the register's contents.  Clones are unlinked rows
+    // sharing the original's immutable text slice and property map.
+    MT_HD void opCopy(int start, int end, int r, int c, int name) {
+        nCol = 0;
+        rangeMap(MT_MAP_COLLECT, start, end, r, c, 0, -1, false);
+        if (status) return;
+        const int e = regFind(c, name, true);
+        if (e < 0 || nCol > MT_REG_SEGS) { status |= MT_DS_UNSUPPORTED; return; }
+        MtReg& g = regs[e];
+        // the entry's previous clones, unless pasted (then they are tree rows), are released
+        const int on = uni(g.client) == c ? uni(g.n) : 0, of = uni(g.flags);
+        if (on > 0 && !(of & 2)) {
+            for (int i = 0; i < on; i++) {
+                const int s = uni(g.rows[i]);
+                row(s).meta = uni(row(s).meta) & ~MT_M_REG;
+                freeRow(s);
+            }
+        }
+        int fl = 0;
+        const int n = nCol;
+        for (int i = 0; i < n; i++) {
+            const int s = uni(sc->hold[i]);
+            const int k = allocRow();
+            if (k < 0) return;
+            const uint32_t mt = uni(row(s).meta);
+            if (mt & MT_M_REMOVED) fl |= 1;
+            row(k).len = row(s).len; row(k).seq = row(s).seq; row(k).rseq = row(s).rseq;
+            row(k).meta = (mt & (MT_M_CLIENT | MT_M_REMOVED | MT_M_MARKER)) | MT_M_REG;
+            row(k).rcl = row(s).rcl; row(k).props = row(s).props; row(k).mid = row(s).mid;
+            row(k).toff = row(s).toff; row(k).tcap = (mt & MT_M_MARKER) ? 0 : uni(row(s).len);
+            row(k).ovl = 0ull; row(k).parent = -1;
+            wave_for(1, [&](int) MT_LAM { g.rows[i] = k; });
+        }
+        wave_for(1, [&](int) MT_LAM { g.client = c; g.name = name; g.n = n; g.flags = fl; });
+        wave_sync();
+    }
+    // Paste (applyInsertOp's register branch, MT/client.ts:436-444, then insertSegments
+    // MT/mergeTree.ts:1974-2011 with blockInsert :2207-2241): every clone in order at
+    // pos, pos + the earlier clones' cachedLength; seq and clientId become the op's.
+    MT_HD void opPaste(int pos, int r, int c, int sq, int name) {
+        const int e = regFind(c, name, false);
+        if (e < 0) return;                                     // registerCollection.get: undefined
+        MtReg& g = regs[e];
+        const int n = uni(g.n), fl = uni(g.flags);
+        if (n == 0) return;                                    // no segments: the op does nothing
+        if (fl & 3) { status |= MT_DS_UNSUPPORTED; return; }   // re-linked objects / removed clones
+        walk(MT_WALK_SPLIT, pos, r, c, -1, 0);                  // ensureIntervalBoundary
+        if (status) return;
+        int ip = pos;
+        for (int i = 0; i < n; i++) {
+            const int k = uni(g.rows[i]);
+            const uint32_t mt = (uni(row(k).meta) & ~(MT_M_REG | MT_M_CLIENT)) | (uint32_t)c;
+            const int L = uni(row(k).len);
+            row(k).meta = mt; row(k).seq = sq;
+            const int mi = uni(row(k).mid);
+            if ((mt & MT_M_MARKER) && mi > 0 && mi <= midCap) midt[mi - 1] = k;    // mapIdToSegment (:2218-2222)
+            wave_sync();
+            landB = -1;
+            const int w = walk(MT_WALK_INSERT, ip, r, c, k, L);
+            if (w != MT_W_OK || landB < 0) { status |= MT_DS_INSERT_FAILED; return; }
+            c_rows += 2;
+            const uint32_t m1 = winAddKnown(k, mt);
+            if (sq > minSeq) addToLRUSetKnown(k, sq, landB, m1);
+            if (FULL && drec) emitDelta(MT_DK_INSERT, obsPosition(k), L, k, uni(row(k).props), -1);
+            ip += L;
+        }
+        wave_for(1, [&](int) MT_LAM { g.flags = fl | 2; });
+        wave_sync();
         zamboni();
     }
     MT_HD void opRange(int mode, int start, int end, int r, int c, int sq, int opset, bool rewrite) {

@@ -17,7 +17,7 @@ struct mt_ctx {
     MtDocLayout tot{};                                                     // pool element totals
     // mt_checkpoint shadows (device)
     void *ck_rows = nullptr, *ck_blk = nullptr, *ck_heap = nullptr, *ck_win = nullptr, *ck_text = nullptr,
-         *ck_pset = nullptr, *ck_hdr = nullptr, *ck_hold = nullptr, *ck_ovx = nullptr, *ck_mid = nullptr;
+         *ck_pset = nullptr, *ck_hdr = nullptr, *ck_hold = nullptr, *ck_ovx = nullptr, *ck_mid = nullptr, *ck_reg = nullptr;
     bool ck_valid = false;
     std::unordered_map<uint32_t, std::vector<std::string>> doc_clients;   // mt_set_doc_client_names
     std::string err;
@@ -32,6 +32,7 @@ struct mt_ctx {
     std::vector<uint32_t> gen_off;     // op offsets of the generated runs
     float last_ms = 0.f;
     // LDS residency of the replay (mt_set_residency): on/off and the pool caps
+    bool batch_reg = false;            // the resident batch holds register ops (FULL kernels)
     int use_lds = 2, lds_rows = MT_L_ROWS, lds_blks = MT_B_BLKS, lds_heap = MT_B_HEAP;
     void* stream = nullptr;
     void* ev0 = nullptr;

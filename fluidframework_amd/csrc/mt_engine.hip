@@ -20,14 +20,15 @@
 #ifndef MT_LDS_WAVES_PER_SIMD
 #define MT_LDS_WAVES_PER_SIMD 1
 #endif
-// REC (every replay kernel): true only while a delta-capture buffer is armed.
-template <bool REC>
+// FULL (every replay kernel): true only while a delta-capture buffer is armed or the
+// resident batch holds register ops (mt_upload_batch found MT_OP_CUT / COPY / PASTE).
+template <bool FULL>
 __global__ __launch_bounds__(64, MT_LDS_WAVES_PER_SIMD) void mt_replay_lds_kernel(MtState S, MtOps ops, uint32_t* cursor, int lr, int lb, int lh) {
     __shared__ MtScratch sc;
     const uint32_t run = blockIdx.x;
     const uint32_t doc = ops.doc_ids[run];
     const uint32_t o0 = ops.op_off[run];
-    MtEngT<MT_RES_LDS, REC> e;
+    MtEngT<MT_RES_LDS, FULL> e;
     e.bind(S, doc, &sc);
     uint32_t cur = o0;
     if (e.toLds(lr, lb, lh)) {
@@ -38,13 +39,13 @@ __global__ __launch_bounds__(64, MT_LDS_WAVES_PER_SIMD) void mt_replay_lds_kerne
     e.store(doc);
 }
 // Blocks + heap in LDS (~9.5 KB per workgroup, 4 waves per SIMD), rows/window in HBM.
-template <bool REC>
+template <bool FULL>
 __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(MtState S, MtOps ops, uint32_t* cursor, int lb, int lh) {
     __shared__ MtScratch sc;
     const uint32_t run = blockIdx.x;
     const uint32_t doc = ops.doc_ids[run];
     const uint32_t o0 = ops.op_off[run];
-    MtEngT<MT_RES_BLK, REC> e;
+    MtEngT<MT_RES_BLK, FULL> e;
     e.bind(S, doc, &sc);
     uint32_t cur = o0;
     if (e.toLds(0, lb, lh)) {
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(Mt
     // A document that outgrew LDS continues here with its pools in HBM (no
     // second launch: long documents, which outgrow it first, keep their head start).
     if (cur < ops.op_off[run + 1]) {
-        MtEngT<MT_RES_HBM, REC> h;
+        MtEngT<MT_RES_HBM, FULL> h;
         h.bind(S, doc, &sc);
         mt_replay_run(h, ops, run, doc, nullptr, nullptr, cur);
         h.store(doc);
@@ -65,13 +66,13 @@ __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(Mt
 // Long documents (MT_RES_BIG): heap, window and U set in LDS (~68 KB, two workgroups per
 // CU), blocks and rows in HBM; one wave per SIMD at most, so the register budget is 256
 // VGPRs and nothing spills.  A document whose heap or height outgrows LDS continues in HBM.
-template <bool REC>
+template <bool FULL>
 __global__ __launch_bounds__(64, 1) void mt_replay_big_kernel(MtState S, MtOps ops, uint32_t* cursor, int lw, int lh) {
     __shared__ MtScratch sc;
     const uint32_t run = blockIdx.x;
     const uint32_t doc = ops.doc_ids[run];
     const uint32_t o0 = ops.op_off[run];
-    MtEngT<MT_RES_BIG, REC> e;
+    MtEngT<MT_RES_BIG, FULL> e;
     e.bind(S, doc, &sc);
     uint32_t cur = o0;
     if (e.toLds(lw, 0, lh)) {
@@ -81,20 +82,20 @@ __global__ __launch_bounds__(64, 1) void mt_replay_big_kernel(MtState S, MtOps o
     cursor[run] = cur;
     e.store(doc);
     if (cur < ops.op_off[run + 1]) {
-        MtEngT<MT_RES_HBM, REC> h;
+        MtEngT<MT_RES_HBM, FULL> h;
         h.bind(S, doc, &sc);
         mt_replay_run(h, ops, run, doc, nullptr, nullptr, cur);
         h.store(doc);
     }
 }
-template <bool REC>
+template <bool FULL>
 __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_kernel(MtState S, MtOps ops, const uint32_t* cursor) {
     __shared__ MtScratch sc;
     const uint32_t run = blockIdx.x;
     const uint32_t o0 = cursor ? cursor[run] : ops.op_off[run];
     if (o0 >= ops.op_off[run + 1]) return;
     const uint32_t doc = ops.doc_ids[run];
-    MtEngT<MT_RES_HBM, REC> e;
+    MtEngT<MT_RES_HBM, FULL> e;
     e.bind(S, doc, &sc);
     mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0);
     e.store(doc);
@@ -198,19 +199,19 @@ static int mtb_check(mt_ctx* c) {
     if (e != hipSuccess) { c->err = hipGetErrorString(e); return MT_E_HIP; }
     return MT_OK;
 }
-template <bool REC>
+template <bool FULL>
 static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs) {
     if (c->use_lds == 3) {
-        hipLaunchKernelGGL(mt_replay_big_kernel<REC>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
+        hipLaunchKernelGGL(mt_replay_big_kernel<FULL>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
                            c->lds_rows, c->lds_heap);
     } else if (c->use_lds == 2) {
-        hipLaunchKernelGGL(mt_replay_blk_kernel<REC>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
+        hipLaunchKernelGGL(mt_replay_blk_kernel<FULL>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
                            c->lds_blks, c->lds_heap);
     } else if (c->use_lds) {
-        hipLaunchKernelGGL(mt_replay_lds_kernel<REC>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
+        hipLaunchKernelGGL(mt_replay_lds_kernel<FULL>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
                            c->lds_rows, c->lds_blks, c->lds_heap);
-        hipLaunchKernelGGL(mt_replay_kernel<REC>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (const uint32_t*)c->b_cursor.p);
-    } else hipLaunchKernelGGL(mt_replay_kernel<REC>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (const uint32_t*)nullptr);
+        hipLaunchKernelGGL(mt_replay_kernel<FULL>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (const uint32_t*)c->b_cursor.p);
+    } else hipLaunchKernelGGL(mt_replay_kernel<FULL>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (const uint32_t*)nullptr);
 }
 static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     if (n_runs == 0) return MT_OK;
@@ -218,7 +219,7 @@ static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     (void)hipGetLastError();
     (void)hipEventRecord((hipEvent_t)c->ev0, s);
     if (g.enabled) hipLaunchKernelGGL(mt_generate_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, g);
-    else if (c->ops.drec) launch_replay<true>(c, s, n_runs);
+    else if (c->ops.drec || c->batch_reg) launch_replay<true>(c, s, n_runs);
     else launch_replay<false>(c, s, n_runs);
     (void)hipEventRecord((hipEvent_t)c->ev1, s);
     c->ev_pending = true;

@@ -77,7 +77,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
     // Replay prefetches op i+1's record while op i runs (generation writes the
     // record at the top of each iteration, so it loads in place).
     auto wn = wave_map(8, [&](int q) MT_LAM { return (!g && o0 < o1) ? ((const int*)&ops.rec[o0])[q] : 0; });
-    if (!g && Eng::kRec) { e.drec = ops.drec; e.dcount = ops.dcount; e.dcap = ops.dcap; }
+    if (!g && Eng::kFull) { e.drec = ops.drec; e.dcount = ops.dcount; e.dcap = ops.dcap; }
     for (uint32_t i = o0; i < o1; i++) {
         e.curOp = i;
         if (Eng::kLds && !e.ldsHeadroom()) return i;
@@ -131,7 +131,15 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
             } else if (ty == MT_OP_ANNOTATE) {
                 if (fl & MT_OPF_COMBINE) { e.status |= MT_DS_UNSUPPORTED; break; }
                 e.opRange(MT_MAP_ANNOTATE, q1, q2, r, c, sq, pid, (fl & MT_OPF_REWRITE) != 0);
-            }
+            } else if (ty >= MT_OP_CUT && ty <= MT_OP_PASTE) {
+                if constexpr (Eng::kFull) {
+                    if (ty == MT_OP_PASTE) e.opPaste(q1, r, c, sq, (int)poff);
+                    else {
+                        e.opCopy(q1, q2, r, c, (int)poff);                   // CUT: copy, then markRangeRemoved
+                        if (ty == MT_OP_CUT && !e.status) e.opRange(MT_MAP_REMOVE, q1, q2, r, c, sq, -1, false);
+                    }
+                } else { e.status |= MT_DS_UNSUPPORTED; break; }            // launched without register support
+            } else { e.status |= MT_DS_BAD_OP; break; }
             e.uValid = false;
 #if defined(MT_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
             e.prof[MT_PH_OP] += __builtin_amdgcn_s_memtime() - top;

@@ -27,6 +27,7 @@ const path = require("path");
 const addon = require(process.env.MTGPU_NAPI || path.join(__dirname, "mtgpu.node"));
 
 const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_GROUP = 3, OP_UNSUPPORTED = 4;
+const OP_CUT = 5, OP_COPY = 6, OP_PASTE = 7;          // register ops (include/mtgpu.h)
 const F_END = 1, F_MARKER = 2, F_REWRITE = 4, F_SEG_PROPS = 8, F_COMBINE = 16, F_REL1 = 0x20, F_REL2 = 0x40,
     F_MARKER_ID = 0x80;
 const MARKER_ID_KEY = "markerId";   // reservedMarkerIdKey, MT/mergeTree.ts:591
@@ -111,7 +112,12 @@ class PropTable {
 /** Per-document interning: long client ids (getOrAddShortClientId order, client.ts:658-682)
  * and marker ids -> the document's idToSegment table on the device (mergeTree.ts:1095). */
 class ClientNames {
-    constructor() { this.ids = new Map(); this.names = []; this.markerIds = new Map(); }
+    constructor() { this.ids = new Map(); this.names = []; this.markerIds = new Map(); this.registerIds = new Map(); }
+    /** The document's index of a register name (RegisterCollection key, with the author). */
+    registerIndex(name) {
+        if (!this.registerIds.has(name)) this.registerIds.set(name, this.registerIds.size);
+        return this.registerIds.get(name);
+    }
     index(longId) {
         let i = this.ids.get(longId);
         if (i === undefined) { i = this.names.length; this.ids.set(longId, i); this.names.push(longId); }
@@ -165,7 +171,19 @@ class BatchBuilder {
         const common = { client, seq, refSeq: ref, msn, propId: -1 };
         if (op.type === OP_INSERT) {
             const seg = op.seg;
-            if (seg === undefined && op.register !== undefined) throw new Error("register-based insert (client.ts:425-440) is not on the batch path");
+            if (!seg && op.register) {
+                // applyInsertOp's register branch (client.ts:425-444): a truthy range end copies
+                // [pos1, pos2) into the register, otherwise the register is pasted at pos1
+                const [pos1, rf] = this.pos(op, 1);
+                if (pos1 === undefined || typeof op.register !== "string" || rf ||
+                    (op.pos2 === undefined && op.relativePos2)) {
+                    this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return;
+                }
+                const copy = op.pos2 !== undefined && op.pos2 !== 0;
+                this.emit({ ...common, type: copy ? OP_COPY : OP_PASTE, flags: fl, pos1, pos2: copy ? op.pos2 : 0,
+                    payloadOff: this.names.registerIndex(op.register) });
+                return;
+            }
             if (!seg) { this.emit({ ...common, type: OP_NOOP, flags: fl }); return; }   // `if (op.seg)` falsy: no tree change
             const [pos1, rf] = this.pos(op, 1);
             if (pos1 === undefined) { this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return; }
@@ -190,7 +208,6 @@ class BatchBuilder {
             this.emit({ ...common, type: OP_INSERT, flags: fl, pos1, pos2, payloadOff: off,
                 payloadLen: text !== null ? text.length : 0, propId: pid });
         } else if (op.type === OP_REMOVE || op.type === OP_ANNOTATE) {
-            if (op.register !== undefined) throw new Error("cut into a register (client.ts:347-350) is not on the batch path");
             const [pos1, f1] = this.pos(op, 1), [pos2, f2] = this.pos(op, 2);
             if (pos1 === undefined || pos2 === undefined) { this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return; }
             let pid = -1;
@@ -200,6 +217,12 @@ class BatchBuilder {
                     this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return;     // re-keyed marker ids
                 }
                 pid = this.props.intern(op.props);
+            }
+            if (op.type === OP_REMOVE && op.register) {     // cut: Client.copy, then markRangeRemoved (:347-350)
+                if (typeof op.register !== "string") { this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return; }
+                this.emit({ ...common, type: OP_CUT, flags: fl | f1 | f2, pos1, pos2,
+                    payloadOff: this.names.registerIndex(op.register) });
+                return;
             }
             this.emit({ ...common, type: op.type, flags: fl | f1 | f2, pos1, pos2, propId: pid });
         } else {

@@ -84,6 +84,19 @@ extern "C" {
 #define MT_OP_UNSUPPORTED 4 /* an op the host found off the batch path (e.g. a
                               second marker with an id already in use): the
                               document gets MT_DS_UNSUPPORTED                    */
+/* Register copy/paste (RegisterCollection, MT/mergeTree.ts:864-896; Client.copy
+ * MT/client.ts:600-608).  payload_off = the register name's per-document index (the
+ * host interns names); the register is keyed by (author client, name). */
+#define MT_OP_CUT   5  /* remove with op.register: the range's segments are cloned into
+                          the register, then removed (client.ts:347-350)              */
+#define MT_OP_COPY  6  /* insert with op.register and a truthy range end: clone
+                          [pos1, pos2) into the register, no insert (client.ts:425-428) */
+#define MT_OP_PASTE 7  /* insert with op.register and no range end: the register's
+                          segments are inserted at pos1 (client.ts:436-439, blockInsert
+                          mergeTree.ts:2207-2241); an empty or unknown register is a no-op.
+                          Pasting a register a second time (the reference re-links the
+                          same segment objects) or one holding clones of removed
+                          segments sets MT_DS_UNSUPPORTED.                              */
 
 #define MT_OPF_END_OF_MSG 0x01u /* last member of one sequenced message: the
                                    engine runs updateSeqNumbers(msn, seq) after it.
@@ -447,7 +460,9 @@ int  mt_generated_copy_dev(mt_ctx* ctx, uint32_t first_run, uint32_t n_runs, mt_
                            uint16_t* payload_dev);
 /* Make a device-resident batch the resident batch (as mt_upload_batch, without
  * the host copy): doc_ids/op_offsets are host arrays, records and payload are
- * device buffers that the engine copies. */
+ * device buffers that the engine copies.  The records are not inspected on the
+ * host, so register ops (MT_OP_CUT / COPY / PASTE) in them set MT_DS_UNSUPPORTED
+ * unless a delta capture is armed; use mt_upload_batch for such streams. */
 int  mt_upload_batch_dev(mt_ctx* ctx, uint32_t n_runs, const uint32_t* doc_ids, const uint32_t* op_offsets,
                          const mt_op_rec* rec_dev, const uint16_t* payload_dev, uint64_t payload_units);
 /* Make the generated stream the resident batch (docs 0..n_docs-1). */

@@ -785,6 +785,43 @@ struct Tree {
         }
         if (collaborating && seq != UnassignedSeq) zamboni();
     }
+    // cloneSegments (MT/mergeTree.ts:1597-1614): every segment mapRange visits in
+    // [start, end) under (refSeq, clientId), whole, cloned by TextSegment/Marker.clone +
+    // cloneInto (MT/mergeTree.ts:476-483, textSegment.ts:45-49): clientId, a shallow
+    // copy of the properties, removedClientId, removedSeq, seq (no overlap list).
+    std::vector<Seg*> cloneSegments(int refSeq, int clientId, int start, int end) {
+        std::vector<Seg*> out;
+        auto leaf = [&](Seg* s, int, int, int) {
+            Seg* b = makeSeg();
+            b->marker = s->marker; b->refType = s->refType; b->text = s->text;
+            b->cachedLength = s->marker ? 1 : (int)s->text.size();
+            if (s->hasProps) { b->hasProps = true; b->props = make_obj(); for (int i : obj_order(s->props)) obj_set(b->props, s->props.okeys[i], s->props.ovals[i]); }
+            b->clientId = s->clientId; b->removedClientId = s->removedClientId; b->hasRemoved = s->hasRemoved;
+            b->removedSeq = s->removedSeq; b->seq = s->seq;
+            out.push_back(b);
+        };
+        nodeMap(root, 0, refSeq, clientId, start, end, leaf, nullptr, nullptr);
+        return out;
+    }
+    // insertSegments (MT/mergeTree.ts:1974-2011) with several segments: one boundary at
+    // pos, then blockInsert (:2207-2241) walks each at insertPos += cachedLength.
+    void insertSegmentsMulti(int pos, const std::vector<Seg*>& in, int refSeq, int clientId, int seq) {
+        ensureIntervalBoundary(pos, refSeq, clientId);
+        int insertPos = pos;
+        for (Seg* seg : in) {
+            if (seg->cachedLength > 0) {
+                seg->seq = seq; seg->clientId = clientId;
+                if (const u16s* id = markerId(seg)) idToSegment[*id] = seg;                      // :2218-2222
+                Block* sn = insertingWalk(root, insertPos, refSeq, clientId, seq, LEAF_INSERT, seg);
+                if (!seg->parent) { status |= MT_DS_INSERT_FAILED; return; }
+                updateRoot(sn);
+                if (collaborating && seg->seq > minSeq) addToLRUSet(seg, seg->seq);
+                insertPos += seg->cachedLength;
+            }
+        }
+        for (Seg* seg : in) drec(0, seg, seg->cachedLength, 0, "null", propsJson(seg));         // INSERT callback :1992-2000
+        if (collaborating && seq != UnassignedSeq) zamboni();
+    }
     template <class F>
     bool nodeMap(Block* node, int pos, int refSeq, int clientId, int start, int end, F& leaf, Block** postList, int* nPost) {
         for (int i = 0; i < node->childCount; i++) {                                         // :2927-2994
@@ -978,6 +1015,24 @@ struct Doc {
     std::vector<int> shortToStream;          // short id -> stream client index (-1 observer)
     std::vector<int> streamToShort;
     int opCounter = 0;                       // op members applied (mt_op_batch indexing of the message stream)
+    // RegisterCollection (MT/mergeTree.ts:864-896), keyed by (short client id, name): the
+    // short id stands for the long id the reference keys by (one-to-one per document).
+    // pasted: the reference would link the same segment objects a second time on a second
+    // paste; that corrupt tree is not modelled (MT_DS_UNSUPPORTED).
+    struct Reg { std::vector<Seg*> segs; bool pasted = false; };
+    std::map<std::pair<int, u16s>, Reg> registers;
+    void regCopy(int start, int end, int refSeq, int cl, const u16s& name) {            // Client.copy, MT/client.ts:600-608
+        Reg& g = registers[{cl, name}];
+        g.segs = t.cloneSegments(refSeq, cl, start, end);
+        g.pasted = false;
+    }
+    void regPaste(int pos, int refSeq, int cl, int seq, const u16s& name) {            // MT/client.ts:436-444
+        auto it = registers.find({cl, name});
+        if (it == registers.end() || it->second.segs.empty()) return;                   // `if (!segments || !length) return false`
+        if (it->second.pasted) { t.status |= MT_DS_UNSUPPORTED; return; }
+        it->second.pasted = true;
+        t.insertSegmentsMulti(pos, it->second.segs, refSeq, cl, seq);
+    }
 
     int shortId(int streamIdx) {             // getOrAddShortClientId, MT/client.ts:658-682
         if (streamIdx < (int)streamToShort.size() && streamToShort[streamIdx] >= 0) return streamToShort[streamIdx];
@@ -1212,6 +1267,14 @@ static uint32_t apply_run(Doc& d, const mt_op_batch* b, uint32_t run) {
             } else if (ty == MT_OP_ANNOTATE) {
                 if (fl & MT_OPF_COMBINE) t.status |= MT_DS_UNSUPPORTED;
                 t.annotateRange(b->pos1[i], b->pos2[i], d.props, b->prop_id[i], fl & MT_OPF_REWRITE, ref, cl, seq);
+            } else if (ty == MT_OP_CUT || ty == MT_OP_COPY || ty == MT_OP_PASTE) {              // register name by index
+                std::string k = std::to_string(b->payload_off[i]);
+                const u16s name(k.begin(), k.end());
+                if (ty == MT_OP_PASTE) d.regPaste(b->pos1[i], ref, cl, seq, name);
+                else {
+                    d.regCopy(b->pos1[i], b->pos2[i], ref, cl, name);
+                    if (ty == MT_OP_CUT) t.markRangeRemoved(b->pos1[i], b->pos2[i], ref, cl, seq);
+                }
             }
         }
         if (fl & MT_OPF_END_OF_MSG) {                                                            // updateSeqNumbers :843-850
@@ -1411,7 +1474,18 @@ static void apply_remote_json(Doc& d, const JVal& op, int cl, int ref, int seq, 
     if (type == MT_OP_INSERT) {                                                                   // applyInsertOp :412-462
         int pos1;
         const JVal* seg = jget(op, u"seg");
-        if (!seg || !truthy(seg)) { if (jget(op, u"register")) t.status |= MT_DS_UNSUPPORTED; return; }
+        if (!seg || !truthy(seg)) {
+            const JVal* reg = jget(op, u"register");
+            if (!truthy(reg)) return;                                                            // neither: nothing happens
+            if (reg->t != JVal::Str) { t.status |= MT_DS_UNSUPPORTED; return; }
+            if (!opPos(u"pos1", u"relativePos1", pos1)) { t.status |= MT_DS_UNSUPPORTED; return; }
+            int pos2 = 0;
+            const bool hasEnd = (jget(op, u"pos2") || jget(op, u"relativePos2")) && opPos(u"pos2", u"relativePos2", pos2);
+            if (hasEnd && pos2 != 0) d.regCopy(pos1, pos2, ref, cl, reg->s);                     // `if (range.end)`: copy only
+            else d.regPaste(pos1, ref, cl, seq, reg->s);
+            complete_op(t, seq, msn);
+            return;
+        }
         if (!opPos(u"pos1", u"relativePos1", pos1)) { t.status |= MT_DS_UNSUPPORTED; return; }
         Seg* s = segFromSpec(d, *seg);
         if (!s) { t.status |= MT_DS_UNSUPPORTED; return; }
@@ -1421,7 +1495,11 @@ static void apply_remote_json(Doc& d, const JVal& op, int cl, int ref, int seq, 
         int p1, p2;
         if (!opPos(u"pos1", u"relativePos1", p1) || !opPos(u"pos2", u"relativePos2", p2)) { t.status |= MT_DS_UNSUPPORTED; return; }
         if (type == MT_OP_REMOVE) {
-            if (jget(op, u"register")) { t.status |= MT_DS_UNSUPPORTED; return; }                 // cut -> copy (:347-350)
+            const JVal* reg = jget(op, u"register");
+            if (truthy(reg)) {                                                                   // cut: copy first (:347-350)
+                if (reg->t != JVal::Str) { t.status |= MT_DS_UNSUPPORTED; return; }
+                d.regCopy(p1, p2, ref, cl, reg->s);
+            }
             t.markRangeRemoved(p1, p2, ref, cl, seq);
         } else {
             const JVal* props = jget(op, u"props");
@@ -1441,6 +1519,24 @@ static void apply_remote_json(Doc& d, const JVal& op, int cl, int ref, int seq, 
         if (ops && ops->t == JVal::Arr)
             for (const JVal& m : ops->arr) { apply_remote_json(d, m, cl, ref, seq, msn); if (t.status & MT_DS_INSERT_FAILED) return; }
     }
+}
+// Test support (the stream generator): the register (client literal, name) as
+// {"n": segments, "len": total cachedLength, "removed": clones of removed segments,
+// "pasted": 0/1}, or {"n": -1} when absent.
+char* ora_register_info_json(ora_doc* o, const char* client_literal, const char* name_literal) {
+    Doc& d = o->d;
+    std::string out = "{\"n\":-1}";
+    auto ci = d.nameToShort.find(jquote(parse_key(client_literal)));        // lookup only: no short id is assigned
+    auto it = ci == d.nameToShort.end() ? d.registers.end() : d.registers.find({ci->second, parse_key(name_literal)});
+    if (it != d.registers.end()) {
+        int len = 0, rm = 0;
+        for (Seg* g : it->second.segs) { len += g->cachedLength; rm += g->hasRemoved ? 1 : 0; }
+        out = "{\"n\":" + std::to_string(it->second.segs.size()) + ",\"len\":" + std::to_string(len) +
+              ",\"removed\":" + std::to_string(rm) + ",\"pasted\":" + (it->second.pasted ? "1" : "0") + "}";
+    }
+    char* r = (char*)malloc(out.size() + 1);
+    memcpy(r, out.c_str(), out.size() + 1);
+    return r;
 }
 uint32_t ora_apply_msg_json(ora_doc* o, const char* json) {
     Doc& d = o->d; Tree& t = d.t;

@@ -28,6 +28,7 @@ uint32_t ora_apply_run(ora_doc* d, const mt_op_batch* b, uint32_t run);
 /* Client.applyMsg (MT/client.ts:790-850) on one ISequencedDocumentMessage given as
  * JSON text: parsed and dispatched here (GROUP, non-"op" types, markers, props),
  * independent of the hosts' batch packers.  Returns the MT_DS_* status. */
+char* ora_register_info_json(ora_doc* o, const char* client_literal, const char* name_literal);
 uint32_t ora_apply_msg_json(ora_doc* d, const char* json);
 /* getLength(refSeq, client) for the client with long id `client_literal` (a JSON
  * string literal, e.g. "\"alice\""). */

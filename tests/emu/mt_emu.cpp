@@ -19,40 +19,40 @@ static void mtb_h2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n)
 static void mtb_d2h(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static void mtb_d2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static int mtb_sync(mt_ctx*) { return MT_OK; }
-// REC as on the device: the capture instantiation only while a delta buffer is armed.
-template <bool REC>
+// FULL as on the device: the capture instantiation only while a delta buffer is armed.
+template <bool FULL>
 static void replay_runs(mt_ctx* c, uint32_t n_runs) {
     uint32_t* cursor = (uint32_t*)c->b_cursor.p;
     for (uint32_t run = 0; run < n_runs; run++) {
         const uint32_t doc = c->ops.doc_ids[run], o0 = c->ops.op_off[run];
         uint32_t cur = o0;
         if (c->use_lds == 3) {
-            MtScratch sc; MtEngT<MT_RES_BIG, REC> e; e.bind(c->S, doc, &sc);
+            MtScratch sc; MtEngT<MT_RES_BIG, FULL> e; e.bind(c->S, doc, &sc);
             if (e.toLds(c->lds_rows, 0, c->lds_heap)) {
                 cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
                 e.fromLds();
             }
             e.store(doc);
             if (cur < c->ops.op_off[run + 1]) {
-                MtEngT<MT_RES_HBM, REC> h; h.bind(c->S, doc, &sc);
+                MtEngT<MT_RES_HBM, FULL> h; h.bind(c->S, doc, &sc);
                 mt_replay_run(h, c->ops, run, doc, nullptr, nullptr, cur);
                 h.store(doc);
             }
         } else if (c->use_lds == 2) {
-            MtScratch sc; MtEngT<MT_RES_BLK, REC> e; e.bind(c->S, doc, &sc);
+            MtScratch sc; MtEngT<MT_RES_BLK, FULL> e; e.bind(c->S, doc, &sc);
             if (e.toLds(0, c->lds_blks, c->lds_heap)) {
                 cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
                 e.fromLds();
             }
             e.store(doc);
             if (cur < c->ops.op_off[run + 1]) {               // continues in HBM within the same "wave"
-                MtEngT<MT_RES_HBM, REC> h; h.bind(c->S, doc, &sc);
+                MtEngT<MT_RES_HBM, FULL> h; h.bind(c->S, doc, &sc);
                 mt_replay_run(h, c->ops, run, doc, nullptr, nullptr, cur);
                 h.store(doc);
                 // cursor keeps the hand-over point (diagnostic); the HBM pass below skips it
             }
         } else if (c->use_lds) {
-            MtScratch sc; MtEngT<MT_RES_LDS, REC> e; e.bind(c->S, doc, &sc);
+            MtScratch sc; MtEngT<MT_RES_LDS, FULL> e; e.bind(c->S, doc, &sc);
             if (e.toLds(c->lds_rows, c->lds_blks, c->lds_heap)) {
                 cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
                 e.fromLds();
@@ -64,7 +64,7 @@ static void replay_runs(mt_ctx* c, uint32_t n_runs) {
     for (uint32_t run = 0; run < n_runs && c->use_lds < 2; run++) {
         if (cursor[run] >= c->ops.op_off[run + 1]) continue;
         const uint32_t doc = c->ops.doc_ids[run];
-        MtScratch sc; MtEngT<MT_RES_HBM, REC> e; e.bind(c->S, doc, &sc);
+        MtScratch sc; MtEngT<MT_RES_HBM, FULL> e; e.bind(c->S, doc, &sc);
         mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, cursor[run]);
         e.store(doc);
     }
@@ -82,7 +82,7 @@ static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
         }
         return MT_OK;
     }
-    if (c->ops.drec) replay_runs<true>(c, n_runs);
+    if (c->ops.drec || c->batch_reg) replay_runs<true>(c, n_runs);
     else replay_runs<false>(c, n_runs);
     return MT_OK;
 }

@@ -44,7 +44,7 @@ class StreamGen:
                  p_group: float = 0.15, p_marker: float = 0.08, p_annotate: float = 0.2, p_remove: float = 0.3,
                  p_special: float = 0.25, long_every: int = 40, max_ins: int = 9, id_prefix: str = "cli",
                  max_total_clients: int | None = None, p_marker_id: float = 0.0, p_relative: float = 0.0,
-                 capture: bool = False):
+                 capture: bool = False, p_register: float = 0.0):
         self.rng = random.Random(seed)
         self.lag, self.churn, self.p_nonop, self.p_group = lag, churn, p_nonop, p_group
         self.p_marker, self.p_annotate, self.p_remove, self.p_special = p_marker, p_annotate, p_remove, p_special
@@ -53,6 +53,7 @@ class StreamGen:
         self.max_total = max_total_clients
         self.p_marker_id, self.p_relative = p_marker_id, p_relative
         self.marker_ids: list[str] = []           # ids of markers inserted so far (idToSegment)
+        self.p_register = p_register
         self.total = 0
         self.active: dict[str, int] = {}          # long id -> latest refSeq
         for _ in range(clients):
@@ -135,7 +136,35 @@ class StreamGen:
                 op["combiningOp"] = {"name": "rewrite"}
         return op, 0
 
+    REGS = ["clip", "ü-reg"]
+
+    def _register(self, L: int) -> tuple[dict, int] | None:
+        """Register ops (MT/client.ts:347-350, :425-444): cut (remove with a register), copy
+        (insert with a register and a range end) and paste (insert with a register).  A paste
+        is emitted only for a register the oracle holds unpasted and free of clones of
+        removed segments: a second paste of one register re-links the same segment objects in
+        the reference (not modelled), and pasted clones of removed segments are off the
+        engine's path.  Its length change is the clones' total cachedLength."""
+        r = self.rng
+        name = r.choice(self.REGS)
+        x = r.random()
+        if x < 0.45:
+            info = self.obs.register_info(self._author, name)
+            if info["n"] > 0 and not info["pasted"] and not info["removed"]:
+                return {"type": 0, "pos1": r.randint(0, L), "register": name}, info["len"]
+        if L == 0:
+            return None
+        s = r.randrange(L)
+        e = min(L, s + 1 + r.randrange(10))
+        if x < 0.75:
+            return {"type": 0, "pos1": s, "pos2": e, "register": name}, 0
+        return {"type": 1, "pos1": s, "pos2": e, "register": name}, -(e - s)
+
     def _member(self, L: int, k: int) -> tuple[dict, int]:
+        if self.p_register and self._first_member and self.rng.random() < self.p_register:
+            got = self._register(L)
+            if got is not None:
+                return got
         x = self.rng.random()
         if L == 0 or x >= self.p_remove + self.p_annotate:
             op, dl = self._insert(L, k)

@@ -50,6 +50,8 @@ def lib():
         L.ora_load_snapshot.argtypes = [P, U32, P]
         L.ora_apply_msg_json.restype = U32
         L.ora_apply_msg_json.argtypes = [P, ctypes.c_char_p]
+        L.ora_register_info_json.restype = P
+        L.ora_register_info_json.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p]
         L.ora_rel_pos_json.restype = I32
         L.ora_rel_pos_json.argtypes = [P, I32, ctypes.c_char_p, ctypes.c_char_p]
         L.ora_delta_capture.argtypes = [P, ctypes.c_int]
@@ -137,6 +139,17 @@ class OracleDoc:
         import json
         buf = self.L.ora_delta_json(self.h)
         out = json.loads(ctypes.string_at(buf).decode("utf-8", "surrogatepass"))
+        self.L.ora_free_buf(buf)
+        return out
+
+    def register_info(self, client_id: str, name: str) -> dict:
+        """The oracle's RegisterCollection entry (client_id, name): {"n": -1} when absent, else
+        {"n", "len", "removed", "pasted"}."""
+        import json
+        from fluidframework_amd.jsjson import quote
+        buf = self.L.ora_register_info_json(self.h, quote(client_id).encode("utf-8", "surrogatepass"),
+                                            quote(name).encode("utf-8", "surrogatepass"))
+        out = json.loads(ctypes.string_at(buf).decode())
         self.L.ora_free_buf(buf)
         return out
 

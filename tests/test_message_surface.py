@@ -32,6 +32,8 @@ SURFACES = {
     # (removedClientOverlap beyond the 63-bit mask: the per-document side list)
     "churn300": dict(clients=6, lag=24, churn=0.42, p_remove=0.5, p_annotate=0.1, p_group=0.05, p_nonop=0.02,
                      max_ins=4, long_every=0),
+    # register cut / copy / paste (MT/client.ts:347-350, :425-444, :600-608), markers included
+    "registers": dict(clients=3, lag=8, p_register=0.3, p_marker=0.15, p_marker_id=0.3, p_group=0.1),
 }
 
 
@@ -88,6 +90,11 @@ def test_stream_generator_covers_the_surface():
     msgs, obs = stream(101, 1200, **SURFACES["churn300"])
     assert len({m["clientId"] for m in msgs}) > 300
     assert obs.stats()[1] > 20          # overlapping removes by clients past the bitmask
+    msgs, _ = stream(10, 1200, **SURFACES["registers"])
+    reg = [x for m in msgs if m["type"] == "op" for x in (m["contents"]["ops"] if m["contents"]["type"] == 3
+                                                           else [m["contents"]]) if "register" in x]
+    kinds = {(x["type"], "pos2" in x) for x in reg}
+    assert kinds == {(0, False), (0, True), (1, True)} and len(reg) > 150     # paste, copy, cut
 
 
 @pytest.mark.gpu
@@ -113,7 +120,7 @@ def check_node(addon, surface, seed=3, n_docs=3, n_msgs=800):
         assert int(got["digests"][d], 16) == dig
 
 
-@pytest.mark.parametrize("surface", ["groups", "unicode", "churn", "relative"])
+@pytest.mark.parametrize("surface", ["groups", "unicode", "churn", "relative", "registers"])
 def test_message_surface_node_host_on_emulation(surface):
     from js_lib import NODE
     from emu_lib import build_emu_napi
@@ -123,7 +130,7 @@ def test_message_surface_node_host_on_emulation(surface):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("surface", ["groups", "markers_props", "unicode", "churn", "relative"])
+@pytest.mark.parametrize("surface", ["groups", "markers_props", "unicode", "churn", "relative", "registers"])
 def test_message_surface_node_host_on_gpu(surface):
     from js_lib import NODE, ROOT
     if NODE is None:
@@ -167,13 +174,13 @@ def check_delta_records(factory, surface, seed=5, n_docs=3, n_msgs=900):
     return kinds
 
 
-@pytest.mark.parametrize("surface", ["mixed", "groups", "markers_props"])
+@pytest.mark.parametrize("surface", ["mixed", "groups", "markers_props", "registers"])
 def test_delta_records_on_emulation(surface):
     kinds = check_delta_records(emu_engine, surface)
     assert {0, 1, 2, -1, -2, -3} <= kinds
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("surface", ["mixed", "groups", "markers_props", "churn300"])
+@pytest.mark.parametrize("surface", ["mixed", "groups", "markers_props", "churn300", "registers"])
 def test_delta_records_on_gpu(surface):
     check_delta_records(lambda n, **kw: Engine(n, device=0, **kw), surface, n_docs=6)
