@@ -376,6 +376,25 @@ static MtLdsBig mt_ldsg_v;
 #endif
 MT_INLINE MtLdsBig& mt_ldsg() { return mt_ldsg_v; }
 
+// Cold per-document state of a bound engine: capacities, prop-table pointers, counters,
+// high-water marks and LDS caps.  It lives in LDS (one instance per one-wave workgroup)
+// instead of SGPRs, which the hot state fills: every field here is read or bumped a
+// few times per op at most, and an SGPR spilled past the limit costs a VGPR lane.
+struct MtCold {
+    MtEngParams S;
+    uint32_t cnt[6];
+    int hw[2];
+    int lcap[3];
+    uint32_t gcap[4];
+    int epoch, ncol, midcap;
+    uint32_t op;
+};
+#if defined(__HIP_DEVICE_COMPILE__)
+__shared__ MtCold mt_cold_v;
+#else
+static MtCold mt_cold_v;
+#endif
+
 // RES: MT_RES_HBM (every pool in HBM), MT_RES_LDS (rows, blocks, heap, window,
 // U set in LDS) or MT_RES_BLK (blocks and heap in LDS).  FULL: the instantiation can
 // capture delta records (mt_set_delta_capture) and apply register ops (MT_OP_CUT / COPY /
@@ -386,16 +405,16 @@ template <int RES, bool FULL = true> struct MtEngT {
     static constexpr bool LDS = RES == MT_RES_LDS;      // all hot pools in LDS
     static constexpr bool BIG = RES == MT_RES_BIG;      // heap, window, U set in LDS; blocks in HBM
     static constexpr bool BLKL = RES == MT_RES_LDS || RES == MT_RES_BLK;   // blocks + heap in LDS
-    MtEngParams S;
+    MtEngParams& S = mt_cold_v.S;      // cold state (MtCold, LDS)
     MtDocHdr* hdrp;
     // doc-local views
     MtRow* R;
     int *win, *uid, *udelta, *uanc;
     MtBlk* blk; MtHeapE* heap; uint16_t* text; MtPSet* pset;
     MtOvx* ovx; int ovxN;
-    int* midt; int midCap;                    // idToSegment (MT/mergeTree.ts:1095, :1175)
+    int* midt; int& midCap = mt_cold_v.midcap;   // idToSegment (MT/mergeTree.ts:1095, :1175)
     MtReg* regs;                              // RegisterCollection (MT_REG_CAP entries)
-    MtDeltaRec* drec; unsigned long long* dcount; unsigned long long dcap; uint32_t curOp;   // delta capture
+    MtDeltaRec* drec; unsigned long long* dcount; unsigned long long dcap; uint32_t& curOp = mt_cold_v.op;   // delta capture
     MtScratch* sc;
     // pool accessors: LDS (MT_RES_LDS, MT_RES_BLK for blocks + heap) or HBM homes
     MT_HD MtRow& row(int s) const { if constexpr (LDS) return mt_lds().rows[s]; else return R[s]; }
@@ -462,24 +481,25 @@ template <int RES, bool FULL = true> struct MtEngT {
     // uniform document state (MtDocHdr)
     int root, height, minSeq, curSeq, rowTop, blkTop, blkFree, heapN, winN, textTop, psetTop;
     uint32_t status;
-    // Counters of this bind (added into the header at store): 32-bit and zero-based, so
-    // they hold 6 SGPRs instead of 12 live across the replay loop.
-    uint32_t c_ops, c_msgs, c_ins, c_rows, c_depth, c_scour;
+    // Counters of this bind (added into the header at store), in LDS (MtCold).
+    uint32_t &c_ops = mt_cold_v.cnt[0], &c_msgs = mt_cold_v.cnt[1], &c_ins = mt_cold_v.cnt[2], &c_rows = mt_cold_v.cnt[3],
+             &c_depth = mt_cold_v.cnt[4], &c_scour = mt_cold_v.cnt[5];
     unsigned long long prof[8];
     int textHalf; uint32_t blkCap;
     int nU; bool uValid; int uRef, uCli;
     int heapTop;                        // hp(1).maxSeq cached (INT_MAX when empty)
-    int gcEpoch;                        // bumped by every text compaction
+    int& gcEpoch = mt_cold_v.epoch;     // bumped by every text compaction
     int lastL, lastIdx; bool lastSplit; // landing spot of the last walk; did it split a block
-    int nCol;                           // rows gathered by rangeMap(MT_MAP_COLLECT) into sc->hold
+    int& nCol = mt_cold_v.ncol;         // rows gathered by rangeMap(MT_MAP_COLLECT) into sc->hold
     int landB;                          // leaf block the last insertAtPath linked its node under
     int rfN; int* rfHbm;                // recycled-row stack: depth, HBM home between runs
     int blkFreeN;                       // blocks on the free list
-    int heapHW, winHW;                  // high-water marks of heapN / winN
+    int &heapHW = mt_cold_v.hw[0], &winHW = mt_cold_v.hw[1];   // high-water marks of heapN / winN
     // LDS residency (toLds/fromLds): LDS caps, and the HBM caps they stand in for
     static constexpr bool kLds = BLKL || BIG;           // runs check ldsHeadroom before each op
-    int lRows, lBlks, lHeap;
-    uint32_t gRowCap, gBlkCap, gHeapCap, gWinCap;
+    int &lRows = mt_cold_v.lcap[0], &lBlks = mt_cold_v.lcap[1], &lHeap = mt_cold_v.lcap[2];
+    uint32_t &gRowCap = mt_cold_v.gcap[0], &gBlkCap = mt_cold_v.gcap[1], &gHeapCap = mt_cold_v.gcap[2],
+             &gWinCap = mt_cold_v.gcap[3];
 
     MT_HD void bind(const MtState& st, uint32_t d, MtScratch* scratch) {
         const MtDocLayout* Ly = st.layout + d;

@@ -8,12 +8,18 @@ L2 memory side, so Infinity-Cache hits are included.
 """
 import csv
 import json
+import re
 import sys
+
+
+def bare(name):
+    """'void mt_replay_blk_kernel<false>(MtState, ...)' -> 'mt_replay_blk_kernel'."""
+    return re.split(r"[<(]", re.sub(r"^void ", "", name.strip()))[0]
 
 
 def per_launch(path, counter, kernel="mt_replay_kernel"):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if r["Kernel_Name"].startswith(kernel) and r["Counter_Name"] == counter]
+            if bare(r["Kernel_Name"]) == kernel and r["Counter_Name"] == counter]
     if not vals:
         raise SystemExit(f"no {counter} rows for {kernel} in {path}")
     return sum(vals) / len(vals) * 1024.0  # rocprofv3 reports kB
