@@ -388,6 +388,8 @@ struct MtCold {
     uint32_t gcap[4];
     int epoch, ncol, midcap;
     uint32_t op;
+    MtDocHdr* hdr; int* rfhbm; MtOvx* ovx; int* midt; MtReg* regs;   // rarely dereferenced pointers
+    int ovxn, blkfreen, texthalf, psettop;
 };
 #if defined(__HIP_DEVICE_COMPILE__)
 __shared__ MtCold mt_cold_v;
@@ -406,14 +408,14 @@ template <int RES, bool FULL = true> struct MtEngT {
     static constexpr bool BIG = RES == MT_RES_BIG;      // heap, window, U set in LDS; blocks in HBM
     static constexpr bool BLKL = RES == MT_RES_LDS || RES == MT_RES_BLK;   // blocks + heap in LDS
     MtEngParams& S = mt_cold_v.S;      // cold state (MtCold, LDS)
-    MtDocHdr* hdrp;
+    MtDocHdr*& hdrp = mt_cold_v.hdr;
     // doc-local views
     MtRow* R;
     int *win, *uid, *udelta, *uanc;
     MtBlk* blk; MtHeapE* heap; uint16_t* text; MtPSet* pset;
-    MtOvx* ovx; int ovxN;
-    int* midt; int& midCap = mt_cold_v.midcap;   // idToSegment (MT/mergeTree.ts:1095, :1175)
-    MtReg* regs;                              // RegisterCollection (MT_REG_CAP entries)
+    MtOvx*& ovx = mt_cold_v.ovx; int& ovxN = mt_cold_v.ovxn;
+    int*& midt = mt_cold_v.midt; int& midCap = mt_cold_v.midcap;   // idToSegment (MT/mergeTree.ts:1095, :1175)
+    MtReg*& regs = mt_cold_v.regs;            // RegisterCollection (MT_REG_CAP entries)
     MtDeltaRec* drec; unsigned long long* dcount; unsigned long long dcap; uint32_t& curOp = mt_cold_v.op;   // delta capture
     MtScratch* sc;
     // pool accessors: LDS (MT_RES_LDS, MT_RES_BLK for blocks + heap) or HBM homes
@@ -479,21 +481,22 @@ template <int RES, bool FULL = true> struct MtEngT {
         }
     }
     // uniform document state (MtDocHdr)
-    int root, height, minSeq, curSeq, rowTop, blkTop, blkFree, heapN, winN, textTop, psetTop;
+    int root, height, minSeq, curSeq, rowTop, blkTop, blkFree, heapN, winN, textTop;
+    int& psetTop = mt_cold_v.psettop;
     uint32_t status;
     // Counters of this bind (added into the header at store), in LDS (MtCold).
     uint32_t &c_ops = mt_cold_v.cnt[0], &c_msgs = mt_cold_v.cnt[1], &c_ins = mt_cold_v.cnt[2], &c_rows = mt_cold_v.cnt[3],
              &c_depth = mt_cold_v.cnt[4], &c_scour = mt_cold_v.cnt[5];
     unsigned long long prof[8];
-    int textHalf; uint32_t blkCap;
+    int& textHalf = mt_cold_v.texthalf; uint32_t blkCap;
     int nU; bool uValid; int uRef, uCli;
     int heapTop;                        // hp(1).maxSeq cached (INT_MAX when empty)
     int& gcEpoch = mt_cold_v.epoch;     // bumped by every text compaction
     int lastL, lastIdx; bool lastSplit; // landing spot of the last walk; did it split a block
     int& nCol = mt_cold_v.ncol;         // rows gathered by rangeMap(MT_MAP_COLLECT) into sc->hold
     int landB;                          // leaf block the last insertAtPath linked its node under
-    int rfN; int* rfHbm;                // recycled-row stack: depth, HBM home between runs
-    int blkFreeN;                       // blocks on the free list
+    int rfN; int*& rfHbm = mt_cold_v.rfhbm;   // recycled-row stack: depth, HBM home between runs
+    int& blkFreeN = mt_cold_v.blkfreen;       // blocks on the free list
     int &heapHW = mt_cold_v.hw[0], &winHW = mt_cold_v.hw[1];   // high-water marks of heapN / winN
     // LDS residency (toLds/fromLds): LDS caps, and the HBM caps they stand in for
     static constexpr bool kLds = BLKL || BIG;           // runs check ldsHeadroom before each op
