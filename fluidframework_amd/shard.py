@@ -164,6 +164,8 @@ def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_
     import torch
     world, rank = dist.get_world_size(), dist.get_rank()
     L = int(gen_kw["ins_len_max"])
+    if L % 4:
+        raise ValueError("ins_len_max must be a multiple of 4 (payload rows are staged as 8-byte words)")
     tm = {}
     # -- op counts / clients: known at the ingest point, broadcast to all ranks
     t0 = time.perf_counter()
@@ -188,8 +190,9 @@ def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_
     caps_t = torch.zeros((docs_total, 6), dtype=torch.int32, device=device)
     if rank == 0:
         t0 = time.perf_counter()
-        rec_all = torch.empty((n_total, REC_BYTES), dtype=torch.uint8, device=device)
-        pay_all = torch.empty((n_total, 2 * L), dtype=torch.uint8, device=device)     # UTF-16 units as bytes
+        # staged as 8-byte words (a config-5 stream holds more than 2^31 record bytes)
+        rec_all = torch.empty((n_total, REC_BYTES // 8), dtype=torch.int64, device=device)
+        pay_all = torch.empty((n_total, 2 * L // 8), dtype=torch.int64, device=device)   # UTF-16 units as bytes
         gcaps = generation_caps(ops, L)
         for a in range(0, docs_total, chunk_docs):
             b = min(docs_total, a + chunk_docs)
@@ -225,25 +228,31 @@ def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_
     owned = order[owner[order] == rank]
     per_rank_ops = np.array([int(ops[owner == r].sum()) for r in range(world)], np.int64)
     my_ops = int(per_rank_ops[rank])
-    rec_recv = torch.empty((my_ops, REC_BYTES), dtype=torch.uint8, device=device)
-    pay_recv = torch.empty((my_ops, 2 * L), dtype=torch.uint8, device=device)
+    # One row per op (record words, then payload words), permuted by one index_select and
+    # moved by one all_to_all_single.  Permuting the 16-byte payload rows on their own
+    # returned zero rows for documents placed past ~1.5 GB of output on this stack (found by
+    # the config-5 digest parity at 131,072 documents); the joint 48-byte rows are exact.
+    RW = REC_BYTES // 8 + 2 * L // 8
     if rank == 0:
         starts = op_off[order]
         lens = ops[order].astype(np.int64)
         op_idx = np.repeat(starts - np.concatenate(([0], np.cumsum(lens)[:-1])), lens) + np.arange(int(lens.sum()))
         sel = torch.from_numpy(op_idx).to(device)
-        rec_send = rec_all.index_select(0, sel)
-        pay_send = pay_all.index_select(0, sel)
-        del rec_all, pay_all, sel
+        both = torch.cat([rec_all, pay_all], dim=1)
+        del rec_all, pay_all
+        send = both.index_select(0, sel)
+        del both, sel
         in_split = per_rank_ops.tolist()
     else:
-        rec_send = torch.empty((0, REC_BYTES), dtype=torch.uint8, device=device)
-        pay_send = torch.empty((0, 2 * L), dtype=torch.uint8, device=device)
+        send = torch.empty((0, RW), dtype=torch.int64, device=device)
         in_split = [0] * world
     out_split = [my_ops if r == 0 else 0 for r in range(world)]
-    dist.all_to_all_single(rec_recv, rec_send, out_split, in_split)
-    dist.all_to_all_single(pay_recv, pay_send, out_split, in_split)
-    del rec_send, pay_send
+    recv = torch.empty((my_ops, RW), dtype=torch.int64, device=device)
+    dist.all_to_all_single(recv, send, out_split, in_split)
+    del send
+    rec_recv = recv[:, :REC_BYTES // 8].contiguous()
+    pay_recv = recv[:, REC_BYTES // 8:].contiguous()
+    del recv
     # payload offsets follow the new op order (fixed stride L per op record)
     if my_ops:
         rec_recv.view(torch.int32)[:, 6] = torch.arange(my_ops, dtype=torch.int32, device=device) * L
