@@ -389,6 +389,7 @@ struct MtCold {
     int epoch, ncol, midcap;
     uint32_t op;
     MtDocHdr* hdr; int* rfhbm; MtOvx* ovx; int* midt; MtReg* regs;   // rarely dereferenced pointers
+    MtBlk* blk; MtHeapE* heap; int *uid, *udelta, *uanc; MtPSet* pset;   // HBM homes (MT_RES_BLK: cold)
     int ovxn, blkfreen, texthalf, psettop;
 };
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -411,8 +412,13 @@ template <int RES, bool FULL = true> struct MtEngT {
     MtDocHdr*& hdrp = mt_cold_v.hdr;
     // doc-local views
     MtRow* R;
-    int *win, *uid, *udelta, *uanc;
-    MtBlk* blk; MtHeapE* heap; uint16_t* text; MtPSet* pset;
+    // Block residency keeps blocks, heap and the first U entries in LDS: their HBM homes (and
+    // the property-set pool) are cold there and live in MtCold; other modes keep them in SGPRs.
+    template <class T> using Home = std::conditional_t<RES == MT_RES_BLK, T&, T>;
+    int* win;
+    Home<int*> uid = mt_cold_v.uid; Home<int*> udelta = mt_cold_v.udelta; Home<int*> uanc = mt_cold_v.uanc;
+    Home<MtBlk*> blk = mt_cold_v.blk; Home<MtHeapE*> heap = mt_cold_v.heap;
+    uint16_t* text; Home<MtPSet*> pset = mt_cold_v.pset;
     MtOvx*& ovx = mt_cold_v.ovx; int& ovxN = mt_cold_v.ovxn;
     int*& midt = mt_cold_v.midt; int& midCap = mt_cold_v.midcap;   // idToSegment (MT/mergeTree.ts:1095, :1175)
     MtReg*& regs = mt_cold_v.regs;            // RegisterCollection (MT_REG_CAP entries)
