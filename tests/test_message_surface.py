@@ -184,3 +184,53 @@ def test_delta_records_on_emulation(surface):
 @pytest.mark.parametrize("surface", ["mixed", "groups", "markers_props", "churn300", "registers"])
 def test_delta_records_on_gpu(surface):
     check_delta_records(lambda n, **kw: Engine(n, device=0, **kw), surface, n_docs=6)
+
+
+def _reg_msgs(paste_twice: bool):
+    m = [dict(clientId="a", sequenceNumber=1, referenceSequenceNumber=0, minimumSequenceNumber=0, type="op",
+              contents={"type": 0, "pos1": 0, "seg": "hello"}),
+         dict(clientId="a", sequenceNumber=2, referenceSequenceNumber=1, minimumSequenceNumber=0, type="op",
+              contents={"type": 0, "pos1": 1, "pos2": 4, "register": "clip"}),            # copy "ell"
+         dict(clientId="b", sequenceNumber=3, referenceSequenceNumber=2, minimumSequenceNumber=0, type="op",
+              contents={"type": 0, "pos1": 0, "register": "clip"}),                       # b has no "clip": no-op
+         dict(clientId="a", sequenceNumber=4, referenceSequenceNumber=3, minimumSequenceNumber=1, type="op",
+              contents={"type": 0, "pos1": 5, "register": "clip"})]                        # paste: whole "hello"
+    if paste_twice:
+        m.append(dict(clientId="a", sequenceNumber=5, referenceSequenceNumber=4, minimumSequenceNumber=2, type="op",
+                      contents={"type": 0, "pos1": 0, "register": "clip"}))
+    return m
+
+
+def check_register_known_answers(factory, twice):
+    """Client.copy clones whole segments (cloneSegments maps segments, it does not split:
+    MT/mergeTree.ts:1597-1614), so copying [1, 4) of the single segment "hello" and pasting
+    it at 5 gives "hellohello"; a paste by a client that never copied is a no-op
+    (registerCollection.get undefined, MT/client.ts:436-444).  A second paste of the same
+    register re-links the same segment objects in the reference: the engine flags it."""
+    from oracle_lib import OracleDoc
+    msgs = _reg_msgs(twice)
+    g = ClientGroup(factory(1, **LIMITS))
+    c = g.new_client({"newMergeTreeSnapshotFormat": True})
+    for m in msgs:
+        c.applyMsg(m)
+    g.flush()
+    st = int(g.engine.status([0])[0])
+    if twice:
+        assert st & 0x08, st                                     # MT_DS_UNSUPPORTED
+        return
+    assert st == 0
+    o = OracleDoc(True)
+    for m in msgs:
+        assert o.apply_msg(m) == 0
+    assert g.engine.get_text([0])[0] == o.get_text() == "hellohello"
+
+
+@pytest.mark.parametrize("twice", [False, True])
+def test_register_known_answers_on_emulation(twice):
+    check_register_known_answers(emu_engine, twice)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("twice", [False, True])
+def test_register_known_answers_on_gpu(twice):
+    check_register_known_answers(lambda n, **kw: Engine(n, device=0, **kw), twice)
