@@ -37,6 +37,10 @@ static int mtb_ensure(mt_ctx* c, mt_ctx::DevBuf& b, size_t bytes) {
 extern "C" {
 
 const char* MT_FN(last_error)(mt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+#ifndef MT_SRC_HASH
+#define MT_SRC_HASH "unhashed"
+#endif
+const char* MT_FN(source_hash)(void) { return MT_SRC_HASH; }
 
 // Pools of every document, laid out back to back with per-document capacities.
 static void mt_caps_default(mt_limits& q) {
@@ -155,7 +159,8 @@ void MT_FN(destroy)(mt_ctx* c) {
     mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_rel, &c->b_drec,
                             &c->b_dcount, &c->b_pset_off,
                             &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3,
-                            &c->b_ld_meta, &c->b_ld_seg, &c->b_ld_pay, &c->b_ld_plan, &c->b_ld_poff};
+                            &c->b_ld_meta, &c->b_ld_seg, &c->b_ld_pay, &c->b_ld_plan, &c->b_ld_poff, &c->b_dtext,
+                            &c->b_resume, &c->b_start};
     for (auto* b : bs) if (b->p) mtb_free(b->p);
     mtb_fini(c);
     delete c;
@@ -257,17 +262,67 @@ int MT_FN(upload_batch)(mt_ctx* c, const mt_op_batch* B) {
     mtb_sync(c);
     return rc;
 }
+// A capture batch (mt_delta_capture armed): each launch appends records until a document
+// has no headroom left for its next message (MtEngT::dReserve); that run stops there, the
+// records and pasted text so far move to the host, and the next launch resumes the stopped
+// runs (ops.start).  The host copies keep op order per document, so one stable sort by op
+// index restores callback order (mt_delta_records).
+static int mt_replay_capture(mt_ctx* c, const MtGen& g) {
+    const uint32_t R = c->n_runs;
+    int rc;
+    if ((rc = mtb_ensure(c, c->b_resume, 4ull * R + 4))) return rc;
+    if ((rc = mtb_ensure(c, c->b_start, 4ull * R + 4))) return rc;
+    std::vector<uint32_t> off(R + 1), resume(R), start(R);
+    mtb_d2h(c, off.data(), c->ops.op_off, 4ull * (R + 1));
+    for (uint32_t r = 0; r < R; r++) start[r] = off[r];
+    c->delta_host.clear(); c->delta_text.clear(); c->delta_over = false; c->delta_launches = 0;
+    MtOps& o = c->ops;
+    o.drec = (MtDeltaRec*)c->b_drec.p; o.dcount = (unsigned long long*)c->b_dcount.p; o.dcap = c->delta_cap;
+    o.dtext = (uint16_t*)c->b_dtext.p; o.dtcap = c->delta_tcap; o.resume = (uint32_t*)c->b_resume.p;
+    o.start = nullptr;
+    for (;;) {
+        const unsigned long long zero[4] = {0, 0, 0, 0};
+        mtb_h2d(c, c->b_dcount.p, zero, sizeof zero);
+        if ((rc = mtb_launch_replay(c, g, R))) break;
+        if ((rc = mtb_sync(c))) break;
+        c->delta_launches++;
+        unsigned long long cnt[4];
+        mtb_d2h(c, cnt, c->b_dcount.p, sizeof cnt);
+        if (cnt[MT_DC_REC] > c->delta_cap || cnt[MT_DC_TXT] > c->delta_tcap) { c->delta_over = true; break; }
+        const size_t r0 = c->delta_host.size(), t0 = c->delta_text.size();
+        c->delta_host.resize(r0 + cnt[MT_DC_REC]);
+        if (cnt[MT_DC_REC]) mtb_d2h(c, c->delta_host.data() + r0, c->b_drec.p, sizeof(MtDeltaRec) * cnt[MT_DC_REC]);
+        c->delta_text.resize(t0 + cnt[MT_DC_TXT]);
+        if (cnt[MT_DC_TXT]) mtb_d2h(c, c->delta_text.data() + t0, c->b_dtext.p, 2ull * cnt[MT_DC_TXT]);
+        for (size_t i = r0; i < c->delta_host.size(); i++) {      // pasted text offsets: into the batch's arena
+            MtDeltaRec& q = c->delta_host[i];
+            if (q.kind == MT_DK_INSERT && q.b == 0 && q.pad >= 0) q.pad += (int)t0;
+        }
+        mtb_d2h(c, resume.data(), c->b_resume.p, 4ull * R);
+        bool done = true, progress = false;
+        for (uint32_t r = 0; r < R; r++) {
+            if (resume[r] < off[r + 1]) done = false;
+            if (resume[r] != start[r]) progress = true;
+        }
+        if (done) break;
+        if (!progress) { c->err = "delta capture capacity below one message's bound"; rc = MT_E_OOM; break; }
+        start = resume;
+        mtb_h2d(c, c->b_start.p, start.data(), 4ull * R);
+        o.start = (const uint32_t*)c->b_start.p;
+    }
+    o.start = nullptr; o.resume = nullptr;
+    c->delta_valid = false;
+    return rc;
+}
 int MT_FN(replay_resident)(mt_ctx* c) {
     if (!c || !c->ops.op_off) return MT_E_INVALID;
     int rc = mtb_ensure(c, c->b_cursor, 4ull * c->n_runs + 4);
     if (rc) return rc;
-    if (c->delta_cap) {                                     // records of this batch only
-        const unsigned long long zero = 0;
-        mtb_h2d(c, c->b_dcount.p, &zero, 8);
-        c->ops.drec = (MtDeltaRec*)c->b_drec.p; c->ops.dcount = (unsigned long long*)c->b_dcount.p; c->ops.dcap = c->delta_cap;
-    } else { c->ops.drec = nullptr; c->ops.dcount = nullptr; c->ops.dcap = 0; }
-    c->delta_valid = false;
     MtGen g{}; g.enabled = 0;
+    c->delta_valid = false;
+    if (c->delta_cap) return mt_replay_capture(c, g);
+    c->ops.drec = nullptr; c->ops.dcount = nullptr; c->ops.dcap = 0; c->ops.dtext = nullptr; c->ops.dtcap = 0;
+    c->ops.resume = nullptr; c->ops.start = nullptr;
     return mtb_launch_replay(c, g, c->n_runs);
 }
 int MT_FN(apply_batch)(mt_ctx* c, const mt_op_batch* B) {
@@ -373,13 +428,22 @@ int MT_FN(load_snapshot)(mt_ctx* c, const mt_load_batch* B) {
 }
 int MT_FN(delta_capture)(mt_ctx* c, uint64_t capacity) {
     if (!c) return MT_E_INVALID;
-    c->delta_cap = 0;
+    c->delta_cap = 0; c->delta_tcap = 0;
     if (capacity) {
+        // one message of the largest document must fit a launch: its range (<= rowCap
+        // records) plus the fixed slack; a paste's text is <= the document's text capacity
+        uint64_t minr = MT_DREC_SLACK, mint = 1;
+        for (const MtDocLayout& y : c->layout_h) {
+            minr = std::max<uint64_t>(minr, (uint64_t)y.rowCap + MT_DREC_SLACK);
+            mint = std::max<uint64_t>(mint, (uint64_t)y.textCap);
+        }
+        const uint64_t cap = std::max<uint64_t>(capacity, minr), tcap = std::max<uint64_t>(4 * capacity, mint);
         int rc;
-        if ((rc = mtb_ensure(c, c->b_drec, sizeof(MtDeltaRec) * capacity))) return rc;
-        if ((rc = mtb_ensure(c, c->b_dcount, 16))) return rc;
+        if ((rc = mtb_ensure(c, c->b_drec, sizeof(MtDeltaRec) * cap))) return rc;
+        if ((rc = mtb_ensure(c, c->b_dcount, 32))) return rc;
+        if ((rc = mtb_ensure(c, c->b_dtext, 2 * tcap))) return rc;
+        c->delta_cap = cap; c->delta_tcap = tcap;
     }
-    c->delta_cap = capacity;
     return MT_OK;
 }
 int MT_FN(delta_records)(mt_ctx* c, const mt_delta_rec** out, uint64_t* n) {
@@ -388,14 +452,9 @@ int MT_FN(delta_records)(mt_ctx* c, const mt_delta_rec** out, uint64_t* n) {
     int rc = mtb_sync(c);
     if (rc) return rc;
     if (!c->delta_valid) {
-        unsigned long long cnt = 0;
-        mtb_d2h(c, &cnt, c->b_dcount.p, 8);
-        c->delta_over = cnt > c->delta_cap;
-        if (cnt > c->delta_cap) cnt = c->delta_cap;
-        c->delta_host.resize(cnt);
-        if (cnt) mtb_d2h(c, c->delta_host.data(), c->b_drec.p, sizeof(MtDeltaRec) * cnt);
         // documents interleave in the buffer; one wave appends a document's records in
-        // program order, so a stable sort by op index restores callback order
+        // program order (and later launches of a run follow earlier ones), so a stable sort
+        // by op index restores callback order
         std::stable_sort(c->delta_host.begin(), c->delta_host.end(),
                          [](const MtDeltaRec& x, const MtDeltaRec& y) { return x.op < y.op; });
         c->delta_valid = true;
@@ -403,6 +462,15 @@ int MT_FN(delta_records)(mt_ctx* c, const mt_delta_rec** out, uint64_t* n) {
     *out = (const mt_delta_rec*)c->delta_host.data();
     *n = c->delta_host.size();
     if (c->delta_over) { c->err = "delta capture capacity exceeded"; return MT_E_OOM; }
+    return MT_OK;
+}
+int MT_FN(delta_text)(mt_ctx* c, const uint16_t** out, uint64_t* n, uint32_t* launches) {
+    if (!c || !out || !n || !c->delta_cap) return MT_E_INVALID;
+    int rc = mtb_sync(c);
+    if (rc) return rc;
+    *out = c->delta_text.data();
+    *n = c->delta_text.size();
+    if (launches) *launches = c->delta_launches;
     return MT_OK;
 }
 int MT_FN(doc_pset)(mt_ctx* c, uint32_t doc, int32_t id, uint16_t* keys, int32_t* vals, uint32_t* n) {
@@ -721,6 +789,7 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs; o.payload_units = PU;
     o.rel = nullptr; o.n_rel = 0; o.drec = nullptr; o.dcount = nullptr; o.dcap = 0;
+    o.dtext = nullptr; o.dtcap = 0; o.resume = nullptr; o.start = nullptr;
     c->n_runs = P->n_docs;
     c->batch_reg = false;                     // generated streams hold no register ops
     c->gen_off.assign(off.begin(), off.end());

@@ -230,10 +230,21 @@ struct MtOps {                                // device copy of an mt_op_batch
     MtOpRec* rec;
     uint16_t* payload;
     const MtRelPos* rel; uint32_t n_rel;
-    MtDeltaRec* drec; unsigned long long* dcount; unsigned long long dcap;   // delta capture (null: off)
+    // Delta capture (null: off).  dcount[0] records appended, [1] records reserved, [2] text
+    // units appended, [3] text units reserved (MT_DC_*); dtext holds pasted segments' text.
+    MtDeltaRec* drec; unsigned long long* dcount; unsigned long long dcap;
+    uint16_t* dtext; unsigned long long dtcap;
+    uint32_t* resume;                         // capture: op index each run stopped at (op_off[run+1]: done)
+    const uint32_t* start;                    // capture resume: first op of each run (null: op_off)
     uint32_t n_runs;
     uint64_t payload_units;                   // records are bounds-checked against it on the device
 };
+enum { MT_DC_REC = 0, MT_DC_RECRES = 1, MT_DC_TXT = 2, MT_DC_TXTRES = 3 };
+// Records one message can emit at most, beyond its own range: 2 ensureIntervalBoundary
+// SPLITs, a paste's clones (MT_REG_SEGS) and two zamboni calls (the op's and setMinSeq's),
+// each popping <= 2 heap entries that scour one leaf block (8) and may packParent its
+// siblings (<= 8 blocks of 8).
+#define MT_DREC_SLACK (2 + MT_REG_SEGS + 2 * 2 * (8 + 64))
 
 // Snapshot load (mt_load_snapshot): the segments of each document (mt_load_seg)
 // and the host's plan of loadBody's insertSegments calls (MT/snapshotLoader.ts:162-206).
@@ -391,6 +402,10 @@ struct MtCold {
     MtDocHdr* hdr; int* rfhbm; MtOvx* ovx; int* midt; MtReg* regs;   // rarely dereferenced pointers
     MtBlk* blk; MtHeapE* heap; int *uid, *udelta, *uanc; MtPSet* pset;   // HBM homes (MT_RES_BLK: cold)
     int ovxn, blkfreen, texthalf, psettop;
+    // delta capture (FULL instantiations): pasted-text arena, this message's record / text
+    // use against its reservation, and whether the run stopped for capture headroom
+    uint16_t* dtext; unsigned long long dtcap;
+    uint32_t dused, tused; int dstop;
 };
 #if defined(__HIP_DEVICE_COMPILE__)
 __shared__ MtCold mt_cold_v;
@@ -423,6 +438,8 @@ template <int RES, bool FULL = true> struct MtEngT {
     int*& midt = mt_cold_v.midt; int& midCap = mt_cold_v.midcap;   // idToSegment (MT/mergeTree.ts:1095, :1175)
     MtReg*& regs = mt_cold_v.regs;            // RegisterCollection (MT_REG_CAP entries)
     MtDeltaRec* drec; unsigned long long* dcount; unsigned long long dcap; uint32_t& curOp = mt_cold_v.op;   // delta capture
+    uint16_t*& dtext = mt_cold_v.dtext; unsigned long long& dtcap = mt_cold_v.dtcap;
+    uint32_t &dUsed = mt_cold_v.dused, &tUsed = mt_cold_v.tused; int& dStop = mt_cold_v.dstop;
     MtScratch* sc;
     // pool accessors: LDS (MT_RES_LDS, MT_RES_BLK for blocks + heap) or HBM homes
     MT_HD MtRow& row(int s) const { if constexpr (LDS) return mt_lds().rows[s]; else return R[s]; }
@@ -529,6 +546,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         regs = st.reg + (size_t)d * MT_REG_CAP;
         midt = st.mid + off(&Ly->mid); midCap = (int)uni(Ly->midCap);
         drec = nullptr; dcount = nullptr; dcap = 0; curOp = 0;
+        dtext = nullptr; dtcap = 0; dUsed = 0; tUsed = 0; dStop = 0;
         sc = scratch;
         const MtDocHdr& h = *hdrp;
         root = uni(h.root); height = uni(h.height); minSeq = uni(h.minSeq); curSeq = uni(h.curSeq); rowTop = uni(h.rowTop);
@@ -974,12 +992,48 @@ template <int RES, bool FULL = true> struct MtEngT {
     /* ------------------------------------------- delta / maintenance records -- */
     // Appends one record at the batch's global cursor (documents interleave; every record
     // carries its op index, and one wave appends a document's records in program order).
-    MT_HD void emitDelta(int kind, int pos, int len, int seg, int a, int b) {
-        const unsigned long long idx = wave_atomic_next(dcount);
+    MT_HD void emitDelta(int kind, int pos, int len, int seg, int a, int b, int pad = 0) {
+        const unsigned long long idx = wave_atomic_add(dcount + MT_DC_REC, 1ull);
+        dUsed++;
         if (idx >= dcap) return;
-        MtDeltaRec q; q.op = curOp; q.kind = kind; q.pos = pos; q.len = len; q.seg = seg; q.a = a; q.b = b; q.pad = 0;
+        MtDeltaRec q; q.op = curOp; q.kind = kind; q.pos = pos; q.len = len; q.seg = seg; q.a = a; q.b = b; q.pad = pad;
         const MtDeltaRec* qp = &q;
         wave_for(8, [&](int k) MT_LAM { ((int*)&drec[idx])[k] = ((const int*)qp)[k]; });
+    }
+    // Capture headroom: before each message the wave reserves the records (nr) and pasted-text
+    // units (nt) the message can emit at most, so the append cursors never pass the capacity
+    // however the document waves interleave.  False: this launch is full; the run stops before
+    // the message and the host resumes it after draining the records.
+    MT_HD bool dReserve(unsigned long long nr, unsigned long long nt) {
+        const unsigned long long r0 = wave_atomic_add(dcount + MT_DC_RECRES, nr);
+        const unsigned long long t0 = wave_atomic_add(dcount + MT_DC_TXTRES, nt);
+        if (r0 + nr <= dcap && t0 + nt <= dtcap) { dUsed = 0; tUsed = 0; return true; }
+        (void)wave_atomic_add(dcount + MT_DC_RECRES, 0ull - nr);
+        (void)wave_atomic_add(dcount + MT_DC_TXTRES, 0ull - nt);
+        return false;
+    }
+    MT_HD void dRelease(unsigned long long nr, unsigned long long nt) {   // the unused part of a reservation
+        const unsigned long long ur = nr > dUsed ? nr - dUsed : 0ull, ut = nt > tUsed ? nt - tUsed : 0ull;
+        if (ur) (void)wave_atomic_add(dcount + MT_DC_RECRES, 0ull - ur);
+        if (ut) (void)wave_atomic_add(dcount + MT_DC_TXTRES, 0ull - ut);
+    }
+    // Text units a paste of register (c, name) inserts (its clones' cachedLength).
+    MT_HD int regTextLen(int c, int name) {
+        const int e = regFind(c, name, false);
+        if (e < 0) return 0;
+        const int n = uni(regs[e].n);
+        return wave_sum(wave_map(n < MT_REG_SEGS ? n : MT_REG_SEGS, [&](int i) MT_LAM { return row(regs[e].rows[i]).len; }));
+    }
+    // A pasted text segment's text into the capture's text arena; returns its offset.
+    MT_HD int dText(int toff, int len) {
+        const unsigned long long o = wave_atomic_add(dcount + MT_DC_TXT, (unsigned long long)len);
+        tUsed += (uint32_t)len;
+        if (o + (unsigned long long)len > dtcap) return -2;
+        for (int base = 0; base < len; base += MT_WAVE) {
+            const int m = (len - base) < MT_WAVE ? (len - base) : MT_WAVE;
+            wave_for(m, [&](int k) MT_LAM { dtext[o + base + k] = text[toff + base + k]; });
+        }
+        return (int)o;
     }
     // Observer-view position of row s (MergeTree.getPosition for the local client, whose
     // view is every sequenced op: removed rows count 0); 0 when unlinked.
@@ -2140,7 +2194,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             c_rows += 2;
             const uint32_t m1 = winAddKnown(n, (uint32_t)c | (marker ? MT_M_MARKER : 0u));
             if (sq > minSeq) addToLRUSetKnown(n, sq, landB, m1);
-            if (FULL && drec) emitDelta(MT_DK_INSERT, obsPosition(n), L, n, uni(row(n).props), -1);   // insertSegments callback
+            if (FULL && drec) emitDelta(MT_DK_INSERT, obsPosition(n), L, n, uni(row(n).props), -1, -1);   // insertSegments callback
         }
         zamboni();
     }
@@ -2166,6 +2220,14 @@ template <int RES, bool FULL = true> struct MtEngT {
         const int e = regFind(c, name, true);
         if (e < 0 || nCol > MT_REG_SEGS) { status |= MT_DS_UNSUPPORTED; return; }
         MtReg& g = regs[e];
+        const int n = nCol;
+        // the new clones' rows first (hold[32..]): on OOM the entry stays as it was
+        for (int i = 0; i < n; i++) {
+            const int k = allocRow();
+            if (k < 0) { for (int j = i - 1; j >= 0; j--) freeRow(uni(sc->hold[32 + j])); return; }
+            wave_for(1, [&](int) MT_LAM { sc->hold[32 + i] = k; });
+        }
+        wave_sync();
         // the entry's previous clones, unless pasted (then they are tree rows), are released
         const int on = uni(g.client) == c ? uni(g.n) : 0, of = uni(g.flags);
         if (on > 0 && !(of & 2)) {
@@ -2176,11 +2238,9 @@ template <int RES, bool FULL = true> struct MtEngT {
             }
         }
         int fl = 0;
-        const int n = nCol;
         for (int i = 0; i < n; i++) {
             const int s = uni(sc->hold[i]);
-            const int k = allocRow();
-            if (k < 0) return;
+            const int k = uni(sc->hold[32 + i]);
             const uint32_t mt = uni(row(s).meta);
             if (mt & MT_M_REMOVED) fl |= 1;
             row(k).len = row(s).len; row(k).seq = row(s).seq; row(k).rseq = row(s).rseq;
@@ -2220,7 +2280,13 @@ template <int RES, bool FULL = true> struct MtEngT {
             c_rows += 2;
             const uint32_t m1 = winAddKnown(k, mt);
             if (sq > minSeq) addToLRUSetKnown(k, sq, landB, m1);
-            if (FULL && drec) emitDelta(MT_DK_INSERT, obsPosition(k), L, k, uni(row(k).props), -1);
+            if (FULL && drec) {   // the pasted clone's own content (createOpsFromDelta: r.segment.clone().toJSONObject())
+                if (mt & MT_M_MARKER) emitDelta(MT_DK_INSERT, obsPosition(k), L, k, uni(row(k).props), 1, uni(row(k).toff));
+                else {
+                    const int to = dText(uni(row(k).toff), L);
+                    emitDelta(MT_DK_INSERT, obsPosition(k), L, k, uni(row(k).props), 0, to);
+                }
+            }
             ip += L;
         }
         wave_for(1, [&](int) MT_LAM { g.flags = fl | 2; });

@@ -24,7 +24,7 @@ struct mt_ctx {
     // device op batch (resident)
     struct DevBuf { void* p = nullptr; size_t cap = 0; };
     DevBuf b_stage, b_pack_docs, b_pack_sz, b_pack_off, b_gencl, b_cursor, b_doc, b_off, b_rec, b_pay, b_rel, b_drec, b_dcount, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3,
-           b_ld_meta, b_ld_seg, b_ld_pay, b_ld_plan, b_ld_poff;
+           b_ld_meta, b_ld_seg, b_ld_pay, b_ld_plan, b_ld_poff, b_dtext, b_resume, b_start;
     MtOps ops{};
     uint32_t n_runs = 0;
     MtGen gen{};
@@ -45,7 +45,9 @@ struct mt_ctx {
     std::vector<uint16_t> text_arena;
     std::vector<uint64_t> text_off;
     // delta capture (mt_delta_capture / mt_delta_records)
-    uint64_t delta_cap = 0;
+    uint64_t delta_cap = 0, delta_tcap = 0;
     bool delta_valid = false, delta_over = false;
-    std::vector<MtDeltaRec> delta_host;
+    std::vector<MtDeltaRec> delta_host;           // the last batch's records over all its launches
+    std::vector<uint16_t> delta_text;             // pasted segments' text (INSERT records with b == 0)
+    uint32_t delta_launches = 0;                  // launches the last capture batch took
 };

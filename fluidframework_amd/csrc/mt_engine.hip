@@ -7,111 +7,8 @@
 // This is the product: there is no CPU path behind any of these entry points.
 #include <hip/hip_runtime.h>
 #include "mt_ctx.h"
+#include "mt_kernels.h"
 
-// ------------------------------------------------------------- kernels ----
-#ifndef MT_WAVES_PER_SIMD
-#define MT_WAVES_PER_SIMD 4
-#endif
-// Replay: Client.applyMsg over each document's resident op run (the timed hot
-// path), in two launches.  mt_replay_lds_kernel moves the document's rows,
-// blocks, heap and window into LDS and runs as far as they fit (cursor[run] =
-// the first op not applied); mt_replay_kernel finishes any remainder with the
-// pools in HBM.
-#ifndef MT_LDS_WAVES_PER_SIMD
-#define MT_LDS_WAVES_PER_SIMD 1
-#endif
-// FULL (every replay kernel): true only while a delta-capture buffer is armed or the
-// resident batch holds register ops (mt_upload_batch found MT_OP_CUT / COPY / PASTE).
-template <bool FULL>
-__global__ __launch_bounds__(64, MT_LDS_WAVES_PER_SIMD) void mt_replay_lds_kernel(MtState S, MtOps ops, uint32_t* cursor, int lr, int lb, int lh) {
-    __shared__ MtScratch sc;
-    const uint32_t run = blockIdx.x;
-    const uint32_t doc = ops.doc_ids[run];
-    const uint32_t o0 = ops.op_off[run];
-    MtEngT<MT_RES_LDS, FULL> e;
-    e.bind(S, doc, &sc);
-    uint32_t cur = o0;
-    if (e.toLds(lr, lb, lh)) {
-        cur = mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0);
-        e.fromLds();
-    }
-    cursor[run] = cur;
-    e.store(doc);
-}
-// Blocks + heap in LDS (~9.5 KB per workgroup, 4 waves per SIMD), rows/window in HBM.
-template <bool FULL>
-__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(MtState S, MtOps ops, uint32_t* cursor, int lb, int lh) {
-    __shared__ MtScratch sc;
-    const uint32_t run = blockIdx.x;
-    const uint32_t doc = ops.doc_ids[run];
-    const uint32_t o0 = ops.op_off[run];
-    MtEngT<MT_RES_BLK, FULL> e;
-    e.bind(S, doc, &sc);
-    uint32_t cur = o0;
-    if (e.toLds(0, lb, lh)) {
-        cur = mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0);
-        e.fromLds();
-    }
-    cursor[run] = cur;
-    e.store(doc);
-    // A document that outgrew LDS continues here with its pools in HBM (no
-    // second launch: long documents, which outgrow it first, keep their head start).
-    if (cur < ops.op_off[run + 1]) {
-        MtEngT<MT_RES_HBM, FULL> h;
-        h.bind(S, doc, &sc);
-        mt_replay_run(h, ops, run, doc, nullptr, nullptr, cur);
-        h.store(doc);
-    }
-}
-// Long documents (MT_RES_BIG): heap, window and U set in LDS (~68 KB, two workgroups per
-// CU), blocks and rows in HBM; one wave per SIMD at most, so the register budget is 256
-// VGPRs and nothing spills.  A document whose heap or height outgrows LDS continues in HBM.
-template <bool FULL>
-__global__ __launch_bounds__(64, 1) void mt_replay_big_kernel(MtState S, MtOps ops, uint32_t* cursor, int lw, int lh) {
-    __shared__ MtScratch sc;
-    const uint32_t run = blockIdx.x;
-    const uint32_t doc = ops.doc_ids[run];
-    const uint32_t o0 = ops.op_off[run];
-    MtEngT<MT_RES_BIG, FULL> e;
-    e.bind(S, doc, &sc);
-    uint32_t cur = o0;
-    if (e.toLds(lw, 0, lh)) {
-        cur = mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0);
-        e.fromLds();
-    }
-    cursor[run] = cur;
-    e.store(doc);
-    if (cur < ops.op_off[run + 1]) {
-        MtEngT<MT_RES_HBM, FULL> h;
-        h.bind(S, doc, &sc);
-        mt_replay_run(h, ops, run, doc, nullptr, nullptr, cur);
-        h.store(doc);
-    }
-}
-template <bool FULL>
-__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_kernel(MtState S, MtOps ops, const uint32_t* cursor) {
-    __shared__ MtScratch sc;
-    const uint32_t run = blockIdx.x;
-    const uint32_t o0 = cursor ? cursor[run] : ops.op_off[run];
-    if (o0 >= ops.op_off[run + 1]) return;
-    const uint32_t doc = ops.doc_ids[run];
-    MtEngT<MT_RES_HBM, FULL> e;
-    e.bind(S, doc, &sc);
-    mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0);
-    e.store(doc);
-}
-// Generation: the same engine acting as sequencer + observer, writing the op
-// records it applies (a separate symbol so profiles never mix it with replay).
-__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_generate_kernel(MtState S, MtOps ops, MtGen gen) {
-    __shared__ MtScratch sc;
-    __shared__ int lastRef[64];
-    const uint32_t run = blockIdx.x;
-    const uint32_t doc = ops.doc_ids[run];
-    MtEng e;
-    e.bind(S, doc, &sc);
-    mt_replay_run(e, ops, run, doc, &gen, lastRef, ops.op_off[run]);
-    e.store(doc);
-}
 __global__ __launch_bounds__(64) void mt_open_kernel(MtState S, uint32_t first) {
     __shared__ MtScratch sc;
     const uint32_t doc = first + blockIdx.x;
@@ -199,28 +96,24 @@ static int mtb_check(mt_ctx* c) {
     if (e != hipSuccess) { c->err = hipGetErrorString(e); return MT_E_HIP; }
     return MT_OK;
 }
-template <bool FULL>
-static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs) {
-    if (c->use_lds == 3) {
-        hipLaunchKernelGGL(mt_replay_big_kernel<FULL>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
-                           c->lds_rows, c->lds_heap);
-    } else if (c->use_lds == 2) {
-        hipLaunchKernelGGL(mt_replay_blk_kernel<FULL>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
-                           c->lds_blks, c->lds_heap);
+static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) {
+    uint32_t* cur = (uint32_t*)c->b_cursor.p;
+    if (c->use_lds == 3) mtk_big(full, s, n_runs, c->S, c->ops, cur, c->lds_rows, c->lds_heap);
+    else if (c->use_lds == 2) {
+        if (full) mtk_blk_full(s, n_runs, c->S, c->ops, cur, c->lds_blks, c->lds_heap);
+        else mtk_blk_fast(s, n_runs, c->S, c->ops, cur, c->lds_blks, c->lds_heap);
     } else if (c->use_lds) {
-        hipLaunchKernelGGL(mt_replay_lds_kernel<FULL>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (uint32_t*)c->b_cursor.p,
-                           c->lds_rows, c->lds_blks, c->lds_heap);
-        hipLaunchKernelGGL(mt_replay_kernel<FULL>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (const uint32_t*)c->b_cursor.p);
-    } else hipLaunchKernelGGL(mt_replay_kernel<FULL>, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, (const uint32_t*)nullptr);
+        mtk_lds(full, s, n_runs, c->S, c->ops, cur, c->lds_rows, c->lds_blks, c->lds_heap);
+        mtk_hbm(full, s, n_runs, c->S, c->ops, cur);
+    } else mtk_hbm(full, s, n_runs, c->S, c->ops, nullptr);
 }
 static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     if (n_runs == 0) return MT_OK;
     hipStream_t s = (hipStream_t)c->stream;
     (void)hipGetLastError();
     (void)hipEventRecord((hipEvent_t)c->ev0, s);
-    if (g.enabled) hipLaunchKernelGGL(mt_generate_kernel, dim3(n_runs), dim3(64), 0, s, c->S, c->ops, g);
-    else if (c->ops.drec || c->batch_reg) launch_replay<true>(c, s, n_runs);
-    else launch_replay<false>(c, s, n_runs);
+    if (g.enabled) mtk_generate(s, n_runs, c->S, c->ops, g);
+    else launch_replay(c, s, n_runs, c->ops.drec || c->batch_reg);
     (void)hipEventRecord((hipEvent_t)c->ev1, s);
     c->ev_pending = true;
     return mtb_check(c);

@@ -1,0 +1,104 @@
+// mt_k_replay.hip — the replay kernels of the MI355X engine, one kernel set per object.
+//
+// Built several times with -DMT_KSET=<n> (see __graft_entry__.build_engine): each object
+// holds one group of template instantiations, so the groups compile in parallel, and
+// mt_engine.hip launches them through the mtk_* functions declared in mt_kernels.h.
+//   MT_KSET 0: mt_replay_blk_kernel<false> (the hot path)   1: mt_replay_blk_kernel<true>
+//   MT_KSET 2: mt_replay_big_kernel<false / true>             3: lds, hbm, generate kernels
+#include <hip/hip_runtime.h>
+#include "mt_ctx.h"
+#include "mt_kernels.h"
+
+#ifndef MT_WAVES_PER_SIMD
+#define MT_WAVES_PER_SIMD 4
+#endif
+// Replay: Client.applyMsg over each document's resident op run (the timed hot
+// path), in two launches.  mt_replay_lds_kernel moves the document's rows,
+// blocks, heap and window into LDS and runs as far as they fit (cursor[run] =
+// the first op not applied); mt_replay_kernel finishes any remainder with the
+// pools in HBM.
+#ifndef MT_LDS_WAVES_PER_SIMD
+#define MT_LDS_WAVES_PER_SIMD 1
+#endif
+// FULL (every replay kernel): true only while a delta-capture buffer is armed or the
+// resident batch holds register ops (mt_upload_batch found MT_OP_CUT / COPY / PASTE).
+// Each kernel runs one document run per one-wave workgroup (mt_replay_doc, mt_replay.h).
+template <bool FULL>
+__global__ __launch_bounds__(64, MT_LDS_WAVES_PER_SIMD) void mt_replay_lds_kernel(MtState S, MtOps ops, uint32_t* cursor, int lr, int lb, int lh) {
+    __shared__ MtScratch sc;
+    const uint32_t cur = mt_replay_doc<MT_RES_LDS, FULL>(S, ops, blockIdx.x, &sc, lr, lb, lh);
+    if (__lane_id() == 0) cursor[blockIdx.x] = cur;
+}
+// Blocks + heap in LDS (~9.5 KB per workgroup, 4 waves per SIMD), rows/window in HBM; a
+// document that outgrows LDS continues in HBM in the same wave.
+template <bool FULL>
+__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(MtState S, MtOps ops, uint32_t* cursor, int lb, int lh) {
+    __shared__ MtScratch sc;
+    const uint32_t cur = mt_replay_doc<MT_RES_BLK, FULL>(S, ops, blockIdx.x, &sc, 0, lb, lh);
+    if (__lane_id() == 0) cursor[blockIdx.x] = cur;
+}
+// Long documents (MT_RES_BIG): heap, window and U set in LDS (~68 KB, two workgroups per
+// CU), blocks and rows in HBM; one wave per SIMD at most, so the register budget is 256
+// VGPRs and nothing spills.  A document whose heap or height outgrows LDS continues in HBM.
+template <bool FULL>
+__global__ __launch_bounds__(64, 1) void mt_replay_big_kernel(MtState S, MtOps ops, uint32_t* cursor, int lw, int lh) {
+    __shared__ MtScratch sc;
+    const uint32_t cur = mt_replay_doc<MT_RES_BIG, FULL>(S, ops, blockIdx.x, &sc, lw, 0, lh);
+    if (__lane_id() == 0) cursor[blockIdx.x] = cur;
+}
+// Every pool in HBM: whole runs, or the rest of each run after mt_replay_lds_kernel.
+template <bool FULL>
+__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_kernel(MtState S, MtOps ops) {
+    __shared__ MtScratch sc;
+    (void)mt_replay_doc<MT_RES_HBM, FULL>(S, ops, blockIdx.x, &sc, 0, 0, 0);
+}
+template <bool FULL>
+__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_rest_kernel(MtState S, MtOps ops, const uint32_t* cursor) {
+    __shared__ MtScratch sc;
+    mt_replay_doc_rest<FULL>(S, ops, blockIdx.x, &sc, cursor[blockIdx.x]);
+}
+#if MT_KSET == 3
+// Generation: the same engine acting as sequencer + observer, writing the op
+// records it applies (a separate symbol so profiles never mix it with replay).
+__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_generate_kernel(MtState S, MtOps ops, MtGen gen) {
+    __shared__ MtScratch sc;
+    __shared__ int lastRef[64];
+    const uint32_t run = blockIdx.x;
+    const uint32_t doc = ops.doc_ids[run];
+    MtEng e;
+    e.bind(S, doc, &sc);
+    mt_replay_run(e, ops, run, doc, &gen, lastRef, ops.op_off[run]);
+    e.store(doc);
+}
+#endif
+
+// ------------------------------------------------------------- launchers ----
+#if MT_KSET == 0
+void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lb, int lh) {
+    hipLaunchKernelGGL(mt_replay_blk_kernel<false>, dim3(n), dim3(64), 0, s, S, o, cur, lb, lh);
+}
+#elif MT_KSET == 1
+void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lb, int lh) {
+    hipLaunchKernelGGL(mt_replay_blk_kernel<true>, dim3(n), dim3(64), 0, s, S, o, cur, lb, lh);
+}
+#elif MT_KSET == 2
+void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lw, int lh) {
+    if (full) hipLaunchKernelGGL(mt_replay_big_kernel<true>, dim3(n), dim3(64), 0, s, S, o, cur, lw, lh);
+    else hipLaunchKernelGGL(mt_replay_big_kernel<false>, dim3(n), dim3(64), 0, s, S, o, cur, lw, lh);
+}
+#else
+void mtk_lds(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lr, int lb, int lh) {
+    if (full) hipLaunchKernelGGL(mt_replay_lds_kernel<true>, dim3(n), dim3(64), 0, s, S, o, cur, lr, lb, lh);
+    else hipLaunchKernelGGL(mt_replay_lds_kernel<false>, dim3(n), dim3(64), 0, s, S, o, cur, lr, lb, lh);
+}
+void mtk_hbm(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* cur) {
+    if (cur) {
+        if (full) hipLaunchKernelGGL(mt_replay_rest_kernel<true>, dim3(n), dim3(64), 0, s, S, o, cur);
+        else hipLaunchKernelGGL(mt_replay_rest_kernel<false>, dim3(n), dim3(64), 0, s, S, o, cur);
+    } else if (full) hipLaunchKernelGGL(mt_replay_kernel<true>, dim3(n), dim3(64), 0, s, S, o);
+    else hipLaunchKernelGGL(mt_replay_kernel<false>, dim3(n), dim3(64), 0, s, S, o);
+}
+void mtk_generate(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const MtGen& g) {
+    hipLaunchKernelGGL(mt_generate_kernel, dim3(n), dim3(64), 0, s, S, o, g);
+}
+#endif

@@ -1,0 +1,11 @@
+// mt_kernels.h — launchers of the replay kernels (mt_k_replay.hip, one object per kernel set).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "mt_core.h"
+
+void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lb, int lh);
+void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lb, int lh);
+void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lw, int lh);
+void mtk_lds(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lr, int lb, int lh);
+void mtk_hbm(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* cur);
+void mtk_generate(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const MtGen& g);

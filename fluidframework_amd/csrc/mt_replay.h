@@ -77,7 +77,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
     // Replay prefetches op i+1's record while op i runs (generation writes the
     // record at the top of each iteration, so it loads in place).
     auto wn = wave_map(8, [&](int q) MT_LAM { return (!g && o0 < o1) ? ((const int*)&ops.rec[o0])[q] : 0; });
-    if (!g && Eng::kFull) { e.drec = ops.drec; e.dcount = ops.dcount; e.dcap = ops.dcap; }
+    if (!g && Eng::kFull) { e.drec = ops.drec; e.dcount = ops.dcount; e.dcap = ops.dcap; e.dtext = ops.dtext; e.dtcap = ops.dtcap; }
     for (uint32_t i = o0; i < o1; i++) {
         e.curOp = i;
         if (Eng::kLds && !e.ldsHeadroom()) return i;
@@ -103,6 +103,23 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
         const uint32_t w7 = (uint32_t)wave_at(w, 7);
         const int plen = (int)(w7 & 0xFFFF), pid = (int)(int16_t)(w7 >> 16);
         if (ty == MT_OP_UNSUPPORTED) { e.status |= MT_DS_UNSUPPORTED; break; }
+        unsigned long long resR = 0, resT = 0;
+        if constexpr (Eng::kFull) {
+            if (!g && e.drec) {
+                // capture headroom for this message: a range op emits at most one record per
+                // character of its range (every segment it touches is visible in it), or per row
+                const bool range = ty == MT_OP_REMOVE || ty == MT_OP_ANNOTATE || ty == MT_OP_CUT;
+                long long k = 1;
+                if (range) {
+                    k = (fl & (MT_OPF_REL1 | MT_OPF_REL2)) ? (long long)e.rowTop : (long long)p2 - (long long)p1;
+                    if (k > (long long)e.rowTop) k = e.rowTop;
+                    if (k < 0) k = 0;
+                }
+                resR = (unsigned long long)k + MT_DREC_SLACK;
+                resT = ty == MT_OP_PASTE ? (unsigned long long)e.regTextLen(c, (int)poff) : 0ull;
+                if (!e.dReserve(resR, resT)) { e.dStop = 1; return i; }
+            }
+        }
         if (ty != MT_OP_NOOP) {
             if (c >= MT_NONCOLLAB) e.status |= MT_DS_UNSUPPORTED;  // 0xFFFE/0xFFFF are reserved ids
             if (e.curSeq >= sq) e.status |= MT_DS_ASSERT_SEQ;       // completeAndLogOp, MT/client.ts:482
@@ -154,8 +171,57 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
             e.setMinSeq(ms);
         }
         if (e.status) break;
+        if constexpr (Eng::kFull) { if (resR) e.dRelease(resR, resT); }
     }
     return o1;
+}
+
+// One document run of a replay launch (every replay kernel and the host emulation run this).
+// The run starts at ops.start[run] (a capture resume) or op_off[run]; RES is the residency it
+// starts in: MT_RES_LDS hands the rest to a second, all-HBM launch (the returned op index goes
+// to cursor[]), MT_RES_BLK / MT_RES_BIG continue in HBM in the same wave.  Capture launches
+// record in ops.resume[run] where the run stopped for headroom (op_off[run + 1]: finished).
+template <int RES, bool FULL>
+MT_HD uint32_t mt_replay_doc(const MtState& S, const MtOps& ops, uint32_t run, MtScratch* sc, int l0, int l1, int l2) {
+    const uint32_t doc = ops.doc_ids[run], o1 = ops.op_off[run + 1];
+    const uint32_t o0 = ops.start ? ops.start[run] : ops.op_off[run];
+    uint32_t cur = o0, stop = o1;
+    if (o0 < o1) {
+        MtEngT<RES, FULL> e;
+        e.bind(S, doc, sc);
+        if constexpr (RES == MT_RES_HBM) { (void)l0; (void)l1; (void)l2; cur = mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0); }
+        else if (e.toLds(l0, l1, l2)) {
+            cur = mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0);
+            e.fromLds();
+        }
+        const bool stopped = e.dStop != 0;
+        e.store(doc);
+        if (stopped) { stop = cur; cur = o1; }                   // no hand-over: the host resumes it
+        else if (RES != MT_RES_LDS && cur < o1) {
+            // A document that outgrew LDS continues here with its pools in HBM (no second
+            // launch: long documents, which outgrow it first, keep their head start).
+            MtEngT<MT_RES_HBM, FULL> h;
+            h.bind(S, doc, sc);
+            const uint32_t c2 = mt_replay_run(h, ops, run, doc, nullptr, nullptr, cur);
+            if (h.dStop) stop = c2;
+            h.store(doc);
+        }
+    }
+    if (FULL && ops.resume && !(RES == MT_RES_LDS && cur < o1)) wave_for(1, [&](int) MT_LAM { ops.resume[run] = stop; });
+    return cur;
+}
+// The all-HBM pass after an MT_RES_LDS launch: the rest of each run from its hand-over point.
+template <bool FULL>
+MT_HD void mt_replay_doc_rest(const MtState& S, const MtOps& ops, uint32_t run, MtScratch* sc, uint32_t o0) {
+    const uint32_t o1 = ops.op_off[run + 1];
+    if (o0 >= o1) return;
+    const uint32_t doc = ops.doc_ids[run];
+    MtEngT<MT_RES_HBM, FULL> e;
+    e.bind(S, doc, sc);
+    const uint32_t c2 = mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0);
+    const uint32_t stop = e.dStop ? c2 : o1;
+    e.store(doc);
+    if (FULL && ops.resume) wave_for(1, [&](int) MT_LAM { ops.resume[run] = stop; });
 }
 
 // Client.updateSeqNumbers(min, seq) (MT/client.ts:843-850) on one document;

@@ -126,12 +126,13 @@ __device__ __forceinline__ int wave_set(int a, int k, int v) { return __lane_id(
 // per-lane add into wave-private LDS (conflicting lanes serialize in hardware)
 __device__ __forceinline__ void lds_add(int* p, int v) { __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
 // Lane 0 takes the next slot of a global 64-bit cursor; every lane gets its index.
-__device__ __forceinline__ unsigned long long wave_atomic_next(unsigned long long* p) {
+__device__ __forceinline__ unsigned long long wave_atomic_add(unsigned long long* p, unsigned long long d) {
     unsigned long long v = 0;
-    if (__lane_id() == 0) v = __hip_atomic_fetch_add(p, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__lane_id() == 0) v = __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
            ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
 }
+__device__ __forceinline__ unsigned long long wave_atomic_next(unsigned long long* p) { return wave_atomic_add(p, 1ull); }
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -216,6 +217,7 @@ template <class F> inline LaneArr<int> wave_shfl(const LaneArr<int>& a, F src) {
 }
 inline LaneArr<int> wave_set(LaneArr<int> a, int k, int v) { if (k >= 0 && k < MT_WAVE) a.v[k] = v; return a; }
 inline void lds_add(int* p, int v) { *p += v; }
-inline unsigned long long wave_atomic_next(unsigned long long* p) { return __atomic_fetch_add(p, 1ull, __ATOMIC_RELAXED); }
+inline unsigned long long wave_atomic_add(unsigned long long* p, unsigned long long d) { return __atomic_fetch_add(p, d, __ATOMIC_RELAXED); }
+inline unsigned long long wave_atomic_next(unsigned long long* p) { return wave_atomic_add(p, 1ull); }
 inline void wave_sync() {}
 #endif

@@ -96,6 +96,8 @@ def _bind(lib, prefix: str):
         load_snapshot=f("load_snapshot", ctypes.c_int, [P, P]),
         delta_capture=f("delta_capture", ctypes.c_int, [P, ctypes.c_uint64]),
         delta_records=f("delta_records", ctypes.c_int, [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_uint64)]),
+        delta_text=f("delta_text", ctypes.c_int, [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_uint64),
+                                                  ctypes.POINTER(U32)]),
         doc_pset=f("doc_pset", ctypes.c_int, [P, U32, I32, P, P, ctypes.POINTER(U32)]),
     )
 
@@ -328,6 +330,14 @@ class Engine:
             return np.zeros(0, DELTA_DTYPE)
         return np.frombuffer(ctypes.string_at(ptr, n.value * DELTA_DTYPE.itemsize), DELTA_DTYPE).copy()
 
+    def delta_text(self) -> tuple[np.ndarray, int]:
+        """(UTF-16 units of the last batch's pasted text segments, device launches the batch took)."""
+        ptr, n, launches = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_uint32()
+        self._check(self.fn["delta_text"](self.h, ctypes.byref(ptr), ctypes.byref(n), ctypes.byref(launches)),
+                    "mt_delta_text")
+        units = np.frombuffer(ctypes.string_at(ptr, 2 * n.value), np.uint16).copy() if n.value else np.zeros(0, np.uint16)
+        return units, int(launches.value)
+
     def doc_pset(self, doc: int, pset_id: int):
         """(key ids, value ids) of a document's device property set, insertion order."""
         k, v, n = np.zeros(16, np.uint16), np.zeros(16, np.int32), ctypes.c_uint32()
@@ -556,17 +566,25 @@ class ClientGroup:
                 c.names_uploaded = len(c.names.names)
         batch = bb.build()
         self.last_batch = batch          # op indexing of delta records (Engine.delta_records)
+        # Capture is armed only around batches with a listener (the other batches run the
+        # kernels without capture code).  The capacity is a launch's buffer, not a bound:
+        # a batch that emits more resumes in further launches (mt_delta_capture).
         if listen:
-            self.engine.delta_capture(max(4096, 64 * batch.n_ops))
-        self.engine.apply(batch)
-        self.engine.sync()
-        if listen:
-            self._deliver(listen)
+            self.engine.delta_capture(max(1 << 16, 512 * len(listen) + 16 * batch.n_ops))
+        try:
+            self.engine.apply(batch)
+            self.engine.sync()
+            if listen:
+                self._deliver(listen)
+        finally:
+            if listen:
+                self.engine.delta_capture(0)
 
     def _deliver(self, listen):
         """Hand each listening client its messages' sequenceDelta events: per op member,
         the INSERT/REMOVE/ANNOTATE records as ranges with their property maps."""
         recs = self.engine.delta_records()
+        units, _ = self.engine.delta_text()
         by_op: dict = {}
         for r in recs:
             if 0 <= int(r["kind"]) <= 2:
@@ -586,9 +604,14 @@ class ClientGroup:
                 out = []
                 for r in by_op.get(op, ()):
                     k = int(r["kind"])
-                    a, b = int(r["a"]), int(r["b"])
-                    out.append({"kind": k, "pos": int(r["pos"]), "len": int(r["len"]),
+                    a, b, pad, ln = int(r["a"]), int(r["b"]), int(r["pad"]), int(r["len"])
+                    spec = None                      # an insert of the op's own seg
+                    if k == 0 and b == 0:            # a pasted text clone: its text from the device
+                        spec = {"text": units[pad:pad + ln].tobytes().decode("utf-16-le", "surrogatepass")}
+                    elif k == 0 and b == 1:          # a pasted marker
+                        spec = {"marker": {"refType": pad}}
+                    out.append({"kind": k, "pos": int(r["pos"]), "len": ln,
                                 "before": pset(a) if k == 2 else None,
-                                "after": pset(b) if k == 2 else (pset(a) if k == 0 else None)})
+                                "after": pset(b) if k == 2 else (pset(a) if k == 0 else None), "spec": spec})
                 return out
             c.delta_listener(entries, events_of)

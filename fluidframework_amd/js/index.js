@@ -427,6 +427,8 @@ class Engine {
     deltaCapture(capacity) { addon.deltaCapture(this.h, capacity); }
     /** The last batch's records: Int32Array, 8 per record (op, kind, pos, len, seg, a, b, pad). */
     deltaRecords() { return addon.deltaRecords(this.h); }
+    /** The last batch's pasted text (mt_delta_text): INSERT records with b === 0 index it. */
+    deltaText() { return addon.deltaText(this.h); }
     /** A document's device property set as a plain object (undefined for -1). */
     psetObject(doc, id) {
         if (id < 0) return undefined;
@@ -580,15 +582,22 @@ class ClientGroup {
             }
         }
         const batch = bb.build();
-        if (listen.length) this.engine.deltaCapture(Math.max(4096, 64 * batch.type.length));
-        this.engine.apply(batch);
-        this.engine.sync();
-        if (listen.length) this.deliver(listen);
+        // Capture only around batches with a listener; the capacity is one launch's buffer
+        // (a batch that emits more resumes in further launches, mt_delta_capture).
+        if (listen.length) this.engine.deltaCapture(Math.max(1 << 16, 512 * listen.length + 16 * batch.type.length));
+        try {
+            this.engine.apply(batch);
+            this.engine.sync();
+            if (listen.length) this.deliver(listen);
+        } finally {
+            if (listen.length) this.engine.deltaCapture(0);
+        }
     }
     /** Each listening client's messages with their sequenceDelta events: per op member, the
      * INSERT / REMOVE / ANNOTATE records as ranges with their property maps. */
     deliver(listen) {
         const r = this.engine.deltaRecords();
+        const text = this.engine.deltaText();
         const byOp = new Map();
         for (let i = 0; i < r.length; i += 8) {
             if (r[i + 1] < 0 || r[i + 1] > 2) continue;
@@ -603,10 +612,14 @@ class ClientGroup {
                 return cache.get(id);
             };
             const eventsOf = (op) => (byOp.get(op) || []).map((i) => {
-                const kind = r[i + 1], a = r[i + 5], b = r[i + 6];
-                return { kind, pos: r[i + 2], len: r[i + 3],
+                const kind = r[i + 1], a = r[i + 5], b = r[i + 6], pad = r[i + 7], len = r[i + 3];
+                // a register paste's clone: its own content as the engine recorded it
+                let spec;
+                if (kind === OP_INSERT && b === 0) spec = { text: text.substr(pad, len) };
+                else if (kind === OP_INSERT && b === 1) spec = { marker: { refType: pad } };
+                return { kind, pos: r[i + 2], len,
                     before: kind === OP_ANNOTATE ? pset(a) : undefined,
-                    after: kind === OP_ANNOTATE ? pset(b) : (kind === OP_INSERT ? pset(a) : undefined) };
+                    after: kind === OP_ANNOTATE ? pset(b) : (kind === OP_INSERT ? pset(a) : undefined), spec };
             });
             c.deltaListener(entries, eventsOf);
         }
@@ -665,7 +678,8 @@ function opsFromDelta(member, ranges) {
             if (last && last.pos2 === r.pos && matchProperties(last.props, props)) last.pos2 += r.len;
             else ops.push({ pos1: r.pos, pos2: r.pos + r.len, props, type: OP_ANNOTATE });
         } else if (r.kind === OP_INSERT) {
-            ops.push({ pos1: r.pos, seg: segmentJson(member.seg, r.after), type: OP_INSERT });
+            // the inserted segment's clone: the op's seg, or a pasted clone's own content
+            ops.push({ pos1: r.pos, seg: segmentJson(r.spec || member.seg, r.after), type: OP_INSERT });
         } else if (r.kind === OP_REMOVE) {
             const last = ops[ops.length - 1];
             if (last && last.pos1 === r.pos) last.pos2 += r.len;

@@ -469,6 +469,20 @@ napi_value DeltaRecords(napi_env env, napi_callback_info info) {
     return make_i32(env, (const int32_t*)r, (size_t)n * 8);
 }
 
+// deltaText(ctx) -> string: the UTF-16 text of the last batch's pasted text segments
+// (INSERT records with b == 0 index it by pad / len), mt_delta_text
+napi_value DeltaText(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
+    const uint16_t* t = nullptr; uint64_t n = 0;
+    int rc = mt_delta_text(c, &t, &n, nullptr);
+    if (rc) return throw_rc(env, c, rc, "mt_delta_text");
+    napi_value s;
+    NAPI_OK(napi_create_string_utf16(env, (const char16_t*)t, (size_t)n, &s));
+    return s;
+}
+
 // docPset(ctx, doc, id) -> {keys: Uint32Array, values: Int32Array} (interned ids, insertion order)
 napi_value DocPset(napi_env env, napi_callback_info info) {
     napi_value argv[3];
@@ -520,6 +534,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"getText", nullptr, GetText, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"deltaCapture", nullptr, DeltaCapture, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"deltaRecords", nullptr, DeltaRecords, nullptr, nullptr, nullptr, kAttr, nullptr},
+        {"deltaText", nullptr, DeltaText, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"docPset", nullptr, DocPset, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"lastError", nullptr, LastError, nullptr, nullptr, nullptr, kAttr, nullptr},
     };

@@ -118,8 +118,9 @@ def annotate_delta_keys(op: dict, before: dict | None) -> list:
 
 def ops_from_delta(member: dict, ranges: list) -> list:
     """createOpsFromDelta for one op's sequenceDelta event.  ranges: the event's
-    deltaSegments in order, each {kind, pos, len, before, after} (before/after: the
-    segment's properties around an annotate; after: an insert's properties)."""
+    deltaSegments in order, each {kind, pos, len, before, after[, spec]} (before/after: the
+    segment's properties around an annotate; after: an insert's properties; spec: a pasted
+    segment's content, {"text": ...} or {"marker": {"refType": n}})."""
     ops: list = []
     for r in ranges:
         if r["kind"] == ANNOTATE:
@@ -131,7 +132,10 @@ def ops_from_delta(member: dict, ranges: list) -> list:
             else:
                 ops.append({"pos1": r["pos"], "pos2": r["pos"] + r["len"], "props": props, "type": ANNOTATE})
         elif r["kind"] == INSERT:
-            ops.append({"pos1": r["pos"], "seg": seg_json(member["seg"], r["after"]), "type": INSERT})
+            # the inserted segment's clone: the op's seg, or (a register paste has none) the
+            # pasted clone's own text / marker as the engine recorded it
+            spec = r.get("spec") or member["seg"]
+            ops.append({"pos1": r["pos"], "seg": seg_json(spec, r["after"]), "type": INSERT})
         elif r["kind"] == REMOVE:
             last = ops[-1] if ops else None
             if last is not None and last.get("pos1") == r["pos"]:

@@ -208,7 +208,10 @@ typedef struct mt_ctx mt_ctx;
  * fires after its ensureIntervalBoundary SPLITs and before the zamboni APPEND/UNLINKs it
  * triggers).  pos is SequenceEvent.ranges[].position: the segment's position in the
  * observer's view (client.getPosition) evaluated when the callback fires.
- *   INSERT   seg = the new segment, len = cachedLength, a = its property set (mt_doc_pset)
+ *   INSERT   seg = the new segment, len = cachedLength, a = its property set (mt_doc_pset);
+ *            b = -1: the op's own seg spec; b = 0: a register paste's text clone whose text
+ *            is units [pad, pad + len) of mt_delta_text; b = 1: a pasted marker of refType pad
+ *            (createOpsFromDelta writes r.segment.clone().toJSONObject(), sequence.ts:83-87)
  *   REMOVE   seg = a newly removed segment (overlapping removes are not reported)
  *   ANNOTATE seg = an annotated segment, a / b = its property set before / after
  *   SPLIT    seg = the left part (len = its new length), a = the right part, b = its length
@@ -397,14 +400,25 @@ int  mt_get_text(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
  * segment object twice the document gets MT_DS_UNSUPPORTED.  Stream-ordered;
  * status words after mt_sync. */
 int  mt_load_snapshot(mt_ctx* ctx, const mt_load_batch* batch);
-/* Delta capture for the following batches (mt_apply_batch / mt_replay_resident):
- * capacity records per batch; 0 turns capture off (the default: the replay kernels
- * then never touch the record buffer). */
+/* The build's source hash (sha256 prefix of csrc/ + this header, __graft_entry__.source_hash):
+ * lets a host prove the library it loaded was compiled from its own tree. */
+const char* mt_source_hash(void);
+/* Delta capture for the following batches (mt_apply_batch / mt_replay_resident): a device
+ * buffer of `capacity` records (raised to one message of the largest document); 0 turns
+ * capture off (the default: the replay kernels then never touch the record buffer).  A
+ * batch never overflows it: before each message a document reserves the records it can
+ * emit, and when a launch is full the run stops before that message, the records move to
+ * the host and a further launch resumes the stopped runs, so a capture batch of any size
+ * completes (mt_apply_batch is synchronous while capture is armed). */
 int  mt_delta_capture(mt_ctx* ctx, uint64_t capacity);
 /* The records of the last batch in callback order per document and op (sorted by op
  * index, program order within an op): a library-owned array valid until the next
  * batch.  MT_E_OOM if the batch produced more than the capacity. */
 int  mt_delta_records(mt_ctx* ctx, const mt_delta_rec** out, uint64_t* n);
+/* The UTF-16 text of the last batch's pasted text segments (INSERT records with b == 0 index
+ * it), a library-owned array valid until the next batch; *launches (optional) = the device
+ * launches the batch took. */
+int  mt_delta_text(mt_ctx* ctx, const uint16_t** out, uint64_t* n, uint32_t* launches);
 /* The keys and values (host-interned ids, value -1 never occurs) of property set
  * pset_id of document doc, in insertion order; returns the count in *n (<= 16). */
 int  mt_doc_pset(mt_ctx* ctx, uint32_t doc, int32_t pset_id, uint16_t* keys, int32_t* values, uint32_t* n);

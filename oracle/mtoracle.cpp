@@ -345,6 +345,9 @@ struct PropTable {                       // host-interned op property sets
     std::vector<JVal> values;
 };
 
+struct Seg;
+static std::string seg_json(const Seg* s, const u16s* textOverride = nullptr);
+
 struct Tree {
     // CollaborationWindow, MT/mergeTree.ts:817-834
     int cwClientId = LocalClientId; bool collaborating = false; int minSeq = 0, currentSeq = 0;
@@ -365,6 +368,30 @@ struct Tree {
     static std::string propsJson(const Seg* s);
     void drec(int kind, Seg* s, int len, int b, const std::string& pa = "null", const std::string& pb = "null") {
         if (capture) capture->push_back({curOp, kind, getPosition(s, currentSeq, cwClientId), len, b, pa, pb});
+    }
+    // processMergeTreeMsg's transformation (packages/dds/sequence/src/sequence.ts:604-642):
+    // while a message with refSeq != seq - 1 is applied, each sequenceDelta range as
+    // createOpsFromDelta (sequence.ts:58-105) reads it when the callback fires: position
+    // (client.getPosition), cachedLength, for an insert segment.clone().toJSONObject(), for
+    // an annotate the segment's current value of every key of its propertyDeltas.
+    struct XRange { int op, kind, pos, len; std::string seg; JVal props; };
+    std::vector<XRange>* xform = nullptr;
+    std::map<const Seg*, JVal> xdeltas;       // propertyDeltas of the annotate being applied
+    void xrec(int kind, Seg* s) {
+        if (!xform) return;
+        XRange x; x.op = curOp; x.kind = kind; x.pos = getPosition(s, currentSeq, cwClientId); x.len = s->cachedLength;
+        if (kind == 0) x.seg = seg_json(s);
+        if (kind == 2) {
+            x.props = make_obj();
+            const JVal& dl = xdeltas[s];
+            for (int i : obj_order(dl)) {
+                const u16s& k = dl.okeys[i];
+                const int j = s->hasProps ? obj_find(s->props, k) : -1;
+                if (j >= 0 && s->props.ovals[j].t != JVal::Undef) obj_set(x.props, k, s->props.ovals[j]);
+                else obj_set(x.props, k, nullv);
+            }
+        }
+        xform->push_back(x);
     }
 
     Tree() { root = makeBlock(0); heap.push_back({nullptr, -2}); }
@@ -782,6 +809,7 @@ struct Tree {
             updateRoot(sn);
             if (collaborating && !(seg->seq == UnassignedSeq && clientId == cwClientId) && seg->seq > minSeq) addToLRUSet(seg, seg->seq);
             drec(0, seg, seg->cachedLength, 0, "null", propsJson(seg));                          // INSERT callback :1992-2000
+            xrec(0, seg);
         }
         if (collaborating && seq != UnassignedSeq) zamboni();
     }
@@ -819,7 +847,7 @@ struct Tree {
                 insertPos += seg->cachedLength;
             }
         }
-        for (Seg* seg : in) drec(0, seg, seg->cachedLength, 0, "null", propsJson(seg));         // INSERT callback :1992-2000
+        for (Seg* seg : in) { drec(0, seg, seg->cachedLength, 0, "null", propsJson(seg)); xrec(0, seg); }   // INSERT callback :1992-2000
         if (collaborating && seq != UnassignedSeq) zamboni();
     }
     template <class F>
@@ -865,7 +893,7 @@ struct Tree {
         };
         auto post = [&](Block* b) { if (overwrite) nodeUpdateLengthNewStructure(b); else blockUpdateLength(b, seq, clientId); };
         nodeMapPost(root, 0, refSeq, clientId, start, end, leaf, post);
-        for (Seg* x : removed) drec(1, x, x->cachedLength, 0);                                    // REMOVE callback :2725-2733
+        for (Seg* x : removed) { drec(1, x, x->cachedLength, 0); xrec(1, x); }                      // REMOVE callback :2725-2733
         if (collaborating && seq != UnassignedSeq) zamboni();
     }
     void addProperties(Seg* s, const PropTable& pt, int set, bool rewrite, int seq, bool collab) {
@@ -873,15 +901,18 @@ struct Tree {
         (void)seq; (void)collab;
         if (!s->hasProps) { s->hasProps = true; s->props = make_obj(); }
         const auto& np = pt.sets[set];
+        JVal* dl = nullptr;                                   // the returned deltas' keys (:66-109)
+        if (xform) { dl = &xdeltas[s]; *dl = make_obj(); }
         auto newVal = [&](const u16s& k) -> const JVal* {
             for (auto& kv : np) if (kv.first == k) return kv.second < 0 ? &nullv : &pt.values[kv.second];
             return nullptr;
         };
         if (rewrite) {
             std::vector<u16s> keys; for (int i : obj_order(s->props)) keys.push_back(s->props.okeys[i]);
-            for (auto& k : keys) if (!truthy(newVal(k))) obj_del(s->props, k);
+            for (auto& k : keys) if (!truthy(newVal(k))) { if (dl) obj_set(*dl, k, nullv); obj_del(s->props, k); }
         }
         for (auto& kv : np) {
+            if (dl) obj_set(*dl, kv.first, nullv);
             if (kv.second < 0) obj_del(s->props, kv.first);
             else obj_set(s->props, kv.first, pt.values[kv.second]);
         }
@@ -894,11 +925,11 @@ struct Tree {
         auto leaf = [&](Seg* s, int, int, int) {
             std::string before = capture ? propsJson(s) : std::string();
             addProperties(s, pt, set, rewrite, seq, collaborating);
-            if (capture) ann.push_back({s, before});
+            if (capture || xform) ann.push_back({s, before});
             if (collaborating && seq != UnassignedSeq) addToLRUSet(s, seq);
         };
         nodeMap(root, 0, refSeq, clientId, start, end, leaf, nullptr, nullptr);
-        for (auto& x : ann) drec(2, x.first, x.first->cachedLength, 0, x.second, propsJson(x.first));   // ANNOTATE :2609-2617
+        for (auto& x : ann) { drec(2, x.first, x.first->cachedLength, 0, x.second, propsJson(x.first)); xrec(2, x.first); }   // ANNOTATE :2609-2617
         if (collaborating && seq != UnassignedSeq) zamboni();
     }
     /* ---- zamboni ---- */
@@ -1015,6 +1046,7 @@ struct Doc {
     std::vector<int> shortToStream;          // short id -> stream client index (-1 observer)
     std::vector<int> streamToShort;
     int opCounter = 0;                       // op members applied (mt_op_batch indexing of the message stream)
+    std::vector<JVal> messagesSinceMSNChange;   // SharedSegmentSequence's legacy stash (sequence.ts:604-658)
     // RegisterCollection (MT/mergeTree.ts:864-896), keyed by (short client id, name): the
     // short id stands for the long id the reference keys by (one-to-one per document).
     // pasted: the reference would link the same segment objects a second time on a second
@@ -1060,7 +1092,7 @@ static Seg* specToSegment(Doc& d, const uint16_t* text, uint32_t n, int refType,
     return s;
 }
 
-static std::string seg_json(const Seg* s, const u16s* textOverride = nullptr) {
+static std::string seg_json(const Seg* s, const u16s* textOverride) {
     std::string o;
     if (s->marker) {                                                                             // Marker.toJSONObject :649-653
         o += "{\"marker\":{\"refType\":"; num_to_js(o, s->refType); o += "}";
@@ -1538,9 +1570,8 @@ char* ora_register_info_json(ora_doc* o, const char* client_literal, const char*
     memcpy(r, out.c_str(), out.size() + 1);
     return r;
 }
-uint32_t ora_apply_msg_json(ora_doc* o, const char* json) {
-    Doc& d = o->d; Tree& t = d.t;
-    JVal m = json_parse(json);
+static uint32_t apply_msg(Doc& d, const JVal& m) {
+    Tree& t = d.t;
     const JVal* cid = jget(m, u"clientId");
     int seq, ref, msn;
     if (!cid || cid->t != JVal::Str || !jnum(m, u"sequenceNumber", seq) || !jnum(m, u"referenceSequenceNumber", ref) ||
@@ -1558,6 +1589,99 @@ uint32_t ora_apply_msg_json(ora_doc* o, const char* json) {
     if (msn > seq) t.status |= MT_DS_ASSERT_MSN;
     t.setMinSeq(msn);
     return t.status;
+}
+uint32_t ora_apply_msg_json(ora_doc* o, const char* json) {
+    JVal m = json_parse(json);
+    return apply_msg(o->d, m);
+}
+/* ---- SharedSegmentSequence.processMergeTreeMsg, legacy format (sequence.ts:604-658) ---- */
+static JVal jnum_val(double v) { JVal x; x.t = JVal::Num; x.n = v; return x; }
+// createOpsFromDelta (sequence.ts:58-105) over the ranges [a, b) of one sequenceDelta event.
+static void ops_from_delta(const std::vector<Tree::XRange>& rs, size_t a, size_t b, std::vector<JVal>& ops) {
+    const size_t first = ops.size();                 // `ops` of this event only: coalescing is per event
+    for (size_t i = a; i < b; i++) {
+        const Tree::XRange& r = rs[i];
+        JVal* last = ops.size() > first ? &ops.back() : nullptr;
+        auto numAt = [](const JVal* o, const char16_t* k) -> const JVal* {
+            if (!o) return nullptr; const int j = obj_find(*o, k); return j >= 0 ? &o->ovals[j] : nullptr; };
+        if (r.kind == 2) {                                                                       // ANNOTATE
+            const JVal* lp2 = numAt(last, u"pos2");
+            const JVal* lpr = numAt(last, u"props");
+            if (last && lp2 && lp2->t == JVal::Num && lp2->n == r.pos && match_properties(lpr, &r.props)) {
+                obj_set(*last, u"pos2", jnum_val(lp2->n + r.len));
+            } else {                                                                             // createAnnotateRangeOp
+                JVal o = make_obj();
+                obj_set(o, u"pos1", jnum_val(r.pos)); obj_set(o, u"pos2", jnum_val(r.pos + r.len));
+                obj_set(o, u"props", r.props); obj_set(o, u"type", jnum_val(2));
+                ops.push_back(o);
+            }
+        } else if (r.kind == 0) {                                                                // createInsertOp
+            JVal o = make_obj();
+            obj_set(o, u"pos1", jnum_val(r.pos)); obj_set(o, u"seg", json_parse(r.seg.c_str())); obj_set(o, u"type", jnum_val(0));
+            ops.push_back(o);
+        } else if (r.kind == 1) {                                                                // REMOVE
+            const JVal* lp1 = numAt(last, u"pos1");
+            const JVal* lp2 = numAt(last, u"pos2");
+            if (last && lp1 && lp1->t == JVal::Num && lp1->n == r.pos && lp2) {
+                obj_set(*last, u"pos2", jnum_val(lp2->n + r.len));
+            } else {                                                                             // createRemoveRangeOp
+                JVal o = make_obj();
+                obj_set(o, u"pos1", jnum_val(r.pos)); obj_set(o, u"pos2", jnum_val(r.pos + r.len)); obj_set(o, u"type", jnum_val(1));
+                ops.push_back(o);
+            }
+        }
+    }
+}
+static void msn_changed(Doc& d, int minSeq) {                                                    // processMinSequenceNumberChanged :648-658
+    auto& st = d.messagesSinceMSNChange;
+    size_t i = 0;
+    for (; i < st.size(); i++) { int sq = 0; jnum(st[i], u"sequenceNumber", sq); if (sq > minSeq) break; }
+    if (i) st.erase(st.begin(), st.begin() + i);
+}
+uint32_t ora_channel_process(ora_doc* o, const char* json) {
+    Doc& d = o->d; Tree& t = d.t;
+    JVal m = json_parse(json);                                     // parseHandles: the DDS's own copy
+    int seq = 0, ref = 0, msn = 0;
+    jnum(m, u"sequenceNumber", seq); jnum(m, u"referenceSequenceNumber", ref); jnum(m, u"minimumSequenceNumber", msn);
+    const bool needs = ref != seq - 1;
+    std::vector<Tree::XRange> xs;
+    if (needs) t.xform = &xs;
+    const uint32_t st = apply_msg(d, m);
+    t.xform = nullptr; t.xdeltas.clear();
+    JVal stash = m;
+    if (needs) {                                                   // {...message, referenceSequenceNumber, contents}
+        std::vector<JVal> ops;
+        for (size_t a = 0; a < xs.size();) {                       // one sequenceDelta event per op member
+            size_t b = a + 1;
+            while (b < xs.size() && xs[b].op == xs[a].op) b++;
+            ops_from_delta(xs, a, b, ops);
+            a = b;
+        }
+        obj_set(stash, u"referenceSequenceNumber", jnum_val(seq - 1));
+        if (ops.size() == 1) obj_set(stash, u"contents", ops[0]);
+        else {                                                     // createGroupOp(...ops)
+            JVal g = make_obj(); JVal arr; arr.t = JVal::Arr; arr.arr = ops;
+            obj_set(g, u"ops", arr); obj_set(g, u"type", jnum_val(3));
+            obj_set(stash, u"contents", g);
+        }
+    }
+    d.messagesSinceMSNChange.push_back(stash);
+    auto& ms = d.messagesSinceMSNChange;
+    int s20 = 0;
+    if (ms.size() > 20 && jnum(ms[20], u"sequenceNumber", s20) && s20 < msn) msn_changed(d, msn);
+    return st;
+}
+// snapshotMergeTree (sequence.ts:592-602): the stash trimmed to the MSN and re-stamped with it,
+// as JSON.stringify writes it into the catch-up blob; NULL when the stash is empty (no blob).
+char* ora_channel_stash_json(ora_doc* o, int32_t min_seq) {
+    Doc& d = o->d;
+    msn_changed(d, min_seq);
+    if (d.messagesSinceMSNChange.empty()) return nullptr;
+    JVal arr; arr.t = JVal::Arr;
+    for (JVal& m : d.messagesSinceMSNChange) { obj_set(m, u"minimumSequenceNumber", jnum_val(min_seq)); arr.arr.push_back(m); }
+    std::string j; stringify(j, arr);
+    char* out = (char*)malloc(j.size() + 1); memcpy(out, j.c_str(), j.size() + 1);
+    return out;
 }
 // posFromRelativePos (MT/mergeTree.ts:1949-1972) of an IRelativePosition given as JSON,
 // under the perspective of the client with this long id; -1: unknown marker id.

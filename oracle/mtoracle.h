@@ -36,6 +36,13 @@ int32_t  ora_get_length_json(ora_doc* d, int32_t ref_seq, const char* client_lit
 /* posFromRelativePos of an IRelativePosition (JSON) under that client's perspective;
  * -1 when no marker carries the id. */
 int32_t  ora_rel_pos_json(ora_doc* d, int32_t ref_seq, const char* client_literal, const char* relpos_json);
+/* SharedSegmentSequence.processMergeTreeMsg for the legacy format (sequence.ts:604-642):
+ * applies the message and stashes it, transformed from its sequenceDelta events by
+ * createOpsFromDelta (sequence.ts:58-105) when refSeq != seq - 1.  Returns the status. */
+uint32_t ora_channel_process(ora_doc* d, const char* json);
+/* snapshotMergeTree's catch-up messages (sequence.ts:592-602): the stash trimmed to and
+ * stamped with min_seq, as JSON text (free with ora_free_buf), or NULL when empty. */
+char*    ora_channel_stash_json(ora_doc* d, int32_t min_seq);
 /* Delta / maintenance callbacks as records (on != 0), and the records so far as a JSON
  * array [op, kind, pos, len, b, propsBefore|null, propsAfter|null] (free with ora_free_buf). */
 void     ora_delta_capture(ora_doc* d, int on);

@@ -20,53 +20,20 @@ static void mtb_d2h(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n)
 static void mtb_d2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static int mtb_sync(mt_ctx*) { return MT_OK; }
 // FULL as on the device: the capture instantiation only while a delta buffer is armed.
+// The same per-run function as the device kernels (mt_replay_doc), one run at a time.
 template <bool FULL>
 static void replay_runs(mt_ctx* c, uint32_t n_runs) {
     uint32_t* cursor = (uint32_t*)c->b_cursor.p;
     for (uint32_t run = 0; run < n_runs; run++) {
-        const uint32_t doc = c->ops.doc_ids[run], o0 = c->ops.op_off[run];
-        uint32_t cur = o0;
-        if (c->use_lds == 3) {
-            MtScratch sc; MtEngT<MT_RES_BIG, FULL> e; e.bind(c->S, doc, &sc);
-            if (e.toLds(c->lds_rows, 0, c->lds_heap)) {
-                cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
-                e.fromLds();
-            }
-            e.store(doc);
-            if (cur < c->ops.op_off[run + 1]) {
-                MtEngT<MT_RES_HBM, FULL> h; h.bind(c->S, doc, &sc);
-                mt_replay_run(h, c->ops, run, doc, nullptr, nullptr, cur);
-                h.store(doc);
-            }
-        } else if (c->use_lds == 2) {
-            MtScratch sc; MtEngT<MT_RES_BLK, FULL> e; e.bind(c->S, doc, &sc);
-            if (e.toLds(0, c->lds_blks, c->lds_heap)) {
-                cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
-                e.fromLds();
-            }
-            e.store(doc);
-            if (cur < c->ops.op_off[run + 1]) {               // continues in HBM within the same "wave"
-                MtEngT<MT_RES_HBM, FULL> h; h.bind(c->S, doc, &sc);
-                mt_replay_run(h, c->ops, run, doc, nullptr, nullptr, cur);
-                h.store(doc);
-                // cursor keeps the hand-over point (diagnostic); the HBM pass below skips it
-            }
-        } else if (c->use_lds) {
-            MtScratch sc; MtEngT<MT_RES_LDS, FULL> e; e.bind(c->S, doc, &sc);
-            if (e.toLds(c->lds_rows, c->lds_blks, c->lds_heap)) {
-                cur = mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, o0);
-                e.fromLds();
-            }
-            e.store(doc);
-        }
-        cursor[run] = cur;
+        MtScratch sc;
+        if (c->use_lds == 3) cursor[run] = mt_replay_doc<MT_RES_BIG, FULL>(c->S, c->ops, run, &sc, c->lds_rows, 0, c->lds_heap);
+        else if (c->use_lds == 2) cursor[run] = mt_replay_doc<MT_RES_BLK, FULL>(c->S, c->ops, run, &sc, 0, c->lds_blks, c->lds_heap);
+        else if (c->use_lds) cursor[run] = mt_replay_doc<MT_RES_LDS, FULL>(c->S, c->ops, run, &sc, c->lds_rows, c->lds_blks, c->lds_heap);
+        else (void)mt_replay_doc<MT_RES_HBM, FULL>(c->S, c->ops, run, &sc, 0, 0, 0);
     }
-    for (uint32_t run = 0; run < n_runs && c->use_lds < 2; run++) {
-        if (cursor[run] >= c->ops.op_off[run + 1]) continue;
-        const uint32_t doc = c->ops.doc_ids[run];
-        MtScratch sc; MtEngT<MT_RES_HBM, FULL> e; e.bind(c->S, doc, &sc);
-        mt_replay_run(e, c->ops, run, doc, nullptr, nullptr, cursor[run]);
-        e.store(doc);
+    for (uint32_t run = 0; run < n_runs && c->use_lds == 1; run++) {
+        MtScratch sc;
+        mt_replay_doc_rest<FULL>(c->S, c->ops, run, &sc, cursor[run]);
     }
 }
 // Same two launches as the device (mt_engine.hip): LDS-resident pass, then the

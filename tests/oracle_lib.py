@@ -54,6 +54,10 @@ def lib():
         L.ora_register_info_json.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p]
         L.ora_rel_pos_json.restype = I32
         L.ora_rel_pos_json.argtypes = [P, I32, ctypes.c_char_p, ctypes.c_char_p]
+        L.ora_channel_process.restype = U32
+        L.ora_channel_process.argtypes = [P, ctypes.c_char_p]
+        L.ora_channel_stash_json.restype = P
+        L.ora_channel_stash_json.argtypes = [P, I32]
         L.ora_delta_capture.argtypes = [P, ctypes.c_int]
         L.ora_delta_json.restype = P
         L.ora_delta_json.argtypes = [P]
@@ -125,6 +129,21 @@ class OracleDoc:
         """Client.applyMsg on the message itself (JSON; the oracle parses and dispatches it)."""
         import json
         return int(self.L.ora_apply_msg_json(self.h, json.dumps(msg, ensure_ascii=True).encode()))
+
+    def channel_process(self, msg: dict) -> int:
+        """SharedSegmentSequence.processMergeTreeMsg, legacy format (sequence.ts:604-642), on
+        the oracle's own restatement: apply, then stash (transformed when refSeq != seq - 1)."""
+        import json
+        return int(self.L.ora_channel_process(self.h, json.dumps(msg, ensure_ascii=True).encode()))
+
+    def channel_stash(self, min_seq: int):
+        """snapshotMergeTree's catch-up messages as the JSON text of the blob (None: no blob)."""
+        buf = self.L.ora_channel_stash_json(self.h, min_seq)
+        if not buf:
+            return None
+        out = ctypes.string_at(buf).decode("utf-8")
+        self.L.ora_free_buf(buf)
+        return out
 
     def get_length_of(self, ref_seq: int, client_id: str) -> int:
         """getLength(refSeq, shortId(client_id)) under the oracle's own registration."""

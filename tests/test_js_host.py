@@ -18,7 +18,7 @@ from test_emu_parity import CONFIGS, ann_props
 
 pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 
-EXPORTS = ["applyBatch", "create", "deltaCapture", "deltaRecords", "destroy", "docPset", "docStatus", "docsOpen", "getLength", "getText", "lastError",
+EXPORTS = ["applyBatch", "create", "deltaCapture", "deltaRecords", "deltaText", "destroy", "docPset", "docStatus", "docsOpen", "getLength", "getText", "lastError",
            "loadSnapshot", "setClientNames", "setDocClientNames", "setProps", "setResidency", "snapshotLegacy", "snapshotV1", "sync",
            "syncAsync",
            "updateSeq"]

@@ -138,14 +138,15 @@ def test_message_surface_node_host_on_gpu(surface):
     check_node(os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"), surface, n_docs=6)
 
 
-def check_delta_records(factory, surface, seed=5, n_docs=3, n_msgs=900):
+def check_delta_records(factory, surface, seed=5, n_docs=3, n_msgs=900, capacity=1 << 20, limits=LIMITS,
+                        min_launches=1):
     """§8(f4): the engine's delta / maintenance records (mt_delta_records) equal the oracle's
     callbacks (MT/mergeTreeDeltaCallback.ts: INSERT / REMOVE / ANNOTATE deltaSegments, SPLIT /
     APPEND / UNLINK maintenance) record for record: op, kind, observer position, lengths,
     and the property maps before / after an annotate."""
     streams = [stream(seed * 31 + d, n_msgs, capture=True, **SURFACES[surface]) for d in range(n_docs)]
-    eng = factory(n_docs, **LIMITS)
-    eng.delta_capture(1 << 20)
+    eng = factory(n_docs, **limits)
+    eng.delta_capture(capacity)
     g = ClientGroup(eng)
     clients = [g.new_client({"newMergeTreeSnapshotFormat": True}) for _ in range(n_docs)]
     for c, (msgs, _) in zip(clients, streams):
@@ -154,6 +155,8 @@ def check_delta_records(factory, surface, seed=5, n_docs=3, n_msgs=900):
     g.flush()
     assert (eng.status(range(n_docs)) == 0).all()
     recs = eng.delta_records()
+    _, launches = eng.delta_text()
+    assert launches >= min_launches, launches
     offs = g.last_batch.op_offsets
     kinds = set()
     for d, (msgs, obs) in enumerate(streams):
@@ -184,6 +187,22 @@ def test_delta_records_on_emulation(surface):
 @pytest.mark.parametrize("surface", ["mixed", "groups", "markers_props", "churn300", "registers"])
 def test_delta_records_on_gpu(surface):
     check_delta_records(lambda n, **kw: Engine(n, device=0, **kw), surface, n_docs=6)
+
+
+# A capture buffer far smaller than the batch's records (the library raises it only to one
+# message of the largest document): runs stop when a launch is full and later launches
+# resume them; the records must come out exactly as from one launch.
+SMALL = dict(LIMITS, rows_per_doc=2500)
+
+
+def test_delta_records_resume_on_emulation():
+    check_delta_records(emu_engine, "registers", n_docs=6, capacity=1, limits=SMALL, min_launches=3)
+
+
+@pytest.mark.gpu
+def test_delta_records_resume_on_gpu():
+    check_delta_records(lambda n, **kw: Engine(n, device=0, **kw), "registers", n_docs=12, capacity=1, limits=SMALL,
+                        min_launches=3)
 
 
 def _reg_msgs(paste_twice: bool):
