@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0
+PARITY_DOCS = 8            # documents per rank the oracle replays for the N > 1 parity check
 RESIDENCY = {"hbm": 0, "lds": 1, "blk": 2, "big": 3}
 REPLAY_KERNEL = {"hbm": "mt_replay_kernel", "lds": "mt_replay_lds_kernel + mt_replay_kernel",
                  "blk": "mt_replay_blk_kernel", "big": "mt_replay_big_kernel"}  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -128,30 +129,54 @@ def caps_for(c):
                 propsets_per_doc=(2 * ops + 64) if c["ins"] + c["rem"] < 100 else 64)
 
 
-def cpu_baseline(eng, c, params_cls, seed, target_s, threads, ops_fn=None):
-    """Oracle ('port' of the reference algorithm) on a bounded sample of the same streams.
-    ops_fn(n) -> (ops_per_doc, clients_per_doc) for skewed workloads (config 5)."""
+def oracle_run(eng, c, params_cls, seed, n_docs, threads, ops_fn=None):
+    """The first n_docs streams of the workload (regenerated by the engine: generation is
+    deterministic per document) replayed by the oracle on `threads` host threads:
+    (seconds, messages, SnapshotV1 digests, status words)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes
     from oracle_lib import lib as oracle
     L = oracle()
-    props = eng.props
+    p = params_cls(seed, n_docs, c["ops"], c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"],
+                   c["rem_len"], c["ann_sets"], c["rewrite"])
+    if ops_fn is None:
+        eng.generate(p)
+    else:
+        o, k = ops_fn(n_docs)
+        eng.generate(p, ops_per_doc=o, clients_per_doc=k)
+    eng.sync()
+    b = eng.generated_download()
+    st = np.zeros(n_docs, np.uint32)
+    dg = np.zeros(n_docs, np.uint64)
+    oc = np.zeros((n_docs, 6), np.uint64)
+    secs = L.ora_replay_batch(ctypes.byref(b.to_c()), ctypes.byref(eng.props.to_c()), threads, dg.ctypes.data,
+                              st.ctypes.data, oc.ctypes.data)
+    oracle_run.counters = oc              # the sample's §8(d) counters by the oracle's own count
+    return secs, int(b.op_offsets[-1]), dg, st
 
+
+def rank_parity(dist, bad_local, checked_local):
+    """Digest parity over every rank (N > 1): each rank checked its own sample against the
+    oracle; the counts are summed (gloo / RCCL all_reduce) for rank 0's line."""
+    import torch
+    t = torch.tensor([bad_local, checked_local], dtype=torch.int64)
+    if dist is not None:
+        torch_, tdist = dist
+        tdist.all_reduce(t)
+    return int(t[0]), int(t[1])
+
+
+def parity_text(bad, checked, world, what="SnapshotV1 digests"):
+    if bad == 0:
+        return f"{what} == oracle on {checked} docs ({world} rank{'s' if world > 1 else ''}, each its own sample)"
+    return f"DIGEST MISMATCH: {bad} of {checked} sample docs differ from the oracle"
+
+
+def cpu_baseline(eng, c, params_cls, seed, target_s, threads, ops_fn=None):
+    """Oracle ('port' of the reference algorithm) on a bounded sample of the same streams.
+    ops_fn(n) -> (ops_per_doc, clients_per_doc) for skewed workloads (config 5)."""
     def run(n_docs):
-        p = params_cls(seed, n_docs, c["ops"], c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"],
-                       c["rem_len"], c["ann_sets"], c["rewrite"])
-        if ops_fn is None:
-            eng.generate(p)
-        else:
-            o, k = ops_fn(n_docs)
-            eng.generate(p, ops_per_doc=o, clients_per_doc=k)
-        eng.sync()
-        b = eng.generated_download()
-        st = np.zeros(n_docs, np.uint32)
-        dg = np.zeros(n_docs, np.uint64)
-        secs = L.ora_replay_batch(ctypes.byref(b.to_c()), ctypes.byref(props.to_c()), threads, dg.ctypes.data,
-                                  st.ctypes.data)
-        return secs, int(b.op_offsets[-1]), dg, st
+        return oracle_run(eng, c, params_cls, seed, n_docs, threads, ops_fn)
 
     pilot_docs = min(c["docs"], max(threads, 16))
     t, n, dg, st = run(pilot_docs)
@@ -164,6 +189,19 @@ def cpu_baseline(eng, c, params_cls, seed, target_s, threads, ops_fn=None):
            "sample": f"{docs} docs ({n} msgs) of the same workload, oracle (C++ restatement of "
                      f"MT/mergeTree.ts + partialLengths.ts) on {threads} host threads, {t:.1f} s"}
     return out, dg, st
+
+
+COUNTER_KEYS = ("ops", "msgs", "ins_units", "rows_rw", "depth", "scoured")
+
+
+def counters_match(cnt, k):
+    """The engine's per-document counters (the roofline numerator) equal the oracle's count
+    of the same §8(d) quantities on the last oracle_run sample's first k documents."""
+    oc = getattr(oracle_run, "counters", None)
+    if oc is None or len(oc) < k:
+        return False
+    eng = np.stack([np.asarray(cnt[key][:k], np.uint64) for key in COUNTER_KEYS], axis=1)
+    return bool(np.array_equal(eng, oc[:k]))
 
 
 def digest_parity(gpu_digests, oracle_digests, oracle_status):
@@ -253,6 +291,12 @@ def run_config4(args, c, world, rank, local):
     t1 = time.perf_counter()
     digs = eng.snapshot_digests(range(n), neg, neg, threads=min(16, os.cpu_count() or 1))
     snap_ms = (time.perf_counter() - t1) * 1e3
+    if world > 1:
+        # every rank checks its own first documents against the oracle (untimed)
+        k = min(2, n)
+        _, odg, ost = cpu_baseline_config4(eng, c, pa, pb, max(1, min(16, (os.cpu_count() or 1) // world)), docs=k)
+        bad_l = int((np.asarray(digs[:k], np.uint64) != odg).sum()) + int(np.asarray(ost).any()) + int(not ok)
+        par_bad, par_checked = rank_parity(dist, bad_l, k)
     if rank != 0:
         return
     kern_s = float(np.mean(kms)) / 1e3
@@ -279,11 +323,13 @@ def run_config4(args, c, world, rank, local):
         out["cpu_baseline"], odg, ost = cpu_baseline_config4(eng, c, pa, pb, min(16, os.cpu_count() or 1))
         if ok:
             out["parity"] = digest_parity(digs, odg, ost)
+    elif world > 1 and ok:
+        out["parity"] = parity_text(par_bad, par_checked, world)
     print(json.dumps(out), flush=True)
 
 
-def cpu_baseline_config4(eng, c, pa, pb, threads):
-    """Oracle ('port') on one pre-built document per host thread: time(prebuild +
+def cpu_baseline_config4(eng, c, pa, pb, threads, docs=0):
+    """Oracle ('port') on one pre-built document per host thread (or `docs`): time(prebuild +
     stream) - time(prebuild), i.e. the measured stream alone, in ops/s."""
     import ctypes
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -291,7 +337,7 @@ def cpu_baseline_config4(eng, c, pa, pb, threads):
     from oracle_lib import lib as oracle
     L = oracle()
     props = eng.props
-    k = threads
+    k = docs or threads
     sa = MtGenParams(*(getattr(pa, f) for f, _ in MtGenParams._fields_))
     sa.n_docs = k
     sb = MtGenParams(*(getattr(pb, f) for f, _ in MtGenParams._fields_))
@@ -306,9 +352,9 @@ def cpu_baseline_config4(eng, c, pa, pb, threads):
     both = concat_runs(a, b)
     st = np.zeros(k, np.uint32)
     dg = np.zeros(k, np.uint64)
-    t_a = L.ora_replay_batch(ctypes.byref(a.to_c()), ctypes.byref(props.to_c()), threads, None, st.ctypes.data)
+    t_a = L.ora_replay_batch(ctypes.byref(a.to_c()), ctypes.byref(props.to_c()), threads, None, st.ctypes.data, None)
     t_ab = L.ora_replay_batch(ctypes.byref(both.to_c()), ctypes.byref(props.to_c()), threads, dg.ctypes.data,
-                              st.ctypes.data)
+                              st.ctypes.data, None)
     n_b = int(b.op_offsets[-1])
     dt = max(t_ab - t_a, 1e-6)
     return {"value": n_b / dt, "unit": "ops/s", "cores": threads, "kind": "port",
@@ -367,9 +413,15 @@ def run_config5(args, c, world, rank, local):
     cnt = eng.counters(range(sh.n_docs))
     bytes_per_launch = algorithmic_bytes(cnt)
     digs = sh.gather_digests(dist, device, threads=min(16, os.cpu_count() or 1))
-    bad = torch.tensor([int(st.any()) + int(int(cnt["msgs"].sum()) != my_msgs)], dtype=torch.int32, device=device)
+    xbad = int(sh.timings.get("exchange_bad_docs", 0))
+    bad = torch.tensor([int(st.any()) + int(int(cnt["msgs"].sum()) != my_msgs), xbad, sh.n_docs],
+                       dtype=torch.int64, device=device)
     if world > 1:
         dist.all_reduce(bad)
+        # every rank checks a sample of its own documents against the oracle (untimed)
+        pb_, pc_ = config5_rank_parity(args, c, sh) if not args.no_cpu_baseline else (0, 0)
+        par = torch.tensor([pb_, pc_], dtype=torch.int64, device=device)
+        dist.all_reduce(par)
     if rank != 0:
         return
     total_msgs = int(sh.all_ops.sum())
@@ -388,7 +440,10 @@ def run_config5(args, c, world, rank, local):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": REPLAY_KERNEL[args.residency] + " (rank 0)",
                      "kernel_ms": kern_s * 1e3, "bytes_per_launch": bytes_per_launch},
-        "parity": "status words clean on every rank" if int(bad.item()) == 0 else "STATUS ERROR",
+        "parity": "status words clean on every rank" if int(bad[0].item()) == 0 else "STATUS ERROR",
+        "exchange": {"docs_checked": int(bad[2].item()), "checksum_mismatch_docs": int(bad[1].item()),
+                     "note": "per-document 64-bit checksums of the exchanged rows: packed by rank 0, verified on "
+                             "arrival by the owning rank (mt_generated_pack_rows / mt_upload_rows_dev)"},
         "sharding": {"rebalance_ms": sh.timings.get("rebalance_ms"), "rebalance_bytes": sh.timings.get("rebalance_bytes"),
                      "digest_gather_ms": sh.timings.get("digest_ms"), "ingest_generate_s": sh.timings.get("generate_s"),
                      "setup_s": setup_s, "digest_xor": f"{int(np.bitwise_xor.reduce(digs)):016x}",
@@ -396,8 +451,12 @@ def run_config5(args, c, world, rank, local):
     }
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline_config5(args, c, local)
-        if int(bad.item()) == 0:
+        if int(bad[0].item()) == 0:
             out["parity"] = config5_parity(args, c, sh, digs)
+    elif world > 1 and int(bad[0].item()) == 0 and not args.no_cpu_baseline:
+        out["parity"] = parity_text(int(par[0].item()), int(par[1].item()), world) + ", all ranks clean"
+    if int(bad[1].item()):
+        out["parity"] = f"EXCHANGE CHECKSUM MISMATCH on {int(bad[1].item())} docs; " + out["parity"]
     print(json.dumps(out), flush=True)
 
 
@@ -419,6 +478,27 @@ def config5_parity(args, c, sh, digs, k=48):
     odg = np.array([kept[d].snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]))[1]
                     for d in range(k)], np.uint64)
     return digest_parity(digs, odg, np.asarray(st)) + ", all ranks clean"
+
+
+def config5_rank_parity(args, c, sh, k=16):
+    """This rank's check: the oracle (its own generator, same seed and per-document counts)
+    replays the k owned documents of smallest global id; their digests must equal this
+    rank's (sh.local_digests, before the gather).  Returns (mismatches, checked)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fluidframework_amd.batch import MtGenParams
+    from oracle_lib import generate
+    loc = np.argsort(sh.owned, kind="stable")[:min(k, sh.n_docs)]
+    if not len(loc):
+        return 0, 0
+    gids = sh.owned[loc]
+    p = MtGenParams(args.seed, len(gids), 0, 2, c["lag"], c["ins"], c["rem"], c["ins_len"], c["rem_len"], c["ann_sets"],
+                    c["rewrite"])
+    batch, st, kept = generate(p, ann_props(), docs=gids, keep=True, ops_per_doc=sh.all_ops[gids],
+                               clients_per_doc=sh.clients_all[gids])
+    last = batch.op_offsets[1:] - 1
+    odg = np.array([kept[j].snapshot(int(batch.arrays["msn"][last[j]]), int(batch.arrays["seq"][last[j]]))[1]
+                    for j in range(len(gids))], np.uint64)
+    return int((sh.local_digests[loc] != odg).sum()) + int(np.asarray(st).any()), len(gids)
 
 
 def cpu_baseline_config5(args, c, local):
@@ -516,7 +596,26 @@ def ingest_leg(local, c, seed, sample_docs=64):
                     "the timed replay starts from resident streams, these rates bound a live ingest path"}
 
 
+def finish_dist():
+    """Every rank leaves together and tears its process group down (a rank that exits with
+    its group still up can abort in the communication library's exit handlers)."""
+    try:
+        import torch.distributed as tdist
+    except ImportError:
+        return
+    if tdist.is_available() and tdist.is_initialized():
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
 def main(argv=None):
+    try:
+        return _main(argv)
+    finally:
+        finish_dist()
+
+
+def _main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -643,6 +742,12 @@ def main(argv=None):
     value = total_msgs / dt
     kern_s = float(np.mean(kms)) / 1e3
     achieved = bytes_per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
+    if world > 1:
+        # every rank checks its own documents against the oracle (untimed), rank 0 reports the sum
+        k = min(PARITY_DOCS, c["docs"])
+        _, _, odg, ost = oracle_run(eng, c, MtGenParams, seed, k, max(1, min(16, (os.cpu_count() or 1) // world)))
+        bad_l = int((np.asarray(digs[:k], np.uint64) != odg).sum()) + int(np.asarray(ost).any()) + int(not ok)
+        par_bad, par_checked = rank_parity(dist, bad_l, k)
     if rank != 0:
         return
     traffic = measured_traffic(args.config, c, REPLAY_KERNEL[args.residency])
@@ -681,6 +786,10 @@ def main(argv=None):
         out["cpu_baseline"], odg, ost = cpu_baseline(eng, c, MtGenParams, seed, args.cpu_seconds, threads)
         if ok:
             out["parity"] = digest_parity(digs, odg, ost)
+            out["roofline"]["bytes_pinned"] = (f"mt_doc_counters == oracle's own §8(d) count on {len(odg)} docs"
+                                               if counters_match(cnt2, len(odg)) else "COUNTER MISMATCH vs oracle")
+    elif world > 1 and ok:
+        out["parity"] = parity_text(par_bad, par_checked, world)
     if world == 1 and not args.no_ingest:
         out["ingest"] = ingest_leg(local, c, seed)
     print(json.dumps(out), flush=True)

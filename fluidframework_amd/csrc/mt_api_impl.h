@@ -23,6 +23,7 @@
 #include <string>
 #include <vector>
 #include "mt_ctx.h"
+#include "mt_shard.h"
 
 static int mtb_ensure(mt_ctx* c, mt_ctx::DevBuf& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
@@ -868,6 +869,70 @@ int MT_FN(upload_batch_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids,
     c->batch_reg = false;                     // device-built streams (shard.py) hold no register ops
     c->gen.enabled = 0;
     return mtb_sync(c);
+}
+// Document exchange rows (mt_shard.h): the sender packs generated runs at their plan
+// positions with per-document checksums; the receiver unpacks rows into its resident batch
+// and checks every document's checksum against the sender's.
+int MT_FN(generated_pack_rows)(mt_ctx* c, uint32_t first, uint32_t n, const uint64_t* dst_row, void* rows_dev,
+                               uint64_t* checksum) {
+    if (!c || !c->gen_docs || (uint64_t)first + n > c->gen_off.size() - 1 || (n && (!dst_row || !rows_dev || !checksum)))
+        return MT_E_INVALID;
+    if (c->gen.ins_len_max % 4) { c->err = "exchange rows need ins_len_max % 4 == 0"; return MT_E_INVALID; }
+    if (n == 0) return MT_OK;
+    int rc;
+    if ((rc = mtb_sync(c))) return rc;
+    if ((rc = mtb_ensure(c, c->b_tmp0, 8ull * n))) return rc;
+    if ((rc = mtb_ensure(c, c->b_tmp1, 8ull * n))) return rc;
+    mtb_h2d(c, c->b_tmp0.p, dst_row, 8ull * n);
+    if ((rc = mtb_launch_rows(c, true, first, n, c->gen.ins_len_max, (const uint64_t*)c->b_tmp0.p, (uint64_t*)rows_dev,
+                              (uint64_t*)c->b_tmp1.p))) return rc;
+    if ((rc = mtb_sync(c))) return rc;
+    mtb_d2h(c, checksum, c->b_tmp1.p, 8ull * n);
+    return MT_OK;
+}
+int MT_FN(upload_rows_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids, const uint32_t* op_offsets,
+                           const void* rows_dev, uint32_t payload_stride, const uint64_t* expect, uint32_t* bad_runs) {
+    if (!c || !op_offsets || (n_runs && (!doc_ids || !expect)) || payload_stride == 0 || payload_stride % 4)
+        return MT_E_INVALID;
+    for (uint32_t r = 0; r < n_runs; r++) {
+        if (doc_ids[r] >= c->S.maxDocs) { c->err = "doc id out of range"; return MT_E_INVALID; }
+        if (op_offsets[r] > op_offsets[r + 1]) { c->err = "op_offsets not monotone"; return MT_E_INVALID; }
+    }
+    const uint64_t N = op_offsets[n_runs], L = payload_stride;
+    if (N && !rows_dev) return MT_E_INVALID;
+    if (N * L >= 0xFFFFFFFFull) { c->err = "payload slots exceed 2^32 units"; return MT_E_INVALID; }
+    int rc;
+#define UP(buf, bytes) if ((rc = mtb_ensure(c, c->buf, (bytes)))) return rc;
+    UP(b_doc, 4ull * n_runs + 4) UP(b_off, 4ull * (n_runs + 1)) UP(b_rec, sizeof(MtOpRec) * N + 32) UP(b_pay, 2 * N * L + 2)
+    UP(b_tmp1, 8ull * n_runs + 8)
+#undef UP
+    mtb_h2d(c, c->b_doc.p, doc_ids, 4ull * n_runs);
+    mtb_h2d(c, c->b_off.p, op_offsets, 4ull * (n_runs + 1));
+    MtOps& o = c->ops;
+    o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
+    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs; o.payload_units = N * L;
+    o.rel = nullptr; o.n_rel = 0;
+    c->n_runs = n_runs;
+    c->batch_reg = false;                     // exchanged generated streams hold no register ops
+    c->gen.enabled = 0;
+    if (n_runs && (rc = mtb_launch_rows(c, false, 0, n_runs, (uint32_t)L, nullptr, (uint64_t*)rows_dev,
+                                        (uint64_t*)c->b_tmp1.p))) return rc;
+    if ((rc = mtb_sync(c))) return rc;
+    std::vector<uint64_t> got(n_runs);
+    if (n_runs) mtb_d2h(c, got.data(), c->b_tmp1.p, 8ull * n_runs);
+    uint32_t bad = 0, first_bad = 0;
+    for (uint32_t r = 0; r < n_runs; r++) {
+        const bool b = got[r] != expect[r];
+        if (bad_runs) bad_runs[r] = b ? 1u : 0u;
+        if (b && !bad++) first_bad = r;
+    }
+    if (bad) {
+        char m[128];
+        snprintf(m, sizeof m, "exchange checksum mismatch on %u of %u documents (first: run %u)", bad, n_runs, first_bad);
+        c->err = m;
+        return MT_E_EXCHANGE;
+    }
+    return MT_OK;
 }
 int MT_FN(generated_to_resident)(mt_ctx* c) {
     if (!c || !c->gen.enabled) return MT_E_INVALID;

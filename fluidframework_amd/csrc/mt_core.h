@@ -2263,7 +2263,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         const int n = uni(g.n), fl = uni(g.flags);
         if (n == 0) return;                                    // no segments: the op does nothing
         if (fl & 3) { status |= MT_DS_UNSUPPORTED; return; }   // re-linked objects / removed clones
-        walk(MT_WALK_SPLIT, pos, r, c, -1, 0);                  // ensureIntervalBoundary
+        if (walk(MT_WALK_SPLIT, pos, r, c, -1, 0) == MT_W_OK) c_rows += 2;   // ensureIntervalBoundary
         if (status) return;
         int ip = pos;
         for (int i = 0; i < n; i++) {

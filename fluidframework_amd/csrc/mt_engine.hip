@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include "mt_ctx.h"
 #include "mt_kernels.h"
+#include "mt_shard.h"
 
 __global__ __launch_bounds__(64) void mt_open_kernel(MtState S, uint32_t first) {
     __shared__ MtScratch sc;
@@ -58,6 +59,14 @@ __global__ __launch_bounds__(64) void mt_pack_kernel(MtState S, const uint32_t* 
     MtEng e;
     e.bind(S, docs[blockIdx.x], &sc);
     mt_pack_doc(e, stage + off[blockIdx.x]);
+}
+
+// Document exchange rows (mt_shard.h): one wave per document run.
+__global__ __launch_bounds__(64) void mt_rows_kernel(MtOps ops, int pack, uint32_t first, uint32_t L, const uint64_t* dst,
+                                                     unsigned long long* rows, uint64_t* cs) {
+    const uint32_t i = blockIdx.x;
+    const unsigned long long h = pack ? mt_pack_rows_doc(ops, first + i, L, dst[i], rows) : mt_unpack_rows_doc(ops, i, L, rows);
+    if (__lane_id() == 0) cs[i] = h;
 }
 
 // ----------------------------------------------------- backend plumbing ----
@@ -142,6 +151,14 @@ static int mtb_launch_get_length(mt_ctx* c, const uint32_t* docs, const int32_t*
     return mtb_check(c);
 }
 
+static int mtb_launch_rows(mt_ctx* c, bool pack, uint32_t first, uint32_t n, uint32_t L, const uint64_t* dst, uint64_t* rows,
+                           uint64_t* cs) {
+    if (!n) return MT_OK;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(mt_rows_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->ops, pack ? 1 : 0, first, L, dst,
+                       (unsigned long long*)rows, cs);
+    return mtb_check(c);
+}
 static int mtb_launch_pack_size(mt_ctx* c, const uint32_t* docs, MtPackSize* out, uint32_t n) {
     if (!n) return MT_OK;
     (void)hipGetLastError();

@@ -4,7 +4,8 @@
 // holds one group of template instantiations, so the groups compile in parallel, and
 // mt_engine.hip launches them through the mtk_* functions declared in mt_kernels.h.
 //   MT_KSET 0: mt_replay_blk_kernel<false> (the hot path)   1: mt_replay_blk_kernel<true>
-//   MT_KSET 2: mt_replay_big_kernel<false / true>             3: lds, hbm, generate kernels
+//   MT_KSET 2: mt_replay_big_kernel<false / true>             3: mt_replay_lds_kernel<false / true>
+//   MT_KSET 4: the all-HBM kernels and the generator
 #include <hip/hip_runtime.h>
 #include "mt_ctx.h"
 #include "mt_kernels.h"
@@ -57,7 +58,7 @@ __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_rest_kernel(M
     __shared__ MtScratch sc;
     mt_replay_doc_rest<FULL>(S, ops, blockIdx.x, &sc, cursor[blockIdx.x]);
 }
-#if MT_KSET == 3
+#if MT_KSET == 4
 // Generation: the same engine acting as sequencer + observer, writing the op
 // records it applies (a separate symbol so profiles never mix it with replay).
 __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_generate_kernel(MtState S, MtOps ops, MtGen gen) {
@@ -86,11 +87,12 @@ void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps
     if (full) hipLaunchKernelGGL(mt_replay_big_kernel<true>, dim3(n), dim3(64), 0, s, S, o, cur, lw, lh);
     else hipLaunchKernelGGL(mt_replay_big_kernel<false>, dim3(n), dim3(64), 0, s, S, o, cur, lw, lh);
 }
-#else
+#elif MT_KSET == 3
 void mtk_lds(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lr, int lb, int lh) {
     if (full) hipLaunchKernelGGL(mt_replay_lds_kernel<true>, dim3(n), dim3(64), 0, s, S, o, cur, lr, lb, lh);
     else hipLaunchKernelGGL(mt_replay_lds_kernel<false>, dim3(n), dim3(64), 0, s, S, o, cur, lr, lb, lh);
 }
+#else
 void mtk_hbm(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* cur) {
     if (cur) {
         if (full) hipLaunchKernelGGL(mt_replay_rest_kernel<true>, dim3(n), dim3(64), 0, s, S, o, cur);

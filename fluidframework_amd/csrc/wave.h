@@ -133,6 +133,11 @@ __device__ __forceinline__ unsigned long long wave_atomic_add(unsigned long long
            ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
 }
 __device__ __forceinline__ unsigned long long wave_atomic_next(unsigned long long* p) { return wave_atomic_add(p, 1ull); }
+// 64-bit sum over all lanes (butterfly of 64-bit shuffles), wave-uniform result
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
+    for (int off = 32; off >= 1; off >>= 1) v += (unsigned long long)__shfl_xor((long)v, off);
+    return uni64(v);
+}
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -219,5 +224,10 @@ inline LaneArr<int> wave_set(LaneArr<int> a, int k, int v) { if (k >= 0 && k < M
 inline void lds_add(int* p, int v) { *p += v; }
 inline unsigned long long wave_atomic_add(unsigned long long* p, unsigned long long d) { return __atomic_fetch_add(p, d, __ATOMIC_RELAXED); }
 inline unsigned long long wave_atomic_next(unsigned long long* p) { return wave_atomic_add(p, 1ull); }
+inline unsigned long long wave_sum64(const LaneArr<unsigned long long>& a) {
+    unsigned long long s = 0;
+    for (int k = 0; k < MT_WAVE; k++) s += a.v[k];
+    return s;
+}
 inline void wave_sync() {}
 #endif

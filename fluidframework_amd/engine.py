@@ -33,6 +33,14 @@ class MergeTreeError(RuntimeError):
     pass
 
 
+class ExchangeError(MergeTreeError):
+    """Exchanged document rows whose checksum differs from the sender's (MT_E_EXCHANGE)."""
+
+    def __init__(self, msg, bad_runs):
+        super().__init__(msg)
+        self.bad_runs = bad_runs
+
+
 class MtLimits(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint32) for n in ("max_docs", "rows_per_doc", "blocks_per_doc", "text_per_doc",
                                                "propsets_per_doc", "heap_per_doc", "window_per_doc",
@@ -93,6 +101,8 @@ def _bind(lib, prefix: str):
         generated_to_resident=f("generated_to_resident", ctypes.c_int, [P]),
         generated_copy_dev=f("generated_copy_dev", ctypes.c_int, [P, U32, U32, P, P]),
         upload_batch_dev=f("upload_batch_dev", ctypes.c_int, [P, U32, P, P, P, P, ctypes.c_uint64]),
+        generated_pack_rows=f("generated_pack_rows", ctypes.c_int, [P, U32, U32, P, P, P]),
+        upload_rows_dev=f("upload_rows_dev", ctypes.c_int, [P, U32, P, P, P, U32, P, P]),
         load_snapshot=f("load_snapshot", ctypes.c_int, [P, P]),
         delta_capture=f("delta_capture", ctypes.c_int, [P, ctypes.c_uint64]),
         delta_records=f("delta_records", ctypes.c_int, [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_uint64)]),
@@ -268,6 +278,29 @@ class Engine:
         d, o = _u32(doc_ids), _u32(op_offsets)
         self._check(self.fn["upload_batch_dev"](self.h, len(d), d.ctypes.data, o.ctypes.data, rec_ptr, payload_ptr,
                                                 int(payload_units)), "mt_upload_batch_dev")
+
+    def generated_pack_rows(self, first_run: int, n_runs: int, dst_row, rows_ptr: int) -> np.ndarray:
+        """mt_generated_pack_rows: generated runs as exchange rows (mt_op_rec + payload slot)
+        at rows dst_row[i] of a device buffer; returns each run's 64-bit row checksum."""
+        d = np.ascontiguousarray(dst_row, np.uint64)
+        cs = np.zeros(n_runs, np.uint64)
+        self._check(self.fn["generated_pack_rows"](self.h, first_run, n_runs, d.ctypes.data, rows_ptr, cs.ctypes.data),
+                    "mt_generated_pack_rows")
+        return cs
+
+    def upload_rows_dev(self, doc_ids, op_offsets, rows_ptr: int, payload_stride: int, expect) -> np.ndarray:
+        """mt_upload_rows_dev: received exchange rows become the resident batch; every run's
+        checksum must equal the sender's (MergeTreeError otherwise).  Returns the per-run
+        mismatch flags (all zero on success)."""
+        d, o = _u32(doc_ids), _u32(op_offsets)
+        e = np.ascontiguousarray(expect, np.uint64)
+        bad = np.zeros(len(d), np.uint32)
+        rc = self.fn["upload_rows_dev"](self.h, len(d), d.ctypes.data, o.ctypes.data, rows_ptr, payload_stride,
+                                         e.ctypes.data, bad.ctypes.data)
+        if rc == 5:                          # MT_E_EXCHANGE: the flags say which documents
+            raise ExchangeError(self.fn["last_error"](self.h).decode(), bad)
+        self._check(rc, "mt_upload_rows_dev")
+        return bad
 
     def generated_to_resident(self):
         self._check(self.fn["generated_to_resident"](self.h), "mt_generated_to_resident")

@@ -9,9 +9,13 @@ in the CPU tests):
 1. a one-shot size-balanced redistribution: rank 0 holds every document's
    sequenced op stream (the ingest point); every rank computes the same LPT
    (longest-processing-time) plan from the broadcast op counts, and rank 0
-   sends each rank its documents' packed 32-byte op records and UTF-16
-   payloads in one all_to_all_single each (per-link bound on xGMI: each
-   destination's share travels on its own link);
+   sends each rank its documents as exchange rows (a 32-byte op record plus the
+   op's UTF-16 payload slot, csrc/mt_shard.h) in one all_to_all_single (per-link
+   bound on xGMI: each destination's share travels on its own link).  The rows
+   are packed at their plan positions and unpacked into the resident batch by
+   the engine's own HIP kernels, and every document's 64-bit row checksum is
+   compared on arrival with rank 0's (round 2 moved them with torch gathers,
+   one of which returned zero rows for 16-byte rows at config-5 size);
 2. the gather of per-document SnapshotV1 digests to rank 0.
 
 Pool capacities are exact: generation runs the same deterministic engine, so
@@ -132,6 +136,7 @@ class ShardedReplay:
         n = self.n_docs
         neg = np.full(n, -1, np.int32)
         dig = self.engine.snapshot_digests(range(n), neg, neg, threads=threads) if n else np.zeros(0, np.uint64)
+        self.local_digests = dig           # engine slot order (owned[i]): each rank's own parity sample
         world, rank = dist.get_world_size(), dist.get_rank()
         counts = np.bincount(self.owner, minlength=world)
         mx = int(counts.max()) if len(counts) else 0
@@ -186,13 +191,23 @@ def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_
     n_total = int(op_off[-1])
     tm["plan_ms"] = (time.perf_counter() - t0) * 1e3
 
-    # -- rank 0: generate all streams in chunks (untimed ingest), staging in device tensors
+    # -- the plan's send order: documents grouped by owning rank, largest first; each
+    #    document's rows start at row_of[doc] of rank 0's send buffer
+    order = rank_order(owner, ops)
+    row_of = np.empty(docs_total, np.int64)
+    row_of[order] = np.concatenate(([0], np.cumsum(ops[order].astype(np.int64))[:-1]))
+    W = REC_BYTES // 8 + 2 * L // 8                  # 8-byte words per exchange row (mt_shard.h)
+    per_rank_ops = np.array([int(ops[owner == r].sum()) for r in range(world)], np.int64)
+    my_ops = int(per_rank_ops[rank])
+
+    # -- rank 0: generate every stream in chunks (untimed ingest); the engine packs each
+    #    chunk's runs straight into their plan positions of the send buffer (a HIP kernel,
+    #    mt_generated_pack_rows) with a 64-bit checksum per document
     caps_t = torch.zeros((docs_total, 6), dtype=torch.int32, device=device)
+    cs_t = torch.zeros(docs_total, dtype=torch.int64, device=device)
     if rank == 0:
         t0 = time.perf_counter()
-        # staged as 8-byte words (a config-5 stream holds more than 2^31 record bytes)
-        rec_all = torch.empty((n_total, REC_BYTES // 8), dtype=torch.int64, device=device)
-        pay_all = torch.empty((n_total, 2 * L // 8), dtype=torch.int64, device=device)   # UTF-16 units as bytes
+        send = torch.empty((n_total, W), dtype=torch.int64, device=device)
         gcaps = generation_caps(ops, L)
         for a in range(0, docs_total, chunk_docs):
             b = min(docs_total, a + chunk_docs)
@@ -210,58 +225,40 @@ def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_
             if st.any():
                 raise RuntimeError(f"generation failed for docs {a}..{b}: status {np.unique(st)}")
             caps_t[a:b] = torch.from_numpy(replay_caps(eng.pools(range(b - a)), gcaps, idx)).to(device)
-            o0, o1 = int(op_off[a]), int(op_off[b])
             if device.type == "cuda":
                 torch.cuda.synchronize(device)
-            eng.generated_copy_dev(0, b - a, rec_all[o0:o1].data_ptr(), pay_all[o0:o1].data_ptr())
+            cs = eng.generated_pack_rows(0, b - a, row_of[a:b].astype(np.uint64), send.data_ptr())
+            cs_t[a:b] = torch.from_numpy(cs.view(np.int64)).to(device)
             eng.close()
         tm["generate_s"] = time.perf_counter() - t0
     dist.broadcast(caps_t, 0)
+    dist.broadcast(cs_t, 0)
     caps = caps_t.cpu().numpy()
+    sums = cs_t.cpu().numpy().view(np.uint64)
 
-    # -- redistribution: rank 0 -> every rank, one all_to_all_single per array
+    # -- redistribution: rank 0 -> every rank, one all_to_all_single of the rows
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     dist.barrier()
     t0 = time.perf_counter()
-    order = rank_order(owner, ops)
     owned = order[owner[order] == rank]
-    per_rank_ops = np.array([int(ops[owner == r].sum()) for r in range(world)], np.int64)
-    my_ops = int(per_rank_ops[rank])
-    # One row per op (record words, then payload words), permuted by one index_select and
-    # moved by one all_to_all_single.  Permuting the 16-byte payload rows on their own
-    # returned zero rows for documents placed past ~1.5 GB of output on this stack (found by
-    # the config-5 digest parity at 131,072 documents); the joint 48-byte rows are exact.
-    RW = REC_BYTES // 8 + 2 * L // 8
     if rank == 0:
-        starts = op_off[order]
-        lens = ops[order].astype(np.int64)
-        op_idx = np.repeat(starts - np.concatenate(([0], np.cumsum(lens)[:-1])), lens) + np.arange(int(lens.sum()))
-        sel = torch.from_numpy(op_idx).to(device)
-        both = torch.cat([rec_all, pay_all], dim=1)
-        del rec_all, pay_all
-        send = both.index_select(0, sel)
-        del both, sel
         in_split = per_rank_ops.tolist()
     else:
-        send = torch.empty((0, RW), dtype=torch.int64, device=device)
+        send = torch.empty((0, W), dtype=torch.int64, device=device)
         in_split = [0] * world
     out_split = [my_ops if r == 0 else 0 for r in range(world)]
-    recv = torch.empty((my_ops, RW), dtype=torch.int64, device=device)
+    recv = torch.empty((my_ops, W), dtype=torch.int64, device=device)
     dist.all_to_all_single(recv, send, out_split, in_split)
     del send
-    rec_recv = recv[:, :REC_BYTES // 8].contiguous()
-    pay_recv = recv[:, REC_BYTES // 8:].contiguous()
-    del recv
-    # payload offsets follow the new op order (fixed stride L per op record)
-    if my_ops:
-        rec_recv.view(torch.int32)[:, 6] = torch.arange(my_ops, dtype=torch.int32, device=device) * L
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     tm["rebalance_ms"] = (time.perf_counter() - t0) * 1e3
     tm["rebalance_bytes"] = int(per_rank_ops.sum()) * (REC_BYTES + 2 * L)
 
-    # -- this rank's engine, sized exactly, with the received stream resident
+    # -- this rank's engine, sized exactly; the received rows become its resident batch
+    #    (mt_upload_rows_dev: unpacked by a HIP kernel, every document's checksum compared
+    #    with rank 0's)
     mine = caps[owned]
     eng = engine_factory(len(owned), {k: mine[:, i] for i, k in enumerate(CAP_KEYS)})
     if props is not None:
@@ -272,7 +269,15 @@ def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_
     loc_off[1:] = np.cumsum(ops[owned], dtype=np.int64)
     if my_ops >= 2 ** 32:
         raise RuntimeError("more than 2^32 ops on one rank")
-    eng.upload_batch_dev(np.arange(len(owned)), loc_off.astype(np.uint32),
-                         rec_recv.data_ptr() if my_ops else 0, pay_recv.data_ptr() if my_ops else 0, my_ops * L)
-    del rec_recv, pay_recv
+    from .engine import ExchangeError
+    t0 = time.perf_counter()
+    try:
+        eng.upload_rows_dev(np.arange(len(owned)), loc_off.astype(np.uint32), recv.data_ptr() if my_ops else 0, L,
+                            sums[owned])
+        tm["exchange_bad_docs"] = 0
+    except ExchangeError as e:          # reported by the caller after every rank checked its share
+        tm["exchange_bad_docs"] = int(e.bad_runs.sum())
+    tm["unpack_ms"] = (time.perf_counter() - t0) * 1e3
+    tm["exchange_checked_docs"] = len(owned)
+    del recv
     return ShardedReplay(eng, owned, ops, owner, tm, cli)

@@ -56,6 +56,7 @@ extern "C" {
 #define MT_E_OOM            3  /* a per-document pool (rows/blocks/text) is full */
 #define MT_E_DOC_STATUS     4  /* a snapshot was asked of a document whose status
                                   word is set (the reference would have thrown)  */
+#define MT_E_EXCHANGE       5  /* exchanged document rows fail their checksum     */
 /* per-document status bits (mt_doc_status) */
 #define MT_DS_ASSERT_SEQ     0x01u /* currentSeq >= seq   (MT/client.ts:482, :846) */
 #define MT_DS_ASSERT_MSN     0x02u /* msn went backwards  (MT/client.ts:484, mergeTree.ts:1716) */
@@ -479,6 +480,19 @@ int  mt_generated_copy_dev(mt_ctx* ctx, uint32_t first_run, uint32_t n_runs, mt_
  * unless a delta capture is armed; use mt_upload_batch for such streams. */
 int  mt_upload_batch_dev(mt_ctx* ctx, uint32_t n_runs, const uint32_t* doc_ids, const uint32_t* op_offsets,
                          const mt_op_rec* rec_dev, const uint16_t* payload_dev, uint64_t payload_units);
+/* ---- document exchange between GPUs (fluidframework_amd/shard.py) ----
+ * A document travels as rows, one per op: its op record (32 B), then its payload slot of
+ * L = ins_len_max UTF-16 units, so one all-to-all moves records and text together.
+ * mt_generated_pack_rows: generated runs first..first+n-1 into rows_dev (device memory)
+ * starting at row dst_row[i] for run first+i, and each run's 64-bit row checksum into
+ * checksum[i] (host).  mt_upload_rows_dev: received rows (run r = rows op_offsets[r] ..
+ * op_offsets[r+1]-1) become the resident batch for doc_ids[r], text inserts' payload_off
+ * re-pointed to their slot; every run's checksum is compared with expect[r] (the sender's)
+ * and MT_E_EXCHANGE returned if any differs (bad_runs[r] = 1 for those, when non-null). */
+int  mt_generated_pack_rows(mt_ctx* ctx, uint32_t first_run, uint32_t n_runs, const uint64_t* dst_row,
+                            void* rows_dev, uint64_t* checksum);
+int  mt_upload_rows_dev(mt_ctx* ctx, uint32_t n_runs, const uint32_t* doc_ids, const uint32_t* op_offsets,
+                        const void* rows_dev, uint32_t payload_stride, const uint64_t* expect, uint32_t* bad_runs);
 /* Make the generated stream the resident batch (docs 0..n_docs-1). */
 int  mt_generated_to_resident(mt_ctx* ctx);
 

@@ -363,6 +363,20 @@ struct Tree {
     // position when the callback fires, its cachedLength, a kind-specific length, and
     // for inserts / annotates the property maps as JSON.
     struct DRec { int op, kind, pos, len, b; std::string pa, pb; };
+    // The §8(d) algorithmic quantities per document (B_op = 32 + 4 L_ins +
+    // 32 (R_r + R_w) + 64 D + 64 Z), counted by their definitions on the reference's own
+    // object model, in mt_doc_counters order: op members, messages, inserted UTF-16 units
+    // (L_ins), segment rows read + written (R_r + R_w: 2 per ensureIntervalBoundary split,
+    // 2 per inserted segment, 2 per segment a range op visits), descent levels (D: the tree's
+    // block levels after each op member) and rows scoured by zamboni (Z).
+    enum { C_OPS, C_MSGS, C_INS, C_ROWS, C_DEPTH, C_SCOUR };
+    uint64_t cnt[6] = {0, 0, 0, 0, 0, 0};
+    int blockLevels() const {
+        int h = 1; const Block* b = root;
+        while (b->childCount > 0 && !b->children[0]->leaf) { b = (const Block*)b->children[0]; h++; }
+        return h;
+    }
+    void countOp() { cnt[C_OPS] += 1; cnt[C_DEPTH] += (uint64_t)blockLevels(); }
     std::vector<DRec>* capture = nullptr;
     int curOp = 0;
     static std::string propsJson(const Seg* s);
@@ -711,7 +725,7 @@ struct Tree {
                     Seg* s = (Seg*)child; Node* next = nullptr;
                     if (kind == LEAF_SPLIT) {
                         next = splitAt(s, _pos);
-                        if (next) drec(-2, s, s->cachedLength, next->cachedLength);             // SPLIT :2249-2255
+                        if (next) { drec(-2, s, s->cachedLength, next->cachedLength); cnt[C_ROWS] += 2; }   // SPLIT :2249-2255
                     }
                     else { assignChild(block, cand, childIndex); next = s; }
                     if (next) { newNode = next; childIndex++; }
@@ -807,6 +821,7 @@ struct Tree {
             Block* sn = insertingWalk(root, pos, refSeq, clientId, seq, LEAF_INSERT, seg);
             if (!seg->parent) { status |= MT_DS_INSERT_FAILED; return; }
             updateRoot(sn);
+            cnt[C_ROWS] += 2; if (!seg->marker) cnt[C_INS] += seg->text.size();
             if (collaborating && !(seg->seq == UnassignedSeq && clientId == cwClientId) && seg->seq > minSeq) addToLRUSet(seg, seg->seq);
             drec(0, seg, seg->cachedLength, 0, "null", propsJson(seg));                          // INSERT callback :1992-2000
             xrec(0, seg);
@@ -843,6 +858,7 @@ struct Tree {
                 Block* sn = insertingWalk(root, insertPos, refSeq, clientId, seq, LEAF_INSERT, seg);
                 if (!seg->parent) { status |= MT_DS_INSERT_FAILED; return; }
                 updateRoot(sn);
+                cnt[C_ROWS] += 2;
                 if (collaborating && seg->seq > minSeq) addToLRUSet(seg, seg->seq);
                 insertPos += seg->cachedLength;
             }
@@ -857,7 +873,7 @@ struct Tree {
             int len = nodeLength(child, refSeq, clientId);
             if (end > 0 && len > 0 && start < len) {
                 if (!child->leaf) nodeMap((Block*)child, pos, refSeq, clientId, start, end, leaf, postList, nPost);
-                else leaf((Seg*)child, pos, start, end);
+                else { cnt[C_ROWS] += 2; leaf((Seg*)child, pos, start, end); }
             }
             pos += len; start -= len; end -= len;
         }
@@ -871,7 +887,7 @@ struct Tree {
             int len = nodeLength(child, refSeq, clientId);
             if (end > 0 && len > 0 && start < len) {
                 if (!child->leaf) nodeMapPost((Block*)child, pos, refSeq, clientId, start, end, leaf, post);
-                else leaf((Seg*)child, pos, start, end);
+                else { cnt[C_ROWS] += 2; leaf((Seg*)child, pos, start, end); }
             }
             pos += len; start -= len; end -= len;
         }
@@ -944,6 +960,7 @@ struct Tree {
             Node* c = node->children[k];
             if (c->leaf) {
                 Seg* s = (Seg*)c;
+                cnt[C_SCOUR] += 1;
                 if (s->hasRemoved) {
                     if (s->removedSeq > minSeq) hold.push_back(s);
                     else { drec(-3, s, s->cachedLength, 0); s->parent = nullptr; }   // UNLINK :1298-1306
@@ -1308,8 +1325,10 @@ static uint32_t apply_run(Doc& d, const mt_op_batch* b, uint32_t run) {
                     if (ty == MT_OP_CUT) t.markRangeRemoved(b->pos1[i], b->pos2[i], ref, cl, seq);
                 }
             }
+            t.countOp();
         }
         if (fl & MT_OPF_END_OF_MSG) {                                                            // updateSeqNumbers :843-850
+            t.cnt[Tree::C_MSGS] += 1;
             if (t.currentSeq > seq) t.status |= MT_DS_ASSERT_SEQ;
             t.currentSeq = seq;
             if (msn > seq) t.status |= MT_DS_ASSERT_MSN;
@@ -1489,7 +1508,14 @@ static void complete_op(Tree& t, int seq, int msn) {
     if (t.currentSeq >= seq) t.status |= MT_DS_ASSERT_SEQ;
     if (t.minSeq > msn) t.status |= MT_DS_ASSERT_MSN;
 }
+static void apply_remote_member(Doc& d, const JVal& op, int cl, int ref, int seq, int msn);
 static void apply_remote_json(Doc& d, const JVal& op, int cl, int ref, int seq, int msn) {       // applyRemoteOp :790-817
+    int type;
+    apply_remote_member(d, op, cl, ref, seq, msn);
+    if (op.t == JVal::Obj && jnum(op, u"type", type) && (type == MT_OP_INSERT || type == MT_OP_REMOVE || type == MT_OP_ANNOTATE))
+        d.t.countOp();
+}
+static void apply_remote_member(Doc& d, const JVal& op, int cl, int ref, int seq, int msn) {
     Tree& t = d.t;
     int type;
     if (op.t != JVal::Obj || !jnum(op, u"type", type)) return;                                  // default: ignored
@@ -1584,6 +1610,7 @@ static uint32_t apply_msg(Doc& d, const JVal& m) {
         if (c) apply_remote_json(d, *c, cl, ref, seq, msn);
     }
     if (d.opCounter == op0) t.curOp = d.opCounter++;            // a message with no member op: one record slot
+    t.cnt[Tree::C_MSGS] += 1;
     if (t.currentSeq > seq) t.status |= MT_DS_ASSERT_SEQ;                                        // updateSeqNumbers :843-850
     t.currentSeq = seq;
     if (msn > seq) t.status |= MT_DS_ASSERT_MSN;
@@ -1821,6 +1848,7 @@ int32_t* ora_dump_segments(ora_doc* o, uint32_t* n_rows) {
     int32_t* buf = (int32_t*)malloc(rows.size() * 4 + 4); memcpy(buf, rows.data(), rows.size() * 4);
     return buf;
 }
+void ora_counters(ora_doc* o, uint64_t* out6) { for (int k = 0; k < 6; k++) out6[k] = o->d.t.cnt[k]; }
 void ora_stats(ora_doc* o, int32_t* out) {
     int h = 0; for (Node* x = o->d.t.root; x && !x->leaf; x = ((Block*)x)->childCount ? ((Block*)x)->children[0] : nullptr) h++;
     int nseg = 0; auto f = [&](Seg*) { nseg++; }; o->d.t.walkAll(o->d.t.root, f);
@@ -1880,7 +1908,8 @@ uint32_t ora_generate_doc(const mt_gen_params* p, uint32_t doc, const mt_prop_ta
     return st;
 }
 
-double ora_replay_batch(const mt_op_batch* b, const mt_prop_table* props, int threads, uint64_t* digests, uint32_t* status) {
+double ora_replay_batch(const mt_op_batch* b, const mt_prop_table* props, int threads, uint64_t* digests, uint32_t* status,
+                        uint64_t* counters) {
     uint32_t R = b->n_runs;
     std::vector<std::pair<uint64_t, uint32_t>> order;
     for (uint32_t r = 0; r < R; r++) order.push_back({(uint64_t)(b->op_offsets[r + 1] - b->op_offsets[r]), r});
@@ -1898,6 +1927,7 @@ double ora_replay_batch(const mt_op_batch* b, const mt_prop_table* props, int th
             ora_doc* o = ora_new(1); o->d.props = pt;
             uint32_t st = apply_run(o->d, b, r);
             if (status) status[r] = st;
+            if (counters) for (int k = 0; k < 6; k++) counters[6ull * r + k] = o->d.t.cnt[k];
             docs.push_back(o);
         }
         secs[w] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

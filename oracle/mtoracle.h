@@ -87,7 +87,11 @@ long long ora_verify_result(long long* checks);
  * `threads` std::threads (LPT-partitioned by op count); returns wall seconds of
  * the apply loop and optionally per-run snapshot digests (msn/seq = last op's). */
 double   ora_replay_batch(const mt_op_batch* b, const mt_prop_table* props, int threads,
-                          uint64_t* out_digests, uint32_t* out_status);
+                          uint64_t* out_digests, uint32_t* out_status, uint64_t* out_counters);
+/* The §8(d) algorithmic counters of a document in mt_doc_counters order (ops, msgs,
+ * ins_units, rows_rw, depth, scoured), counted by their definitions on the oracle's own
+ * object model; ora_replay_batch's out_counters (optional) holds 6 per run. */
+void     ora_counters(ora_doc* d, uint64_t* out6);
 
 #ifdef __cplusplus
 }

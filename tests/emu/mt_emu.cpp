@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include "../../fluidframework_amd/csrc/mt_ctx.h"
+#include "../../fluidframework_amd/csrc/mt_shard.h"
 
 static int mtb_init(mt_ctx*) { return 0; }
 static void mtb_fini(mt_ctx*) {}
@@ -86,6 +87,13 @@ static int mtb_launch_pack_size(mt_ctx* c, const uint32_t* docs, MtPackSize* out
 }
 static int mtb_launch_pack(mt_ctx* c, const uint32_t* docs, const uint64_t* off, uint8_t* stage, uint32_t n) {
     for (uint32_t i = 0; i < n; i++) { MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc); mt_pack_doc(e, stage + off[i]); }
+    return MT_OK;
+}
+static int mtb_launch_rows(mt_ctx* c, bool pack, uint32_t first, uint32_t n, uint32_t L, const uint64_t* dst, uint64_t* rows,
+                           uint64_t* cs) {
+    for (uint32_t i = 0; i < n; i++)
+        cs[i] = pack ? mt_pack_rows_doc(c->ops, first + i, L, dst[i], (unsigned long long*)rows)
+                     : mt_unpack_rows_doc(c->ops, i, L, (const unsigned long long*)rows);
     return MT_OK;
 }
 #define MT_FN(name) emu_##name

@@ -80,7 +80,8 @@ def lib():
         L.ora_verify_result.restype = ctypes.c_longlong
         L.ora_verify_result.argtypes = [ctypes.POINTER(ctypes.c_longlong)]
         L.ora_replay_batch.restype = ctypes.c_double
-        L.ora_replay_batch.argtypes = [ctypes.POINTER(MtOpBatch), ctypes.POINTER(MtPropTable), ctypes.c_int, P, P]
+        L.ora_replay_batch.argtypes = [ctypes.POINTER(MtOpBatch), ctypes.POINTER(MtPropTable), ctypes.c_int, P, P, P]
+        L.ora_counters.argtypes = [P, P]
         _lib = L
     return _lib
 
@@ -236,6 +237,12 @@ class OracleDoc:
         a = np.frombuffer(ctypes.string_at(buf, n.value * 48), np.int32).reshape(-1, 12).copy()
         self.L.ora_free_buf(buf)
         return a
+
+    def counters(self) -> dict:
+        """The §8(d) algorithmic counters (mt_doc_counters order) by the oracle's own count."""
+        out = np.zeros(6, np.uint64)
+        self.L.ora_counters(self.h, out.ctypes.data)
+        return dict(zip(("ops", "msgs", "ins_units", "rows_rw", "depth", "scoured"), (int(x) for x in out)))
 
     def stats(self):
         out = np.zeros(4, np.int32)

@@ -23,7 +23,7 @@ def test_header_declares_entry_points():
 
 def test_product_library_exports_every_symbol():
     import __graft_entry__
-    lib = ctypes.CDLL(__graft_entry__.build_engine())  # rebuilds only if a source is newer
+    lib = ctypes.CDLL(__graft_entry__.build_engine())  # rebuilds unless it carries this tree's source hash
     missing = [n for n in declared() if not hasattr(lib, n)]
     assert not missing, missing
 
@@ -33,3 +33,12 @@ def test_emulation_library_exports_same_symbols():
     lib = ctypes.CDLL(build_emu())
     missing = [n for n in declared() if not hasattr(lib, "emu_" + n[3:])]
     assert not missing, missing
+
+
+def test_product_library_is_built_from_this_tree():
+    """The library carries the sha256 of the sources it was compiled from (mt_source_hash):
+    a stale libmtgpu.so (older than csrc/ or include/) fails here, on CPU, before any GPU run."""
+    import __graft_entry__
+    lib = ctypes.CDLL(__graft_entry__.build_engine())
+    lib.mt_source_hash.restype = ctypes.c_char_p
+    assert lib.mt_source_hash().decode() == __graft_entry__.source_hash()

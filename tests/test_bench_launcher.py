@@ -28,7 +28,8 @@ def test_launcher_config2_two_ranks():
     out = run("--gpus", "2", "--config", "config2", "--docs", "3", "--ops", "400", "--steps", "2", "--warmup", "1",
               "--no-cpu-baseline")
     assert out["n_gpus"] == 2 and out["scaling"] == "weak"
-    assert out["parity"] == "status words clean"
+    # every rank replays its own sample on the oracle; rank 0 reports the sum (N > 1 parity)
+    assert out["parity"].startswith("SnapshotV1 digests == oracle on 6 docs (2 ranks"), out["parity"]
     assert out["value"] > 0 and out["steps"] == 2
 
 
@@ -38,6 +39,14 @@ def test_launcher_config5_two_ranks():
     assert out["n_gpus"] == 2
     assert out["config"]["docs_total"] == 10
     assert out["parity"].startswith("status words clean on every rank")
+    assert out["exchange"]["docs_checked"] == 10 and out["exchange"]["checksum_mismatch_docs"] == 0
+
+
+def test_launcher_config5_two_ranks_oracle_parity():
+    out = run("--gpus", "2", "--config", "config5", "--docs", "6", "--steps", "1", "--warmup", "0")
+    assert out["n_gpus"] == 2 and out["config"]["docs_total"] == 12
+    assert out["parity"].startswith("SnapshotV1 digests == oracle on 12 docs (2 ranks"), out["parity"]
+    assert out["exchange"]["checksum_mismatch_docs"] == 0
 
 
 def test_single_rank_digest_parity_against_oracle():
@@ -46,3 +55,4 @@ def test_single_rank_digest_parity_against_oracle():
     assert out["n_gpus"] == 1
     assert out["parity"].startswith("SnapshotV1 digests == oracle on"), out["parity"]
     assert out["cpu_baseline"]["kind"] == "port"
+    assert out["roofline"]["bytes_pinned"].startswith("mt_doc_counters == oracle"), out["roofline"]

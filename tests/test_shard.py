@@ -59,6 +59,8 @@ def _worker(rank, world, port, docs, counts, clients, out):
     fac = lambda n, caps: Engine(n, lib_path=lib, prefix="emu_", per_doc=caps)
     sh = build_sharded(dist, torch.device("cpu"), fac, docs, 77, MtGenParams, GEN, names=NAMES, chunk_docs=5,
                        counts=counts, clients=clients)
+    # every received document's rows matched rank 0's checksum (mt_upload_rows_dev)
+    assert sh.timings["exchange_bad_docs"] == 0 and sh.timings["exchange_checked_docs"] == sh.n_docs
     sh.replay()
     sh.engine.sync()
     assert (sh.engine.status(range(sh.n_docs)) == 0).all()
@@ -92,3 +94,52 @@ def test_sharded_replay_gloo_world2_matches_oracle(tmp_path):
     last = batch.op_offsets[1:] - 1
     want = [kept[d].snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]))[1] for d in range(docs)]
     assert [int(x) for x in d2] == want
+
+
+def test_exchange_rows_checksum_catches_corruption():
+    """mt_generated_pack_rows / mt_upload_rows_dev on the host emulation (device pointers are
+    host pointers there): rows round-trip into a resident batch that replays exactly like the
+    generated one, and any flipped bit or zeroed row of a document is reported for that
+    document only (MT_E_EXCHANGE)."""
+    from emu_lib import emu_engine
+    from fluidframework_amd.batch import MtGenParams, PropTable
+    from fluidframework_amd.engine import ExchangeError
+    from fluidframework_amd.shard import generation_caps
+    counts = np.array([30, 7, 120, 64], np.uint32)
+    clients = np.array([3, 2, 9, 4], np.uint32)
+    L = GEN["ins_len_max"]
+    caps = generation_caps(counts, L)
+    src = emu_engine(4, per_doc=caps)
+    src.upload_props(PropTable())
+    src.upload_names(NAMES)
+    src.generate(MtGenParams(**{**GEN, "seed": 5, "n_docs": 4, "ops_per_doc": 0, "clients": 2}),
+                 ops_per_doc=counts, clients_per_doc=clients)
+    src.sync()
+    W = 4 + L // 4
+    order = np.array([2, 0, 3, 1])                         # a plan: send order differs from generation order
+    row_of = np.empty(4, np.int64)
+    row_of[order] = np.concatenate(([0], np.cumsum(counts[order].astype(np.int64))[:-1]))
+    rows = np.zeros((int(counts.sum()), W), np.uint64)
+    sums = src.generated_pack_rows(0, 4, row_of.astype(np.uint64), rows.ctypes.data)
+    off = np.concatenate(([0], np.cumsum(counts[order]))).astype(np.uint32)
+    dst = emu_engine(4, per_doc={k: np.asarray(v)[order] for k, v in caps.items()})
+    dst.upload_props(PropTable())
+    dst.upload_names(NAMES)
+    assert not dst.upload_rows_dev(range(4), off, rows.ctypes.data, L, sums[order]).any()
+    dst.open_docs(0, 4)
+    dst.replay_resident()
+    dst.sync()
+    assert (dst.status(range(4)) == 0).all()
+    neg = np.full(4, -1, np.int32)
+    want = src.snapshot_digests(range(4), neg, neg, threads=1)
+    assert np.array_equal(dst.snapshot_digests(range(4), neg, neg, threads=1), want[order])
+    for how in ("bit", "zero"):                             # corrupt the third document of the plan (doc 3)
+        bad = rows.copy()
+        r = int(row_of[3]) + 5
+        if how == "bit":
+            bad[r, W - 1] ^= np.uint64(1 << 17)
+        else:
+            bad[r, :] = 0
+        with pytest.raises(ExchangeError) as ei:
+            dst.upload_rows_dev(range(4), off, bad.ctypes.data, L, sums[order])
+        assert list(ei.value.bad_runs) == [0, 0, 1, 0]
