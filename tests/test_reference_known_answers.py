@@ -18,6 +18,17 @@ Python `Client` drop-in) must produce it.
   splits twice; once the MSN passes it zamboni unlinks the removed segment and the
   survivors on either side are not merged across it (scourNode resets prev,
   mergeTree.ts:1296-1303).
+* mergeTree.insert.deltaCallback.spec.ts:35-150 and mergeTree.annotate.deltaCallback.spec.ts:
+  36-153 — the countOperations tallies (delta callbacks per op, SPLIT maintenance records)
+  of inserts at the start / end / middle, a marker insert, and annotates over an insertion
+  or deletion the annotating client has or has not seen.
+* client.walkSegments.spec.ts:22-65 — a range walk with splits visits 2 segments of 4
+  characters (annotateRange's boundaries), without splits 2 whole segments of 10
+  (cloneSegments, observed through a register copy and paste).
+* client.getPostion.spec.ts:29-60 — event positions (Client.getPosition) of an existing, a
+  removed, a moved and an about-to-be-detached segment.
+* snapshotlegacy.spec.ts:14-83 — SnapshotLegacy of 10,000 (header only) and 10,010 (header
+  and body) one-character segments loads back to the same length and text, twice.
 """
 import json
 
@@ -284,3 +295,173 @@ def test_unlink_known_answer_on_emulation():
 @pytest.mark.gpu
 def test_unlink_known_answer_on_gpu():
     check_unlink(GPU)
+
+
+# ---- delta-callback counts (testUtils.countOperations) as a passive observer sees them ------
+# The reference specs call MergeTree methods as a local client; the observer restatement has a
+# remote client send the same op, so the same splits and callbacks happen in the observer's
+# tree.  A delta callback counts once per op (its deltaSegments are the op's records), a
+# maintenance callback once per record.
+HELLO_WORLD = {"header": v1_header(["hello world"], 0, 0).decode()}
+HW_CHARS = {"header": v1_header(list("hello world"), 0, 0).decode()}     # 11 one-character segments
+HW_TWO = {"header": v1_header(["hello", "world"], 0, 0).decode()}       # client.walkSegments.spec.ts:16-21
+
+
+def op_events(factory, load, msgs):
+    """Apply msgs (one device batch each) on the engine with delta capture and on the oracle;
+    both sides' records must agree; returns the per-message records [(kind, pos, len)] and
+    countOperations-style counts."""
+    od = OracleDoc(False)
+    blobs = [load["header"]] + [load[k] for k in sorted(load) if k != "header"]
+    assert od.load_snapshot(blobs) == 0
+    od.delta_capture(True)
+    eng = factory(1, **LIMITS)
+    g = ClientGroup(eng)
+    c = g.new_client({"newMergeTreeSnapshotFormat": True})
+    c.load(load)
+    out = []
+    for m in msgs:
+        od.delta_capture(False)
+        od.delta_capture(True)
+        assert od.apply_msg(m) == 0, m
+        eng.delta_capture(1 << 16)
+        c.applyMsg(m)
+        g.flush()
+        recs = eng.delta_records()
+        eng.delta_capture(0)
+        got = [(int(r["kind"]), int(r["pos"]), int(r["len"])) for r in recs]
+        want = [(k, p, ln) for _, k, p, ln, *_ in od.delta_records()]
+        assert got == want, (m, got, want)
+        counts: dict = {}
+        for k in {k for k, _, _ in got}:
+            counts[k] = 1 if k >= 0 else sum(1 for x in got if x[0] == k)
+        out.append((got, counts))
+    assert c.getText() == od.get_text()
+    return out, od, c
+
+
+INSERT, REMOVE, ANNOTATE, APPEND, SPLIT, UNLINK = 0, 1, 2, -1, -2, -3
+
+
+def check_insert_delta_counts(factory):
+    # mergeTree.insert.deltaCallback.spec.ts:35-118 on "hello world!" (universal)
+    hw = {"header": v1_header(["hello world!"], 0, 0).decode()}
+    ev, _, _ = op_events(factory, hw, [msg("remote", 1, 0, 0, ins(0, "more "))])          # Insert text remote
+    assert ev[0][1] == {INSERT: 1}
+    ev, _, _ = op_events(factory, hw, [msg("remote", 1, 0, 0, ins(12, "more "))])         # Insert ending text
+    assert ev[0][1] == {INSERT: 1}
+    ev, _, _ = op_events(factory, hw, [msg("remote", 1, 0, 0, ins(4, "more "))])          # Insert middle text
+    assert ev[0][1] == {INSERT: 1, SPLIT: 1}
+    ev, _, _ = op_events(factory, hw, [msg("remote", 1, 0, 0, ins(4, {"marker": {"refType": 1}}))])   # Insert marker
+    assert ev[0][1] == {INSERT: 1, SPLIT: 1}
+
+
+def check_annotate_delta_counts(factory):
+    # mergeTree.annotate.deltaCallback.spec.ts:36-153 on "hello world" (universal)
+    foo = {"foo": "bar"}
+    ev, _, _ = op_events(factory, HELLO_WORLD, [msg("B", 1, 0, 0, ann(4, 6, foo))])       # Event on annotation
+    assert ev[0][1] == {ANNOTATE: 1, SPLIT: 2}
+    # Annotate over local insertion: the annotating client's own insert is visible to it
+    ev, _, _ = op_events(factory, HELLO_WORLD, [msg("B", 1, 0, 0, ins(4, "a")), msg("B", 2, 0, 0, ann(3, 8, foo))])
+    assert ev[1][1] == {ANNOTATE: 1, SPLIT: 2}
+    assert sum(ln for k, _, ln in ev[1][0] if k == ANNOTATE) == 5
+    # Annotate over remote insertion: A's insert (seq 1) is not in B's refSeq-0 view
+    ev, _, _ = op_events(factory, HELLO_WORLD, [msg("A", 1, 0, 0, ins(4, "a")), msg("B", 2, 0, 0, ann(3, 8, foo))])
+    assert ev[1][1] == {ANNOTATE: 1, SPLIT: 2}
+    assert sum(ln for k, _, ln in ev[1][0] if k == ANNOTATE) == 5
+    # Annotate over remote deletion: A's removal (seq 1) is not in B's view either
+    ev, _, _ = op_events(factory, HELLO_WORLD, [msg("A", 1, 0, 0, rem(4, 6)), msg("B", 2, 0, 0, ann(3, 8, foo))])
+    assert ev[1][1] == {ANNOTATE: 1, SPLIT: 2}
+
+
+def check_walk_segments(factory):
+    # client.walkSegments.spec.ts:22-65 on "hello" + "world": a walk of [3, 7) visits both
+    # segments (10 characters) without splitting, 2 segments of 4 characters with splitting.
+    # With split (ensureIntervalBoundary at both ends, as annotateRange does):
+    ev, _, _ = op_events(factory, HW_TWO, [msg("B", 1, 0, 0, ann(3, 7, {"k": 1}))])
+    annot = [(p, ln) for k, p, ln in ev[0][0] if k == ANNOTATE]
+    assert len(annot) == 2 and sum(ln for _, ln in annot) == 4 and ev[0][1] == {ANNOTATE: 1, SPLIT: 2}
+    # Without split (mapRange, as cloneSegments' register copy does): 2 whole segments, 10 characters
+    copy = msg("B", 1, 0, 0, {"type": 0, "pos1": 3, "pos2": 7, "register": "r"})
+    paste = msg("B", 2, 1, 1, {"type": 0, "pos1": 0, "register": "r"})
+    ev, od, c = op_events(factory, HW_TWO, [copy, paste])
+    assert od.register_info("B", "r") == {"n": 2, "len": 10, "removed": 0, "pasted": 1}
+    assert [(k, ln) for k, _, ln in ev[1][0] if k == INSERT] == [(INSERT, 5), (INSERT, 5)]
+    assert c.getText() == "helloworldhelloworld"
+
+
+def check_get_position(factory):
+    # client.getPostion.spec.ts:29-60 on "hello world" as 11 one-character segments; the
+    # "o" segment at 4.  SequenceDeltaEvent positions are Client.getPosition of the segment.
+    ev, _, _ = op_events(factory, HW_CHARS, [msg("B", 1, 0, 0, ann(4, 5, {"k": 1}))])      # Existing Segment
+    assert [(k, p) for k, p, _ in ev[0][0]] == [(ANNOTATE, 4)]
+    ev, _, _ = op_events(factory, HW_CHARS, [msg("B", 1, 0, 0, rem(4, 5))])               # Deleted Segment
+    assert [(k, p) for k, p, _ in ev[0][0]] == [(REMOVE, 4)]
+    ev, _, _ = op_events(factory, HW_CHARS, [msg("B", 1, 0, 0, rem(3, 4)),                 # Moved Segment
+                                             msg("B", 2, 1, 0, ann(3, 4, {"k": 1}))])
+    assert [(k, p) for k, p, _ in ev[1][0]] == [(ANNOTATE, 3)]
+    # Detached Segment: once the MSN passes the removal, zamboni scours the block: "h" takes
+    # "e", "l", "l" (APPEND at 0, lengths 2, 3, 4), then unlinks "o".  The UNLINK callback
+    # fires before segment.parent is cleared (mergeTree.ts:1296-1306) and getPosition walks
+    # parent.children, which still holds the appended segments until the block is rebuilt,
+    # so the reference names it at 4 + 1 + 1 + 1 = 7.  Afterwards it is detached: no later
+    # event reaches it.
+    ev, _, c = op_events(factory, HW_CHARS, [msg("B", 1, 0, 0, rem(4, 5)), msg("B", 2, 1, 1, None, type="noop"),
+                                             msg("B", 3, 2, 2, ins(0, "x"))])
+    assert ev[1][0][:4] == [(APPEND, 0, 2), (APPEND, 0, 3), (APPEND, 0, 4), (UNLINK, 7, 1)]
+    assert all(k != UNLINK for k, _, _ in ev[2][0])
+    assert c.getText() == "xhell world"
+
+
+@pytest.mark.parametrize("check", [check_insert_delta_counts, check_annotate_delta_counts, check_walk_segments,
+                                   check_get_position])
+def test_delta_known_answers_on_emulation(check):
+    check(emu_engine)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("check", [check_insert_delta_counts, check_annotate_delta_counts, check_walk_segments,
+                                   check_get_position])
+def test_delta_known_answers_on_gpu(check):
+    check(GPU)
+
+
+# ---- snapshotlegacy.spec.ts:14-83 --------------------------------------------------------
+def check_snapshot_legacy(factory, n):
+    """Client "0" appends `${i % 10}` with props {segment: i}, msn = seq, n times; the observer's
+    SnapshotLegacy loads back to the same length and text, and again from the loaded copy."""
+    msgs = [msg("0", i + 1, i, i + 1, ins(i, {"text": str(i % 10), "props": {"segment": i}})) for i in range(n)]
+    lim = dict(LIMITS, propsets_per_doc=2 * n + 64)
+    g = ClientGroup(factory(3, **lim))
+    c0 = g.new_client()                                  # default options: SnapshotLegacy
+    od = OracleDoc(True)
+    for m in msgs:
+        c0.applyMsg(m)
+        assert od.apply_msg(m) == 0
+    text, length = od.get_text(), od.get_length()
+    assert c0.getText() == text and c0.getLength() == length == n
+    prev_o, prev_c = od, c0
+    for hop in range(2):                                  # client1 -> client2 -> client3 (:46-80)
+        tree = prev_c.snapshot()
+        blobs = {e["path"]: e["value"]["contents"] for e in tree["entries"]}
+        ob, _ = prev_o.snapshot(n, n, legacy=True)
+        assert [blobs["header"].encode()] + ([blobs["body"].encode()] if "body" in blobs else []) == ob
+        assert ("body" in blobs) == (n > 10000)           # sizeOfFirstChunk (snapshotlegacy.ts:57)
+        o2 = OracleDoc(False)
+        assert o2.load_snapshot([blobs["header"]] + ([blobs["body"]] if "body" in blobs else [])) == 0
+        c2 = g.new_client()
+        c2.load(blobs)
+        assert c2.getLength() == o2.get_length() == length
+        assert c2.getText() == o2.get_text() == text
+        prev_o, prev_c = o2, c2
+
+
+@pytest.mark.parametrize("n", [10000, 10010])
+def test_snapshot_legacy_known_answers_on_emulation(n):
+    check_snapshot_legacy(emu_engine, n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [10000, 10010])
+def test_snapshot_legacy_known_answers_on_gpu(n):
+    check_snapshot_legacy(GPU, n)
