@@ -161,7 +161,7 @@ void MT_FN(destroy)(mt_ctx* c) {
                             &c->b_dcount, &c->b_pset_off,
                             &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3,
                             &c->b_ld_meta, &c->b_ld_seg, &c->b_ld_pay, &c->b_ld_plan, &c->b_ld_poff, &c->b_dtext,
-                            &c->b_resume, &c->b_start};
+                            &c->b_resume, &c->b_start, &c->b_batch};
     for (auto* b : bs) if (b->p) mtb_free(b->p);
     mtb_fini(c);
     delete c;
@@ -208,29 +208,43 @@ int MT_FN(set_doc_client_names)(mt_ctx* c, uint32_t doc, uint32_t n, const char*
     return MT_OK;
 }
 
+// The batch's arrays in one device region, one pinned staging copy and one asynchronous H2D
+// (stream-ordered before the replay that follows; no host synchronization): doc ids, op
+// offsets, the op records packed to mt_op_rec, the payload and the relative positions.  The
+// caller's arrays are consumed before this returns.
 static int mt_upload_ops(mt_ctx* c, const mt_op_batch* B) {
     const size_t N = B->n_ops, R = B->n_runs;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_doc = 0, o_off = al(o_doc + 4 * R), o_rec = al(o_off + 4 * (R + 1)),
+                 o_pay = al(o_rec + sizeof(MtOpRec) * N), o_rel = al(o_pay + 2 * (size_t)B->payload_units),
+                 total = al(o_rel + sizeof(MtRelPos) * (size_t)(B->rel ? B->n_rel : 0)) + 256;
+    static_assert(sizeof(mt_rel_pos) == sizeof(MtRelPos), "relative position layout");
     int rc;
-    std::vector<MtOpRec> rec(N ? N : 1);
+    if ((rc = mtb_ensure(c, c->b_batch, total))) return rc;
+    uint8_t* h = (uint8_t*)mtb_stage_get(c, total);
+    if (!h) { c->err = "pinned staging allocation failed"; return MT_E_OOM; }
+    if (R) memcpy(h + o_doc, B->doc_ids, 4 * R);
+    memcpy(h + o_off, B->op_offsets, 4 * (R + 1));
+    MtOpRec* rec = (MtOpRec*)(h + o_rec);
+    bool reg = false;
     for (size_t i = 0; i < N; i++) {
         MtOpRec& o = rec[i];
         o.type = B->type[i]; o.flags = B->flags[i]; o.client = B->client[i]; o.seq = B->seq[i]; o.ref_seq = B->ref_seq[i];
         o.msn = B->msn[i]; o.pos1 = B->pos1[i]; o.pos2 = B->pos2[i]; o.payload_off = B->payload_off[i];
         o.payload_len = (uint16_t)B->payload_len[i]; o.prop_id = (int16_t)B->prop_id[i];
+        reg |= B->type[i] >= MT_OP_CUT && B->type[i] <= MT_OP_PASTE;
     }
-#define UP(buf, src, bytes) if ((rc = mtb_ensure(c, c->buf, (bytes)))) return rc; if ((bytes) && (src)) mtb_h2d(c, c->buf.p, (src), (bytes));
-    UP(b_doc, B->doc_ids, 4 * R) UP(b_off, B->op_offsets, 4 * (R + 1)) UP(b_rec, rec.data(), sizeof(MtOpRec) * N)
-    UP(b_pay, B->payload, 2 * B->payload_units)
-    static_assert(sizeof(mt_rel_pos) == sizeof(MtRelPos), "relative position layout");
-    UP(b_rel, B->rel, sizeof(MtRelPos) * (size_t)B->n_rel)
-#undef UP
+    if (B->payload_units) memcpy(h + o_pay, B->payload, 2 * (size_t)B->payload_units);
+    if (B->rel && B->n_rel) memcpy(h + o_rel, B->rel, sizeof(MtRelPos) * (size_t)B->n_rel);
+    mtb_stage_send(c, c->b_batch.p, total);
+    uint8_t* d = (uint8_t*)c->b_batch.p;
     MtOps& o = c->ops;
-    o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
-    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = B->n_runs; o.payload_units = B->payload_units;
-    o.rel = (const MtRelPos*)c->b_rel.p; o.n_rel = B->rel ? B->n_rel : 0;
+    o.doc_ids = (const uint32_t*)(d + o_doc); o.op_off = (const uint32_t*)(d + o_off); o.rec = (MtOpRec*)(d + o_rec);
+    o.payload = (uint16_t*)(d + o_pay); o.n_runs = B->n_runs; o.payload_units = B->payload_units;
+    o.rel = (const MtRelPos*)(d + o_rel); o.n_rel = B->rel ? B->n_rel : 0;
     c->n_runs = B->n_runs;
-    c->batch_reg = false;
-    for (size_t i = 0; i < N && !c->batch_reg; i++) c->batch_reg = B->type[i] >= MT_OP_CUT && B->type[i] <= MT_OP_PASTE;
+    c->run_off.assign(B->op_offsets, B->op_offsets + R + 1);
+    c->batch_reg = reg;
     return MT_OK;
 }
 
@@ -259,9 +273,7 @@ int MT_FN(upload_batch)(mt_ctx* c, const mt_op_batch* B) {
     if (!c) return MT_E_INVALID;
     int rc = mt_check_batch(c, B);
     if (rc) return rc;
-    rc = mt_upload_ops(c, B);
-    mtb_sync(c);
-    return rc;
+    return mt_upload_ops(c, B);                           // stream-ordered: no synchronization
 }
 // A capture batch (mt_delta_capture armed): each launch appends records until a document
 // has no headroom left for its next message (MtEngT::dReserve); that run stops there, the
@@ -274,7 +286,8 @@ static int mt_replay_capture(mt_ctx* c, const MtGen& g) {
     if ((rc = mtb_ensure(c, c->b_resume, 4ull * R + 4))) return rc;
     if ((rc = mtb_ensure(c, c->b_start, 4ull * R + 4))) return rc;
     std::vector<uint32_t> off(R + 1), resume(R), start(R);
-    mtb_d2h(c, off.data(), c->ops.op_off, 4ull * (R + 1));
+    if (c->run_off.size() == R + 1) off = c->run_off;
+    else mtb_d2h(c, off.data(), c->ops.op_off, 4ull * (R + 1));
     for (uint32_t r = 0; r < R; r++) start[r] = off[r];
     c->delta_host.clear(); c->delta_text.clear(); c->delta_over = false; c->delta_launches = 0;
     MtOps& o = c->ops;
@@ -794,6 +807,7 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     c->n_runs = P->n_docs;
     c->batch_reg = false;                     // generated streams hold no register ops
     c->gen_off.assign(off.begin(), off.end());
+    c->run_off = c->gen_off;
     if (!P->continue_docs) {
         rc = MT_FN(docs_open)(c, 0, P->n_docs);
         if (rc) return rc;
@@ -866,6 +880,7 @@ int MT_FN(upload_batch_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids,
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs; o.payload_units = payload_units;
     o.rel = nullptr; o.n_rel = 0;
     c->n_runs = n_runs;
+    c->run_off.assign(op_offsets, op_offsets + n_runs + 1);
     c->batch_reg = false;                     // device-built streams (shard.py) hold no register ops
     c->gen.enabled = 0;
     return mtb_sync(c);
@@ -913,6 +928,7 @@ int MT_FN(upload_rows_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids, 
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs; o.payload_units = N * L;
     o.rel = nullptr; o.n_rel = 0;
     c->n_runs = n_runs;
+    c->run_off.assign(op_offsets, op_offsets + n_runs + 1);
     c->batch_reg = false;                     // exchanged generated streams hold no register ops
     c->gen.enabled = 0;
     if (n_runs && (rc = mtb_launch_rows(c, false, 0, n_runs, (uint32_t)L, nullptr, (uint64_t*)rows_dev,

@@ -837,10 +837,18 @@ template <int RES, bool FULL = true> struct MtEngT {
         MT_EV(0, 1); MT_EV(2, winN);
         MT_QB(q0); MT_QC(4);
         int newWin = 0; nU = 0;
-        for (int base = 0; base < winN; base += MT_WAVE) {
+        // Window rows, one 64-entry chunk at a time, software-pipelined: chunk i+1's row
+        // fields are in flight while chunk i is processed, and chunk i+2's window ids behind
+        // them (the window entries are distinct rows and compaction only writes entries below
+        // the chunk being read, so the early reads see what in-order reads would).
+        auto winIds = [&](int base) MT_LAM {
             const int m = (winN - base) < MT_WAVE ? (winN - base) : MT_WAVE;
-            auto wi = wave_map(m, [&](int k) MT_LAM {
-                WinI w; w.id = wn(base + k);
+            return wave_map(m, [&](int k) MT_LAM { return wn(base + k); });
+        };
+        auto winRows = [&](const LaneArr<int>& ids, int base) MT_LAM {
+            const int m = (winN - base) < MT_WAVE ? (winN - base) : MT_WAVE;
+            return wave_map(m, [&](int k) MT_LAM {
+                WinI w; w.id = own(ids, k);
                 const int s = w.id;
                 const uint32_t mt = row(s).meta;
                 const bool removed = (mt & MT_M_REMOVED) != 0;
@@ -854,6 +862,19 @@ template <int RES, bool FULL = true> struct MtEngT {
                 w.delta = w.live ? ((vr ? row(s).len : 0) - (vo ? row(s).len : 0)) : 0;
                 return w;
             });
+        };
+        const int wN0 = winN;
+        LaneArr<WinI> wiNext{};
+        LaneArr<int> idNext{};
+        if (wN0 > 0) wiNext = winRows(winIds(0), 0);
+        if (wN0 > MT_WAVE) idNext = winIds(MT_WAVE);
+        for (int base = 0; base < wN0; base += MT_WAVE) {
+            const int m = (wN0 - base) < MT_WAVE ? (wN0 - base) : MT_WAVE;
+            const auto wi = wiNext;
+            if (base + MT_WAVE < wN0) {
+                wiNext = winRows(idNext, base + MT_WAVE);
+                if (base + 2 * MT_WAVE < wN0) idNext = winIds(base + 2 * MT_WAVE);
+            }
             auto live = wave_map(m, [&](int k) MT_LAM { return own(wi, k).live; });
             if (prune) {
                 auto rk = wave_rank(live);
@@ -900,24 +921,24 @@ template <int RES, bool FULL = true> struct MtEngT {
             nU += cntU;
         }
         wave_sync();
-        // Blocks in HBM: ancestor chains level by level for up to four 64-entry chunks at
+        // Blocks in HBM: ancestor chains level by level for up to eight 64-entry chunks at
         // once; the parent loads of one level are independent, so a level costs one round
-        // trip for 256 entries instead of one per chunk.
+        // trip for 512 entries instead of one per chunk.
         const int H = height;
-        for (int g0 = 0; !BLKL && g0 < nU; g0 += 4 * MT_WAVE) {
+        for (int g0 = 0; !BLKL && g0 < nU; g0 += 8 * MT_WAVE) {
             const int nu = nU;
             wave_for(MT_WAVE, [&](int k) MT_LAM {
-                int a[4]; int pos[4];
+                int a[8]; int pos[8];
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
+                for (int q = 0; q < 8; q++) {
                     pos[q] = g0 + q * MT_WAVE + k;
                     a[q] = pos[q] < nu ? ancGetAny(pos[q], 0) : -1;
                 }
                 for (int h = 1; h <= H; h++) {
 #pragma unroll
-                    for (int q = 0; q < 4; q++) a[q] = a[q] >= 0 ? bk(a[q]).parent : -1;
+                    for (int q = 0; q < 8; q++) a[q] = a[q] >= 0 ? bk(a[q]).parent : -1;
 #pragma unroll
-                    for (int q = 0; q < 4; q++) if (pos[q] < nu) ancPutAny(pos[q], h, a[q]);
+                    for (int q = 0; q < 8; q++) if (pos[q] < nu) ancPutAny(pos[q], h, a[q]);
                 }
             });
         }
@@ -1736,7 +1757,8 @@ template <int RES, bool FULL = true> struct MtEngT {
             bk(P).n = cc;
             wave_sync();
             if (cc < MT_MAXN / 2 && ph.parent >= 0) { P = ph.parent; continue; }
-            updatePathLens(P);
+            // The reference refreshes the path here (blockUpdatePathLengths, :1406) for its
+            // partial lengths; observer lengths cannot have changed (see zamboniInner).
             return;
         }
     }
@@ -1774,12 +1796,11 @@ template <int RES, bool FULL = true> struct MtEngT {
                     wave_for(8, [&](int j) MT_LAM { bk(p).c[j] = j < nh ? sc->hold[j] : -1; });
                     bk(p).n = nh;
                     wave_sync();
+                    // A scour keeps every block's observer length: unlinked rows were removed
+                    // (length 0 in the observer's view) and a merged run keeps its sum, so the
+                    // reference's blockUpdatePathLengths (:1456-1460; it rebuilds partial
+                    // lengths, which this engine does not keep) changes no observer length here.
                     if (nh < MT_MAXN / 2 && h.parent >= 0) { MT_ZB(z3); packParent(h.parent); MT_ZE(3, z3); }
-                    else {
-                        MT_ZB(z4);
-                        updatePathLens(p, wave_sum8(wave_map(nh, [&](int i) MT_LAM { return sc->holdLen[i]; })));
-                        MT_ZE(4, z4);
-                    }
                 }
                 MT_ZE(6, z6);
             }

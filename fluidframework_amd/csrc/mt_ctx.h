@@ -27,6 +27,13 @@ struct mt_ctx {
            b_ld_meta, b_ld_seg, b_ld_pay, b_ld_plan, b_ld_poff, b_dtext, b_resume, b_start;
     MtOps ops{};
     uint32_t n_runs = 0;
+    std::vector<uint32_t> run_off;     // host copy of the resident batch's op offsets (n_runs + 1)
+    // mt_apply_batch / mt_upload_batch staging: two pinned host slots used alternately, each
+    // with the event of its last H2D, and one device region the batch lands in
+    struct Stage { void* p = nullptr; size_t cap = 0; void* ev = nullptr; };
+    Stage stage[2];
+    int stage_k = 0;
+    DevBuf b_batch;
     MtGen gen{};
     uint32_t gen_docs = 0;
     std::vector<uint32_t> gen_off;     // op offsets of the generated runs

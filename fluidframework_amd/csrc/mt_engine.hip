@@ -80,6 +80,10 @@ static int mtb_init(mt_ctx* c) {
 }
 static void mtb_fini(mt_ctx* c) {
     if (c->stream) { (void)hipStreamSynchronize((hipStream_t)c->stream); (void)hipStreamDestroy((hipStream_t)c->stream); }
+    for (auto& st : c->stage) {
+        if (st.ev) (void)hipEventDestroy((hipEvent_t)st.ev);
+        if (st.p) (void)hipHostFree(st.p);
+    }
     if (c->ev0) (void)hipEventDestroy((hipEvent_t)c->ev0);
     if (c->ev1) (void)hipEventDestroy((hipEvent_t)c->ev1);
 }
@@ -89,6 +93,27 @@ static void mtb_memset(void* p, int v, size_t n) { (void)hipMemset(p, v, n); }
 static void mtb_h2d(mt_ctx* c, void* d, const void* s, size_t n) { (void)hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, (hipStream_t)c->stream); (void)hipStreamSynchronize((hipStream_t)c->stream); }
 static void mtb_d2d(mt_ctx* c, void* d, const void* s, size_t n) { (void)hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, (hipStream_t)c->stream); (void)hipStreamSynchronize((hipStream_t)c->stream); }
 static void mtb_d2h(mt_ctx* c, void* d, const void* s, size_t n) { (void)hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, (hipStream_t)c->stream); (void)hipStreamSynchronize((hipStream_t)c->stream); }
+// Pinned staging for batch uploads: the next slot, grown if needed, once its previous H2D
+// is done (the slot's event); mtb_stage_send then copies it to the device asynchronously.
+static void* mtb_stage_get(mt_ctx* c, size_t n) {
+    mt_ctx::Stage& st = c->stage[c->stage_k];
+    if (st.ev) (void)hipEventSynchronize((hipEvent_t)st.ev);
+    else { hipEvent_t e; (void)hipEventCreateWithFlags(&e, hipEventDisableTiming); st.ev = e; }
+    if (st.cap < n) {
+        if (st.p) (void)hipHostFree(st.p);
+        st.p = nullptr; st.cap = 0;
+        const size_t cap = n + n / 4 + 4096;
+        if (hipHostMalloc(&st.p, cap, hipHostMallocDefault) != hipSuccess) { st.p = nullptr; return nullptr; }
+        st.cap = cap;
+    }
+    return st.p;
+}
+static void mtb_stage_send(mt_ctx* c, void* dev, size_t n) {
+    mt_ctx::Stage& st = c->stage[c->stage_k];
+    (void)hipMemcpyAsync(dev, st.p, n, hipMemcpyHostToDevice, (hipStream_t)c->stream);
+    (void)hipEventRecord((hipEvent_t)st.ev, (hipStream_t)c->stream);
+    c->stage_k ^= 1;
+}
 static int mtb_sync(mt_ctx* c) {
     hipError_t e = hipStreamSynchronize((hipStream_t)c->stream);
     if (e != hipSuccess) { c->err = hipGetErrorString(e); return MT_E_HIP; }

@@ -1,0 +1,253 @@
+"use strict";
+/*
+ * The packing half of the Node host (no GPU addon: index.js and the ParallelPacker workers
+ * both use it).  BatchBuilder restates Client.applyMsg's dispatch (packages/dds/merge-tree/
+ * src/client.ts:790-841, MT/ below) into mt_op_batch columns: long client ids become
+ * per-document indices, GROUP members share the message's seq, and property sets are
+ * interned with JS semantics (Object.keys order, JSON.stringify text, falsiness for
+ * "rewrite", matchProperties classes, MT/properties.ts:64-95).
+ */
+const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_GROUP = 3, OP_UNSUPPORTED = 4;
+const OP_CUT = 5, OP_COPY = 6, OP_PASTE = 7;          // register ops (include/mtgpu.h)
+const F_END = 1, F_MARKER = 2, F_REWRITE = 4, F_SEG_PROPS = 8, F_COMBINE = 16, F_REL1 = 0x20, F_REL2 = 0x40,
+    F_MARKER_ID = 0x80;
+const MARKER_ID_KEY = "markerId";   // reservedMarkerIdKey, MT/mergeTree.ts:591
+function arrayIndex(k) {
+    // canonical array index (OrdinaryOwnPropertyKeys orders these first)
+    if (!/^(0|[1-9][0-9]{0,9})$/.test(k)) return undefined;
+    const v = Number(k);
+    return v < 4294967295 ? v : undefined;
+}
+
+// matchProperties equivalence (MT/properties.ts:64-95): objects compare
+// order-insensitively and recursively, primitives with ===.
+function matchClassKey(v) {
+    if (v !== null && typeof v === "object") {
+        return "o{" + Object.keys(v).sort().map((k) => JSON.stringify(k) + ":" + matchClassKey(v[k])).join(",") + "}";
+    }
+    if (typeof v === "number") return "n" + String(v);
+    if (typeof v === "boolean") return "b" + String(v);
+    if (typeof v === "string") return "s" + JSON.stringify(v);
+    return "z";
+}
+
+class PropTable {
+    constructor() {
+        this.keyIds = new Map(); this.keys = [];
+        this.valueIds = new Map(); this.valueJson = []; this.valueFalsy = []; this.valueClass = [];
+        this.classIds = new Map();
+        this.setIds = new Map(); this.sets = [];
+    }
+    keyId(k) {
+        let i = this.keyIds.get(k);
+        if (i === undefined) { i = this.keys.length; this.keyIds.set(k, i); this.keys.push(k); }
+        return i;
+    }
+    valueId(v) {
+        if (v === null) return -1;                       // null deletes the key
+        const txt = JSON.stringify(v);
+        let i = this.valueIds.get(txt);
+        if (i === undefined) {
+            i = this.valueJson.length;
+            this.valueIds.set(txt, i);
+            this.valueJson.push(txt);
+            this.valueFalsy.push(v ? 0 : 1);
+            const ck = matchClassKey(v);
+            let c = this.classIds.get(ck);
+            if (c === undefined) { c = this.classIds.size; this.classIds.set(ck, c); }
+            this.valueClass.push(c);
+        }
+        return i;
+    }
+    intern(props) {
+        const pairs = Object.keys(props).map((k) => [this.keyId(k), this.valueId(props[k])]);
+        const sig = pairs.map((p) => p.join(":")).join(",");
+        let i = this.setIds.get(sig);
+        if (i === undefined) { i = this.sets.length; this.setIds.set(sig, i); this.sets.push(pairs); }
+        return i;
+    }
+    toNative() {
+        const setOff = new Uint32Array(this.sets.length + 1);
+        const key = [], value = [];
+        this.sets.forEach((s, i) => { setOff[i + 1] = setOff[i] + s.length; for (const [k, v] of s) { key.push(k); value.push(v); } });
+        return {
+            setOff, key: Uint16Array.from(key.length ? key : [0]), value: Int32Array.from(value.length ? value : [0]),
+            keyJson: this.keys.map((k) => JSON.stringify(k)),
+            keyIndex: Uint32Array.from(this.keys.length ? this.keys.map((k) => { const a = arrayIndex(k); return a === undefined ? 0xFFFFFFFF : a; }) : [0]),
+            valueJson: this.valueJson,
+            valueFalsy: Uint8Array.from(this.valueFalsy.length ? this.valueFalsy : [0]),
+            valueClass: Uint32Array.from(this.valueClass.length ? this.valueClass : [0]),
+        };
+    }
+}
+
+/** Per-document interning: long client ids (getOrAddShortClientId order, client.ts:658-682)
+ * and marker ids -> the document's idToSegment table on the device (mergeTree.ts:1095). */
+class ClientNames {
+    constructor() { this.ids = new Map(); this.names = []; this.markerIds = new Map(); this.registerIds = new Map(); }
+    /** The document's index of a register name (RegisterCollection key, with the author). */
+    registerIndex(name) {
+        if (!this.registerIds.has(name)) this.registerIds.set(name, this.registerIds.size);
+        return this.registerIds.get(name);
+    }
+    index(longId) {
+        let i = this.ids.get(longId);
+        if (i === undefined) { i = this.names.length; this.ids.set(longId, i); this.names.push(longId); }
+        return i;
+    }
+    /** A marker carrying this id joins the document; null for a non-string or reused id. */
+    markerDefine(id) {
+        if (typeof id !== "string" || this.markerIds.has(id)) return null;
+        const i = this.markerIds.size;
+        this.markerIds.set(id, i);
+        return i;
+    }
+    /** getMarkerFromId: the table index, -1 when never mapped. */
+    markerLookup(id) { return typeof id === "string" && this.markerIds.has(id) ? this.markerIds.get(id) : -1; }
+}
+
+// applyRemoteOp's GROUP recursion (client.ts:804-812), flattened; members share the seq
+function mergeTreeMembers(contents) {
+    const flat = (op) => (op && typeof op === "object") ? (op.type === OP_GROUP ? (op.ops || []).flatMap(flat) : [op]) : [];
+    return flat(contents).filter((m) => m.type === OP_INSERT || m.type === OP_REMOVE || m.type === OP_ANNOTATE);
+}
+
+const COLS = [["type", Uint8Array], ["flags", Uint8Array], ["client", Uint16Array], ["seq", Int32Array],
+    ["refSeq", Int32Array], ["msn", Int32Array], ["pos1", Int32Array], ["pos2", Int32Array],
+    ["payloadOff", Uint32Array], ["payloadLen", Uint32Array], ["propId", Int32Array]];
+
+/** A growable typed-array column (amortized doubling; no per-element JS objects). */
+class Col {
+    constructor(T, cap = 1024) { this.T = T; this.a = new T(cap); this.n = 0; }
+    push(v) {
+        if (this.n === this.a.length) { const b = new this.T(this.a.length * 2); b.set(this.a); this.a = b; }
+        this.a[this.n++] = v;
+    }
+    view() { return this.a.subarray(0, this.n); }
+}
+
+/** Packs ISequencedDocumentMessages (protocol.ts:126-166) into mt_op_batch runs, straight
+ * into typed-array columns. */
+class BatchBuilder {
+    constructor(props, names) {
+        this.props = props; this.names = names;
+        this.cols = {}; for (const [n, T] of COLS) this.cols[n] = new Col(T);
+        this.payload = new Col(Uint16Array, 4096); this.docIds = []; this.offsets = [0]; this.rel = [];
+    }
+    get nOps() { return this.cols.type.n; }
+    /** op.pos{k}, or op.relativePos{k} as an index into rel (getValidOpRange, client.ts:506-523). */
+    pos(op, k) {
+        const v = op["pos" + k];
+        if (v !== undefined) return [v, 0];
+        const rp = op["relativePos" + k];
+        if (!rp) return [undefined, 0];
+        const idx = rp.id ? this.names.markerLookup(rp.id) : -1;
+        this.rel.push([idx, rp.before ? 1 : 0, rp.offset !== undefined ? rp.offset : 0, 0]);
+        return [this.rel.length - 1, k === 1 ? F_REL1 : F_REL2];
+    }
+    beginDoc(docId) { this.docIds.push(docId); this.offsets.push(this.offsets[this.offsets.length - 1]); }
+    push(type, flags, client, seq, refSeq, msn, pos1, pos2, payloadOff, payloadLen, propId) {
+        const c = this.cols;
+        c.type.push(type); c.flags.push(flags); c.client.push(client); c.seq.push(seq); c.refSeq.push(refSeq);
+        c.msn.push(msn); c.pos1.push(pos1 || 0); c.pos2.push(pos2 || 0); c.payloadOff.push(payloadOff);
+        c.payloadLen.push(payloadLen); c.propId.push(propId);
+        this.offsets[this.offsets.length - 1] += 1;
+    }
+    member(op, client, seq, ref, msn, last) {
+        let fl = last ? F_END : 0;
+        const bad = () => this.push(OP_UNSUPPORTED, fl, client, seq, ref, msn, 0, 0, 0, 0, -1);
+        if (op.type === OP_INSERT) {
+            const seg = op.seg;
+            if (!seg && op.register) {
+                // applyInsertOp's register branch (client.ts:425-444): a truthy range end copies
+                // [pos1, pos2) into the register, otherwise the register is pasted at pos1
+                const [pos1, rf] = this.pos(op, 1);
+                if (pos1 === undefined || typeof op.register !== "string" || rf ||
+                    (op.pos2 === undefined && op.relativePos2)) { bad(); return; }
+                const copy = op.pos2 !== undefined && op.pos2 !== 0;
+                this.push(copy ? OP_COPY : OP_PASTE, fl, client, seq, ref, msn, pos1, copy ? op.pos2 : 0,
+                    this.names.registerIndex(op.register), 0, -1);
+                return;
+            }
+            if (!seg) { this.push(OP_NOOP, fl, client, seq, ref, msn, 0, 0, 0, 0, -1); return; }   // `if (op.seg)` falsy
+            const [pos1, rf] = this.pos(op, 1);
+            if (pos1 === undefined) { bad(); return; }
+            fl |= rf;
+            let text = null, props, pos2 = 0;
+            if (typeof seg === "string") text = seg;
+            else if (seg.text !== undefined) { text = seg.text; props = seg.props; }
+            else if (seg.marker !== undefined) { props = seg.props; fl |= F_MARKER; pos2 = seg.marker.refType || 0; }
+            else throw new Error("Unrecognized IJSONSegment type");
+            let pid = -1;
+            if (props) {                                       // `if (props)` in TextSegment/Marker.make
+                if (typeof props !== "object") throw new Error("segment props must be an object");
+                pid = this.props.intern(props); fl |= F_SEG_PROPS;
+            }
+            let off = this.payload.n;
+            if (text !== null) for (let i = 0; i < text.length; i++) this.payload.push(text.charCodeAt(i));
+            if (text === null && pid >= 0 && props[MARKER_ID_KEY]) {           // Marker.getId
+                const m = this.names.markerDefine(props[MARKER_ID_KEY]);
+                if (m === null) { bad(); return; }
+                fl |= F_MARKER_ID; off = m;
+            }
+            this.push(OP_INSERT, fl, client, seq, ref, msn, pos1, pos2, off, text !== null ? text.length : 0, pid);
+        } else if (op.type === OP_REMOVE || op.type === OP_ANNOTATE) {
+            const [pos1, f1] = this.pos(op, 1), [pos2, f2] = this.pos(op, 2);
+            if (pos1 === undefined || pos2 === undefined) { bad(); return; }
+            let pid = -1;
+            if (op.type === OP_ANNOTATE) {
+                if (op.combiningOp) fl |= op.combiningOp.name === "rewrite" ? F_REWRITE : F_COMBINE;
+                if (op.props && typeof op.props === "object" && MARKER_ID_KEY in op.props) { bad(); return; }   // re-keyed marker ids
+                pid = this.props.intern(op.props);
+            }
+            if (op.type === OP_REMOVE && op.register) {     // cut: Client.copy, then markRangeRemoved (:347-350)
+                if (typeof op.register !== "string") { bad(); return; }
+                this.push(OP_CUT, fl | f1 | f2, client, seq, ref, msn, pos1, pos2, this.names.registerIndex(op.register), 0, -1);
+                return;
+            }
+            this.push(op.type, fl | f1 | f2, client, seq, ref, msn, pos1, pos2, 0, 0, pid);
+        } else {
+            this.push(OP_NOOP, fl, client, seq, ref, msn, 0, 0, 0, 0, -1);
+        }
+    }
+    /** One sequenced message (Client.applyMsg, client.ts:819-841); returns the batch op
+     * index of each merge-tree member (GROUP order; [] for none). */
+    addMessage(msg) {
+        // getOrAddShortClientId keys a RedBlackTree with localeCompare (client.ts:73, :658)
+        if (typeof msg.clientId !== "string") throw new Error("clientId must be a string on the batch path");
+        const client = this.names.index(msg.clientId);
+        const seq = msg.sequenceNumber, ref = msg.referenceSequenceNumber, msn = msg.minimumSequenceNumber;
+        if ((msg.type === undefined ? "op" : msg.type) !== "op") {
+            this.push(OP_NOOP, F_END, client, seq, ref, msn, 0, 0, 0, 0, -1);
+            return [];
+        }
+        const c = msg.contents;
+        // the common case without a GROUP: one member, no array building
+        if (c && typeof c === "object" && c.type !== OP_GROUP) {
+            if (c.type !== OP_INSERT && c.type !== OP_REMOVE && c.type !== OP_ANNOTATE) {
+                this.push(OP_NOOP, F_END, client, seq, ref, msn, 0, 0, 0, 0, -1);
+                return [];
+            }
+            const first = this.cols.type.n;
+            this.member(c, client, seq, ref, msn, true);
+            return [first];
+        }
+        const members = mergeTreeMembers(c);
+        if (!members.length) { this.push(OP_NOOP, F_END, client, seq, ref, msn, 0, 0, 0, 0, -1); return []; }
+        const first = this.cols.type.n;
+        members.forEach((m, i) => this.member(m, client, seq, ref, msn, i === members.length - 1));
+        return members.map((_, i) => first + i);
+    }
+    build() {
+        const b = { docIds: Uint32Array.from(this.docIds), opOffsets: Uint32Array.from(this.offsets),
+            payload: this.payload.n ? this.payload.view() : new Uint16Array(1),
+            rel: Int32Array.from(this.rel.flat()) };
+        for (const [n] of COLS) b[n] = this.cols[n].view();
+        return b;
+    }
+}
+
+
+module.exports = { OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_GROUP, OP_UNSUPPORTED, OP_CUT, OP_COPY, OP_PASTE,
+    F_END, F_MARKER, F_REWRITE, F_SEG_PROPS, F_COMBINE, F_REL1, F_REL2, F_MARKER_ID, MARKER_ID_KEY, arrayIndex,
+    matchClassKey, PropTable, ClientNames, mergeTreeMembers, COLS, Col, BatchBuilder };

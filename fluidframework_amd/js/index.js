@@ -26,11 +26,9 @@ const path = require("path");
 // MTGPU_NAPI: an alternate build of this addon (the tests' host-emulation build)
 const addon = require(process.env.MTGPU_NAPI || path.join(__dirname, "mtgpu.node"));
 
-const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_GROUP = 3, OP_UNSUPPORTED = 4;
-const OP_CUT = 5, OP_COPY = 6, OP_PASTE = 7;          // register ops (include/mtgpu.h)
-const F_END = 1, F_MARKER = 2, F_REWRITE = 4, F_SEG_PROPS = 8, F_COMBINE = 16, F_REL1 = 0x20, F_REL2 = 0x40,
-    F_MARKER_ID = 0x80;
-const MARKER_ID_KEY = "markerId";   // reservedMarkerIdKey, MT/mergeTree.ts:591
+const { OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_GROUP, OP_UNSUPPORTED, OP_CUT, OP_COPY, OP_PASTE,
+    F_END, F_MARKER, F_REWRITE, F_SEG_PROPS, F_COMBINE, F_REL1, F_REL2, F_MARKER_ID, MARKER_ID_KEY, arrayIndex,
+    matchClassKey, PropTable, ClientNames, mergeTreeMembers, BatchBuilder } = require("./builder.js");
 const STATUS = {
     0x01: "ASSERT_SEQ", 0x02: "ASSERT_MSN", 0x04: "INSERT_FAILED", 0x08: "UNSUPPORTED",
     0x10: "OOM_ROWS", 0x20: "OOM_BLOCKS", 0x40: "OOM_TEXT", 0x80: "OOM_PROPS",
@@ -38,221 +36,6 @@ const STATUS = {
 };
 function statusNames(st) {
     return Object.keys(STATUS).filter((b) => st & Number(b)).map((b) => STATUS[b]);
-}
-
-function arrayIndex(k) {
-    // canonical array index (OrdinaryOwnPropertyKeys orders these first)
-    if (!/^(0|[1-9][0-9]{0,9})$/.test(k)) return undefined;
-    const v = Number(k);
-    return v < 4294967295 ? v : undefined;
-}
-
-// matchProperties equivalence (MT/properties.ts:64-95): objects compare
-// order-insensitively and recursively, primitives with ===.
-function matchClassKey(v) {
-    if (v !== null && typeof v === "object") {
-        return "o{" + Object.keys(v).sort().map((k) => JSON.stringify(k) + ":" + matchClassKey(v[k])).join(",") + "}";
-    }
-    if (typeof v === "number") return "n" + String(v);
-    if (typeof v === "boolean") return "b" + String(v);
-    if (typeof v === "string") return "s" + JSON.stringify(v);
-    return "z";
-}
-
-class PropTable {
-    constructor() {
-        this.keyIds = new Map(); this.keys = [];
-        this.valueIds = new Map(); this.valueJson = []; this.valueFalsy = []; this.valueClass = [];
-        this.classIds = new Map();
-        this.setIds = new Map(); this.sets = [];
-    }
-    keyId(k) {
-        let i = this.keyIds.get(k);
-        if (i === undefined) { i = this.keys.length; this.keyIds.set(k, i); this.keys.push(k); }
-        return i;
-    }
-    valueId(v) {
-        if (v === null) return -1;                       // null deletes the key
-        const txt = JSON.stringify(v);
-        let i = this.valueIds.get(txt);
-        if (i === undefined) {
-            i = this.valueJson.length;
-            this.valueIds.set(txt, i);
-            this.valueJson.push(txt);
-            this.valueFalsy.push(v ? 0 : 1);
-            const ck = matchClassKey(v);
-            let c = this.classIds.get(ck);
-            if (c === undefined) { c = this.classIds.size; this.classIds.set(ck, c); }
-            this.valueClass.push(c);
-        }
-        return i;
-    }
-    intern(props) {
-        const pairs = Object.keys(props).map((k) => [this.keyId(k), this.valueId(props[k])]);
-        const sig = pairs.map((p) => p.join(":")).join(",");
-        let i = this.setIds.get(sig);
-        if (i === undefined) { i = this.sets.length; this.setIds.set(sig, i); this.sets.push(pairs); }
-        return i;
-    }
-    toNative() {
-        const setOff = new Uint32Array(this.sets.length + 1);
-        const key = [], value = [];
-        this.sets.forEach((s, i) => { setOff[i + 1] = setOff[i] + s.length; for (const [k, v] of s) { key.push(k); value.push(v); } });
-        return {
-            setOff, key: Uint16Array.from(key.length ? key : [0]), value: Int32Array.from(value.length ? value : [0]),
-            keyJson: this.keys.map((k) => JSON.stringify(k)),
-            keyIndex: Uint32Array.from(this.keys.length ? this.keys.map((k) => { const a = arrayIndex(k); return a === undefined ? 0xFFFFFFFF : a; }) : [0]),
-            valueJson: this.valueJson,
-            valueFalsy: Uint8Array.from(this.valueFalsy.length ? this.valueFalsy : [0]),
-            valueClass: Uint32Array.from(this.valueClass.length ? this.valueClass : [0]),
-        };
-    }
-}
-
-/** Per-document interning: long client ids (getOrAddShortClientId order, client.ts:658-682)
- * and marker ids -> the document's idToSegment table on the device (mergeTree.ts:1095). */
-class ClientNames {
-    constructor() { this.ids = new Map(); this.names = []; this.markerIds = new Map(); this.registerIds = new Map(); }
-    /** The document's index of a register name (RegisterCollection key, with the author). */
-    registerIndex(name) {
-        if (!this.registerIds.has(name)) this.registerIds.set(name, this.registerIds.size);
-        return this.registerIds.get(name);
-    }
-    index(longId) {
-        let i = this.ids.get(longId);
-        if (i === undefined) { i = this.names.length; this.ids.set(longId, i); this.names.push(longId); }
-        return i;
-    }
-    /** A marker carrying this id joins the document; null for a non-string or reused id. */
-    markerDefine(id) {
-        if (typeof id !== "string" || this.markerIds.has(id)) return null;
-        const i = this.markerIds.size;
-        this.markerIds.set(id, i);
-        return i;
-    }
-    /** getMarkerFromId: the table index, -1 when never mapped. */
-    markerLookup(id) { return typeof id === "string" && this.markerIds.has(id) ? this.markerIds.get(id) : -1; }
-}
-
-// applyRemoteOp's GROUP recursion (client.ts:804-812), flattened; members share the seq
-function mergeTreeMembers(contents) {
-    const flat = (op) => (op && typeof op === "object") ? (op.type === OP_GROUP ? (op.ops || []).flatMap(flat) : [op]) : [];
-    return flat(contents).filter((m) => m.type === OP_INSERT || m.type === OP_REMOVE || m.type === OP_ANNOTATE);
-}
-
-const COLS = [["type", Uint8Array], ["flags", Uint8Array], ["client", Uint16Array], ["seq", Int32Array],
-    ["refSeq", Int32Array], ["msn", Int32Array], ["pos1", Int32Array], ["pos2", Int32Array],
-    ["payloadOff", Uint32Array], ["payloadLen", Uint32Array], ["propId", Int32Array]];
-
-/** Packs ISequencedDocumentMessages (protocol.ts:126-166) into mt_op_batch runs. */
-class BatchBuilder {
-    constructor(props, names) {
-        this.props = props; this.names = names;
-        this.cols = {}; for (const [n] of COLS) this.cols[n] = [];
-        this.payload = []; this.docIds = []; this.offsets = [0]; this.rel = [];
-    }
-    /** op.pos{k}, or op.relativePos{k} as an index into rel (getValidOpRange, client.ts:506-523). */
-    pos(op, k) {
-        const v = op["pos" + k];
-        if (v !== undefined) return [v, 0];
-        const rp = op["relativePos" + k];
-        if (!rp) return [undefined, 0];
-        const idx = rp.id ? this.names.markerLookup(rp.id) : -1;
-        this.rel.push([idx, rp.before ? 1 : 0, rp.offset !== undefined ? rp.offset : 0, 0]);
-        return [this.rel.length - 1, k === 1 ? F_REL1 : F_REL2];
-    }
-    beginDoc(docId) { this.docIds.push(docId); this.offsets.push(this.offsets[this.offsets.length - 1]); }
-    emit(o) {
-        for (const [n] of COLS) this.cols[n].push(o[n] || 0);
-        this.offsets[this.offsets.length - 1] += 1;
-    }
-    member(op, client, seq, ref, msn, last) {
-        let fl = last ? F_END : 0;
-        const common = { client, seq, refSeq: ref, msn, propId: -1 };
-        if (op.type === OP_INSERT) {
-            const seg = op.seg;
-            if (!seg && op.register) {
-                // applyInsertOp's register branch (client.ts:425-444): a truthy range end copies
-                // [pos1, pos2) into the register, otherwise the register is pasted at pos1
-                const [pos1, rf] = this.pos(op, 1);
-                if (pos1 === undefined || typeof op.register !== "string" || rf ||
-                    (op.pos2 === undefined && op.relativePos2)) {
-                    this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return;
-                }
-                const copy = op.pos2 !== undefined && op.pos2 !== 0;
-                this.emit({ ...common, type: copy ? OP_COPY : OP_PASTE, flags: fl, pos1, pos2: copy ? op.pos2 : 0,
-                    payloadOff: this.names.registerIndex(op.register) });
-                return;
-            }
-            if (!seg) { this.emit({ ...common, type: OP_NOOP, flags: fl }); return; }   // `if (op.seg)` falsy: no tree change
-            const [pos1, rf] = this.pos(op, 1);
-            if (pos1 === undefined) { this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return; }
-            fl |= rf;
-            let text = null, props, pos2 = 0;
-            if (typeof seg === "string") text = seg;
-            else if (seg.text !== undefined) { text = seg.text; props = seg.props; }
-            else if (seg.marker !== undefined) { props = seg.props; fl |= F_MARKER; pos2 = seg.marker.refType || 0; }
-            else throw new Error("Unrecognized IJSONSegment type");
-            let pid = -1;
-            if (props) {                                       // `if (props)` in TextSegment/Marker.make
-                if (typeof props !== "object") throw new Error("segment props must be an object");
-                pid = this.props.intern(props); fl |= F_SEG_PROPS;
-            }
-            let off = this.payload.length;
-            if (text !== null) for (let i = 0; i < text.length; i++) this.payload.push(text.charCodeAt(i));
-            if (text === null && pid >= 0 && props[MARKER_ID_KEY]) {           // Marker.getId
-                const m = this.names.markerDefine(props[MARKER_ID_KEY]);
-                if (m === null) { this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return; }
-                fl |= F_MARKER_ID; off = m;
-            }
-            this.emit({ ...common, type: OP_INSERT, flags: fl, pos1, pos2, payloadOff: off,
-                payloadLen: text !== null ? text.length : 0, propId: pid });
-        } else if (op.type === OP_REMOVE || op.type === OP_ANNOTATE) {
-            const [pos1, f1] = this.pos(op, 1), [pos2, f2] = this.pos(op, 2);
-            if (pos1 === undefined || pos2 === undefined) { this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return; }
-            let pid = -1;
-            if (op.type === OP_ANNOTATE) {
-                if (op.combiningOp) fl |= op.combiningOp.name === "rewrite" ? F_REWRITE : F_COMBINE;
-                if (op.props && typeof op.props === "object" && MARKER_ID_KEY in op.props) {
-                    this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return;     // re-keyed marker ids
-                }
-                pid = this.props.intern(op.props);
-            }
-            if (op.type === OP_REMOVE && op.register) {     // cut: Client.copy, then markRangeRemoved (:347-350)
-                if (typeof op.register !== "string") { this.emit({ ...common, type: OP_UNSUPPORTED, flags: fl }); return; }
-                this.emit({ ...common, type: OP_CUT, flags: fl | f1 | f2, pos1, pos2,
-                    payloadOff: this.names.registerIndex(op.register) });
-                return;
-            }
-            this.emit({ ...common, type: op.type, flags: fl | f1 | f2, pos1, pos2, propId: pid });
-        } else {
-            this.emit({ ...common, type: OP_NOOP, flags: fl });
-        }
-    }
-    /** One sequenced message (Client.applyMsg, client.ts:819-841); returns the batch op
-     * index of each merge-tree member (GROUP order; [] for none). */
-    addMessage(msg) {
-        // getOrAddShortClientId keys a RedBlackTree with localeCompare (client.ts:73, :658)
-        if (typeof msg.clientId !== "string") throw new Error("clientId must be a string on the batch path");
-        const client = this.names.index(msg.clientId);
-        const seq = msg.sequenceNumber, ref = msg.referenceSequenceNumber, msn = msg.minimumSequenceNumber;
-        if ((msg.type === undefined ? "op" : msg.type) !== "op") {
-            this.emit({ type: OP_NOOP, flags: F_END, client, seq, refSeq: ref, msn, propId: -1 });
-            return [];
-        }
-        const members = mergeTreeMembers(msg.contents);
-        if (!members.length) { this.emit({ type: OP_NOOP, flags: F_END, client, seq, refSeq: ref, msn, propId: -1 }); return []; }
-        const first = this.cols.type.length;
-        members.forEach((m, i) => this.member(m, client, seq, ref, msn, i === members.length - 1));
-        return members.map((_, i) => first + i);
-    }
-    build() {
-        const b = { docIds: Uint32Array.from(this.docIds), opOffsets: Uint32Array.from(this.offsets),
-            payload: Uint16Array.from(this.payload.length ? this.payload : [0]),
-            rel: Int32Array.from(this.rel.flat()) };
-        for (const [n, T] of COLS) b[n] = T.from(this.cols[n]);
-        return b;
-    }
 }
 
 // ---- snapshot load: the JSON half of SnapshotLoader (MT/snapshotLoader.ts) ----

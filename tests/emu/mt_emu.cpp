@@ -12,7 +12,7 @@
 #include "../../fluidframework_amd/csrc/mt_shard.h"
 
 static int mtb_init(mt_ctx*) { return 0; }
-static void mtb_fini(mt_ctx*) {}
+static void mtb_fini(mt_ctx* c) { for (auto& st : c->stage) free(st.p); }
 static int mtb_malloc(void** p, size_t n) { *p = calloc(1, n ? n : 16); return *p ? 0 : 1; }
 static void mtb_free(void* p) { free(p); }
 static void mtb_memset(void* p, int v, size_t n) { memset(p, v, n); }
@@ -20,6 +20,12 @@ static void mtb_h2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n)
 static void mtb_d2h(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static void mtb_d2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static int mtb_sync(mt_ctx*) { return MT_OK; }
+static void* mtb_stage_get(mt_ctx* c, size_t n) {
+    mt_ctx::Stage& st = c->stage[c->stage_k];
+    if (st.cap < n) { free(st.p); st.p = malloc(n); st.cap = st.p ? n : 0; }
+    return st.p;
+}
+static void mtb_stage_send(mt_ctx* c, void* dev, size_t n) { memcpy(dev, c->stage[c->stage_k].p, n); c->stage_k ^= 1; }
 // FULL as on the device: the capture instantiation only while a delta buffer is armed.
 // The same per-run function as the device kernels (mt_replay_doc), one run at a time.
 template <bool FULL>

@@ -116,3 +116,37 @@ def test_node_host_load_on_emulation_matches_oracle():
 @pytest.mark.gpu
 def test_node_host_load_on_gpu_matches_oracle():
     check_load(os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"))
+
+
+def check_parallel_ingest(addon, n_docs, tmp_path, cfg="cfg3", workers=3):
+    """The Node ingest path (fluidframework_amd/js/ingest_bench.js): per-document JSON streams
+    parsed and packed by a worker_threads pool (parallel.js) equal the single-thread packing
+    column for column, and, applied through the addon, give every document the oracle's
+    SnapshotV1 digest (their xor)."""
+    props = ann_props()
+    p = gen_params(seed=43, n_docs=n_docs, **dict(CONFIGS[cfg], ops=400))
+    batch, st, kept = generate(p, props, keep=True)
+    assert st == [0] * n_docs
+    for d in range(n_docs):
+        with open(tmp_path / f"doc{d}.json", "w") as f:
+            json.dump(batch_to_messages(batch, props, d), f)
+    env = dict(os.environ, MTGPU_NAPI=addon)
+    r = subprocess.run([NODE, os.path.join(ROOT, "fluidframework_amd", "js", "ingest_bench.js"), str(tmp_path),
+                        str(workers), "--gpu"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["parallel_equals_single"] and out["msgs"] == int(batch.op_offsets[-1])
+    last = batch.op_offsets[1:] - 1
+    x = 0
+    for d in range(n_docs):
+        x ^= kept[d].snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]))[1]
+    assert out["digest_xor"] == f"{x:016x}"
+
+
+def test_parallel_ingest_on_emulation(tmp_path):
+    check_parallel_ingest(build_emu_napi(), 7, tmp_path)
+
+
+@pytest.mark.gpu
+def test_parallel_ingest_on_gpu(tmp_path):
+    check_parallel_ingest(os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"), 16, tmp_path, workers=8)
