@@ -391,6 +391,9 @@ def run_config5(args, c, world, rank, local):
     setup_s = time.time() - t0
     eng = sh.engine
     eng.set_residency(RESIDENCY[args.residency])
+    big = c.get("big_min_ops", 0) if args.big_min_ops < 0 else args.big_min_ops
+    if args.residency == "blk" and big:
+        eng.set_size_class(big)
     my_msgs = int(sh.ops.sum())
     for _ in range(args.warmup):
         sh.replay()
@@ -436,7 +439,7 @@ def run_config5(args, c, world, rank, local):
         "config": {"workload": f"config5: {c['desc']}", "docs_per_gpu": c["docs"], "docs_total": total_docs,
                    "msgs_total": total_msgs, "msgs_mean": total_msgs / total_docs,
                    "msgs_max": int(sh.all_ops.max()), "parallelism": f"doc-sharded x{world} (LPT)",
-                   "residency": args.residency},
+                   "residency": args.residency, "big_min_ops": big if args.residency == "blk" else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": REPLAY_KERNEL[args.residency] + " (rank 0)",
                      "kernel_ms": kern_s * 1e3, "bytes_per_launch": bytes_per_launch},
@@ -645,6 +648,9 @@ def _main(argv=None):
                          "for long documents; hbm: every pool in HBM; lds: rows/blocks/heap/window in LDS; "
                          "auto (default): big for config4, blk otherwise")
     ap.add_argument("--caps", default="", help="override pool caps, e.g. rows_per_doc=400,text_per_doc=16384")
+    ap.add_argument("--big-min-ops", type=int, default=-1,
+                    help="size classes under blk residency: runs of at least this many messages replay in the "
+                         "long-document kernel on a second stream (0: off; default: the config's)")
     args = ap.parse_args(argv)
     if args.residency == "auto":
         args.residency = "big" if args.config == "config4" else "blk"
@@ -691,6 +697,9 @@ def _main(argv=None):
         caps[k] = int(v)
     eng = Host.engine(c["docs"], local, **caps)
     eng.set_residency(RESIDENCY[args.residency])
+    big = c.get("big_min_ops", 0) if args.big_min_ops < 0 else args.big_min_ops
+    if args.residency == "blk" and big:
+        eng.set_size_class(big)
     eng.upload_props(ann_props())
     eng.upload_names(['"c%d"' % i for i in range(64)])
     seed = args.seed ^ (rank * 0x9E3779B1)
@@ -780,7 +789,7 @@ def _main(argv=None):
                    "clients": c["clients"], "lag_max": c["lag"], "mix_ins_rem_ann": [c["ins"], c["rem"],
                                                                                    100 - c["ins"] - c["rem"]],
                    "parallelism": f"doc-sharded x{world}", "residency": args.residency,
-                   "lds_handover_docs": handover},
+                   "big_min_ops": big if args.residency == "blk" else None, "lds_handover_docs": handover},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic[0] if traffic else None,

@@ -35,6 +35,25 @@ static int mtb_ensure(mt_ctx* c, mt_ctx::DevBuf& b, size_t bytes) {
     return MT_OK;
 }
 
+// The run lists of the size classes for the resident batch (host lists uploaded once per
+// batch): long runs (>= big_min_ops op records) in [0, n_long), the rest after them.
+static int mt_size_class_lists(mt_ctx* c) {
+    if (c->runs_gen == c->batch_gen && c->runs_min == c->big_min_ops) return MT_OK;
+    const uint32_t R = c->n_runs;
+    std::vector<uint32_t> lst; lst.reserve(R);
+    for (uint32_t r = 0; r < R && c->run_off.size() == R + 1; r++)
+        if (c->run_off[r + 1] - c->run_off[r] >= c->big_min_ops) lst.push_back(r);
+    c->n_long = (uint32_t)lst.size();
+    for (uint32_t r = 0; r < R && c->run_off.size() == R + 1; r++)
+        if (c->run_off[r + 1] - c->run_off[r] < c->big_min_ops) lst.push_back(r);
+    c->n_short = (uint32_t)lst.size() - c->n_long;
+    int rc;
+    if ((rc = mtb_ensure(c, c->b_runs, 4ull * lst.size() + 4))) return rc;
+    if (!lst.empty()) mtb_h2d(c, c->b_runs.p, lst.data(), 4ull * lst.size());
+    c->runs_gen = c->batch_gen; c->runs_min = c->big_min_ops;
+    return MT_OK;
+}
+
 extern "C" {
 
 const char* MT_FN(last_error)(mt_ctx* c) { return c ? c->err.c_str() : "null context"; }
@@ -161,7 +180,7 @@ void MT_FN(destroy)(mt_ctx* c) {
                             &c->b_dcount, &c->b_pset_off,
                             &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3,
                             &c->b_ld_meta, &c->b_ld_seg, &c->b_ld_pay, &c->b_ld_plan, &c->b_ld_poff, &c->b_dtext,
-                            &c->b_resume, &c->b_start, &c->b_batch};
+                            &c->b_resume, &c->b_start, &c->b_batch, &c->b_runs};
     for (auto* b : bs) if (b->p) mtb_free(b->p);
     mtb_fini(c);
     delete c;
@@ -243,7 +262,7 @@ static int mt_upload_ops(mt_ctx* c, const mt_op_batch* B) {
     o.payload = (uint16_t*)(d + o_pay); o.n_runs = B->n_runs; o.payload_units = B->payload_units;
     o.rel = (const MtRelPos*)(d + o_rel); o.n_rel = B->rel ? B->n_rel : 0;
     c->n_runs = B->n_runs;
-    c->run_off.assign(B->op_offsets, B->op_offsets + R + 1);
+    c->run_off.assign(B->op_offsets, B->op_offsets + R + 1); c->batch_gen++;
     c->batch_reg = reg;
     return MT_OK;
 }
@@ -497,6 +516,11 @@ int MT_FN(doc_pset)(mt_ctx* c, uint32_t doc, int32_t id, uint16_t* keys, int32_t
     mtb_d2h(c, &p, c->S.pset + y.pset + (size_t)id, sizeof(MtPSet));
     *n = p.n < 0 ? 0u : (uint32_t)p.n;
     for (uint32_t i = 0; i < *n && i < MT_PSK; i++) { keys[i] = p.key[i]; vals[i] = p.val[i]; }
+    return MT_OK;
+}
+int MT_FN(set_size_class)(mt_ctx* c, uint32_t big_min_ops) {
+    if (!c) return MT_E_INVALID;
+    c->big_min_ops = big_min_ops;
     return MT_OK;
 }
 int MT_FN(set_residency)(mt_ctx* c, int use_lds, int rows, int blocks, int heap) {
@@ -807,7 +831,7 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     c->n_runs = P->n_docs;
     c->batch_reg = false;                     // generated streams hold no register ops
     c->gen_off.assign(off.begin(), off.end());
-    c->run_off = c->gen_off;
+    c->run_off = c->gen_off; c->batch_gen++;
     if (!P->continue_docs) {
         rc = MT_FN(docs_open)(c, 0, P->n_docs);
         if (rc) return rc;
@@ -880,7 +904,7 @@ int MT_FN(upload_batch_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids,
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs; o.payload_units = payload_units;
     o.rel = nullptr; o.n_rel = 0;
     c->n_runs = n_runs;
-    c->run_off.assign(op_offsets, op_offsets + n_runs + 1);
+    c->run_off.assign(op_offsets, op_offsets + n_runs + 1); c->batch_gen++;
     c->batch_reg = false;                     // device-built streams (shard.py) hold no register ops
     c->gen.enabled = 0;
     return mtb_sync(c);
@@ -928,7 +952,7 @@ int MT_FN(upload_rows_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids, 
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs; o.payload_units = N * L;
     o.rel = nullptr; o.n_rel = 0;
     c->n_runs = n_runs;
-    c->run_off.assign(op_offsets, op_offsets + n_runs + 1);
+    c->run_off.assign(op_offsets, op_offsets + n_runs + 1); c->batch_gen++;
     c->batch_reg = false;                     // exchanged generated streams hold no register ops
     c->gen.enabled = 0;
     if (n_runs && (rc = mtb_launch_rows(c, false, 0, n_runs, (uint32_t)L, nullptr, (uint64_t*)rows_dev,

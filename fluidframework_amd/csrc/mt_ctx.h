@@ -28,6 +28,14 @@ struct mt_ctx {
     MtOps ops{};
     uint32_t n_runs = 0;
     std::vector<uint32_t> run_off;     // host copy of the resident batch's op offsets (n_runs + 1)
+    uint64_t batch_gen = 0;            // bumped whenever a batch becomes resident
+    // Size classes (mt_set_size_class): runs of at least big_min_ops op records replay in the
+    // long-document kernel on stream2, concurrently with the block-residency kernel for the
+    // rest; the run lists live in b_runs (long runs first), rebuilt per resident batch.
+    uint32_t big_min_ops = 0;
+    uint64_t runs_gen = ~0ull; uint32_t runs_min = 0, n_long = 0, n_short = 0;
+    DevBuf b_runs;
+    void* stream2 = nullptr; void* ev_fork = nullptr; void* ev_join = nullptr;
     // mt_apply_batch / mt_upload_batch staging: two pinned host slots used alternately, each
     // with the event of its last H2D, and one device region the batch lands in
     struct Stage { void* p = nullptr; size_t cap = 0; void* ev = nullptr; };

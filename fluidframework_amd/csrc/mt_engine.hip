@@ -76,6 +76,10 @@ static int mtb_init(mt_ctx* c) {
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { c->err = "hipStreamCreate failed"; return 1; }
     (void)hipEventCreate(&a); (void)hipEventCreate(&b);
     c->stream = s; c->ev0 = a; c->ev1 = b;
+    hipStream_t s2; hipEvent_t f, j;
+    if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess) { c->err = "hipStreamCreate failed"; return 1; }
+    (void)hipEventCreateWithFlags(&f, hipEventDisableTiming); (void)hipEventCreateWithFlags(&j, hipEventDisableTiming);
+    c->stream2 = s2; c->ev_fork = f; c->ev_join = j;
     return 0;
 }
 static void mtb_fini(mt_ctx* c) {
@@ -86,6 +90,9 @@ static void mtb_fini(mt_ctx* c) {
     }
     if (c->ev0) (void)hipEventDestroy((hipEvent_t)c->ev0);
     if (c->ev1) (void)hipEventDestroy((hipEvent_t)c->ev1);
+    if (c->stream2) { (void)hipStreamSynchronize((hipStream_t)c->stream2); (void)hipStreamDestroy((hipStream_t)c->stream2); }
+    if (c->ev_fork) (void)hipEventDestroy((hipEvent_t)c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy((hipEvent_t)c->ev_join);
 }
 static int mtb_malloc(void** p, size_t n) { return hipMalloc(p, n) == hipSuccess ? 0 : 1; }
 static void mtb_free(void* p) { (void)hipFree(p); }
@@ -132,18 +139,38 @@ static int mtb_check(mt_ctx* c) {
 }
 static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) {
     uint32_t* cur = (uint32_t*)c->b_cursor.p;
-    if (c->use_lds == 3) mtk_big(full, s, n_runs, c->S, c->ops, cur, c->lds_rows, c->lds_heap);
+    if (c->use_lds == 2 && c->big_min_ops && c->n_long) {
+        // size classes: long runs on stream2 in the long-document kernel, the rest here, joined
+        const uint32_t* runs = (const uint32_t*)c->b_runs.p;
+        hipStream_t s2 = (hipStream_t)c->stream2;
+        (void)hipEventRecord((hipEvent_t)c->ev_fork, s);
+        (void)hipStreamWaitEvent(s2, (hipEvent_t)c->ev_fork, 0);
+        mtk_big(full, s2, c->n_long, c->S, c->ops, runs, cur, MT_G_WIN, MT_G_HEAP);
+        if (c->n_short) {
+            if (full) mtk_blk_full(s, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);
+            else mtk_blk_fast(s, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);
+        }
+        (void)hipEventRecord((hipEvent_t)c->ev_join, s2);
+        (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_join, 0);
+        return;
+    }
+    if (c->use_lds == 3) mtk_big(full, s, n_runs, c->S, c->ops, nullptr, cur, c->lds_rows, c->lds_heap);
     else if (c->use_lds == 2) {
-        if (full) mtk_blk_full(s, n_runs, c->S, c->ops, cur, c->lds_blks, c->lds_heap);
-        else mtk_blk_fast(s, n_runs, c->S, c->ops, cur, c->lds_blks, c->lds_heap);
+        if (full) mtk_blk_full(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);
+        else mtk_blk_fast(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);
     } else if (c->use_lds) {
         mtk_lds(full, s, n_runs, c->S, c->ops, cur, c->lds_rows, c->lds_blks, c->lds_heap);
         mtk_hbm(full, s, n_runs, c->S, c->ops, cur);
     } else mtk_hbm(full, s, n_runs, c->S, c->ops, nullptr);
 }
+static int mt_size_class_lists(mt_ctx* c);
 static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     if (n_runs == 0) return MT_OK;
     hipStream_t s = (hipStream_t)c->stream;
+    if (!g.enabled && c->use_lds == 2 && c->big_min_ops) {
+        int rc = mt_size_class_lists(c);
+        if (rc) return rc;
+    }
     (void)hipGetLastError();
     (void)hipEventRecord((hipEvent_t)c->ev0, s);
     if (g.enabled) mtk_generate(s, n_runs, c->S, c->ops, g);

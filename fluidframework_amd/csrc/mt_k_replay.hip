@@ -33,19 +33,23 @@ __global__ __launch_bounds__(64, MT_LDS_WAVES_PER_SIMD) void mt_replay_lds_kerne
 // Blocks + heap in LDS (~9.5 KB per workgroup, 4 waves per SIMD), rows/window in HBM; a
 // document that outgrows LDS continues in HBM in the same wave.
 template <bool FULL>
-__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(MtState S, MtOps ops, uint32_t* cursor, int lb, int lh) {
+__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(MtState S, MtOps ops, const uint32_t* runs,
+                                                                               uint32_t* cursor, int lb, int lh) {
     __shared__ MtScratch sc;
-    const uint32_t cur = mt_replay_doc<MT_RES_BLK, FULL>(S, ops, blockIdx.x, &sc, 0, lb, lh);
-    if (__lane_id() == 0) cursor[blockIdx.x] = cur;
+    const uint32_t run = runs ? runs[blockIdx.x] : blockIdx.x;          // size classes: a run list
+    const uint32_t cur = mt_replay_doc<MT_RES_BLK, FULL>(S, ops, run, &sc, 0, lb, lh);
+    if (__lane_id() == 0) cursor[run] = cur;
 }
 // Long documents (MT_RES_BIG): heap, window and U set in LDS (~68 KB, two workgroups per
 // CU), blocks and rows in HBM; one wave per SIMD at most, so the register budget is 256
 // VGPRs and nothing spills.  A document whose heap or height outgrows LDS continues in HBM.
 template <bool FULL>
-__global__ __launch_bounds__(64, 1) void mt_replay_big_kernel(MtState S, MtOps ops, uint32_t* cursor, int lw, int lh) {
+__global__ __launch_bounds__(64, 1) void mt_replay_big_kernel(MtState S, MtOps ops, const uint32_t* runs, uint32_t* cursor,
+                                                                int lw, int lh) {
     __shared__ MtScratch sc;
-    const uint32_t cur = mt_replay_doc<MT_RES_BIG, FULL>(S, ops, blockIdx.x, &sc, lw, 0, lh);
-    if (__lane_id() == 0) cursor[blockIdx.x] = cur;
+    const uint32_t run = runs ? runs[blockIdx.x] : blockIdx.x;
+    const uint32_t cur = mt_replay_doc<MT_RES_BIG, FULL>(S, ops, run, &sc, lw, 0, lh);
+    if (__lane_id() == 0) cursor[run] = cur;
 }
 // Every pool in HBM: whole runs, or the rest of each run after mt_replay_lds_kernel.
 template <bool FULL>
@@ -75,17 +79,20 @@ __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_generate_kernel(MtSt
 
 // ------------------------------------------------------------- launchers ----
 #if MT_KSET == 0
-void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lb, int lh) {
-    hipLaunchKernelGGL(mt_replay_blk_kernel<false>, dim3(n), dim3(64), 0, s, S, o, cur, lb, lh);
+void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
+                  int lh) {
+    hipLaunchKernelGGL(mt_replay_blk_kernel<false>, dim3(n), dim3(64), 0, s, S, o, runs, cur, lb, lh);
 }
 #elif MT_KSET == 1
-void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lb, int lh) {
-    hipLaunchKernelGGL(mt_replay_blk_kernel<true>, dim3(n), dim3(64), 0, s, S, o, cur, lb, lh);
+void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
+                  int lh) {
+    hipLaunchKernelGGL(mt_replay_blk_kernel<true>, dim3(n), dim3(64), 0, s, S, o, runs, cur, lb, lh);
 }
 #elif MT_KSET == 2
-void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lw, int lh) {
-    if (full) hipLaunchKernelGGL(mt_replay_big_kernel<true>, dim3(n), dim3(64), 0, s, S, o, cur, lw, lh);
-    else hipLaunchKernelGGL(mt_replay_big_kernel<false>, dim3(n), dim3(64), 0, s, S, o, cur, lw, lh);
+void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,
+             int lw, int lh) {
+    if (full) hipLaunchKernelGGL(mt_replay_big_kernel<true>, dim3(n), dim3(64), 0, s, S, o, runs, cur, lw, lh);
+    else hipLaunchKernelGGL(mt_replay_big_kernel<false>, dim3(n), dim3(64), 0, s, S, o, runs, cur, lw, lh);
 }
 #elif MT_KSET == 3
 void mtk_lds(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lr, int lb, int lh) {

@@ -3,9 +3,13 @@
 #include <hip/hip_runtime.h>
 #include "mt_core.h"
 
-void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lb, int lh);
-void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lb, int lh);
-void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lw, int lh);
+// runs: the run each workgroup replays (size classes), or null for run = blockIdx.x
+void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
+                  int lh);
+void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
+                  int lh);
+void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,
+             int lw, int lh);
 void mtk_lds(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lr, int lb, int lh);
 void mtk_hbm(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* cur);
 void mtk_generate(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const MtGen& g);

@@ -73,6 +73,7 @@ def _bind(lib, prefix: str):
         docs_open=f("docs_open", ctypes.c_int, [P, U32, U32]),
         doc_pools=f("doc_pools", ctypes.c_int, [P, U32, P, P]),
         set_residency=f("set_residency", ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+        set_size_class=f("set_size_class", ctypes.c_int, [P, U32]),
         set_props=f("set_props", ctypes.c_int, [P, ctypes.POINTER(MtPropTable)]),
         set_client_names=f("set_client_names", ctypes.c_int, [P, U32, P]),
         set_doc_client_names=f("set_doc_client_names", ctypes.c_int, [P, U32, U32, P]),
@@ -323,6 +324,11 @@ class Engine:
         """mt_set_residency: 0/False HBM pools, 1/True LDS-resident, 2 blocks+heap in LDS;
         optional (lowered) LDS pool caps."""
         self._check(self.fn["set_residency"](self.h, int(use_lds), rows, blocks, heap), "mt_set_residency")
+
+    def set_size_class(self, big_min_ops: int):
+        """mt_set_size_class: under block residency, runs of at least big_min_ops op records
+        replay in the long-document kernel on a second stream (0: off)."""
+        self._check(self.fn["set_size_class"](self.h, int(big_min_ops)), "mt_set_size_class")
 
     def checkpoint(self):
         """mt_checkpoint: device copy of every document's state."""

@@ -315,6 +315,11 @@ int  mt_replay_resident(mt_ctx* ctx);
  * rows/blocks/heap (0 = compiled maximum) may only lower the caps; tests use
  * small caps to force the hand-over. */
 int  mt_set_residency(mt_ctx* ctx, int use_lds, int rows, int blocks, int heap);
+/* Size classes under block residency (mt_set_residency 2): runs of at least big_min_ops op
+ * records replay in the long-document kernel (heap, window and U set in LDS, blocks and rows
+ * in HBM, one wave per SIMD) on a second stream, concurrently with the block-residency kernel
+ * for the other runs; 0 (the default) turns it off.  Results are identical either way. */
+int  mt_set_size_class(mt_ctx* ctx, uint32_t big_min_ops);
 /* Per run of the last LDS-resident replay: the op index where it handed over to
  * the HBM kernel (== the run's end when it finished in LDS).  Diagnostic. */
 int  mt_last_cursors(mt_ctx* ctx, uint32_t n_runs, uint32_t* out);

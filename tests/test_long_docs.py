@@ -94,3 +94,42 @@ def test_gpu_config4_downscaled_matches_oracle(lag, res):
     generated on top and replayed from the restored checkpoint."""
     check_deep_window(lambda n, **kw: Engine(n, device=0, **kw), 2, 20000, 4000, lag,
                       rows=40000, window=16384, text=1 << 18, psets=40000, residency=res)
+
+
+def check_size_classes(factory, counts, big_min_ops):
+    """mt_set_size_class: the longer runs of a batch go to the long-document kernel (LDS heap,
+    window and U set) while the rest stay under block residency; every document must still
+    match the oracle."""
+    props = ann_props()
+    n = len(counts)
+    p = gen_params(seed=77, n_docs=n, ops=8, clients=5, lag=48, ins=60, rem=30, ins_len=8, rem_len=8, ann_sets=24,
+                   rewrite=5)
+    batch, st, _ = generate(p, props, ops_per_doc=counts, clients_per_doc=[5] * n)
+    assert st == [0] * n
+    eng = factory(n, rows_per_doc=3 * max(counts) + 64, window_per_doc=8192, propsets_per_doc=2 * max(counts) + 64,
+                  text_per_doc=8 * max(counts) + 4096)
+    eng.upload_props(props)
+    eng.upload_names(NAMES)
+    eng.set_residency(2)
+    eng.set_size_class(big_min_ops)
+    eng.open_docs(0, n)
+    eng.apply(batch)
+    eng.sync()
+    assert (eng.status(range(n)) == 0).all()
+    last = batch.op_offsets[1:] - 1
+    neg = np.full(n, -1, np.int32)
+    dig = eng.snapshot_digests(range(n), neg, neg, threads=2)
+    for d, (od, ost) in enumerate(replay(batch, props, NAMES)):
+        assert ost == 0
+        assert eng.get_text([d])[0] == od.get_text(), d
+        assert np.array_equal(eng.dump(d), od.dump()), d
+        assert int(dig[d]) == od.snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]))[1], d
+
+
+def test_size_classes_match_oracle_on_emulation():
+    check_size_classes(emu_engine, [300, 2500, 80, 1200, 40, 3000], 1000)
+
+
+@pytest.mark.gpu
+def test_size_classes_match_oracle_on_gpu():
+    check_size_classes(lambda n, **kw: Engine(n, device=0, **kw), [300, 2500, 80, 1200, 40, 3000, 9000, 700] * 4, 1000)

@@ -9,9 +9,10 @@ from fluidframework_amd.batch import MtGenParams
 import bench
 flag = os.environ.get("MT_PROF_FLAG", "MT_PROFILE")
 lib = os.path.join(ROOT, "fluidframework_amd", f"libmtgpu_{flag.lower()}.so")
-if not os.path.exists(lib):
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared",
-                           f"-D{flag}", "-o", lib, os.path.join(ROOT, "fluidframework_amd", "csrc", "mt_engine.hip")])
+if not os.path.exists(lib):                       # build here (CPU) before shipping it to a GPU run
+    sys.path.insert(0, ROOT)
+    import __graft_entry__
+    __graft_entry__.build_engine(extra=[f"-D{flag}"], out=lib, force=True)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 pre = int(sys.argv[2]) if len(sys.argv) > 2 else 200000
 ops = int(sys.argv[3]) if len(sys.argv) > 3 else 20000

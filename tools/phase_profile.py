@@ -14,16 +14,17 @@ import bench
 
 flag = os.environ.get("MT_PROF_FLAG", "MT_PROFILE")
 lib = os.path.join(ROOT, "fluidframework_amd", f"libmtgpu_{flag.lower()}.so")
-if not os.path.exists(lib):
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared",
-                           f"-D{flag}", "-o", lib, os.path.join(ROOT, "fluidframework_amd", "csrc", "mt_engine.hip")])
+if not os.path.exists(lib):                       # build here (CPU) before shipping it to a GPU run
+    sys.path.insert(0, ROOT)
+    import __graft_entry__
+    __graft_entry__.build_engine(extra=[f"-D{flag}"], out=lib, force=True)
 cfg = sys.argv[1] if len(sys.argv) > 1 else "config2"
 docs = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 c = dict(bench.CONFIGS[cfg]); c["docs"] = docs
 if len(sys.argv) > 3: c["ops"] = int(sys.argv[3])
 res = sys.argv[4] if len(sys.argv) > 4 else "lds"
 eng = Engine(docs, lib_path=lib, **bench.caps_for(c))
-eng.set_residency({"hbm": 0, "lds": 1, "blk": 2}[res])
+eng.set_residency({"hbm": 0, "lds": 1, "blk": 2, "big": 3}[res])
 eng.upload_props(bench.ann_props()); eng.upload_names(['"c%d"' % i for i in range(64)])
 p = MtGenParams(7, docs, c["ops"], c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"], c["rem_len"], c["ann_sets"], c["rewrite"])
 eng.generate(p); eng.sync(); eng.generated_to_resident()
