@@ -232,7 +232,7 @@ def run_config4(args, c, world, rank, local):
     eng = Host.engine(n, local, rows_per_doc=rows, blocks_per_doc=rows // 2 + 64, heap_per_doc=rows,
                  window_per_doc=16384, text_per_doc=5 * pre + c["ins_len"] * ops + 4096,
                  propsets_per_doc=pre + ops + 64)
-    eng.set_residency(RESIDENCY[args.residency])
+    set_residency(eng, args)
     eng.upload_props(ann_props())
     eng.upload_names(['"c%d"' % i for i in range(64)])
     seed = args.seed ^ (rank * 0x9E3779B1)
@@ -390,7 +390,7 @@ def run_config5(args, c, world, rank, local):
     sh = build_sharded(dist, device, fac, total_docs, args.seed, MtGenParams, gen_kw, names=names)
     setup_s = time.time() - t0
     eng = sh.engine
-    eng.set_residency(RESIDENCY[args.residency])
+    set_residency(eng, args)
     big = c.get("big_min_ops", 0) if args.big_min_ops < 0 else args.big_min_ops
     if args.residency == "blk" and big:
         eng.set_size_class(big)
@@ -574,10 +574,15 @@ def ingest_leg(local, c, seed, sample_docs=64):
     py_s = time.perf_counter() - t0
     eng.open_docs(0, n)
     eng.sync()
-    t0 = time.perf_counter()
-    eng.upload(batch)
+    for _ in range(2):                                  # both pinned staging buffers allocated
+        eng.upload(batch)
     eng.sync()
-    h2d_s = time.perf_counter() - t0
+    reps = 4
+    t0 = time.perf_counter()
+    for _ in range(reps):                               # steady state: staging reused, no allocation
+        eng.upload(batch)
+    eng.sync()
+    h2d_s = (time.perf_counter() - t0) / reps
     h2d_bytes = int(batch.n_ops) * 32 + int(batch.payload.nbytes)
     node = None
     exe = shutil.which("node")
@@ -606,8 +611,9 @@ def ingest_leg(local, c, seed, sample_docs=64):
             "node": node,
             "h2d_msgs_per_s": msgs / h2d_s, "h2d_GBps": h2d_bytes / h2d_s / 1e9, "h2d_bytes": h2d_bytes,
             "note": "packers: JSON text per document -> mt_op_batch (Node: parse + pack, one thread, and a "
-                    "worker_threads pool reading its own documents' streams); H2D = mt_upload_batch (one pinned "
-                    "staging copy, one async copy) + sync; node e2e = parallel parse + pack, mt_apply_batch, sync, "
+                    "worker_threads pool reading its own documents' streams); H2D = mt_upload_batch (validation and "
+                    "record packing on up to 16 host threads into reused pinned staging, one async copy), mean of 4 "
+                    "back-to-back batches + sync; node e2e = parallel parse + pack, mt_apply_batch, sync, "
                     "SnapshotV1 digests of every document; the timed replay starts from resident streams"}
 
 
@@ -621,6 +627,13 @@ def finish_dist():
     if tdist.is_available() and tdist.is_initialized():
         tdist.barrier()
         tdist.destroy_process_group()
+
+
+def set_residency(eng, args):
+    if args.residency == "big" and args.big_flags:
+        eng.set_residency(RESIDENCY["big"], 0, args.big_flags, 0)  # blocks = MT_BIGF_* switches
+    else:
+        eng.set_residency(RESIDENCY[args.residency])
 
 
 def main(argv=None):
@@ -648,6 +661,9 @@ def _main(argv=None):
                          "for long documents; hbm: every pool in HBM; lds: rows/blocks/heap/window in LDS; "
                          "auto (default): big for config4, blk otherwise")
     ap.add_argument("--caps", default="", help="override pool caps, e.g. rows_per_doc=400,text_per_doc=16384")
+    ap.add_argument("--big-flags", type=int, default=0,
+                    help="big residency A/B switches (MT_BIGF_*): 1 block cache off, 2 zamboni prefetch off, "
+                         "4 corrections table off")
     ap.add_argument("--big-min-ops", type=int, default=-1,
                     help="size classes under blk residency: runs of at least this many messages replay in the "
                          "long-document kernel on a second stream (0: off; default: the config's)")
@@ -696,7 +712,7 @@ def _main(argv=None):
         k, v = kv.split("=")
         caps[k] = int(v)
     eng = Host.engine(c["docs"], local, **caps)
-    eng.set_residency(RESIDENCY[args.residency])
+    set_residency(eng, args)
     big = c.get("big_min_ops", 0) if args.big_min_ops < 0 else args.big_min_ops
     if args.residency == "blk" and big:
         eng.set_size_class(big)

@@ -54,6 +54,22 @@ static int mt_size_class_lists(mt_ctx* c) {
     return MT_OK;
 }
 
+// Host loops over a batch's ops run on up to 16 threads once a batch is large enough to pay
+// for them (ingest: validation and the SoA -> 32-byte record packing).
+template <class F> static void mt_par_for(size_t n, F f) {
+    unsigned T = std::thread::hardware_concurrency();
+    T = T < 1 ? 1 : (T > 16 ? 16 : T);
+    if (n < (size_t)1 << 16 || T == 1) { f((size_t)0, n, 0u); return; }
+    const size_t per = (n + T - 1) / T;
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < T; t++) {
+        const size_t a = per * t, b = a + per < n ? a + per : n;
+        if (a < b) pool.emplace_back(f, a, b, t);
+    }
+    f((size_t)0, per < n ? per : n, 0u);
+    for (auto& th : pool) th.join();
+}
+
 extern "C" {
 
 const char* MT_FN(last_error)(mt_ctx* c) { return c ? c->err.c_str() : "null context"; }
@@ -245,15 +261,25 @@ static int mt_upload_ops(mt_ctx* c, const mt_op_batch* B) {
     if (R) memcpy(h + o_doc, B->doc_ids, 4 * R);
     memcpy(h + o_off, B->op_offsets, 4 * (R + 1));
     MtOpRec* rec = (MtOpRec*)(h + o_rec);
+    uint8_t regT[16] = {0};
+    const size_t PU = (size_t)B->payload_units;
+    mt_par_for(N, [&](size_t i0, size_t i1, unsigned t) {
+        bool reg = false;
+        for (size_t i = i0; i < i1; i++) {
+            MtOpRec& o = rec[i];
+            o.type = B->type[i]; o.flags = B->flags[i]; o.client = B->client[i]; o.seq = B->seq[i]; o.ref_seq = B->ref_seq[i];
+            o.msn = B->msn[i]; o.pos1 = B->pos1[i]; o.pos2 = B->pos2[i]; o.payload_off = B->payload_off[i];
+            o.payload_len = (uint16_t)B->payload_len[i]; o.prop_id = (int16_t)B->prop_id[i];
+            reg |= B->type[i] >= MT_OP_CUT && B->type[i] <= MT_OP_PASTE;
+        }
+        // this thread's share of the payload (same split, in units)
+        const size_t p0 = N ? PU * i0 / N : 0, p1 = N ? PU * i1 / N : PU;
+        if (p1 > p0) memcpy(h + o_pay + 2 * p0, B->payload + p0, 2 * (p1 - p0));
+        regT[t] = reg;
+    });
+    if (!N && PU) memcpy(h + o_pay, B->payload, 2 * PU);
     bool reg = false;
-    for (size_t i = 0; i < N; i++) {
-        MtOpRec& o = rec[i];
-        o.type = B->type[i]; o.flags = B->flags[i]; o.client = B->client[i]; o.seq = B->seq[i]; o.ref_seq = B->ref_seq[i];
-        o.msn = B->msn[i]; o.pos1 = B->pos1[i]; o.pos2 = B->pos2[i]; o.payload_off = B->payload_off[i];
-        o.payload_len = (uint16_t)B->payload_len[i]; o.prop_id = (int16_t)B->prop_id[i];
-        reg |= B->type[i] >= MT_OP_CUT && B->type[i] <= MT_OP_PASTE;
-    }
-    if (B->payload_units) memcpy(h + o_pay, B->payload, 2 * (size_t)B->payload_units);
+    for (int t = 0; t < 16; t++) reg |= regT[t] != 0;
     if (B->rel && B->n_rel) memcpy(h + o_rel, B->rel, sizeof(MtRelPos) * (size_t)B->n_rel);
     mtb_stage_send(c, c->b_batch.p, total);
     uint8_t* d = (uint8_t*)c->b_batch.p;
@@ -275,16 +301,27 @@ static int mt_check_batch(mt_ctx* c, const mt_op_batch* B) {
         if (B->doc_ids[r] >= c->S.maxDocs) { c->err = "doc id out of range"; return MT_E_INVALID; }
         if (B->op_offsets[r] > B->op_offsets[r + 1]) { c->err = "op_offsets not monotone"; return MT_E_INVALID; }
     }
-    for (uint32_t i = 0; i < B->n_ops; i++) {
-        if (B->type[i] > MT_OP_PASTE) { c->err = "unknown op type"; return MT_E_INVALID; }
-        if (B->type[i] == MT_OP_INSERT && !(B->flags[i] & MT_OPF_MARKER) &&
-            (uint64_t)B->payload_off[i] + B->payload_len[i] > B->payload_units) { c->err = "payload out of range"; return MT_E_INVALID; }
-        if (B->prop_id[i] >= 0 && (uint32_t)B->prop_id[i] >= c->S.p_nsets) { c->err = "prop_id out of range (mt_set_props first)"; return MT_E_INVALID; }
-        if (B->prop_id[i] > 32767) { c->err = "more than 32767 property sets"; return MT_E_INVALID; }
-        if (B->payload_len[i] > 65535) { c->err = "insert longer than 65535 UTF-16 units"; return MT_E_INVALID; }
-        if (((B->flags[i] & MT_OPF_REL1) && (uint32_t)B->pos1[i] >= B->n_rel) ||
-            ((B->flags[i] & MT_OPF_REL2) && (uint32_t)B->pos2[i] >= B->n_rel)) { c->err = "relative position index out of range"; return MT_E_INVALID; }
-    }
+    // per op: the first violation's message (threads check disjoint ranges; the lowest op wins)
+    const char* errT[16] = {nullptr};
+    size_t errI[16];
+    const uint32_t nsets = c->S.p_nsets;
+    mt_par_for(B->n_ops, [&](size_t i0, size_t i1, unsigned t) {
+        for (size_t i = i0; i < i1; i++) {
+            const char* e = nullptr;
+            if (B->type[i] > MT_OP_PASTE) e = "unknown op type";
+            else if (B->type[i] == MT_OP_INSERT && !(B->flags[i] & MT_OPF_MARKER) &&
+                     (uint64_t)B->payload_off[i] + B->payload_len[i] > B->payload_units) e = "payload out of range";
+            else if (B->prop_id[i] >= 0 && (uint32_t)B->prop_id[i] >= nsets) e = "prop_id out of range (mt_set_props first)";
+            else if (B->prop_id[i] > 32767) e = "more than 32767 property sets";
+            else if (B->payload_len[i] > 65535) e = "insert longer than 65535 UTF-16 units";
+            else if (((B->flags[i] & MT_OPF_REL1) && (uint32_t)B->pos1[i] >= B->n_rel) ||
+                     ((B->flags[i] & MT_OPF_REL2) && (uint32_t)B->pos2[i] >= B->n_rel)) e = "relative position index out of range";
+            if (e) { errT[t] = e; errI[t] = i; return; }
+        }
+    });
+    const char* e = nullptr; size_t ei = 0;
+    for (int t = 0; t < 16; t++) if (errT[t] && (!e || errI[t] < ei)) { e = errT[t]; ei = errI[t]; }
+    if (e) { c->err = e; return MT_E_INVALID; }
     return MT_OK;
 }
 
@@ -527,11 +564,12 @@ int MT_FN(set_residency)(mt_ctx* c, int use_lds, int rows, int blocks, int heap)
     const int maxHeap = use_lds == 3 ? MT_G_HEAP : (use_lds == 2 ? MT_B_HEAP : MT_L_HEAP);
     if (!c || use_lds < 0 || use_lds > 3 || rows < 0 || blocks < 0 || heap < 0 ||
         rows > (use_lds == 3 ? MT_G_WIN : MT_L_ROWS) ||
-        blocks > (use_lds == 2 ? MT_B_BLKS : MT_L_BLKS) || heap > maxHeap)
+        blocks > (use_lds == 2 ? MT_B_BLKS : (use_lds == 3 ? 7 : MT_L_BLKS)) || heap > maxHeap)
         return MT_E_INVALID;
     c->use_lds = use_lds;
     c->lds_rows = rows ? rows : (use_lds == 3 ? MT_G_WIN : MT_L_ROWS);   // 3: window entries in LDS
-    c->lds_blks = blocks ? blocks : (use_lds == 2 ? MT_B_BLKS : MT_L_BLKS);
+    // 3: blocks = MT_BIGF_* switches (block cache, zamboni prefetch, corrections table off; A/B)
+    c->lds_blks = use_lds == 3 ? blocks : (blocks ? blocks : (use_lds == 2 ? MT_B_BLKS : MT_L_BLKS));
     c->lds_heap = heap ? heap : maxHeap;
     return MT_OK;
 }

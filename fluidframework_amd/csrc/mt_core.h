@@ -72,6 +72,38 @@
 #define MT_G_WIN 2048
 #endif
 #define MT_G_H 12                     // ancestor-chain levels kept per U entry (tree height < MT_G_H - 2)
+// Long-document residency also keeps an LDS block cache: MT_G_BC direct-mapped slots (slot =
+// block id mod MT_G_BC), write-back, filled by the descents with blocks of height >= MT_G_BCH.
+// A slot holding a higher block is not taken by a lower one, so the top of the tree stays
+// resident and the descents, ancestor chains and path updates reach HBM only near the leaves.
+#ifndef MT_G_BC
+#define MT_G_BC 512
+#endif
+#ifndef MT_G_BCH
+#define MT_G_BCH 1
+#endif
+#define MT_BC_EMPTY ((int)0x80000000)
+// ... and runs as a workgroup of MT_G_NW waves: wave 0 applies the ops; the others take
+// shares of computeU's window scan (MT_G_STG window entries staged in LDS per round) and of
+// its ancestor-chain walks (mwRun / mwShare; the host emulation runs every share in turn).
+#ifndef MT_G_NW
+#define MT_G_NW 4
+#endif
+#define MT_G_STG 1024
+enum { MT_MW_EXIT = 0, MT_MW_SCAN = 1, MT_MW_CHAIN = 2, MT_MW_PREFETCH = 3 };
+// Jobs alternate between two LDS slots, so wave 0 can post an asynchronous job (PREFETCH: no
+// completion barrier) and write the next one while helpers still read the last.
+// Runtime switches of the long-document residency (mt_set_residency(ctx, 3, rows, flags, heap)):
+enum { MT_BIGF_NO_BCACHE = 1, MT_BIGF_NO_PREFETCH = 2, MT_BIGF_NO_TABLE = 4 };
+// Per-block perspective corrections of the long-document residency: an LDS hash table
+// block id -> Σ delta of the U rows under the block, built bottom-up once per U set (each
+// distinct block's parent is loaded once), so a descent level looks its children up instead
+// of scanning U.  Up to MT_G_HTN distinct blocks (load <= 3/4); beyond that computeU falls
+// back to per-entry ancestor chains.
+#ifndef MT_G_HT
+#define MT_G_HT 4096
+#endif
+#define MT_G_HTN (MT_G_HT * 3 / 4)
 enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2, MT_RES_BIG = 3 };
 // Diagnostic builds keep per-document phase/event counters (prof[]) across binds;
 // product builds never load or store them (8 SGPR pairs fewer live in the replay loop).
@@ -309,6 +341,17 @@ struct __attribute__((aligned(16))) MtLdsBig {
     int uid[MT_G_U], udelta[MT_G_U];
     int uanc[MT_G_U * MT_G_H];        // block ids (-1 = none)
     uint16_t ulist[MT_G_U];           // a descent's U entries under the current block (walk)
+    MtBlk bc[MT_G_BC];                // block cache (write-back; HBM copies of cached blocks are stale)
+    int btag[MT_G_BC];                // block id held by each slot, MT_BC_EMPTY if none
+    // computeU's staged window entries (one round): row, delta, (parent + 1) | live << 30 | recycle << 31
+    int sid[MT_G_STG], sdel[MT_G_STG], spf[MT_G_STG];
+    int htk[MT_G_HT], htv[MT_G_HT];   // corrections table: block id (MT_BC_EMPTY: free), Σ delta
+    uint16_t hlist[MT_G_HT];          // occupied slots in insertion (level) order
+    struct Job {                      // a job wave 0 posts to the workgroup (mwRun / mwPost)
+        int op, r, c, r0, n, H, minSeq, heapN;
+        MtRow* R; int* win; MtBlk* blk; int* uanc; uint16_t* text;
+    } mw[2];
+    int posted;                       // jobs wave 0 has posted (the exit job goes to slot posted & 1)
 };
 
 // per-wave scratch (LDS on the device)
@@ -351,6 +394,7 @@ MT_INLINE bool vis_rc(int seq, uint32_t meta, int rseq, uint32_t rcl, unsigned l
 
 struct BlkH { int len, parent, n, height, scour; };
 struct ChildL { int len; bool tie; };
+struct LeafR { int len, seq, rseq, toff, props, tcap; uint32_t meta, rcl; unsigned long long ovl; };   // a leaf row's fields
 struct WinI { int id; int delta; int parent; bool live; bool recycle; };
 
 enum { MT_WALK_SPLIT = 0, MT_WALK_INSERT = 1 };
@@ -444,7 +488,32 @@ template <int RES, bool FULL = true> struct MtEngT {
     // pool accessors: LDS (MT_RES_LDS, MT_RES_BLK for blocks + heap) or HBM homes
     MT_HD MtRow& row(int s) const { if constexpr (LDS) return mt_lds().rows[s]; else return R[s]; }
     MT_HD MtBlk& bk(int b) const {
-        if constexpr (LDS) return mt_lds().blk[b]; else if constexpr (BLKL) return mt_ldsb().blk[b]; else return blk[b];
+        if constexpr (LDS) return mt_lds().blk[b]; else if constexpr (BLKL) return mt_ldsb().blk[b];
+        else if constexpr (BIG) {                       // block cache hit: the LDS copy is the current one
+            const int s = b & (MT_G_BC - 1);
+            return mt_ldsg().btag[s] == b ? mt_ldsg().bc[s] : blk[b];
+        } else return blk[b];
+    }
+    // MT_RES_BIG: install block B (its current record in lanes 0..15) in its cache slot, whose
+    // tag is tg, unless the slot holds a higher live block; the evicted block is written back.
+    MT_HD void bcInstall(int B, int tg, const LaneArr<int>& w, int hb) {
+        if constexpr (BIG) {
+            if (!bcOn || hb < MT_G_BCH || tg == B) return;
+            const int s = B & (MT_G_BC - 1);
+            MtLdsBig& G = mt_ldsg();
+            if (tg != MT_BC_EMPTY) {
+                if (uni(G.bc[s].n) >= 0 && uni(G.bc[s].height) > hb) return;
+                const auto old = wave_map(16, [&](int i) MT_LAM { return ((const int*)&G.bc[s])[i]; });
+                wave_for(16, [&](int i) MT_LAM { ((int*)&blk[tg])[i] = own(old, i); });
+            }
+            wave_for(16, [&](int i) MT_LAM { ((int*)&G.bc[s])[i] = own(w, i); });
+            wave_for(1, [&](int) MT_LAM { G.btag[s] = B; });
+            wave_sync();
+        } else { (void)B; (void)tg; (void)w; (void)hb; }
+    }
+    MT_HD int bcTag(int B) const {
+        if constexpr (BIG) return uni(mt_ldsg().btag[B & (MT_G_BC - 1)]);
+        else { (void)B; return 0; }
     }
     MT_HD MtHeapE& hp(int k) const {
         if constexpr (LDS) return mt_lds().heap[k]; else if constexpr (BLKL) return mt_ldsb().heap[k];
@@ -516,6 +585,9 @@ template <int RES, bool FULL = true> struct MtEngT {
     int heapTop;                        // hp(1).maxSeq cached (INT_MAX when empty)
     int& gcEpoch = mt_cold_v.epoch;     // bumped by every text compaction
     int lastL, lastIdx; bool lastSplit; // landing spot of the last walk; did it split a block
+    bool bcOn;                          // MT_RES_BIG: descents fill the LDS block cache
+    bool htOk; int hlistN;              // MT_RES_BIG: the corrections table is built for U; occupied slots
+    bool htOn, pfOn; int mwSeq;         // MT_RES_BIG: table / zamboni prefetch enabled; jobs posted so far
     int& nCol = mt_cold_v.ncol;         // rows gathered by rangeMap(MT_MAP_COLLECT) into sc->hold
     int landB;                          // leaf block the last insertAtPath linked its node under
     int rfN; int*& rfHbm = mt_cold_v.rfhbm;   // recycled-row stack: depth, HBM home between runs
@@ -559,7 +631,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         c_ops = c_msgs = c_ins = c_rows = c_depth = c_scour = 0;
         nU = 0; uValid = false; uRef = -1; uCli = -1;
         heapTop = heapN > 0 ? uni(heap[1].maxSeq) : 0x7FFFFFFF;     // HBM home: bind precedes toLds
-        lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0;
+        lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0; bcOn = false; htOk = false; hlistN = 0; htOn = pfOn = false; mwSeq = 0;
         rfHbm = st.hold + (size_t)d * MT_RFL; rfN = uni(h.rfN); blkFreeN = uni(h.blkFreeN);
         heapHW = uni(h.heapHW); winHW = uni(h.winHW); ovxN = uni(h.ovxN);
         if (ovxN < 0 || ovxN > MT_OVX_CAP) ovxN = 0;
@@ -652,6 +724,13 @@ template <int RES, bool FULL = true> struct MtEngT {
             MtLdsBig& G = mt_ldsg();
             copyI((int*)G.heap, (const int*)heap, 2 * (heapN + 1));
             copyI(G.win, win, winN < lr ? winN : lr);
+            for (int base = 0; base < MT_G_BC; base += MT_WAVE) wave_for(MT_WAVE, [&](int k) MT_LAM { G.btag[base + k] = MT_BC_EMPTY; });
+            for (int base = 0; base < MT_G_HT; base += MT_WAVE)
+                wave_for(MT_WAVE, [&](int k) MT_LAM { G.htk[base + k] = MT_BC_EMPTY; G.htv[base + k] = 0; });
+            htOk = false; hlistN = 0;
+            bcOn = !(lb & MT_BIGF_NO_BCACHE);                   // lb: MT_BIGF_* switches (A/B)
+            pfOn = MT_G_NW > 1 && !(lb & MT_BIGF_NO_PREFETCH);
+            htOn = !(lb & MT_BIGF_NO_TABLE);
             wave_sync();
             gRowCap = S.rowCap; gBlkCap = blkCap; gHeapCap = S.heapCap; gWinCap = S.winCap;
             S.heapCap = gHeapCap < (uint32_t)lh ? gHeapCap : (uint32_t)lh;
@@ -695,6 +774,20 @@ template <int RES, bool FULL = true> struct MtEngT {
             MtLdsBig& G = mt_ldsg();
             copyI((int*)heap, (const int*)G.heap, 2 * (heapN + 1));
             copyI(win, G.win, winN < lRows ? winN : lRows);
+            // write the cached blocks back (lane k: slot base + k, four 16-byte quads)
+            for (int base = 0; base < MT_G_BC; base += MT_WAVE) {
+                wave_for(MT_WAVE, [&](int k) MT_LAM {
+                    const int t = G.btag[base + k];
+                    if (t != MT_BC_EMPTY) {
+                        const MtQ16* src = (const MtQ16*)&G.bc[base + k];
+                        MtQ16* dst = (MtQ16*)&blk[t];
+                        const MtQ16 a = src[0], b = src[1], c2 = src[2], d = src[3];
+                        dst[0] = a; dst[1] = b; dst[2] = c2; dst[3] = d;
+                    }
+                    G.btag[base + k] = MT_BC_EMPTY;
+                });
+            }
+            bcOn = false; htOk = false; pfOn = false;
             wave_sync();
             S.heapCap = gHeapCap;
             nU = 0; uValid = false;
@@ -788,9 +881,16 @@ template <int RES, bool FULL = true> struct MtEngT {
     MT_HD LaneArr<int> kids(int B, int n) const { return wave_map(n, [&](int j) MT_LAM { return bk(B).c[j]; }); }
     // Whole 64-byte block record in one transaction: lane i loads dword i;
     // children stay in lanes 0..n-1, scalar fields are broadcast to SGPRs.
-    MT_HD LaneArr<int> blkLoad(int B, BlkH& h) const {
-        auto w = wave_map(16, [&](int i) MT_LAM { return ((const int*)&bk(B))[i]; });
+    MT_HD LaneArr<int> blkLoad(int B, BlkH& h) {
+        LaneArr<int> w;
+        int tg = 0;
+        if constexpr (BIG) {                              // explicit LDS / HBM load, then fill
+            tg = bcTag(B);
+            if (tg == B) w = wave_map(16, [&](int i) MT_LAM { return ((const int*)&mt_ldsg().bc[B & (MT_G_BC - 1)])[i]; });
+            else w = wave_map(16, [&](int i) MT_LAM { return ((const int*)&blk[B])[i]; });
+        } else w = wave_map(16, [&](int i) MT_LAM { return ((const int*)&bk(B))[i]; });
         h.len = wave_at(w, 8); h.parent = wave_at(w, 9); h.n = wave_at(w, 10); h.height = wave_at(w, 11); h.scour = wave_at(w, 12);
+        if constexpr (BIG) bcInstall(B, tg, w, h.height);
         const int n = h.n;
         return wave_map(8, [&](int j) MT_LAM { return j < n ? own(w, j) : -1; });
     }
@@ -810,10 +910,12 @@ template <int RES, bool FULL = true> struct MtEngT {
         return wave_map(8, [&](int j) MT_LAM { return j < 4 ? own(a, j) : own(b, j); });
     }
     // child j's record as blkLoad returns it (j uniform)
-    MT_HD static LaneArr<int> kidRec(const LaneArr<int>& r0, const LaneArr<int>& r1, int j, BlkH& h) {
+    // (MT_RES_BIG: the child, block id b, is installed in the block cache.)
+    MT_HD LaneArr<int> kidRec(const LaneArr<int>& r0, const LaneArr<int>& r1, int j, BlkH& h, int b) {
         const int o = (j & 3) << 4;
         const auto w = wave_shfl(j < 4 ? r0 : r1, [o](int t) MT_LAM { return o + (t & 15); });
         h.len = wave_at(w, 8); h.parent = wave_at(w, 9); h.n = wave_at(w, 10); h.height = wave_at(w, 11); h.scour = wave_at(w, 12);
+        if constexpr (BIG) { if (bcOn && h.height >= MT_G_BCH) bcInstall(b, bcTag(b), w, h.height); } else (void)b;
         const int n = h.n;
         return wave_map(8, [&](int i) MT_LAM { return i < n ? own(w, i) : -1; });
     }
@@ -830,9 +932,300 @@ template <int RES, bool FULL = true> struct MtEngT {
     }
 
     /* ------------------------------------- perspective window (U set) -- */
+    // One window entry (row s) under perspective (r, c): still live in the window, recyclable,
+    // and its U delta (perspective length - observer length).
+    MT_HD WinI winEntry(int s, int r, int c) const {
+        WinI w; w.id = s;
+        const uint32_t mt = row(s).meta;
+        const bool removed = (mt & MT_M_REMOVED) != 0;
+        const int sq = row(s).seq, rs = row(s).rseq;
+        w.parent = row(s).parent;
+        const bool linked = w.parent >= 0;
+        w.live = linked && (sq > minSeq || (removed && rs > minSeq));
+        w.recycle = !linked && !(mt & MT_M_HREF);
+        const bool vr = vis_rc(sq, mt, rs, row(s).rcl, row(s).ovl, r, c, ovx, ovxN, s);
+        const bool vo = !removed;
+        w.delta = w.live ? ((vr ? row(s).len : 0) - (vo ? row(s).len : 0)) : 0;
+        return w;
+    }
+    // One 64-entry chunk of the window scan, in order: compaction of live entries (prune),
+    // recycled rows onto the stack, U entries with their level-0 ancestor (the leaf block).
+    MT_HD void placeChunk(const LaneArr<WinI>& wi, int base, int m, bool prune, int& newWin) {
+        auto live = wave_map(m, [&](int k) MT_LAM { return own(wi, k).live; });
+        if (prune) {
+            auto rk = wave_rank(live);
+            const int cntLive = wave_count(live);
+            auto rc = wave_map(m, [&](int k) MT_LAM { return own(wi, k).recycle; });
+            auto rkr = wave_rank(rc);
+            const int cntR = wave_count(rc), f0 = rfN;
+            const int nw0 = newWin;
+            wave_for(m, [&](int k) MT_LAM {
+                const WinI w = own(wi, k);
+                if (w.live) { if (nw0 + own(rk, k) != base + k) wn(nw0 + own(rk, k)) = w.id; }
+                else row(w.id).meta = row(w.id).meta & ~MT_M_INWIN;
+                if (w.recycle && f0 + own(rkr, k) < MT_RFL) sc->rfree[f0 + own(rkr, k)] = w.id;
+            });
+            rfN = (f0 + cntR) < MT_RFL ? (f0 + cntR) : MT_RFL;
+            newWin += cntLive;
+        }
+        auto du = wave_map(m, [&](int k) MT_LAM { return own(wi, k).delta != 0; });
+        auto rk2 = wave_rank(du);
+        const int cntU = wave_count(du);
+        const int nu0 = nU;
+        wave_for(m, [&](int k) MT_LAM {
+            if (!own(du, k)) return;
+            const int pos = nu0 + own(rk2, k);
+            const WinI w = own(wi, k);
+            if (pos < UCAP) { uPutAt<true>(pos, w.id, w.delta); ancPutAt<true>(pos, 0, w.parent); }
+            else { uPutAt<false>(pos, w.id, w.delta); ancPutAt<false>(pos, 0, w.parent); }
+        });
+        nU += cntU;
+    }
+    // Ancestor chains (levels 1..H) of U entries [g0, g0 + 512) from their level-0 entries,
+    // blocks in HBM (or the MT_RES_BIG block cache): the parent loads of one level are
+    // independent, so a level costs one round trip for 512 entries.
+    MT_HD void chainGroup(int g0, int nu, int H) {
+        wave_for(MT_WAVE, [&](int k) MT_LAM {
+            int a[8]; int pos[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                pos[q] = g0 + q * MT_WAVE + k;
+                a[q] = pos[q] < nu ? ancGetAny(pos[q], 0) : -1;
+            }
+            for (int h = 1; h <= H; h++) {
+#pragma unroll
+                for (int q = 0; q < 8; q++) a[q] = a[q] >= 0 ? bk(a[q]).parent : -1;
+#pragma unroll
+                for (int q = 0; q < 8; q++) if (pos[q] < nu) ancPutAny(pos[q], h, a[q]);
+            }
+        });
+    }
+    // Multi-wave long-document residency: wave 0 posts a job to the workgroup; every wave
+    // (helpers in mt_replay_big_kernel's loop) takes its share between two barriers (mwRun),
+    // or the helpers alone run it while wave 0 goes on (mwPost: no completion barrier).
+    MT_HD void mwPut(int op, int r, int c, int r0, int n) {
+        auto& J = mt_ldsg().mw[mwSeq & 1];
+        wave_for(1, [&](int) MT_LAM {
+            J.op = op; J.r = r; J.c = c; J.r0 = r0; J.n = n; J.H = height; J.minSeq = minSeq; J.heapN = heapN;
+            J.R = R; J.win = win; J.blk = blk; J.uanc = uanc; J.text = text;
+        });
+        mwSeq++;
+        wave_for(1, [&](int) MT_LAM { mt_ldsg().posted = mwSeq; });
+    }
+    MT_HD void mwRun(int op, int r, int c, int r0, int n) {
+        if constexpr (BIG) {
+            mwPut(op, r, c, r0, n);
+#if defined(__HIP_DEVICE_COMPILE__)
+            __syncthreads();
+            mwShare(0, mwSeq - 1);
+            __syncthreads();
+#else
+            for (int w = 0; w < MT_G_NW; w++) mwShare(w, mwSeq - 1);   // host emulation: every share in turn
+#endif
+        } else { (void)op; (void)r; (void)c; (void)r0; (void)n; }
+    }
+    MT_HD void mwPost(int op) {
+        if constexpr (BIG) {
+            mwPut(op, 0, 0, 0, 0);
+#if defined(__HIP_DEVICE_COMPILE__)
+            __syncthreads();
+#else
+            for (int w = 1; w < MT_G_NW; w++) mwShare(w, mwSeq - 1);
+#endif
+        } else (void)op;
+    }
+    MT_HD static bool mwSync(int op) { return op != MT_MW_PREFETCH; }
+    // This wave's share (wave index wv) of job number k; helpers first adopt the document's
+    // pool homes and window state from it.
+    MT_HD void mwShare(int wv, int k) {
+        if constexpr (BIG) {
+            MtLdsBig& G = mt_ldsg();
+            const auto& J = G.mw[k & 1];
+            const int op = uni(J.op);
+            if (wv != 0) {
+                R = J.R; win = J.win; blk = J.blk; uanc = J.uanc; text = J.text;
+                minSeq = uni(J.minSeq);
+            }
+            if (op == MT_MW_SCAN) {
+                const int r = uni(J.r), c = uni(J.c), r0 = uni(J.r0), n = uni(J.n);
+                // chunks wv, wv + NW, ... of the round, two per step (both chunks' loads in flight)
+                for (int q = wv * MT_WAVE; q < n; q += 2 * MT_G_NW * MT_WAVE) {
+                    const int q2 = q + MT_G_NW * MT_WAVE;
+                    const int m = (n - q) < MT_WAVE ? (n - q) : MT_WAVE;
+                    const int m2 = q2 < n ? ((n - q2) < MT_WAVE ? (n - q2) : MT_WAVE) : 0;
+                    const auto id1 = wave_map(m, [&](int k) MT_LAM { return wn(r0 + q + k); });
+                    const auto id2 = wave_map(m2, [&](int k) MT_LAM { return wn(r0 + q2 + k); });
+                    const auto w1 = wave_map(m, [&](int k) MT_LAM { return winEntry(own(id1, k), r, c); });
+                    const auto w2 = wave_map(m2, [&](int k) MT_LAM { return winEntry(own(id2, k), r, c); });
+                    auto put = [&](const LaneArr<WinI>& w, int qq, int mm) MT_LAM {
+                        wave_for(mm, [&](int k) MT_LAM {
+                            const WinI e = own(w, k);
+                            G.sid[qq + k] = e.id; G.sdel[qq + k] = e.delta;
+                            G.spf[qq + k] = (e.parent + 1) | (e.live ? 1 << 30 : 0) | (e.recycle ? (int)0x80000000 : 0);
+                        });
+                    };
+                    put(w1, q, m);
+                    put(w2, q2, m2);
+                }
+            } else if (op == MT_MW_CHAIN) {
+                const int nu = uni(J.n), H = uni(J.H);
+                for (int g0 = wv * 8 * MT_WAVE; g0 < nu; g0 += MT_G_NW * 8 * MT_WAVE) chainGroup(g0, nu, H);
+            } else if (op == MT_MW_PREFETCH && wv == 1) {
+                // zamboni's next pops come from the top of the heap: touch entries 1..7's rows,
+                // their leaf blocks, the blocks' rows and those rows' last text unit, so wave 0's
+                // scour finds them in cache (values are discarded; nothing is written)
+                // (wave 0 writes these pools meanwhile: every index read is bounds-checked)
+                const int hn = uni(J.heapN);
+                const unsigned rc = S.rowCap, bc = gBlkCap, tc = S.textCap;
+                wave_for(56, [&](int t) MT_LAM {
+                    const int e = 1 + (t >> 3);
+                    if (e > hn || e > (int)MT_G_HEAP) return;
+                    const int sg = hp(e).seg;
+                    if ((unsigned)sg >= rc) return;
+                    const int p = row(sg).parent;
+                    if ((unsigned)p >= bc) return;
+                    const int cnt = bk(p).n, j = t & 7;
+                    if (j >= cnt) return;
+                    const int ch = bk(p).c[j];
+                    if ((unsigned)ch >= rc) return;
+                    const int tf = row(ch).toff, ln = row(ch).len;
+                    const uint32_t mt = row(ch).meta;
+                    int v = row(ch).seq ^ row(ch).rseq ^ row(ch).props ^ row(ch).tcap ^ (int)mt;
+                    const int ix = tf + ln - 1;
+                    if (!(mt & MT_M_MARKER) && ix >= 0 && (unsigned)ix < tc) v ^= (int)text[ix];
+                    mt_keep(v);
+                });
+            }
+            wave_sync();
+        } else { (void)wv; (void)k; }
+    }
+    // Posted after each op's U set: the zamboni prefetch runs beside the op's descents.
+    MT_HD void mwPrefetch() {
+        if constexpr (BIG) { if (pfOn && heapN > 0 && heapTop <= minSeq + 1024) mwPost(MT_MW_PREFETCH); }
+    }
+    // computeU of the long-document residency: the window scan in rounds of MT_G_STG entries
+    // (all waves stage the entries' rows, wave 0 places them in order), then the chains.
+    MT_HD void computeUmw(int r, int c, bool prune) {
+        MtLdsBig& G = mt_ldsg();
+        int newWin = 0; nU = 0;
+        const int wN0 = winN;
+        for (int r0 = 0; r0 < wN0; r0 += MT_G_STG) {
+            const int n = (wN0 - r0) < MT_G_STG ? (wN0 - r0) : MT_G_STG;
+            mwRun(MT_MW_SCAN, r, c, r0, n);
+            for (int q = 0; q < n; q += MT_WAVE) {
+                const int m = (n - q) < MT_WAVE ? (n - q) : MT_WAVE;
+                const auto wi = wave_map(m, [&](int k) MT_LAM {
+                    WinI w; w.id = G.sid[q + k]; w.delta = G.sdel[q + k];
+                    const int pf = G.spf[q + k];
+                    w.parent = (pf & 0x3FFFFFFF) - 1; w.live = ((pf >> 30) & 1) != 0; w.recycle = pf < 0;
+                    return w;
+                });
+                placeChunk(wi, r0 + q, m, prune, newWin);
+            }
+        }
+        wave_sync();
+        htOk = false;
+        if (nU > 0 && height > 0 && !(htOn && htBuild())) mwRun(MT_MW_CHAIN, r, c, 0, nU);
+        if (prune) winN = newWin;
+        wave_sync();
+        uValid = true; uRef = r; uCli = c;
+    }
+    MT_HD static unsigned htHash(int b) { return ((unsigned)b * 2654435761u) >> (32 - __builtin_ctz(MT_G_HT)); }
+    // Lane-parallel insert: adds val to key's slot (claiming a free one); returns the slot and
+    // whether this lane claimed it.
+    MT_HD int htAdd(int key, int val, bool& won) {
+        MtLdsBig& G = mt_ldsg();
+        int sl = (int)htHash(key);
+        won = false;
+        for (;;) {
+            const int old = lds_cas(&G.htk[sl], MT_BC_EMPTY, key);
+            if (old == MT_BC_EMPTY) { won = true; break; }
+            if (old == key) break;
+            sl = (sl + 1) & (MT_G_HT - 1);
+        }
+        lds_add(&G.htv[sl], val);
+        return sl;
+    }
+    MT_HD int htGet(int key) const {
+        const MtLdsBig& G = mt_ldsg();
+        int sl = (int)htHash(key);
+        for (;;) {
+            const int k = G.htk[sl];
+            if (k == key) return G.htv[sl];
+            if (k == MT_BC_EMPTY) return 0;
+            sl = (sl + 1) & (MT_G_HT - 1);
+        }
+    }
+    // Appends the slots lanes claimed to hlist (in lane order).
+    MT_HD void htList(const LaneArr<int>& sl, const LaneArr<bool>& won, int m) {
+        const auto rk = wave_rank(won);
+        const int cnt = wave_count(won), h0 = hlistN;
+        wave_for(m, [&](int k) MT_LAM { if (own(won, k)) mt_ldsg().hlist[h0 + own(rk, k)] = (uint16_t)own(sl, k); });
+        hlistN += cnt;
+    }
+    // The corrections table for the current U set, bottom-up: leaf blocks get their U rows'
+    // deltas, then every distinct block of one height passes its sum to its parent (root
+    // excluded: no descent asks for it).  False if it would outgrow MT_G_HTN (table left
+    // empty, htOk false: the caller computes ancestor chains instead).
+    MT_HD bool htBuild() {
+        MtLdsBig& G = mt_ldsg();
+        for (int base = 0; base < hlistN; base += MT_WAVE) {               // the last U set's slots
+            const int m = (hlistN - base) < MT_WAVE ? (hlistN - base) : MT_WAVE;
+            wave_for(m, [&](int k) MT_LAM { const int sl = G.hlist[base + k]; G.htk[sl] = MT_BC_EMPTY; G.htv[sl] = 0; });
+        }
+        hlistN = 0;
+        wave_sync();
+        if (nU > MT_G_HTN) return false;
+        forU([&](auto inL, int base, int m) MT_LAM {
+            constexpr bool L = decltype(inL)::value;
+            const auto a = wave_map(m, [&](int k) MT_LAM {
+                bool w; const int x = htAdd(ancGetAt<L>(base + k, 0), udAt<L>(base + k), w); return w ? x : ~x;
+            });
+            htList(wave_map(m, [&](int k) MT_LAM { return own(a, k) >= 0 ? own(a, k) : ~own(a, k); }),
+                   wave_map(m, [&](int k) MT_LAM { return own(a, k) >= 0; }), m);
+        });
+        wave_sync();
+        int l0 = 0, l1 = hlistN;
+        const int rt = root;
+        for (int h = 1; h < height; h++) {                                  // blocks of height h
+            if (hlistN + (l1 - l0) > MT_G_HTN) {
+                for (int base = 0; base < hlistN; base += MT_WAVE) {
+                    const int m = (hlistN - base) < MT_WAVE ? (hlistN - base) : MT_WAVE;
+                    wave_for(m, [&](int k) MT_LAM { const int sl = G.hlist[base + k]; G.htk[sl] = MT_BC_EMPTY; G.htv[sl] = 0; });
+                }
+                hlistN = 0;
+                wave_sync();
+                return false;
+            }
+            for (int base = l0; base < l1; base += MT_WAVE) {
+                const int m = (l1 - base) < MT_WAVE ? (l1 - base) : MT_WAVE;
+                const auto ch = wave_map(m, [&](int k) MT_LAM { return (int)G.hlist[base + k]; });
+                const auto par = wave_map(m, [&](int k) MT_LAM { return bk(G.htk[own(ch, k)]).parent; });
+                const auto val = wave_map(m, [&](int k) MT_LAM { return G.htv[own(ch, k)]; });
+                const auto a = wave_map(m, [&](int k) MT_LAM {
+                    const int p = own(par, k);
+                    bool w = false; int x = 0;
+                    if (p >= 0 && p != rt) x = htAdd(p, own(val, k), w);
+                    return w ? x : ~x;
+                });
+                htList(wave_map(m, [&](int k) MT_LAM { return own(a, k) >= 0 ? own(a, k) : ~own(a, k); }),
+                       wave_map(m, [&](int k) MT_LAM { return own(a, k) >= 0; }), m);
+            }
+            wave_sync();
+            l0 = l1; l1 = hlistN;
+        }
+        htOk = true;
+        return true;
+    }
     // Scan the window list: prune settled/unlinked rows (if prune) and collect
     // U = rows whose visibility differs between the observer and (r, c).
     MT_HD void computeU(int r, int c, bool prune) {
+        if constexpr (BIG && MT_G_NW > 1) {
+            MT_PB(tm);
+            computeUmw(r, c, prune);
+            MT_PE(MT_PH_U, tm);
+            return;
+        }
         MT_PB(t0);
         MT_EV(0, 1); MT_EV(2, winN);
         MT_QB(q0); MT_QC(4);
@@ -847,21 +1240,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         };
         auto winRows = [&](const LaneArr<int>& ids, int base) MT_LAM {
             const int m = (winN - base) < MT_WAVE ? (winN - base) : MT_WAVE;
-            return wave_map(m, [&](int k) MT_LAM {
-                WinI w; w.id = own(ids, k);
-                const int s = w.id;
-                const uint32_t mt = row(s).meta;
-                const bool removed = (mt & MT_M_REMOVED) != 0;
-                const int sq = row(s).seq, rs = row(s).rseq;
-                w.parent = row(s).parent;
-                const bool linked = w.parent >= 0;
-                w.live = linked && (sq > minSeq || (removed && rs > minSeq));
-                w.recycle = !linked && !(mt & MT_M_HREF);
-                const bool vr = vis_rc(sq, mt, rs, row(s).rcl, row(s).ovl, r, c, ovx, ovxN, s);
-                const bool vo = !removed;
-                w.delta = w.live ? ((vr ? row(s).len : 0) - (vo ? row(s).len : 0)) : 0;
-                return w;
-            });
+            return wave_map(m, [&](int k) MT_LAM { return winEntry(own(ids, k), r, c); });
         };
         const int wN0 = winN;
         LaneArr<WinI> wiNext{};
@@ -1096,6 +1475,14 @@ template <int RES, bool FULL = true> struct MtEngT {
                 return o;
             });
         }
+        if constexpr (BIG) {
+            if (htOk) {                                  // the children's corrections from the table
+                return wave_map(h.n, [&](int j) MT_LAM {
+                    const int b = own(ch, j);
+                    ChildL o; o.len = (haveLen ? own(kl, j) : bk(b).len) + htGet(b); o.tie = true; return o;
+                });
+            }
+        }
         // Each U row (one per lane) finds the child it lies under and adds its
         // delta into that child's LDS slot.
         const int hc = h.height - 1, n = h.n;
@@ -1220,8 +1607,53 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (ov >> 63) ovxCopy(s, n);
         row(n).toff = row(s).toff + pos; row(n).props = row(s).props; row(n).parent = row(s).parent;
         row(n).tcap = row(s).tcap - pos; row(s).tcap = pos;   // each row owns [toff, toff+tcap) of the arena
-        if (mt & MT_M_INWIN) winAdd(n);
+        if (mt & MT_M_INWIN) winAddKnown(n, mt & ~(MT_M_INWIN | MT_M_HREF));   // n's meta as just written
         return n;
+    }
+    // splitRow with row s's fields already loaded (f) and its leaf block B: the right half's
+    // record is written by 12 lanes in one store, and nothing of s is read again.
+    MT_HD int splitRowKnown(int s, int pos, const LeafR& f, int B) {
+        MT_EV2(5, 1);
+        const int n = allocRow();
+        if (n < 0) return -1;
+        const uint32_t nm = f.meta & ~(MT_M_INWIN | MT_M_HREF);
+        const int v0 = f.len - pos, v1 = f.seq, v2 = f.rseq, v3 = (int)nm, v4 = f.toff + pos, v5 = f.props, v6 = B,
+                  v7 = f.tcap - pos, v8 = (int)(uint32_t)f.ovl, v9 = (int)(uint32_t)(f.ovl >> 32), v10 = (int)f.rcl;
+        wave_for(12, [&](int k) MT_LAM {
+            const int v = k == 0 ? v0 : k == 1 ? v1 : k == 2 ? v2 : k == 3 ? v3 : k == 4 ? v4 : k == 5 ? v5 : k == 6 ? v6 :
+                          k == 7 ? v7 : k == 8 ? v8 : k == 9 ? v9 : k == 10 ? v10 : 0;
+            ((int*)&row(n))[k] = v;
+        });
+        row(s).len = pos; row(s).tcap = pos;                // each row owns [toff, toff+tcap) of the arena
+        if (f.ovl >> 63) ovxCopy(s, n);
+        if (f.meta & MT_M_INWIN) winAddKnown(n, nm);
+        return n;
+    }
+    // The fields of leaf block rows ch[0..n) (one row per lane, one round trip).
+    MT_HD LaneArr<LeafR> leafLoad(const LaneArr<int>& ch, int n) const {
+        return wave_map(n, [&](int j) MT_LAM {
+            const int s = own(ch, j);
+            LeafR f;
+            f.len = row(s).len; f.seq = row(s).seq; f.rseq = row(s).rseq; f.toff = row(s).toff; f.props = row(s).props;
+            f.tcap = row(s).tcap; f.meta = row(s).meta; f.rcl = row(s).rcl; f.ovl = row(s).ovl;
+            return f;
+        });
+    }
+    // Lane j's leaf row (j uniform).
+    MT_HD static LeafR leafAt(const LaneArr<LeafR>& a, int j) {
+        LeafR f;
+        f.len = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).len; }), j);
+        f.seq = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).seq; }), j);
+        f.rseq = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).rseq; }), j);
+        f.toff = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).toff; }), j);
+        f.props = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).props; }), j);
+        f.tcap = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).tcap; }), j);
+        f.meta = (uint32_t)wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return (int)own(a, k).meta; }), j);
+        f.rcl = (uint32_t)wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return (int)own(a, k).rcl; }), j);
+        const uint32_t lo = (uint32_t)wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return (int)(uint32_t)own(a, k).ovl; }), j);
+        const uint32_t hi = (uint32_t)wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return (int)(uint32_t)(own(a, k).ovl >> 32); }), j);
+        f.ovl = (unsigned long long)lo | ((unsigned long long)hi << 32);
+        return f;
     }
     // Insert `node` at child index idx of path level L, splitting full blocks
     // 4/4 upward (insertingWalk :2465-2489, split :2495-2508, updateRoot :1868).
@@ -1284,7 +1716,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     MT_HD int walk(int kind, int pos, int r, int c, int cand, int candLen) {
         if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
         int B = root, L = 0, p = pos;
-        const bool narrow = BIG && nU <= UCAP;   // U entries all in LDS: narrow them per level
+        const bool narrow = BIG && nU <= UCAP && !htOk;   // U entries all in LDS: narrow them per level
         int lsN = -1;
         BlkH h;
         MT_QB(q0); MT_QC(2);
@@ -1297,8 +1729,19 @@ template <int RES, bool FULL = true> struct MtEngT {
             // blocks in HBM: children's records (lengths + the next level's block) in one trip
             const bool kpre = !BLKL && h.height > 0;
             LaneArr<int> r0{}, r1{};
+            LaneArr<LeafR> lf{};
             if (kpre) kidsLoad(ch, h.n, r0, r1);
-            auto cl = kpre ? childLens(B, h, ch, r, c, true, kidsLen(r0, r1), lsN) : childLens(B, h, ch, r, c);
+            LaneArr<ChildL> cl;
+            if (h.height == 0) {                           // leaf rows: every field in one trip (a split needs them)
+                lf = leafLoad(ch, h.n);
+                cl = wave_map(h.n, [&](int j) MT_LAM {
+                    const LeafR f = own(lf, j);
+                    ChildL o;
+                    o.len = vis_rc(f.seq, f.meta, f.rseq, f.rcl, f.ovl, r, c, ovx, ovxN, own(ch, j)) ? f.len : 0;
+                    o.tie = !((f.meta & MT_M_REMOVED) && f.rseq <= r);     // breakTie, as childLens
+                    return o;
+                });
+            } else cl = kpre ? childLens(B, h, ch, r, c, true, kidsLen(r0, r1), lsN) : childLens(B, h, ch, r, c);
             MT_QE(1, q1);
             auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
             auto pre = wave_excl_scan8(lens);
@@ -1315,14 +1758,15 @@ template <int RES, bool FULL = true> struct MtEngT {
                 if (interior) {
                     sc->pathJ[L] = j; L++; B = wave_at(ch, j); p = pj;
                     if (narrow && h.height > 1) lsN = narrowU(lsN, h.height - 1, B);
-                    if (kpre) ch = kidRec(r0, r1, j, h); else ch = blkLoad(B, h);
+                    if (kpre) ch = kidRec(r0, r1, j, h, B); else ch = blkLoad(B, h);
                     continue;
                 }
                 const int s = wave_at(ch, j);
                 lastL = L; lastSplit = false;
                 if (kind == MT_WALK_SPLIT) {
-                    if (pj > 0 && !(uni(row(s).meta) & MT_M_MARKER)) {
-                        const int n = splitRow(s, pj);
+                    const LeafR f = leafAt(lf, j);
+                    if (pj > 0 && !(f.meta & MT_M_MARKER)) {
+                        const int n = splitRowKnown(s, pj, f, B);
                         if (n < 0) return MT_W_FAIL;
                         insertAtPath(L, j + 1, n, 0);
                         if (FULL && drec) {                     // SPLIT, splitLeafSegment (mergeTree.ts:2243-2258)

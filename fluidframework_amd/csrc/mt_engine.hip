@@ -145,7 +145,7 @@ static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) 
         hipStream_t s2 = (hipStream_t)c->stream2;
         (void)hipEventRecord((hipEvent_t)c->ev_fork, s);
         (void)hipStreamWaitEvent(s2, (hipEvent_t)c->ev_fork, 0);
-        mtk_big(full, s2, c->n_long, c->S, c->ops, runs, cur, MT_G_WIN, MT_G_HEAP);
+        mtk_big(full, s2, c->n_long, c->S, c->ops, runs, cur, MT_G_WIN, 0, MT_G_HEAP);
         if (c->n_short) {
             if (full) mtk_blk_full(s, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);
             else mtk_blk_fast(s, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);
@@ -154,7 +154,7 @@ static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) 
         (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_join, 0);
         return;
     }
-    if (c->use_lds == 3) mtk_big(full, s, n_runs, c->S, c->ops, nullptr, cur, c->lds_rows, c->lds_heap);
+    if (c->use_lds == 3) mtk_big(full, s, n_runs, c->S, c->ops, nullptr, cur, c->lds_rows, c->lds_blks, c->lds_heap);
     else if (c->use_lds == 2) {
         if (full) mtk_blk_full(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);
         else mtk_blk_fast(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);

@@ -40,16 +40,36 @@ __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(Mt
     const uint32_t cur = mt_replay_doc<MT_RES_BLK, FULL>(S, ops, run, &sc, 0, lb, lh);
     if (__lane_id() == 0) cursor[run] = cur;
 }
-// Long documents (MT_RES_BIG): heap, window and U set in LDS (~68 KB, two workgroups per
-// CU), blocks and rows in HBM; one wave per SIMD at most, so the register budget is 256
-// VGPRs and nothing spills.  A document whose heap or height outgrows LDS continues in HBM.
+// Long documents (MT_RES_BIG): heap, window, U set and a block cache of the tree's upper
+// levels in LDS (~137 KB, one workgroup per CU), rows and the other blocks in HBM; one wave
+// per SIMD at most, so the register budget is 256 VGPRs.  A document whose heap or height
+// outgrows LDS continues in HBM.  lb < 0: block cache off.
+// A workgroup of MT_G_NW waves per document: wave 0 replays, the others serve its posted
+// computeU shares (MtEngT::mwRun / mwShare) until it posts MT_MW_EXIT; every wave reaches
+// the same barriers, and wave 0 posts the exit on every path.
 template <bool FULL>
-__global__ __launch_bounds__(64, 1) void mt_replay_big_kernel(MtState S, MtOps ops, const uint32_t* runs, uint32_t* cursor,
-                                                                int lw, int lh) {
+__global__ __launch_bounds__(64 * MT_G_NW, 1) void mt_replay_big_kernel(MtState S, MtOps ops, const uint32_t* runs,
+                                                                         uint32_t* cursor, int lw, int lb, int lh) {
     __shared__ MtScratch sc;
-    const uint32_t run = runs ? runs[blockIdx.x] : blockIdx.x;
-    const uint32_t cur = mt_replay_doc<MT_RES_BIG, FULL>(S, ops, run, &sc, lw, 0, lh);
-    if (__lane_id() == 0) cursor[run] = cur;
+    const int wv = (int)(threadIdx.x >> 6);
+    if (wv == 0) {
+        if (__lane_id() == 0) mt_ldsg().posted = 0;
+        const uint32_t run = runs ? runs[blockIdx.x] : blockIdx.x;
+        const uint32_t cur = mt_replay_doc<MT_RES_BIG, FULL>(S, ops, run, &sc, lw, lb, lh);
+        if (__lane_id() == 0) cursor[run] = cur;
+        // the exit job goes to the slot after the last one posted
+        if (__lane_id() == 0) mt_ldsg().mw[mt_ldsg().posted & 1].op = MT_MW_EXIT;
+        __syncthreads();
+    } else {
+        MtEngT<MT_RES_BIG, FULL> h;
+        for (int k = 0;; k++) {
+            __syncthreads();
+            const int op = __builtin_amdgcn_readfirstlane(mt_ldsg().mw[k & 1].op);
+            if (op == MT_MW_EXIT) break;
+            h.mwShare(wv, k);
+            if (MtEngT<MT_RES_BIG, FULL>::mwSync(op)) __syncthreads();
+        }
+    }
 }
 // Every pool in HBM: whole runs, or the rest of each run after mt_replay_lds_kernel.
 template <bool FULL>
@@ -90,9 +110,9 @@ void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, c
 }
 #elif MT_KSET == 2
 void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,
-             int lw, int lh) {
-    if (full) hipLaunchKernelGGL(mt_replay_big_kernel<true>, dim3(n), dim3(64), 0, s, S, o, runs, cur, lw, lh);
-    else hipLaunchKernelGGL(mt_replay_big_kernel<false>, dim3(n), dim3(64), 0, s, S, o, runs, cur, lw, lh);
+             int lw, int lb, int lh) {
+    if (full) hipLaunchKernelGGL(mt_replay_big_kernel<true>, dim3(n), dim3(64 * MT_G_NW), 0, s, S, o, runs, cur, lw, lb, lh);
+    else hipLaunchKernelGGL(mt_replay_big_kernel<false>, dim3(n), dim3(64 * MT_G_NW), 0, s, S, o, runs, cur, lw, lb, lh);
 }
 #elif MT_KSET == 3
 void mtk_lds(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lr, int lb, int lh) {

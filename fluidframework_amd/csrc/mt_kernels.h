@@ -9,7 +9,7 @@ void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, c
 void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
                   int lh);
 void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,
-             int lw, int lh);
+             int lw, int lb, int lh);
 void mtk_lds(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lr, int lb, int lh);
 void mtk_hbm(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* cur);
 void mtk_generate(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const MtGen& g);

@@ -131,6 +131,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
             const bool pre = ty == MT_OP_INSERT && !(fl & MT_OPF_MARKER) && plen <= MT_WAVE;
             const auto pay = wave_map(pre ? plen : 0, [&](int k) MT_LAM { return (int)ops.payload[poff + (uint32_t)k]; });
             if (!(e.uValid && e.uRef == r && e.uCli == c)) e.computeU(r, c, true);
+            e.mwPrefetch();                                      // long documents: warm zamboni's rows
             int q1 = p1, q2 = p2;
             if (fl & (MT_OPF_REL1 | MT_OPF_REL2)) {       // getValidOpRange (MT/client.ts:506-523)
                 if ((fl & MT_OPF_REL1) && (p1 < 0 || (uint32_t)p1 >= ops.n_rel)) { e.status |= MT_DS_BAD_OP; break; }

@@ -125,6 +125,13 @@ template <class F> __device__ __forceinline__ int wave_shfl(int a, F src) { retu
 __device__ __forceinline__ int wave_set(int a, int k, int v) { return __lane_id() == k ? v : a; }
 // per-lane add into wave-private LDS (conflicting lanes serialize in hardware)
 __device__ __forceinline__ void lds_add(int* p, int v) { __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
+// keeps a loaded value alive (a prefetch whose result is otherwise unused)
+__device__ __forceinline__ void mt_keep(int v) { __asm__ volatile("" ::"v"(v)); }
+// per-lane compare-and-swap on LDS; returns the old value
+__device__ __forceinline__ int lds_cas(int* p, int cmp, int v) {
+    __hip_atomic_compare_exchange_strong(p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    return cmp;
+}
 // Lane 0 takes the next slot of a global 64-bit cursor; every lane gets its index.
 __device__ __forceinline__ unsigned long long wave_atomic_add(unsigned long long* p, unsigned long long d) {
     unsigned long long v = 0;
@@ -222,6 +229,8 @@ template <class F> inline LaneArr<int> wave_shfl(const LaneArr<int>& a, F src) {
 }
 inline LaneArr<int> wave_set(LaneArr<int> a, int k, int v) { if (k >= 0 && k < MT_WAVE) a.v[k] = v; return a; }
 inline void lds_add(int* p, int v) { *p += v; }
+inline int lds_cas(int* p, int cmp, int v) { const int o = *p; if (o == cmp) *p = v; return o; }
+inline void mt_keep(int) {}
 inline unsigned long long wave_atomic_add(unsigned long long* p, unsigned long long d) { return __atomic_fetch_add(p, d, __ATOMIC_RELAXED); }
 inline unsigned long long wave_atomic_next(unsigned long long* p) { return wave_atomic_add(p, 1ull); }
 inline unsigned long long wave_sum64(const LaneArr<unsigned long long>& a) {

@@ -89,7 +89,7 @@ def test_emu_matches_oracle(cfg):
 # different ops, with different pools the binding one) and finish from HBM;
 # (0, ...) runs the HBM-pool kernel alone.  Results must not change.
 @pytest.mark.parametrize("res", [(1, 40, 40, 12), (1, 90, 48, 24), (1, 256, 96, 96), (0, 0, 0, 0),
-                                 (2, 0, 40, 12), (2, 0, 104, 94), (3, 0, 0, 0), (3, 16, 0, 12)])
+                                 (2, 0, 40, 12), (2, 0, 104, 94), (3, 0, 0, 0), (3, 16, 0, 12), (3, 0, 7, 0), (3, 0, 4, 0)])
 @pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "grow"])
 def test_emu_residency_handover_matches_oracle(cfg, res):
     props = ann_props()
