@@ -87,6 +87,7 @@ static void mt_caps_default(mt_limits& q) {
     if (!q.text_per_doc) q.text_per_doc = q.rows_per_doc * 8;
     if (!q.propsets_per_doc) q.propsets_per_doc = 1024;
     if (!q.markers_per_doc) q.markers_per_doc = 1024;
+    if (!q.register_rows_per_doc) q.register_rows_per_doc = 256;
 }
 static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bool uniform, mt_ctx** out) {
     mt_ctx* c = new mt_ctx();
@@ -101,17 +102,19 @@ static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bo
     for (uint32_t d = 0; d < n_docs; d++) {
         mt_limits q = caps[uniform ? 0 : d];
         mt_caps_default(q);
-        if (q.rows_per_doc > (1u << 30) || q.text_per_doc > (1u << 30) || q.window_per_doc > (1u << 26)) {
+        if (q.rows_per_doc > (1u << 30) || q.text_per_doc > (1u << 30) || q.window_per_doc > (1u << 26) ||
+            q.register_rows_per_doc > (1u << 24)) {
             c->err = "per-document capacity too large"; return MT_E_INVALID;
         }
         MtDocLayout& y = c->layout_h[d];
         y.row = tot.row; y.blk = tot.blk; y.heap = tot.heap; y.win = tot.win; y.anc = tot.anc; y.text = tot.text; y.pset = tot.pset;
-        y.mid = tot.mid;
+        y.mid = tot.mid; y.regr = tot.regr;
         y.rowCap = q.rows_per_doc; y.blkCap = q.blocks_per_doc; y.heapCap = q.heap_per_doc; y.winCap = q.window_per_doc;
         y.textCap = q.text_per_doc; y.psetCap = q.propsets_per_doc; y.midCap = q.markers_per_doc;
+        y.regCap = q.register_rows_per_doc;
         tot.row += y.rowCap; tot.blk += y.blkCap; tot.heap += y.heapCap + 1; tot.win += y.winCap;
         tot.anc += (unsigned long long)y.winCap * MT_MAXH; tot.text += 2ull * y.textCap; tot.pset += y.psetCap;
-        tot.mid += y.midCap;
+        tot.mid += y.midCap; tot.regr += 2ull * y.regCap;
         S.rowCap = std::max(S.rowCap, y.rowCap); S.blkCap = std::max(S.blkCap, y.blkCap); S.heapCap = std::max(S.heapCap, y.heapCap);
         S.winCap = std::max(S.winCap, y.winCap); S.textCap = std::max(S.textCap, y.textCap); S.psetCap = std::max(S.psetCap, y.psetCap);
     }
@@ -125,7 +128,7 @@ static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bo
     MT_ALLOC(uid, int, tot.win) MT_ALLOC(udelta, int, tot.win) MT_ALLOC(uanc, int, tot.anc)
     MT_ALLOC(text, uint16_t, tot.text) MT_ALLOC(pset, MtPSet, tot.pset) MT_ALLOC(hdr, MtDocHdr, D)
     MT_ALLOC(hold, int, D * MT_RFL) MT_ALLOC(ovx, MtOvx, D * MT_OVX_CAP) MT_ALLOC(mid, int, tot.mid)
-    MT_ALLOC(reg, MtReg, D * MT_REG_CAP)
+    MT_ALLOC(reg, MtReg, D * MT_REG_CAP) MT_ALLOC(regr, int, tot.regr)
 #undef MT_ALLOC
     if (mtb_malloc(&p, sizeof(MtDocLayout) * D) != 0) { c->err = "pool allocation failed: layout"; return MT_E_OOM; }
     S.layout = (const MtDocLayout*)p;
@@ -135,7 +138,7 @@ static int mt_create_impl(int device, uint32_t n_docs, const mt_limits* caps, bo
     c->pool_bytes = sizeof(MtRow) * tot.row + sizeof(MtBlk) * tot.blk + sizeof(MtHeapE) * tot.heap + 12ull * tot.win +
                     4ull * tot.anc + 2ull * tot.text + sizeof(MtPSet) * tot.pset +
                     (sizeof(MtDocHdr) + 4ull * MT_RFL + sizeof(MtDocLayout) + sizeof(MtOvx) * MT_OVX_CAP +
-                     sizeof(MtReg) * MT_REG_CAP) * D + 4ull * tot.mid;
+                     sizeof(MtReg) * MT_REG_CAP) * D + 4ull * tot.mid + 4ull * tot.regr;
     return MT_OK;
 }
 
@@ -159,7 +162,7 @@ static std::vector<MtCkPart> mt_ck_parts(mt_ctx* c) {
             {&c->ck_text, S.text, 2ull * t.text}, {&c->ck_pset, S.pset, sizeof(MtPSet) * t.pset},
             {&c->ck_hdr, S.hdr, sizeof(MtDocHdr) * D}, {&c->ck_hold, S.hold, 4ull * MT_RFL * D},
             {&c->ck_ovx, S.ovx, sizeof(MtOvx) * MT_OVX_CAP * D}, {&c->ck_mid, S.mid, 4ull * t.mid},
-            {&c->ck_reg, S.reg, sizeof(MtReg) * MT_REG_CAP * D}};
+            {&c->ck_reg, S.reg, sizeof(MtReg) * MT_REG_CAP * D}, {&c->ck_regr, S.regr, 4ull * t.regr}};
 }
 int MT_FN(checkpoint)(mt_ctx* c) {
     if (!c) return MT_E_INVALID;
@@ -190,7 +193,7 @@ void MT_FN(destroy)(mt_ctx* c) {
     MtState& S = c->S;
     void* ps[] = {S.rows, S.blk, S.heap, S.win, S.uid, S.udelta, S.uanc, S.text, S.pset, S.hdr, S.hold, (void*)S.layout,
                   S.ovx, S.mid, S.reg, c->ck_rows, c->ck_blk, c->ck_heap, c->ck_win, c->ck_text, c->ck_pset, c->ck_hdr,
-                  c->ck_hold, c->ck_ovx, c->ck_mid, c->ck_reg};
+                  c->ck_hold, c->ck_ovx, c->ck_mid, c->ck_reg, c->ck_regr, S.regr};
     for (void* p : ps) if (p) mtb_free(p);
     mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_rel, &c->b_drec,
                             &c->b_dcount, &c->b_pset_off,
@@ -549,10 +552,14 @@ int MT_FN(doc_pset)(mt_ctx* c, uint32_t doc, int32_t id, uint16_t* keys, int32_t
     if (rc) return rc;
     const MtDocLayout& y = c->layout_h[doc];
     if ((uint32_t)id >= y.psetCap) return MT_E_INVALID;
-    MtPSet p;
-    mtb_d2h(c, &p, c->S.pset + y.pset + (size_t)id, sizeof(MtPSet));
-    *n = p.n < 0 ? 0u : (uint32_t)p.n;
-    for (uint32_t i = 0; i < *n && i < MT_PSK; i++) { keys[i] = p.key[i]; vals[i] = p.val[i]; }
+    MtPSet p[MT_PKEYS / MT_PSK];
+    mtb_d2h(c, p, c->S.pset + y.pset + (size_t)id, sizeof(MtPSet));
+    const uint32_t nk = p[0].n < 0 ? 0u : ((uint32_t)p[0].n > MT_PKEYS ? MT_PKEYS : (uint32_t)p[0].n);
+    const uint32_t nch = nk > MT_PSK ? (nk + MT_PSK - 1) / MT_PSK : 1;
+    if ((uint32_t)id + nch > y.psetCap) return MT_E_INVALID;
+    if (nch > 1) mtb_d2h(c, p + 1, c->S.pset + y.pset + (size_t)id + 1, sizeof(MtPSet) * (nch - 1));
+    *n = nk;
+    for (uint32_t i = 0; i < nk; i++) { keys[i] = p[i >> 4].key[i & 15]; vals[i] = p[i >> 4].val[i & 15]; }
     return MT_OK;
 }
 int MT_FN(set_size_class)(mt_ctx* c, uint32_t big_min_ops) {

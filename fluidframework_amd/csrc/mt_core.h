@@ -30,7 +30,8 @@
 #include "../../include/mtgpu.h"
 
 #define MT_MAXH 16                    // max tree height (7^16 segments)
-#define MT_PSK 16                     // property keys per segment, one per lane (more: PROPS_TOO_MANY)
+#define MT_PSK 16                     // property keys per MtPSet chunk
+#define MT_PKEYS 64                   // keys of one property map, one per lane (more: PROPS_TOO_MANY)
 #define MT_MAXN 8                     // MaxNodesInBlock, MT/mergeTree.ts:350
 #define MT_GRAN 256                   // TextSegmentGranularity, MT/mergeTree.ts:1056
 #define MT_ZMAX 2                     // zamboniSegmentsMaxCount, MT/mergeTree.ts:1058
@@ -192,7 +193,9 @@ struct __attribute__((aligned(16))) MtBlk {   // one 64-byte record per B-tree b
     int scour;       // needsScour: -1 undefined, 0 false, 1 true
     int pad[3];
 };
-struct __attribute__((aligned(16))) MtPSet {  // immutable property map (insertion order)
+// An immutable property map of n keys (insertion order) occupies ceil(n / 16) consecutive
+// chunks (at least one): key i is chunk i / 16's key[i % 16]; every chunk carries n.
+struct __attribute__((aligned(16))) MtPSet {
     uint16_t key[MT_PSK];
     int32_t val[MT_PSK];
     int32_t n;
@@ -207,9 +210,10 @@ struct MtOvx { int row; int rseq; int client; int pad; };
 // RegisterCollection entries (MT/mergeTree.ts:864-896) per document: the cloned segments
 // of one (client, register name), as unlinked rows.  flags: 1 = holds a clone of a
 // removed segment, 2 = pasted (its rows are in the tree now).
-#define MT_REG_CAP 8
-#define MT_REG_SEGS 28
-struct MtReg { int client, name, n, flags; int rows[MT_REG_SEGS]; };
+#define MT_REG_CAP 64                  // registers per document (one per lane)
+// An entry's clone rows are n consecutive ids at off in the document's register row arena
+// (two halves of regCap ids: copying compaction, MtEngT::regCompact).
+struct MtReg { int client, name, n, flags, off, pad[3]; };
 struct __attribute__((aligned(16))) MtDocHdr {
     int root, height, minSeq, curSeq, rowTop, blkTop, blkFree, heapN, winN, textTop, psetTop;
     uint32_t status;
@@ -219,7 +223,7 @@ struct __attribute__((aligned(16))) MtDocHdr {
     int blkFreeN;                            // blocks on the free list
     int heapHW, winHW;                       // high-water marks (pool sizing, mt_doc_pools)
     int ovxN;                                // overlap side-list entries
-    int pad[2];
+    int regTop, regHalf;                     // register row arena: used ids, live half
     unsigned long long prof[8];              // MT_PROFILE builds: s_memtime cycles per phase
 };
 
@@ -227,9 +231,8 @@ struct __attribute__((aligned(16))) MtDocHdr {
 // their capacities: documents of one context may be sized differently
 // (mt_create_docs), e.g. by their op counts.
 struct __attribute__((aligned(16))) MtDocLayout {
-    unsigned long long row, blk, heap, win, anc, text, pset, mid;   // heap: cap+1 entries; text: 2 halves
-    uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap, midCap;
-    uint32_t pad[1];
+    unsigned long long row, blk, heap, win, anc, text, pset, mid, regr;   // heap: cap+1 entries; text, regr: 2 halves
+    uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap, midCap, regCap;
 };
 
 struct MtState {                              // device pools, doc-major
@@ -239,6 +242,7 @@ struct MtState {                              // device pools, doc-major
     MtOvx* ovx;                               // overlap side lists, MT_OVX_CAP per doc
     int* mid;                                 // marker-id tables (idToSegment): row per id, -1 unmapped
     MtReg* reg;                               // register collections, MT_REG_CAP per doc
+    int* regr;                                // register row arenas (MtDocLayout::regr, two halves)
     uint32_t rowCap, blkCap, heapCap, winCap, textCap, psetCap, holdCap, maxDocs;   // largest per-doc caps
     const MtDocLayout* layout;                // [maxDocs]
     // interned op property sets (mt_prop_table)
@@ -272,11 +276,11 @@ struct MtOps {                                // device copy of an mt_op_batch
     uint64_t payload_units;                   // records are bounds-checked against it on the device
 };
 enum { MT_DC_REC = 0, MT_DC_RECRES = 1, MT_DC_TXT = 2, MT_DC_TXTRES = 3 };
-// Records one message can emit at most, beyond its own range: 2 ensureIntervalBoundary
-// SPLITs, a paste's clones (MT_REG_SEGS) and two zamboni calls (the op's and setMinSeq's),
+// Records one message can emit at most, beyond its own range or paste: 2 ensureIntervalBoundary
+// SPLITs and two zamboni calls (the op's and setMinSeq's),
 // each popping <= 2 heap entries that scour one leaf block (8) and may packParent its
 // siblings (<= 8 blocks of 8).
-#define MT_DREC_SLACK (2 + MT_REG_SEGS + 2 * 2 * (8 + 64))
+#define MT_DREC_SLACK (2 + 2 * 2 * (8 + 64))
 
 // Snapshot load (mt_load_snapshot): the segments of each document (mt_load_seg)
 // and the host's plan of loadBody's insertSegments calls (MT/snapshotLoader.ts:162-206).
@@ -359,7 +363,6 @@ struct MtScratch {
     int pathB[MT_MAXH + 2], pathJ[MT_MAXH + 2];
     int hold[64];
     int holdLen[64];                  // observer length of each held child (scourLeaves)
-    int pk[MT_PSK], pv[MT_PSK];
     int rfree[MT_RFL];                // recycled rows (unlinked, out of the window, no heap entry)
     int corr[MT_MAXN];                // per-child perspective corrections (childLens)
 };
@@ -450,6 +453,7 @@ struct MtCold {
     // use against its reservation, and whether the run stopped for capture headroom
     uint16_t* dtext; unsigned long long dtcap;
     uint32_t dused, tused; int dstop;
+    int* regr; int regTop, regHalf, regCap;   // register row arena (this document's)
 };
 #if defined(__HIP_DEVICE_COMPILE__)
 __shared__ MtCold mt_cold_v;
@@ -481,6 +485,9 @@ template <int RES, bool FULL = true> struct MtEngT {
     MtOvx*& ovx = mt_cold_v.ovx; int& ovxN = mt_cold_v.ovxn;
     int*& midt = mt_cold_v.midt; int& midCap = mt_cold_v.midcap;   // idToSegment (MT/mergeTree.ts:1095, :1175)
     MtReg*& regs = mt_cold_v.regs;            // RegisterCollection (MT_REG_CAP entries)
+    int*& regr = mt_cold_v.regr; int& regTop = mt_cold_v.regTop; int& regHalf = mt_cold_v.regHalf;
+    int& regCap = mt_cold_v.regCap;
+    MT_HD int& regRow(int i) const { return regr[(size_t)regHalf * regCap + i]; }
     MtDeltaRec* drec; unsigned long long* dcount; unsigned long long dcap; uint32_t& curOp = mt_cold_v.op;   // delta capture
     uint16_t*& dtext = mt_cold_v.dtext; unsigned long long& dtcap = mt_cold_v.dtcap;
     uint32_t &dUsed = mt_cold_v.dused, &tUsed = mt_cold_v.tused; int& dStop = mt_cold_v.dstop;
@@ -588,7 +595,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     bool bcOn;                          // MT_RES_BIG: descents fill the LDS block cache
     bool htOk; int hlistN;              // MT_RES_BIG: the corrections table is built for U; occupied slots
     bool htOn, pfOn; int mwSeq;         // MT_RES_BIG: table / zamboni prefetch enabled; jobs posted so far
-    int& nCol = mt_cold_v.ncol;         // rows gathered by rangeMap(MT_MAP_COLLECT) into sc->hold
+    int& nCol = mt_cold_v.ncol;         // rows gathered by rangeMap(MT_MAP_COLLECT) at the register arena's tail
     int landB;                          // leaf block the last insertAtPath linked its node under
     int rfN; int*& rfHbm = mt_cold_v.rfhbm;   // recycled-row stack: depth, HBM home between runs
     int& blkFreeN = mt_cold_v.blkfreen;       // blocks on the free list
@@ -616,6 +623,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         pset = st.pset + off(&Ly->pset);
         ovx = st.ovx + (size_t)d * MT_OVX_CAP;
         regs = st.reg + (size_t)d * MT_REG_CAP;
+        regr = st.regr + off(&Ly->regr); regCap = (int)uni(Ly->regCap);
         midt = st.mid + off(&Ly->mid); midCap = (int)uni(Ly->midCap);
         drec = nullptr; dcount = nullptr; dcap = 0; curOp = 0;
         dtext = nullptr; dtcap = 0; dUsed = 0; tUsed = 0; dStop = 0;
@@ -634,6 +642,8 @@ template <int RES, bool FULL = true> struct MtEngT {
         lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0; bcOn = false; htOk = false; hlistN = 0; htOn = pfOn = false; mwSeq = 0;
         rfHbm = st.hold + (size_t)d * MT_RFL; rfN = uni(h.rfN); blkFreeN = uni(h.blkFreeN);
         heapHW = uni(h.heapHW); winHW = uni(h.winHW); ovxN = uni(h.ovxN);
+        regTop = uni(h.regTop); regHalf = uni(h.regHalf) & 1;
+        if (regTop < 0 || regTop > regCap) regTop = 0;
         if (ovxN < 0 || ovxN > MT_OVX_CAP) ovxN = 0;
         lRows = lBlks = lHeap = 0; gRowCap = gBlkCap = gHeapCap = gWinCap = 0;
         if (rfN < 0 || rfN > MT_RFL) rfN = 0;
@@ -649,7 +659,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         h.root = root; h.height = height; h.minSeq = minSeq; h.curSeq = curSeq; h.rowTop = rowTop;
         h.blkTop = blkTop; h.blkFree = blkFree; h.heapN = heapN; h.winN = winN; h.textTop = textTop;
         h.psetTop = psetTop; h.status = status; h.textHalf = textHalf; h.rfN = rfN; h.blkFreeN = blkFreeN;
-        h.heapHW = heapHW; h.winHW = winHW; h.ovxN = ovxN;
+        h.heapHW = heapHW; h.winHW = winHW; h.ovxN = ovxN; h.regTop = regTop; h.regHalf = regHalf;
         { const int n = rfN; int* dst = rfHbm;
           for (int base = 0; base < n; base += MT_WAVE) {
               const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
@@ -676,7 +686,8 @@ template <int RES, bool FULL = true> struct MtEngT {
 #endif
         wave_for(8, [&](int i) MT_LAM { bk(0).c[i] = -1; });
         bk(0).len = 0; bk(0).parent = -1; bk(0).n = 0; bk(0).height = 0; bk(0).scour = -1;
-        wave_for(MT_REG_CAP, [&](int i) MT_LAM { regs[i].client = -1; regs[i].n = 0; regs[i].flags = 0; });
+        wave_for(MT_REG_CAP, [&](int i) MT_LAM { regs[i].client = -1; regs[i].n = 0; regs[i].flags = 0; regs[i].off = 0; });
+        regTop = 0; regHalf = 0;
         // idToSegment entries are not reset: an entry is read only for an id the host
         // already saw mapped in this document (mt_rel_pos.marker >= 0), and relPos
         // checks that the row still carries that id.
@@ -1421,8 +1432,18 @@ template <int RES, bool FULL = true> struct MtEngT {
     MT_HD int regTextLen(int c, int name) {
         const int e = regFind(c, name, false);
         if (e < 0) return 0;
-        const int n = uni(regs[e].n);
-        return wave_sum(wave_map(n < MT_REG_SEGS ? n : MT_REG_SEGS, [&](int i) MT_LAM { return row(regs[e].rows[i]).len; }));
+        const int n = uni(regs[e].n), o = uni(regs[e].off);
+        int t = 0;
+        for (int base = 0; base < n; base += MT_WAVE) {
+            const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
+            t += wave_sum(wave_map(m, [&](int i) MT_LAM { return row(regRow(o + base + i)).len; }));
+        }
+        return t;
+    }
+    // Clones a paste of register (c, name) inserts.
+    MT_HD int regCount(int c, int name) {
+        const int e = regFind(c, name, false);
+        return e < 0 ? 0 : uni(regs[e].n);
     }
     // A pasted text segment's text into the capture's text arena; returns its offset.
     MT_HD int dText(int toff, int len) {
@@ -1901,16 +1922,18 @@ template <int RES, bool FULL = true> struct MtEngT {
             heapAdd(s, sq);
         }
     }
+    MT_HD int pkey(int id, int i) const { return (int)pset[id + (i >> 4)].key[i & 15]; }
+    MT_HD int pval(int id, int i) const { return pset[id + (i >> 4)].val[i & 15]; }
     MT_HD bool propsMatch(int a, int b) {                      // matchProperties, MT/properties.ts:64-95
         if (a == b) return true;
         if (a < 0 || b < 0) return false;
         const int na = uni(pset[a].n), nb = uni(pset[b].n);
         if (na != nb) return false;
         auto ok = wave_map(na, [&](int k) MT_LAM {
-            const int key = pset[a].key[k];
-            const uint32_t ca = S.p_class[pset[a].val[k]];
+            const int key = pkey(a, k);
+            const uint32_t ca = S.p_class[pval(a, k)];
             bool f = false;
-            for (int i = 0; i < nb; i++) if (pset[b].key[i] == key && S.p_class[pset[b].val[i]] == ca) f = true;
+            for (int i = 0; i < nb; i++) if (pkey(b, i) == key && S.p_class[pval(b, i)] == ca) f = true;
             return f;
         });
         return wave_count(ok) == na;
@@ -2264,11 +2287,9 @@ template <int RES, bool FULL = true> struct MtEngT {
     // Keys live one per lane (insertion order).
     MT_HD int applyPropSet(int old, int opset, bool rewrite) {
         if (opset < 0 || opset >= (int)S.p_nsets) { status |= MT_DS_UNSUPPORTED; return old; }
-        if (psetTop >= (int)S.psetCap) { status |= MT_DS_OOM_PROPS; return old; }
-        const int id = psetTop++;
         int n = old >= 0 ? uni(pset[old].n) : 0;
-        auto kk = wave_map(n, [&](int i) MT_LAM { return (int)pset[old].key[i]; });
-        auto vv = wave_map(n, [&](int i) MT_LAM { return (int)pset[old].val[i]; });
+        auto kk = wave_map(n, [&](int i) MT_LAM { return pkey(old, i); });
+        auto vv = wave_map(n, [&](int i) MT_LAM { return pval(old, i); });
         const int o0 = uni((int)S.p_off[opset]), o1 = uni((int)S.p_off[opset + 1]);
         if (rewrite && n > 0) {
             auto keep = wave_map(n, [&](int i) MT_LAM {
@@ -2279,11 +2300,12 @@ template <int RES, bool FULL = true> struct MtEngT {
             });
             auto rk = wave_rank(keep);
             const int cntk = wave_count(keep);
-            wave_for(n, [&](int i) MT_LAM { if (own(keep, i)) { sc->pk[own(rk, i)] = own(kk, i); sc->pv[own(rk, i)] = own(vv, i); } });
+            // compaction through the hold scratch (free here: no scour or collect is in flight)
+            wave_for(n, [&](int i) MT_LAM { if (own(keep, i)) { sc->hold[own(rk, i)] = own(kk, i); sc->holdLen[own(rk, i)] = own(vv, i); } });
             wave_sync();
             n = cntk;
-            kk = wave_map(n, [&](int i) MT_LAM { return sc->pk[i]; });
-            vv = wave_map(n, [&](int i) MT_LAM { return sc->pv[i]; });
+            kk = wave_map(n, [&](int i) MT_LAM { return sc->hold[i]; });
+            vv = wave_map(n, [&](int i) MT_LAM { return sc->holdLen[i]; });
             wave_sync();
         }
         for (int q = o0; q < o1; q++) {
@@ -2291,27 +2313,30 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int at = wave_first(wave_map(n, [&](int i) MT_LAM { return own(kk, i) == key; }));
             if (nv < 0) {
                 if (at >= 0) {
-                    auto k1 = wave_from8<1>(kk), v1 = wave_from8<1>(vv);
-                    kk = wave_map(MT_PSK, [&](int i) MT_LAM { const int a = own(kk, i), b = own(k1, i); return i < at ? a : b; });
-                    vv = wave_map(MT_PSK, [&](int i) MT_LAM { const int a = own(vv, i), b = own(v1, i); return i < at ? a : b; });
+                    auto k1 = wave_from(kk, 1), v1 = wave_from(vv, 1);
+                    kk = wave_map(MT_PKEYS, [&](int i) MT_LAM { const int a = own(kk, i), b = own(k1, i); return i < at ? a : b; });
+                    vv = wave_map(MT_PKEYS, [&](int i) MT_LAM { const int a = own(vv, i), b = own(v1, i); return i < at ? a : b; });
                     n--;
                 }
             } else if (at >= 0) {
-                vv = wave_map(MT_PSK, [&](int i) MT_LAM { return i == at ? nv : own(vv, i); });
+                vv = wave_map(MT_PKEYS, [&](int i) MT_LAM { return i == at ? nv : own(vv, i); });
             } else {
-                if (n >= MT_PSK) { status |= MT_DS_PROPS_TOO_MANY; psetTop--; return old; }
+                if (n >= MT_PKEYS) { status |= MT_DS_PROPS_TOO_MANY; return old; }
                 const int at2 = n;
-                kk = wave_map(MT_PSK, [&](int i) MT_LAM { return i == at2 ? key : own(kk, i); });
-                vv = wave_map(MT_PSK, [&](int i) MT_LAM { return i == at2 ? nv : own(vv, i); });
+                kk = wave_map(MT_PKEYS, [&](int i) MT_LAM { return i == at2 ? key : own(kk, i); });
+                vv = wave_map(MT_PKEYS, [&](int i) MT_LAM { return i == at2 ? nv : own(vv, i); });
                 n++;
             }
         }
-        const int nn = n;
-        wave_for(MT_PSK, [&](int i) MT_LAM {
-            pset[id].key[i] = (uint16_t)(i < nn ? own(kk, i) : 0);
-            pset[id].val[i] = i < nn ? own(vv, i) : 0;
+        const int nn = n, nch = nn > MT_PSK ? (nn + MT_PSK - 1) / MT_PSK : 1;
+        if (psetTop + nch > (int)S.psetCap) { status |= MT_DS_OOM_PROPS; return old; }
+        const int id = psetTop;
+        psetTop += nch;
+        wave_for(nch * MT_PSK, [&](int i) MT_LAM {
+            pset[id + (i >> 4)].key[i & 15] = (uint16_t)(i < nn ? own(kk, i) : 0);
+            pset[id + (i >> 4)].val[i & 15] = i < nn ? own(vv, i) : 0;
         });
-        pset[id].n = nn;
+        wave_for(nch, [&](int k) MT_LAM { pset[id + k].n = nn; });
         return id;
     }
 
@@ -2353,9 +2378,9 @@ template <int RES, bool FULL = true> struct MtEngT {
                     c_rows += 2ull * (uint64_t)nact;
                     if (mode == MT_MAP_COLLECT) {                      // cloneSegments' gatherSegment (:1599-1604)
                         const auto rk = wave_rank(cond);
-                        const int k0 = nCol;
+                        const int k0 = regTop + nCol;               // into the register arena's free tail
                         wave_for(h.n, [&](int j) MT_LAM {
-                            if (own(cond, j) && k0 + own(rk, j) < MT_REG_SEGS) sc->hold[k0 + own(rk, j)] = own(ch, j);
+                            if (own(cond, j) && k0 + own(rk, j) < regCap) regRow(k0 + own(rk, j)) = own(ch, j);
                         });
                         nCol += nact;
                     } else if (mode == MT_MAP_REMOVE) {
@@ -2679,44 +2704,78 @@ template <int RES, bool FULL = true> struct MtEngT {
     // MT/mergeTree.ts:476-483) replaces the register's contents.  Clones are unlinked rows
     // sharing the original's immutable text slice and property map.
     MT_HD void opCopy(int start, int end, int r, int c, int name) {
-        nCol = 0;
-        rangeMap(MT_MAP_COLLECT, start, end, r, c, 0, -1, false);
-        if (status) return;
         const int e = regFind(c, name, true);
-        if (e < 0 || nCol > MT_REG_SEGS) { status |= MT_DS_UNSUPPORTED; return; }
-        MtReg& g = regs[e];
-        const int n = nCol;
-        // the new clones' rows first (hold[32..]): on OOM the entry stays as it was
-        for (int i = 0; i < n; i++) {
-            const int k = allocRow();
-            if (k < 0) { for (int j = i - 1; j >= 0; j--) freeRow(uni(sc->hold[32 + j])); return; }
-            wave_for(1, [&](int) MT_LAM { sc->hold[32 + i] = k; });
+        if (e < 0) { status |= MT_DS_UNSUPPORTED; return; }          // MT_REG_CAP registers in use
+        nCol = 0;
+        const uint32_t cr0 = c_rows;
+        rangeMap(MT_MAP_COLLECT, start, end, r, c, 0, -1, false);   // sources into the arena's tail
+        if (status) return;
+        if (regTop + nCol > regCap) {                               // compact, then collect again
+            regCompact();
+            if (regTop + nCol > regCap) { status |= MT_DS_UNSUPPORTED; return; }
+            nCol = 0; c_rows = cr0;                                 // (counted once)
+            rangeMap(MT_MAP_COLLECT, start, end, r, c, 0, -1, false);
+            if (status) return;
         }
+        const int n = nCol, base = regTop;
+        // the clones' rows, all or none: recycled rows first (allocRow's order), then the pool top
+        if (n > rfN + ((int)S.rowCap - rowTop)) { status |= MT_DS_OOM_ROWS; return; }
+        const int f0 = rfN, t0 = rowTop;
+        uint64_t rem = 0;
+        for (int b0 = 0; b0 < n; b0 += MT_WAVE) {
+            const int m = (n - b0) < MT_WAVE ? (n - b0) : MT_WAVE;
+            const auto rm = wave_map(m, [&](int k) MT_LAM {
+                const int i = b0 + k, s = regRow(base + i);
+                const int d = i < f0 ? sc->rfree[f0 - 1 - i] : t0 + (i - f0);
+                const uint32_t mt = row(s).meta;
+                row(d).len = row(s).len; row(d).seq = row(s).seq; row(d).rseq = row(s).rseq;
+                row(d).meta = (mt & (MT_M_CLIENT | MT_M_REMOVED | MT_M_MARKER)) | MT_M_REG;
+                row(d).rcl = row(s).rcl; row(d).props = row(s).props; row(d).mid = row(s).mid;
+                row(d).toff = row(s).toff; row(d).tcap = (mt & MT_M_MARKER) ? 0 : row(s).len;
+                row(d).ovl = 0ull; row(d).parent = -1;
+                regRow(base + i) = d;
+                return (mt & MT_M_REMOVED) != 0;
+            });
+            rem |= wave_ballot(rm);
+        }
+        rfN = n < f0 ? f0 - n : 0;
+        rowTop = t0 + (n > f0 ? n - f0 : 0);
         wave_sync();
         // the entry's previous clones, unless pasted (then they are tree rows), are released
-        const int on = uni(g.client) == c ? uni(g.n) : 0, of = uni(g.flags);
+        MtReg& g = regs[e];
+        const int on = uni(g.client) == c ? uni(g.n) : 0, of = uni(g.flags), oo = uni(g.off);
         if (on > 0 && !(of & 2)) {
             for (int i = 0; i < on; i++) {
-                const int s = uni(g.rows[i]);
+                const int s = uni(regRow(oo + i));
                 row(s).meta = uni(row(s).meta) & ~MT_M_REG;
                 freeRow(s);
             }
         }
-        int fl = 0;
-        for (int i = 0; i < n; i++) {
-            const int s = uni(sc->hold[i]);
-            const int k = uni(sc->hold[32 + i]);
-            const uint32_t mt = uni(row(s).meta);
-            if (mt & MT_M_REMOVED) fl |= 1;
-            row(k).len = row(s).len; row(k).seq = row(s).seq; row(k).rseq = row(s).rseq;
-            row(k).meta = (mt & (MT_M_CLIENT | MT_M_REMOVED | MT_M_MARKER)) | MT_M_REG;
-            row(k).rcl = row(s).rcl; row(k).props = row(s).props; row(k).mid = row(s).mid;
-            row(k).toff = row(s).toff; row(k).tcap = (mt & MT_M_MARKER) ? 0 : uni(row(s).len);
-            row(k).ovl = 0ull; row(k).parent = -1;
-            wave_for(1, [&](int) MT_LAM { g.rows[i] = k; });
-        }
-        wave_for(1, [&](int) MT_LAM { g.client = c; g.name = name; g.n = n; g.flags = fl; });
+        const int fl = rem ? 1 : 0;
+        wave_for(1, [&](int) MT_LAM { g.client = c; g.name = name; g.n = n; g.flags = fl; g.off = base; });
+        regTop = base + n;
         wave_sync();
+    }
+    // Copying compaction of the register row arena: every entry's ids into the other half.
+    MT_HD void regCompact() {
+        const auto ns = wave_map(MT_REG_CAP, [&](int i) MT_LAM { return regs[i].client >= 0 ? regs[i].n : 0; });
+        const auto os = wave_map(MT_REG_CAP, [&](int i) MT_LAM { return regs[i].off; });
+        const int other = regHalf ^ 1;
+        int* dst = regr + (size_t)other * regCap;
+        int w = 0;
+        for (int e = 0; e < MT_REG_CAP; e++) {
+            const int n = wave_at(ns, e), o = wave_at(os, e);
+            if (n <= 0) continue;
+            for (int b0 = 0; b0 < n; b0 += MT_WAVE) {
+                const int m = (n - b0) < MT_WAVE ? (n - b0) : MT_WAVE;
+                wave_for(m, [&](int k) MT_LAM { dst[w + b0 + k] = regRow(o + b0 + k); });
+            }
+            const int w0 = w;
+            wave_for(1, [&](int) MT_LAM { regs[e].off = w0; });
+            w += n;
+        }
+        wave_sync();
+        regHalf = other; regTop = w;
     }
     // Paste (applyInsertOp's register branch, MT/client.ts:436-444, then insertSegments
     // MT/mergeTree.ts:1974-2011 with blockInsert :2207-2241): every clone in order at
@@ -2725,14 +2784,14 @@ template <int RES, bool FULL = true> struct MtEngT {
         const int e = regFind(c, name, false);
         if (e < 0) return;                                     // registerCollection.get: undefined
         MtReg& g = regs[e];
-        const int n = uni(g.n), fl = uni(g.flags);
+        const int n = uni(g.n), fl = uni(g.flags), o = uni(g.off);
         if (n == 0) return;                                    // no segments: the op does nothing
         if (fl & 3) { status |= MT_DS_UNSUPPORTED; return; }   // re-linked objects / removed clones
         if (walk(MT_WALK_SPLIT, pos, r, c, -1, 0) == MT_W_OK) c_rows += 2;   // ensureIntervalBoundary
         if (status) return;
         int ip = pos;
         for (int i = 0; i < n; i++) {
-            const int k = uni(g.rows[i]);
+            const int k = uni(regRow(o + i));
             const uint32_t mt = (uni(row(k).meta) & ~(MT_M_REG | MT_M_CLIENT)) | (uint32_t)c;
             const int L = uni(row(k).len);
             row(k).meta = mt; row(k).seq = sq;

@@ -17,7 +17,7 @@ struct mt_ctx {
     MtDocLayout tot{};                                                     // pool element totals
     // mt_checkpoint shadows (device)
     void *ck_rows = nullptr, *ck_blk = nullptr, *ck_heap = nullptr, *ck_win = nullptr, *ck_text = nullptr,
-         *ck_pset = nullptr, *ck_hdr = nullptr, *ck_hold = nullptr, *ck_ovx = nullptr, *ck_mid = nullptr, *ck_reg = nullptr;
+         *ck_pset = nullptr, *ck_hdr = nullptr, *ck_hold = nullptr, *ck_ovx = nullptr, *ck_mid = nullptr, *ck_reg = nullptr, *ck_regr = nullptr;
     bool ck_valid = false;
     std::unordered_map<uint32_t, std::vector<std::string>> doc_clients;   // mt_set_doc_client_names
     std::string err;

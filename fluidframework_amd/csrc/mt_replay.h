@@ -109,7 +109,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
                 // capture headroom for this message: a range op emits at most one record per
                 // character of its range (every segment it touches is visible in it), or per row
                 const bool range = ty == MT_OP_REMOVE || ty == MT_OP_ANNOTATE || ty == MT_OP_CUT;
-                long long k = 1;
+                long long k = ty == MT_OP_PASTE ? (long long)e.regCount(c, (int)poff) : 1;   // a paste: its clones
                 if (range) {
                     k = (fl & (MT_OPF_REL1 | MT_OPF_REL2)) ? (long long)e.rowTop : (long long)p2 - (long long)p1;
                     if (k > (long long)e.rowTop) k = e.rowTop;

@@ -66,18 +66,22 @@ inline void quote16(std::string& o, const uint16_t* s, size_t n) {
 inline void put_int(std::string& o, long long v) { o += std::to_string(v); }
 
 // A property map as JSON: array-index keys ascending, then insertion order.
-inline void props_json(std::string& o, const MtPSet& p, const MtNames& nm) {
-    int order[MT_PSK]; int m = 0;
-    int idx[MT_PSK]; int ni = 0;
-    for (int i = 0; i < p.n; i++) if (nm.key_index[p.key[i]] != 0xFFFFFFFFu) idx[ni++] = i;
-    std::sort(idx, idx + ni, [&](int a, int b) { return nm.key_index[p.key[a]] < nm.key_index[p.key[b]]; });
+// (p: the map's first chunk; key i is in chunk i / 16, MtPSet)
+inline int pset_key(const MtPSet* p, int i) { return p[i >> 4].key[i & 15]; }
+inline int pset_val(const MtPSet* p, int i) { return p[i >> 4].val[i & 15]; }
+inline void props_json(std::string& o, const MtPSet* p, const MtNames& nm) {
+    const int n = p->n < MT_PKEYS ? p->n : MT_PKEYS;
+    int order[MT_PKEYS]; int m = 0;
+    int idx[MT_PKEYS]; int ni = 0;
+    for (int i = 0; i < n; i++) if (nm.key_index[pset_key(p, i)] != 0xFFFFFFFFu) idx[ni++] = i;
+    std::sort(idx, idx + ni, [&](int a, int b) { return nm.key_index[pset_key(p, a)] < nm.key_index[pset_key(p, b)]; });
     for (int i = 0; i < ni; i++) order[m++] = idx[i];
-    for (int i = 0; i < p.n; i++) if (nm.key_index[p.key[i]] == 0xFFFFFFFFu) order[m++] = i;
+    for (int i = 0; i < n; i++) if (nm.key_index[pset_key(p, i)] == 0xFFFFFFFFu) order[m++] = i;
     o.push_back('{');
     for (int q = 0; q < m; q++) {
         if (q) o.push_back(',');
         const int i = order[q];
-        o += nm.key_json[p.key[i]]; o.push_back(':'); o += nm.value_json[p.val[i]];
+        o += nm.key_json[pset_key(p, i)]; o.push_back(':'); o += nm.value_json[pset_val(p, i)];
     }
     o.push_back('}');
 }
@@ -96,10 +100,10 @@ inline void seg_json(std::string& o, const MtSnapView& v, const MtNames& nm, int
     const int ps = v.R[s].props;
     if (marker) {
         o += "{\"marker\":{\"refType\":"; put_int(o, v.R[s].toff); o += "}";
-        if (ps >= 0) { o += ",\"props\":"; props_json(o, v.pset[ps], nm); }
+        if (ps >= 0) { o += ",\"props\":"; props_json(o, v.pset + ps, nm); }
         o += "}";
     } else if (ps >= 0) {
-        o += "{\"text\":"; quote16(o, txt, tn); o += ",\"props\":"; props_json(o, v.pset[ps], nm); o += "}";
+        o += "{\"text\":"; quote16(o, txt, tn); o += ",\"props\":"; props_json(o, v.pset + ps, nm); o += "}";
     } else {
         quote16(o, txt, tn);
     }
@@ -108,11 +112,12 @@ inline void seg_json(std::string& o, const MtSnapView& v, const MtNames& nm, int
 inline bool props_match(const MtSnapView& v, const MtNames& nm, int a, int b) {
     if (a == b) return true;
     if (a < 0 || b < 0) return false;
-    const MtPSet& pa = v.pset[a]; const MtPSet& pb = v.pset[b];
-    if (pa.n != pb.n) return false;
-    for (int i = 0; i < pa.n; i++) {
+    const MtPSet* pa = v.pset + a; const MtPSet* pb = v.pset + b;
+    if (pa->n != pb->n) return false;
+    for (int i = 0; i < pa->n; i++) {
         bool f = false;
-        for (int j = 0; j < pb.n; j++) if (pb.key[j] == pa.key[i] && nm.value_class[pb.val[j]] == nm.value_class[pa.val[i]]) f = true;
+        for (int j = 0; j < pb->n; j++)
+            if (pset_key(pb, j) == pset_key(pa, i) && nm.value_class[pset_val(pb, j)] == nm.value_class[pset_val(pa, i)]) f = true;
         if (!f) return false;
     }
     return true;
@@ -316,7 +321,7 @@ inline void dump_rows(const MtSnapView& v, const MtNames& nm, std::vector<int32_
         const bool removed = (mt & MT_M_REMOVED) != 0;
         r[3] = removed ? v.R[s].rseq : INT32_MIN; r[4] = removed ? (int32_t)v.R[s].rcl : -1;
         r[5] = (int32_t)(v.R[s].ovl & 0xFFFFFFFFull); r[6] = (int32_t)(v.R[s].ovl >> 32);
-        if (v.R[s].props >= 0) { std::string js; props_json(js, v.pset[v.R[s].props], nm); r[7] = (int32_t)(fnv1a(js) & 0x7FFFFFFF); }
+        if (v.R[s].props >= 0) { std::string js; props_json(js, v.pset + v.R[s].props, nm); r[7] = (int32_t)(fnv1a(js) & 0x7FFFFFFF); }
         else r[7] = -1;
         r[8] = (mt & MT_M_MARKER) ? v.R[s].toff : -1;
         int ix[MT_MAXH + 2]; int depth = 0;

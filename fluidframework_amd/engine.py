@@ -44,7 +44,7 @@ class ExchangeError(MergeTreeError):
 class MtLimits(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint32) for n in ("max_docs", "rows_per_doc", "blocks_per_doc", "text_per_doc",
                                                "propsets_per_doc", "heap_per_doc", "window_per_doc",
-                                               "markers_per_doc")]
+                                               "markers_per_doc", "register_rows_per_doc")]
 
 
 class MtDocCounters(ctypes.Structure):
@@ -132,10 +132,11 @@ class Engine:
     def __init__(self, max_docs: int, rows_per_doc: int = 4096, blocks_per_doc: int = 0, text_per_doc: int = 0,
                  propsets_per_doc: int = 0, heap_per_doc: int = 0, window_per_doc: int = 0, device: int = 0,
                  lib_path: str | None = None, prefix: str = "mt_", per_doc: dict | None = None,
-                 markers_per_doc: int = 0):
+                 markers_per_doc: int = 0, register_rows_per_doc: int = 0):
         """per_doc: optional dict of per-document capacity arrays (keys rows_per_doc,
-        blocks_per_doc, text_per_doc, propsets_per_doc, heap_per_doc, window_per_doc;
-        missing keys use the scalar arguments) -> mt_create_docs."""
+        blocks_per_doc, text_per_doc, propsets_per_doc, heap_per_doc, window_per_doc,
+        markers_per_doc, register_rows_per_doc; missing keys use the scalar arguments) ->
+        mt_create_docs."""
         # MTGPU_LIB: an alternate build of the same HIP engine (e.g. another occupancy target)
         path = lib_path or os.environ.get("MTGPU_LIB") or LIB_PATH
         if not os.path.exists(path):
@@ -144,13 +145,13 @@ class Engine:
         self.fn = _bind(self.lib, prefix)
         self.max_docs = max_docs
         lim = MtLimits(max_docs, rows_per_doc, blocks_per_doc, text_per_doc, propsets_per_doc, heap_per_doc,
-                       window_per_doc, markers_per_doc)
+                       window_per_doc, markers_per_doc, register_rows_per_doc)
         h = ctypes.c_void_p()
         if per_doc:
             arr = (MtLimits * max_docs)()
             scal = dict(rows_per_doc=rows_per_doc, blocks_per_doc=blocks_per_doc, text_per_doc=text_per_doc,
                         propsets_per_doc=propsets_per_doc, heap_per_doc=heap_per_doc, window_per_doc=window_per_doc,
-                        markers_per_doc=markers_per_doc)
+                        markers_per_doc=markers_per_doc, register_rows_per_doc=register_rows_per_doc)
             cols = {k: (np.asarray(per_doc[k], np.uint32) if k in per_doc else None) for k in scal}
             for i in range(max_docs):
                 for k, v in scal.items():
@@ -379,7 +380,7 @@ class Engine:
 
     def doc_pset(self, doc: int, pset_id: int):
         """(key ids, value ids) of a document's device property set, insertion order."""
-        k, v, n = np.zeros(16, np.uint16), np.zeros(16, np.int32), ctypes.c_uint32()
+        k, v, n = np.zeros(64, np.uint16), np.zeros(64, np.int32), ctypes.c_uint32()
         self._check(self.fn["doc_pset"](self.h, doc, pset_id, k.ctypes.data, v.ctypes.data, ctypes.byref(n)),
                     "mt_doc_pset")
         return k[:n.value].copy(), v[:n.value].copy()

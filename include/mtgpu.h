@@ -191,6 +191,7 @@ typedef struct mt_limits {
     uint32_t heap_per_doc;      /* zamboni heap entries                           */
     uint32_t window_per_doc;    /* collab-window row list                         */
     uint32_t markers_per_doc;   /* marker-id table (idToSegment); 0 = 1024        */
+    uint32_t register_rows_per_doc; /* clone rows all registers hold at once; 0 = 256 */
 } mt_limits;
 
 typedef struct mt_ctx mt_ctx;
@@ -426,7 +427,8 @@ int  mt_delta_records(mt_ctx* ctx, const mt_delta_rec** out, uint64_t* n);
  * launches the batch took. */
 int  mt_delta_text(mt_ctx* ctx, const uint16_t** out, uint64_t* n, uint32_t* launches);
 /* The keys and values (host-interned ids, value -1 never occurs) of property set
- * pset_id of document doc, in insertion order; returns the count in *n (<= 16). */
+ * pset_id of document doc, in insertion order; returns the count in *n (<= 64: keys and
+ * values must have room for 64 entries). */
 int  mt_doc_pset(mt_ctx* ctx, uint32_t doc, int32_t pset_id, uint16_t* keys, int32_t* values, uint32_t* n);
 int  mt_dump_segments(mt_ctx* ctx, uint32_t doc_id, int32_t** rows, uint32_t* n_rows);
 void mt_free(void* p);

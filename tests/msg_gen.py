@@ -35,6 +35,9 @@ from oracle_lib import OracleDoc
 SPECIAL = ['"', "\\", "\n", "\t", "\r", "\x01", "\x1f", "\x7f", "/", "é", "中", " ", "😀", "𝄞",
            "\ud800", "\udfff", "\udc00", " ", "<", "&"]
 KEYS = ["0", "1", "2", "10", "k", "bold", "a b", "ключ", "x\"y", "4294967295", "01"]
+# wide property maps (the "wide_props" surface): 45 more keys, index-like ones among them, so
+# one segment's map grows well past 16 keys (56 distinct keys at most: within MT_PKEYS = 64)
+WIDE_KEYS = KEYS + [f"w{i}" for i in range(36)] + ["3", "7", "11", "12", "40", "99", "100", "1000", "255"]
 VALUES = ["s", "ü", "", 0, 1, -3, 1.5, 1e21, 0.25, True, False, {"a": 1}, [1, 2], {"0": "x", "b": [True]},
           {"n": None}, "😀"]
 
@@ -44,7 +47,8 @@ class StreamGen:
                  p_group: float = 0.15, p_marker: float = 0.08, p_annotate: float = 0.2, p_remove: float = 0.3,
                  p_special: float = 0.25, long_every: int = 40, max_ins: int = 9, id_prefix: str = "cli",
                  max_total_clients: int | None = None, p_marker_id: float = 0.0, p_relative: float = 0.0,
-                 capture: bool = False, p_register: float = 0.0):
+                 capture: bool = False, p_register: float = 0.0, p_wide: float = 0.0, reg_names: int = 0,
+                 reg_span: int = 10):
         self.rng = random.Random(seed)
         self.lag, self.churn, self.p_nonop, self.p_group = lag, churn, p_nonop, p_group
         self.p_marker, self.p_annotate, self.p_remove, self.p_special = p_marker, p_annotate, p_remove, p_special
@@ -54,6 +58,10 @@ class StreamGen:
         self.p_marker_id, self.p_relative = p_marker_id, p_relative
         self.marker_ids: list[str] = []           # ids of markers inserted so far (idToSegment)
         self.p_register = p_register
+        self.p_wide = p_wide
+        # register names per client (0: REGS) and the longest copy / cut range
+        self.reg_names = [f"r{i}" for i in range(reg_names)] if reg_names else self.REGS
+        self.reg_span = reg_span
         self.total = 0
         self.active: dict[str, int] = {}          # long id -> latest refSeq
         for _ in range(clients):
@@ -84,8 +92,9 @@ class StreamGen:
     def _props(self, allow_null=True) -> dict:
         r = self.rng
         d = {}
-        for _ in range(r.randint(1, 3)):
-            k = r.choice(KEYS)
+        wide = self.p_wide > 0 and r.random() < self.p_wide     # (no draw otherwise: other surfaces keep their streams)
+        for _ in range(r.randint(18, 45) if wide else r.randint(1, 3)):
+            k = r.choice(WIDE_KEYS if wide else KEYS)
             d[k] = None if (allow_null and r.random() < 0.2) else r.choice(VALUES)
         return d
 
@@ -146,7 +155,7 @@ class StreamGen:
         the reference (not modelled), and pasted clones of removed segments are off the
         engine's path.  Its length change is the clones' total cachedLength."""
         r = self.rng
-        name = r.choice(self.REGS)
+        name = r.choice(self.reg_names)
         x = r.random()
         if x < 0.45:
             info = self.obs.register_info(self._author, name)
@@ -155,7 +164,7 @@ class StreamGen:
         if L == 0:
             return None
         s = r.randrange(L)
-        e = min(L, s + 1 + r.randrange(10))
+        e = min(L, s + 1 + r.randrange(self.reg_span))
         if x < 0.75:
             return {"type": 0, "pos1": s, "pos2": e, "register": name}, 0
         return {"type": 1, "pos1": s, "pos2": e, "register": name}, -(e - s)

@@ -14,8 +14,8 @@ from emu_lib import emu_engine
 from fluidframework_amd.engine import ClientGroup, Engine
 from msg_gen import stream
 
-LIMITS = dict(rows_per_doc=30000, window_per_doc=8192, propsets_per_doc=30000, text_per_doc=1 << 19,
-              blocks_per_doc=16384, heap_per_doc=30000)
+LIMITS = dict(rows_per_doc=60000, window_per_doc=8192, propsets_per_doc=30000, text_per_doc=1 << 19,
+              blocks_per_doc=16384, heap_per_doc=30000, register_rows_per_doc=20000)
 # dump columns that do not depend on how each side numbers clients (len, seq,
 # removedSeq, props hash, marker refType, tree depth and path)
 COLS = [0, 1, 3, 7, 8, 9, 10, 11]
@@ -34,12 +34,23 @@ SURFACES = {
                      max_ins=4, long_every=0),
     # register cut / copy / paste (MT/client.ts:347-350, :425-444, :600-608), markers included
     "registers": dict(clients=3, lag=8, p_register=0.3, p_marker=0.15, p_marker_id=0.3, p_group=0.1),
+    # 20 register names per client (60 registers in use) and copies spanning up to ~250
+    # segments: the register row arena's compaction and clone lists past the old caps
+    "registers_wide": dict(clients=3, lag=8, p_register=0.25, reg_names=20, reg_span=700, max_ins=2, p_remove=0.15,
+                           p_annotate=0.35, long_every=0),
+    # property maps of 18-56 keys (segment specs and annotates): several MtPSet chunks per map
+    "wide_props": dict(clients=3, lag=10, p_annotate=0.45, p_marker=0.15, p_wide=0.5),
 }
+
+
+# per-surface limit overrides: a register row arena small enough that the stream's copies
+# overflow it many times over (copying compaction), large enough for the clones live at once
+SURFACE_LIMITS = {"registers_wide": dict(register_rows_per_doc=8192)}
 
 
 def check(factory, surface, seed=1, n_docs=3, n_msgs=1200):
     streams = [stream(seed * 101 + d, n_msgs, **SURFACES[surface]) for d in range(n_docs)]
-    g = ClientGroup(factory(n_docs, **LIMITS))
+    g = ClientGroup(factory(n_docs, **{**LIMITS, **SURFACE_LIMITS.get(surface, {})}))
     clients = [g.new_client({"newMergeTreeSnapshotFormat": True}) for _ in range(n_docs)]
     for c, (msgs, _) in zip(clients, streams):
         c.startOrUpdateCollaboration("observer")
@@ -95,6 +106,17 @@ def test_stream_generator_covers_the_surface():
                                                            else [m["contents"]]) if "register" in x]
     kinds = {(x["type"], "pos2" in x) for x in reg}
     assert kinds == {(0, False), (0, True), (1, True)} and len(reg) > 150     # paste, copy, cut
+    msgs, obs = stream(12, 1200, **SURFACES["registers_wide"])
+    names = {(m["clientId"], x["register"]) for m in msgs if m["type"] == "op"
+             for x in (m["contents"]["ops"] if m["contents"]["type"] == 3 else [m["contents"]]) if "register" in x}
+    assert len(names) > 40                                            # registers in use at once (cap was 8)
+    assert max(obs.register_info(cl, nm)["n"] for cl, nm in names) > 28   # clones of one copy (cap was 28)
+    msgs, obs = stream(11, 1200, **SURFACES["wide_props"])
+    import json
+    blobs, _ = obs.snapshot(msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"])
+    segs = [x["json"] if isinstance(x, dict) and "json" in x else x for b in blobs for x in json.loads(b).get("segments", [])]
+    widths = [len(j["props"]) for j in segs if isinstance(j, dict) and "props" in j]
+    assert max(widths) > 32 and sum(w > 16 for w in widths) > 20      # maps of several MtPSet chunks
 
 
 @pytest.mark.gpu
