@@ -397,7 +397,6 @@ MT_INLINE bool vis_rc(int seq, uint32_t meta, int rseq, uint32_t rcl, unsigned l
 
 struct BlkH { int len, parent, n, height, scour; };
 struct ChildL { int len; bool tie; };
-struct LeafR { int len, seq, rseq, toff, props, tcap; uint32_t meta, rcl; unsigned long long ovl; };   // a leaf row's fields
 struct WinI { int id; int delta; int parent; bool live; bool recycle; };
 
 enum { MT_WALK_SPLIT = 0, MT_WALK_INSERT = 1 };
@@ -1631,51 +1630,6 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (mt & MT_M_INWIN) winAddKnown(n, mt & ~(MT_M_INWIN | MT_M_HREF));   // n's meta as just written
         return n;
     }
-    // splitRow with row s's fields already loaded (f) and its leaf block B: the right half's
-    // record is written by 12 lanes in one store, and nothing of s is read again.
-    MT_HD int splitRowKnown(int s, int pos, const LeafR& f, int B) {
-        MT_EV2(5, 1);
-        const int n = allocRow();
-        if (n < 0) return -1;
-        const uint32_t nm = f.meta & ~(MT_M_INWIN | MT_M_HREF);
-        const int v0 = f.len - pos, v1 = f.seq, v2 = f.rseq, v3 = (int)nm, v4 = f.toff + pos, v5 = f.props, v6 = B,
-                  v7 = f.tcap - pos, v8 = (int)(uint32_t)f.ovl, v9 = (int)(uint32_t)(f.ovl >> 32), v10 = (int)f.rcl;
-        wave_for(12, [&](int k) MT_LAM {
-            const int v = k == 0 ? v0 : k == 1 ? v1 : k == 2 ? v2 : k == 3 ? v3 : k == 4 ? v4 : k == 5 ? v5 : k == 6 ? v6 :
-                          k == 7 ? v7 : k == 8 ? v8 : k == 9 ? v9 : k == 10 ? v10 : 0;
-            ((int*)&row(n))[k] = v;
-        });
-        row(s).len = pos; row(s).tcap = pos;                // each row owns [toff, toff+tcap) of the arena
-        if (f.ovl >> 63) ovxCopy(s, n);
-        if (f.meta & MT_M_INWIN) winAddKnown(n, nm);
-        return n;
-    }
-    // The fields of leaf block rows ch[0..n) (one row per lane, one round trip).
-    MT_HD LaneArr<LeafR> leafLoad(const LaneArr<int>& ch, int n) const {
-        return wave_map(n, [&](int j) MT_LAM {
-            const int s = own(ch, j);
-            LeafR f;
-            f.len = row(s).len; f.seq = row(s).seq; f.rseq = row(s).rseq; f.toff = row(s).toff; f.props = row(s).props;
-            f.tcap = row(s).tcap; f.meta = row(s).meta; f.rcl = row(s).rcl; f.ovl = row(s).ovl;
-            return f;
-        });
-    }
-    // Lane j's leaf row (j uniform).
-    MT_HD static LeafR leafAt(const LaneArr<LeafR>& a, int j) {
-        LeafR f;
-        f.len = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).len; }), j);
-        f.seq = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).seq; }), j);
-        f.rseq = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).rseq; }), j);
-        f.toff = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).toff; }), j);
-        f.props = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).props; }), j);
-        f.tcap = wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return own(a, k).tcap; }), j);
-        f.meta = (uint32_t)wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return (int)own(a, k).meta; }), j);
-        f.rcl = (uint32_t)wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return (int)own(a, k).rcl; }), j);
-        const uint32_t lo = (uint32_t)wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return (int)(uint32_t)own(a, k).ovl; }), j);
-        const uint32_t hi = (uint32_t)wave_at(wave_map(MT_WAVE, [&](int k) MT_LAM { return (int)(uint32_t)(own(a, k).ovl >> 32); }), j);
-        f.ovl = (unsigned long long)lo | ((unsigned long long)hi << 32);
-        return f;
-    }
     // Insert `node` at child index idx of path level L, splitting full blocks
     // 4/4 upward (insertingWalk :2465-2489, split :2495-2508, updateRoot :1868).
     // `delta` = observer length added under the path (0 for a row split).
@@ -1750,19 +1704,8 @@ template <int RES, bool FULL = true> struct MtEngT {
             // blocks in HBM: children's records (lengths + the next level's block) in one trip
             const bool kpre = !BLKL && h.height > 0;
             LaneArr<int> r0{}, r1{};
-            LaneArr<LeafR> lf{};
             if (kpre) kidsLoad(ch, h.n, r0, r1);
-            LaneArr<ChildL> cl;
-            if (h.height == 0) {                           // leaf rows: every field in one trip (a split needs them)
-                lf = leafLoad(ch, h.n);
-                cl = wave_map(h.n, [&](int j) MT_LAM {
-                    const LeafR f = own(lf, j);
-                    ChildL o;
-                    o.len = vis_rc(f.seq, f.meta, f.rseq, f.rcl, f.ovl, r, c, ovx, ovxN, own(ch, j)) ? f.len : 0;
-                    o.tie = !((f.meta & MT_M_REMOVED) && f.rseq <= r);     // breakTie, as childLens
-                    return o;
-                });
-            } else cl = kpre ? childLens(B, h, ch, r, c, true, kidsLen(r0, r1), lsN) : childLens(B, h, ch, r, c);
+            auto cl = kpre ? childLens(B, h, ch, r, c, true, kidsLen(r0, r1), lsN) : childLens(B, h, ch, r, c);
             MT_QE(1, q1);
             auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
             auto pre = wave_excl_scan8(lens);
@@ -1785,9 +1728,8 @@ template <int RES, bool FULL = true> struct MtEngT {
                 const int s = wave_at(ch, j);
                 lastL = L; lastSplit = false;
                 if (kind == MT_WALK_SPLIT) {
-                    const LeafR f = leafAt(lf, j);
-                    if (pj > 0 && !(f.meta & MT_M_MARKER)) {
-                        const int n = splitRowKnown(s, pj, f, B);
+                    if (pj > 0 && !(uni(row(s).meta) & MT_M_MARKER)) {
+                        const int n = splitRow(s, pj);
                         if (n < 0) return MT_W_FAIL;
                         insertAtPath(L, j + 1, n, 0);
                         if (FULL && drec) {                     // SPLIT, splitLeafSegment (mergeTree.ts:2243-2258)
