@@ -1253,17 +1253,28 @@ template <int RES, bool FULL = true> struct MtEngT {
             return wave_map(m, [&](int k) MT_LAM { return winEntry(own(ids, k), r, c); });
         };
         const int wN0 = winN;
+#ifndef MT_CU_PIPE
+#define MT_CU_PIPE 0
+#endif
+#if MT_CU_PIPE
         LaneArr<WinI> wiNext{};
         LaneArr<int> idNext{};
         if (wN0 > 0) wiNext = winRows(winIds(0), 0);
         if (wN0 > MT_WAVE) idNext = winIds(MT_WAVE);
+#endif
         for (int base = 0; base < wN0; base += MT_WAVE) {
             const int m = (wN0 - base) < MT_WAVE ? (wN0 - base) : MT_WAVE;
+#if MT_CU_PIPE
             const auto wi = wiNext;
             if (base + MT_WAVE < wN0) {
                 wiNext = winRows(idNext, base + MT_WAVE);
                 if (base + 2 * MT_WAVE < wN0) idNext = winIds(base + 2 * MT_WAVE);
             }
+#else
+            // one chunk at a time (the software-pipelined variant, MT_CU_PIPE, holds two chunks
+            // in VGPRs and costs the hot kernel spills)
+            const auto wi = winRows(winIds(base), base);
+#endif
             auto live = wave_map(m, [&](int k) MT_LAM { return own(wi, k).live; });
             if (prune) {
                 auto rk = wave_rank(live);
