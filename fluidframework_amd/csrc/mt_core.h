@@ -77,8 +77,13 @@
 // block id mod MT_G_BC), write-back, filled by the descents with blocks of height >= MT_G_BCH.
 // A slot holding a higher block is not taken by a lower one, so the top of the tree stays
 // resident and the descents, ancestor chains and path updates reach HBM only near the leaves.
+// Compiled in with -DMT_G_BCACHE=1 only: measured -1 % on config 4 (upper levels already hit
+// L2, and every block access then pays a tag check and flat addressing).
+#ifndef MT_G_BCACHE
+#define MT_G_BCACHE 0
+#endif
 #ifndef MT_G_BC
-#define MT_G_BC 512
+#define MT_G_BC (MT_G_BCACHE ? 512 : 1)
 #endif
 #ifndef MT_G_BCH
 #define MT_G_BCH 1
@@ -91,6 +96,9 @@
 #define MT_G_NW 4
 #endif
 #define MT_G_STG 1024
+#ifndef MT_G_MWMIN
+#define MT_G_MWMIN 512                 // windows up to this many entries are scanned by wave 0 alone
+#endif
 enum { MT_MW_EXIT = 0, MT_MW_SCAN = 1, MT_MW_CHAIN = 2, MT_MW_PREFETCH = 3 };
 // Jobs alternate between two LDS slots, so wave 0 can post an asynchronous job (PREFETCH: no
 // completion barrier) and write the next one while helpers still read the last.
@@ -476,7 +484,10 @@ template <int RES, bool FULL = true> struct MtEngT {
     MtRow* R;
     // Block residency keeps blocks, heap and the first U entries in LDS: their HBM homes (and
     // the property-set pool) are cold there and live in MtCold; other modes keep them in SGPRs.
-    template <class T> using Home = std::conditional_t<RES == MT_RES_BLK, T&, T>;
+#ifndef MT_HBM_COLD_HOMES
+#define MT_HBM_COLD_HOMES 0
+#endif
+    template <class T> using Home = std::conditional_t<RES == MT_RES_BLK || (MT_HBM_COLD_HOMES && RES == MT_RES_HBM), T&, T>;
     int* win;
     Home<int*> uid = mt_cold_v.uid; Home<int*> udelta = mt_cold_v.udelta; Home<int*> uanc = mt_cold_v.uanc;
     Home<MtBlk*> blk = mt_cold_v.blk; Home<MtHeapE*> heap = mt_cold_v.heap;
@@ -495,7 +506,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     MT_HD MtRow& row(int s) const { if constexpr (LDS) return mt_lds().rows[s]; else return R[s]; }
     MT_HD MtBlk& bk(int b) const {
         if constexpr (LDS) return mt_lds().blk[b]; else if constexpr (BLKL) return mt_ldsb().blk[b];
-        else if constexpr (BIG) {                       // block cache hit: the LDS copy is the current one
+        else if constexpr (BIG && MT_G_BCACHE) {        // block cache hit: the LDS copy is the current one
             const int s = b & (MT_G_BC - 1);
             return mt_ldsg().btag[s] == b ? mt_ldsg().bc[s] : blk[b];
         } else return blk[b];
@@ -503,7 +514,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     // MT_RES_BIG: install block B (its current record in lanes 0..15) in its cache slot, whose
     // tag is tg, unless the slot holds a higher live block; the evicted block is written back.
     MT_HD void bcInstall(int B, int tg, const LaneArr<int>& w, int hb) {
-        if constexpr (BIG) {
+        if constexpr (BIG && MT_G_BCACHE) {
             if (!bcOn || hb < MT_G_BCH || tg == B) return;
             const int s = B & (MT_G_BC - 1);
             MtLdsBig& G = mt_ldsg();
@@ -518,7 +529,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         } else { (void)B; (void)tg; (void)w; (void)hb; }
     }
     MT_HD int bcTag(int B) const {
-        if constexpr (BIG) return uni(mt_ldsg().btag[B & (MT_G_BC - 1)]);
+        if constexpr (BIG && MT_G_BCACHE) return uni(mt_ldsg().btag[B & (MT_G_BC - 1)]);
         else { (void)B; return 0; }
     }
     MT_HD MtHeapE& hp(int k) const {
@@ -734,11 +745,12 @@ template <int RES, bool FULL = true> struct MtEngT {
             MtLdsBig& G = mt_ldsg();
             copyI((int*)G.heap, (const int*)heap, 2 * (heapN + 1));
             copyI(G.win, win, winN < lr ? winN : lr);
-            for (int base = 0; base < MT_G_BC; base += MT_WAVE) wave_for(MT_WAVE, [&](int k) MT_LAM { G.btag[base + k] = MT_BC_EMPTY; });
+            for (int base = 0; MT_G_BCACHE && base < MT_G_BC; base += MT_WAVE)
+                wave_for(MT_WAVE, [&](int k) MT_LAM { G.btag[base + k] = MT_BC_EMPTY; });
             for (int base = 0; base < MT_G_HT; base += MT_WAVE)
                 wave_for(MT_WAVE, [&](int k) MT_LAM { G.htk[base + k] = MT_BC_EMPTY; G.htv[base + k] = 0; });
             htOk = false; hlistN = 0;
-            bcOn = !(lb & MT_BIGF_NO_BCACHE);                   // lb: MT_BIGF_* switches (A/B)
+            bcOn = MT_G_BCACHE && !(lb & MT_BIGF_NO_BCACHE);    // lb: MT_BIGF_* switches (A/B)
             pfOn = MT_G_NW > 1 && !(lb & MT_BIGF_NO_PREFETCH);
             htOn = !(lb & MT_BIGF_NO_TABLE);
             wave_sync();
@@ -785,7 +797,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             copyI((int*)heap, (const int*)G.heap, 2 * (heapN + 1));
             copyI(win, G.win, winN < lRows ? winN : lRows);
             // write the cached blocks back (lane k: slot base + k, four 16-byte quads)
-            for (int base = 0; base < MT_G_BC; base += MT_WAVE) {
+            for (int base = 0; MT_G_BCACHE && base < MT_G_BC; base += MT_WAVE) {
                 wave_for(MT_WAVE, [&](int k) MT_LAM {
                     const int t = G.btag[base + k];
                     if (t != MT_BC_EMPTY) {
@@ -894,13 +906,13 @@ template <int RES, bool FULL = true> struct MtEngT {
     MT_HD LaneArr<int> blkLoad(int B, BlkH& h) {
         LaneArr<int> w;
         int tg = 0;
-        if constexpr (BIG) {                              // explicit LDS / HBM load, then fill
+        if constexpr (BIG && MT_G_BCACHE) {               // explicit LDS / HBM load, then fill
             tg = bcTag(B);
             if (tg == B) w = wave_map(16, [&](int i) MT_LAM { return ((const int*)&mt_ldsg().bc[B & (MT_G_BC - 1)])[i]; });
             else w = wave_map(16, [&](int i) MT_LAM { return ((const int*)&blk[B])[i]; });
         } else w = wave_map(16, [&](int i) MT_LAM { return ((const int*)&bk(B))[i]; });
         h.len = wave_at(w, 8); h.parent = wave_at(w, 9); h.n = wave_at(w, 10); h.height = wave_at(w, 11); h.scour = wave_at(w, 12);
-        if constexpr (BIG) bcInstall(B, tg, w, h.height);
+        if constexpr (BIG && MT_G_BCACHE) bcInstall(B, tg, w, h.height);
         const int n = h.n;
         return wave_map(8, [&](int j) MT_LAM { return j < n ? own(w, j) : -1; });
     }
@@ -925,7 +937,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         const int o = (j & 3) << 4;
         const auto w = wave_shfl(j < 4 ? r0 : r1, [o](int t) MT_LAM { return o + (t & 15); });
         h.len = wave_at(w, 8); h.parent = wave_at(w, 9); h.n = wave_at(w, 10); h.height = wave_at(w, 11); h.scour = wave_at(w, 12);
-        if constexpr (BIG) { if (bcOn && h.height >= MT_G_BCH) bcInstall(b, bcTag(b), w, h.height); } else (void)b;
+        if constexpr (BIG && MT_G_BCACHE) { if (bcOn && h.height >= MT_G_BCH) bcInstall(b, bcTag(b), w, h.height); } else (void)b;
         const int n = h.n;
         return wave_map(8, [&](int i) MT_LAM { return i < n ? own(w, i) : -1; });
     }
@@ -1119,7 +1131,15 @@ template <int RES, bool FULL = true> struct MtEngT {
         MtLdsBig& G = mt_ldsg();
         int newWin = 0; nU = 0;
         const int wN0 = winN;
-        for (int r0 = 0; r0 < wN0; r0 += MT_G_STG) {
+        if (wN0 <= MT_G_MWMIN) {                    // a few chunks: wave 0 alone, no barriers
+            for (int base = 0; base < wN0; base += MT_WAVE) {
+                const int m = (wN0 - base) < MT_WAVE ? (wN0 - base) : MT_WAVE;
+                const auto ids = wave_map(m, [&](int k) MT_LAM { return wn(base + k); });
+                const auto wi = wave_map(m, [&](int k) MT_LAM { return winEntry(own(ids, k), r, c); });
+                placeChunk(wi, base, m, prune, newWin);
+            }
+        }
+        for (int r0 = 0; wN0 > MT_G_MWMIN && r0 < wN0; r0 += MT_G_STG) {
             const int n = (wN0 - r0) < MT_G_STG ? (wN0 - r0) : MT_G_STG;
             mwRun(MT_MW_SCAN, r, c, r0, n);
             for (int q = 0; q < n; q += MT_WAVE) {
