@@ -484,10 +484,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     MtRow* R;
     // Block residency keeps blocks, heap and the first U entries in LDS: their HBM homes (and
     // the property-set pool) are cold there and live in MtCold; other modes keep them in SGPRs.
-#ifndef MT_HBM_COLD_HOMES
-#define MT_HBM_COLD_HOMES 0
-#endif
-    template <class T> using Home = std::conditional_t<RES == MT_RES_BLK || (MT_HBM_COLD_HOMES && RES == MT_RES_HBM), T&, T>;
+    template <class T> using Home = std::conditional_t<RES == MT_RES_BLK, T&, T>;
     int* win;
     Home<int*> uid = mt_cold_v.uid; Home<int*> udelta = mt_cold_v.udelta; Home<int*> uanc = mt_cold_v.uanc;
     Home<MtBlk*> blk = mt_cold_v.blk; Home<MtHeapE*> heap = mt_cold_v.heap;
