@@ -32,6 +32,9 @@
 #define MT_MAXH 16                    // max tree height (7^16 segments)
 #define MT_PSK 16                     // property keys per MtPSet chunk
 #define MT_PKEYS 64                   // keys of one property map, one per lane (more: PROPS_TOO_MANY)
+#ifndef MT_PATH_RESUME
+#define MT_PATH_RESUME 1              // opRange: end walk and range walk start below the root
+#endif
 #define MT_MAXN 8                     // MaxNodesInBlock, MT/mergeTree.ts:350
 #define MT_GRAN 256                   // TextSegmentGranularity, MT/mergeTree.ts:1056
 #define MT_ZMAX 2                     // zamboniSegmentsMaxCount, MT/mergeTree.ts:1058
@@ -369,6 +372,7 @@ struct __attribute__((aligned(16))) MtLdsBig {
 // per-wave scratch (LDS on the device)
 struct MtScratch {
     int pathB[MT_MAXH + 2], pathJ[MT_MAXH + 2];
+    int pathOff[MT_MAXH + 2], pathLen[MT_MAXH + 2];   // a walk's path blocks: perspective start, length
     int hold[64];
     int holdLen[64];                  // observer length of each held child (scourLeaves)
     int rfree[MT_RFL];                // recycled rows (unlinked, out of the window, no heap entry)
@@ -1715,10 +1719,13 @@ template <int RES, bool FULL = true> struct MtEngT {
             node = NB; idx = uni(sc->pathJ[L - 1]) + 1; L = L - 1;
         }
     }
-    // insertingWalk (MT/mergeTree.ts:2363-2493) for one remote op perspective.
-    MT_HD int walk(int kind, int pos, int r, int c, int cand, int candLen) {
-        if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
+    // insertingWalk (MT/mergeTree.ts:2363-2493) for one remote op perspective.  L0 > 0
+    // resumes at level L0 of the previous walk's path (pathB/pathJ/pathOff above L0 still
+    // valid, U unchanged): the root descent would pick the same children down to there.
+    MT_HD int walk(int kind, int pos, int r, int c, int cand, int candLen, int L0 = 0) {
+        if (!(uValid && uRef == r && uCli == c)) { computeU(r, c, false); L0 = 0; }
         int B = root, L = 0, p = pos;
+        if (L0 > 0) { B = uni(sc->pathB[L0]); L = L0; p = pos - uni(sc->pathOff[L0]); }
         const bool narrow = BIG && nU <= UCAP && !htOk;   // U entries all in LDS: narrow them per level
         int lsN = -1;
         BlkH h;
@@ -1738,6 +1745,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
             auto pre = wave_excl_scan8(lens);
             const int total = wave_sum8(lens);
+            sc->pathOff[L] = pos - p; sc->pathLen[L] = total;
             const bool interior = h.height > 0;
             auto cond = wave_map(h.n, [&](int j) MT_LAM {
                 const int pj = p - own(pre, j), lj = own(cl, j).len;
@@ -2318,12 +2326,19 @@ template <int RES, bool FULL = true> struct MtEngT {
     // lanes (lane L = level L: readlane/writelane, no LDS round trips): block, next
     // child, start/end relative to the block, the child's length, the observer-length
     // delta under the block and (delta capture) the block's observer-view position.
-    MT_HD void rangeMap(int mode, int start, int end, int r, int c, int sq, int opset, bool rewrite) {
-        if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
+    // L0 > 0: the range lies under path block pathB[L0] of the last walks (the deepest block
+    // both boundary walks passed through, tree unchanged since): the root walk would visit
+    // only that branch above it, so the walk starts there and the observer-length change is
+    // added to the ancestors above.  Delta capture starts at the root (observer offsets).
+    MT_HD void rangeMap(int mode, int start, int end, int r, int c, int sq, int opset, bool rewrite, int L0 = 0) {
+        if (!(uValid && uRef == r && uCli == c)) { computeU(r, c, false); L0 = 0; }
         const bool rec = FULL && drec != nullptr;
+        if (rec) L0 = 0;
         LaneArr<int> fB{}, fJ{}, fS{}, fE{}, fL{}, fD{}, fO{};
-        fB = wave_set(fB, 0, root); fS = wave_set(fS, 0, start); fE = wave_set(fE, 0, end);
-        int lastOld = -2, lastNew = -1;
+        const int off0 = L0 > 0 ? uni(sc->pathOff[L0]) : 0;
+        fB = wave_set(fB, 0, L0 > 0 ? uni(sc->pathB[L0]) : root); fS = wave_set(fS, 0, start - off0);
+        fE = wave_set(fE, 0, end - off0);
+        int lastOld = -2, lastNew = -1, topD = 0;
         int L = 0;
         while (L >= 0) {
             const int B = wave_at(fB, L);
@@ -2416,6 +2431,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                 if (mode == MT_MAP_REMOVE) bk(B).len = h.len + obsDelta;
                 const int d = wave_at(fD, L) + obsDelta;
                 L--;
+                if (L < 0) topD = d;
                 if (L >= 0) {
                     const int fl = wave_at(fL, L);
                     fD = wave_set(fD, L, wave_at(fD, L) + d); fS = wave_set(fS, L, wave_at(fS, L) - fl);
@@ -2439,11 +2455,17 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int d = wave_at(fD, L);
             if (d != 0) bk(B).len = h.len + d;
             L--;
+            if (L < 0) topD = d;
             if (L >= 0) {
                 const int fl = wave_at(fL, L);
                 fD = wave_set(fD, L, wave_at(fD, L) + d); fS = wave_set(fS, L, wave_at(fS, L) - fl);
                 fE = wave_set(fE, L, wave_at(fE, L) - fl); fJ = wave_set(fJ, L, wave_at(fJ, L) + 1);
             }
+        }
+        if (L0 > 0 && topD != 0) {                           // ancestors above the start block: one lane each
+            const int dd = topD;
+            wave_for(L0, [&](int l) MT_LAM { const int pb = sc->pathB[l]; bk(pb).len = bk(pb).len + dd; });
+            wave_sync();
         }
         uValid = false;
     }
@@ -2792,12 +2814,21 @@ template <int RES, bool FULL = true> struct MtEngT {
         int w = walk(MT_WALK_SPLIT, start, r, c, -1, 0);
         if (w == MT_W_OK) c_rows += 2;
         if (status) return;
-        w = walk(MT_WALK_SPLIT, end, r, c, -1, 0);
+        // The end boundary's walk resumes at the deepest block of the start walk's path whose
+        // perspective range still holds end (tree and U unchanged unless a block split).
+        int L0 = 0;
+        if (MT_PATH_RESUME && !lastSplit && uValid && uRef == r && uCli == c) {
+            for (int l = lastL; l > 0; l--) {
+                if (end - uni(sc->pathOff[l]) <= uni(sc->pathLen[l])) { L0 = l; break; }
+            }
+        }
+        w = walk(MT_WALK_SPLIT, end, r, c, -1, 0, L0);
         if (w == MT_W_OK) c_rows += 2;
         if (status) return;
+        if (lastSplit || !uValid) L0 = 0;
         MT_PE(MT_PH_SPLIT, t0);
         MT_PB(t1);
-        rangeMap(mode, start, end, r, c, sq, opset, rewrite);
+        rangeMap(mode, start, end, r, c, sq, opset, rewrite, L0);
         MT_PE(MT_PH_RANGE, t1);
         if (status) return;
         zamboni();
