@@ -58,6 +58,7 @@
 #ifndef MT_B_BLKS
 #define MT_B_BLKS 104
 #endif
+#define MT_B_BT 128                   // corrections-table slots (block ids < MT_B_BLKS)
 #define MT_B_U 64                     // U-set entries kept in LDS (the rest, if any, in HBM)
 #ifndef MT_B_HEAP
 #define MT_B_HEAP 94
@@ -346,8 +347,12 @@ struct __attribute__((aligned(16))) MtLdsBlk {
     MtBlk blk[MT_B_BLKS];
     MtHeapE heap[MT_B_HEAP + 2];
     int uid[MT_B_U], udelta[MT_B_U];
-    uint8_t uanc[MT_B_U * MT_L_H];    // block ids < MT_B_BLKS < 255; 255 = none
+    // Per-block perspective corrections of the current U set (Σ delta of the U rows beneath
+    // each block, indexed by block id): a descent level reads its children's lengths as
+    // observer length + correction instead of scanning U (no ancestor chains kept).
+    int bcorr[MT_B_BT];
 };
+static_assert(MT_B_BLKS <= MT_B_BT, "block ids index the corrections table");
 
 // LDS home of a long document's heap, window and U set while mt_replay_big_kernel runs it.
 struct __attribute__((aligned(16))) MtLdsBig {
@@ -548,6 +553,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     // MT_G_U.  U loops run per 64-entry chunk (chunks never straddle the cap), so each
     // chunk picks its home at compile time: forU calls f(std::bool_constant<inLds>, base, m).
     static constexpr bool UL = RES == MT_RES_BLK || RES == MT_RES_BIG;
+    static constexpr bool BT = RES == MT_RES_BLK;   // per-block corrections table (MtLdsBlk::bcorr)
     static constexpr int UCAP = RES == MT_RES_BLK ? MT_B_U : (RES == MT_RES_BIG ? MT_G_U : 0);
     template <bool L> MT_HD int uiAt(int k) const {
         if constexpr (UL && L) { if constexpr (BIG) return mt_ldsg().uid[k]; else return mt_ldsb().uid[k]; }
@@ -565,14 +571,14 @@ template <int RES, bool FULL = true> struct MtEngT {
     }
     template <bool L> MT_HD void ancPutAt(int u, int h, int a) {
         if constexpr (UL && L) {
-            if constexpr (BIG) mt_ldsg().uanc[u * MT_G_H + h] = a;
-            else mt_ldsb().uanc[u * MT_L_H + h] = (uint8_t)(a < 0 ? 255 : a);
+            static_assert(BIG, "block residency keeps per-block corrections, not ancestor chains");
+            mt_ldsg().uanc[u * MT_G_H + h] = a;
         } else ancPut(u, h, a);
     }
     template <bool L> MT_HD int ancGetAt(int u, int h) const {
         if constexpr (UL && L) {
-            if constexpr (BIG) return mt_ldsg().uanc[u * MT_G_H + h];
-            else { const int a = mt_ldsb().uanc[u * MT_L_H + h]; return a == 255 ? -1 : a; }
+            static_assert(BIG, "block residency keeps per-block corrections, not ancestor chains");
+            return mt_ldsg().uanc[u * MT_G_H + h];
         } else return ancGet(u, h);
     }
     MT_HD void ancPutAny(int u, int h, int a) {
@@ -1261,6 +1267,13 @@ template <int RES, bool FULL = true> struct MtEngT {
         MT_EV(0, 1); MT_EV(2, winN);
         MT_QB(q0); MT_QC(4);
         int newWin = 0; nU = 0;
+        if constexpr (BT) {                               // corrections table: cleared per U set
+            for (int base = 0; base < blkTop; base += MT_WAVE) {
+                const int m = (blkTop - base) < MT_WAVE ? (blkTop - base) : MT_WAVE;
+                wave_for(m, [&](int k) MT_LAM { mt_ldsb().bcorr[base + k] = 0; });
+            }
+            wave_sync();
+        }
         // Window rows, one 64-entry chunk at a time, software-pipelined: chunk i+1's row
         // fields are in flight while chunk i is processed, and chunk i+2's window ids behind
         // them (the window entries are distinct rows and compaction only writes entries below
@@ -1326,7 +1339,10 @@ template <int RES, bool FULL = true> struct MtEngT {
                 // blocks in LDS: the chain is walked here; in HBM: level 0 only, the rest below
                 const int HH = BLKL ? H : 0;
                 int a = w.parent;
-                if constexpr (UL) {
+                if constexpr (BT) {                       // the row's delta into every block above it
+                    if (pos < UCAP) uPutAt<true>(pos, w.id, w.delta); else uPutAt<false>(pos, w.id, w.delta);
+                    for (int h = 0; h <= HH && a >= 0; h++) { lds_add(&mt_ldsb().bcorr[a], w.delta); a = bk(a).parent; }
+                } else if constexpr (UL) {
                     if (pos < UCAP) {
                         uPutAt<true>(pos, w.id, w.delta);
                         for (int h = 0; h <= HH; h++) { ancPutAt<true>(pos, h, a); a = (a >= 0) ? bk(a).parent : -1; }
@@ -1346,7 +1362,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         // once; the parent loads of one level are independent, so a level costs one round
         // trip for 512 entries instead of one per chunk.
         const int H = height;
-        for (int g0 = 0; !BLKL && g0 < nU; g0 += 8 * MT_WAVE) {
+        if constexpr (!BLKL) for (int g0 = 0; g0 < nU; g0 += 8 * MT_WAVE) {
             const int nu = nU;
             wave_for(MT_WAVE, [&](int k) MT_LAM {
                 int a[8]; int pos[8];
@@ -1527,6 +1543,16 @@ template <int RES, bool FULL = true> struct MtEngT {
                 return o;
             });
         }
+        if constexpr (BT) {                              // the children's corrections from the table
+            return wave_map(h.n, [&](int j) MT_LAM {
+                const int b = own(ch, j);
+                ChildL o; o.len = bk(b).len + mt_ldsb().bcorr[b]; o.tie = true; return o;
+            });
+        } else return childLensU(B, h, ch, r, c, haveLen, kl, lsN);
+    }
+    // The U-scan form (every residency but block residency).
+    MT_HD LaneArr<ChildL> childLensU(int B, const BlkH& h, const LaneArr<int>& ch, int r, int c,
+                                     bool haveLen, const LaneArr<int>& kl, int lsN) {
         if constexpr (BIG) {
             if (htOk) {                                  // the children's corrections from the table
                 return wave_map(h.n, [&](int j) MT_LAM {
