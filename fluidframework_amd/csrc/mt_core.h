@@ -1295,6 +1295,9 @@ template <int RES, bool FULL = true> struct MtEngT {
         LaneArr<int> idNext{};
         if (wN0 > 0) wiNext = winRows(winIds(0), 0);
         if (wN0 > MT_WAVE) idNext = winIds(MT_WAVE);
+#else
+        LaneArr<int> idn{};
+        if (wN0 > 0) idn = winIds(0);
 #endif
         for (int base = 0; base < wN0; base += MT_WAVE) {
             const int m = (wN0 - base) < MT_WAVE ? (wN0 - base) : MT_WAVE;
@@ -1305,9 +1308,11 @@ template <int RES, bool FULL = true> struct MtEngT {
                 if (base + 2 * MT_WAVE < wN0) idNext = winIds(base + 2 * MT_WAVE);
             }
 #else
-            // one chunk at a time (the software-pipelined variant, MT_CU_PIPE, holds two chunks
-            // in VGPRs and costs the hot kernel spills)
-            const auto wi = winRows(winIds(base), base);
+            // one chunk's rows at a time (the software-pipelined variant, MT_CU_PIPE, holds two
+            // chunks in VGPRs and costs the hot kernel spills); the next chunk's window ids load
+            // behind this chunk's rows
+            const auto wi = winRows(idn, base);
+            if (base + MT_WAVE < wN0) idn = winIds(base + MT_WAVE);
 #endif
             auto live = wave_map(m, [&](int k) MT_LAM { return own(wi, k).live; });
             if (prune) {
@@ -1525,23 +1530,30 @@ template <int RES, bool FULL = true> struct MtEngT {
             node = B; B = h.parent; leaf = false;
         }
     }
+    // A leaf's rows under (r, c); their meta and props come back from the same round trip.
+    MT_HD LaneArr<ChildL> leafLens(const LaneArr<int>& ch, int n, int r, int c, LaneArr<uint32_t>& lm, LaneArr<int>& lp) {
+        lm = wave_map(n, [&](int j) MT_LAM { return row(own(ch, j)).meta; });
+        lp = wave_map(n, [&](int j) MT_LAM { return row(own(ch, j)).props; });
+        return wave_map(n, [&](int j) MT_LAM {
+            const int s = own(ch, j);
+            const uint32_t mt = own(lm, j);
+            const int rs = row(s).rseq;
+            ChildL o;
+            o.len = vis_rc(row(s).seq, mt, rs, row(s).rcl, row(s).ovl, r, c, ovx, ovxN, s) ? row(s).len : 0;
+            // breakTie for a leaf at pos 0 (MT/mergeTree.ts:2270-2292): false if a
+            // removal the author has seen (removedSeq <= refSeq); true otherwise
+            // (every row has an assigned seq on the replay path).
+            o.tie = !((mt & MT_M_REMOVED) && rs <= r);
+            return o;
+        });
+    }
     // Perspective lengths of block B's children (nodeLength, MT/mergeTree.ts:1652-1692).
     // lsN >= 0 (MT_RES_BIG descents): only the lsN U entries listed in ulist lie under B.
     MT_HD LaneArr<ChildL> childLens(int B, const BlkH& h, const LaneArr<int>& ch, int r, int c,
                                     bool haveLen = false, const LaneArr<int>& kl = LaneArr<int>{}, int lsN = -1) {
         if (h.height == 0) {
-            return wave_map(h.n, [&](int j) MT_LAM {
-                const int s = own(ch, j);
-                const uint32_t mt = row(s).meta;
-                const int rs = row(s).rseq;
-                ChildL o;
-                o.len = vis_rc(row(s).seq, mt, rs, row(s).rcl, row(s).ovl, r, c, ovx, ovxN, s) ? row(s).len : 0;
-                // breakTie for a leaf at pos 0 (MT/mergeTree.ts:2270-2292): false if a
-                // removal the author has seen (removedSeq <= refSeq); true otherwise
-                // (every row has an assigned seq on the replay path).
-                o.tie = !((mt & MT_M_REMOVED) && rs <= r);
-                return o;
-            });
+            LaneArr<uint32_t> lm; LaneArr<int> lp;
+            return leafLens(ch, h.n, r, c, lm, lp);
         }
         if constexpr (BT) {                              // the children's corrections from the table
             return wave_map(h.n, [&](int j) MT_LAM {
@@ -2370,7 +2382,8 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int B = wave_at(fB, L);
             BlkH h;
             auto ch = blkLoad(B, h);
-            auto cl = childLens(B, h, ch, r, c);
+            LaneArr<uint32_t> lm{}; LaneArr<int> lp{};
+            auto cl = h.height == 0 ? leafLens(ch, h.n, r, c, lm, lp) : childLens(B, h, ch, r, c);
             auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
             const int j0 = wave_at(fJ, L);
             auto lensFrom = wave_map(h.n, [&](int j) MT_LAM { return j >= j0 ? own(lens, j) : 0; });
@@ -2398,7 +2411,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                         auto nd = wave_map(h.n, [&](int j) MT_LAM {
                             if (!own(cond, j)) return 0;
                             const int s = own(ch, j);
-                            const uint32_t mt = row(s).meta;
+                            const uint32_t mt = own(lm, j);
                             if (mt & MT_M_REMOVED) {                   // overlapping remove: keep first remover
                                 row(s).ovl = row(s).ovl | (1ull << (c < 63 ? c : 63));
                                 return 0;
@@ -2444,7 +2457,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                         for (int j = 0; j < h.n; j++) {
                             if (!wave_at(cond, j)) continue;
                             const int s = wave_at(ch, j);
-                            const int old = uni(row(s).props);
+                            const int old = wave_at(lp, j);
                             int nw;
                             if (old == lastOld) nw = lastNew;
                             else { nw = applyPropSet(old, opset, rewrite); lastOld = old; lastNew = nw; }
