@@ -2218,14 +2218,19 @@ template <int RES, bool FULL = true> struct MtEngT {
                     nh += n;
                 }
             }
-            for (int i = 0; i < ph.n; i++) freeBlock(wave_at(pch, i));
-            wave_sync();
             int cc = nh / (MT_MAXN / 2); if (cc > MT_MAXN - 1) cc = MT_MAXN - 1; if (cc < 1) cc = 1;
+            // The old children go on the free list and the new blocks come off it, LIFO: the first
+            // min(cc, n) new blocks are the last old children, in reverse order, so those are taken
+            // directly and only the rest are freed (the same blocks and free list as freeing all,
+            // then allocating, without a dependent LDS load per allocation).
+            const int reuse = cc < ph.n ? cc : ph.n;
+            for (int i = 0; i < ph.n - reuse; i++) freeBlock(wave_at(pch, i));
+            wave_sync();
             const int base = nh / cc; int extra = nh % cc; int rd = 0;
             auto packed = wave_map(8, [&](int i) MT_LAM { return -1; });
             for (int ni = 0; ni < cc; ni++) {
                 int cntc = base; if (extra > 0) { cntc++; extra--; }
-                const int NB = allocBlock();
+                const int NB = ni < reuse ? wave_at(pch, ph.n - 1 - ni) : allocBlock();
                 if (NB < 0) return;
                 const int r0 = rd;
                 wave_for(8, [&](int i) MT_LAM { bk(NB).c[i] = i < cntc ? sc->hold[r0 + i] : -1; });
