@@ -390,6 +390,12 @@ def run_config5(args, c, world, rank, local):
     sh = build_sharded(dist, device, fac, total_docs, args.seed, MtGenParams, gen_kw, names=names)
     setup_s = time.time() - t0
     eng = sh.engine
+    # corrupt exchange rows on any rank: every rank stops before replaying (no value published)
+    xb = torch.tensor([int(sh.timings.get("exchange_bad_docs", 0))], dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(xb)
+    if int(xb.item()):
+        raise SystemExit(f"config5: {int(xb.item())} documents failed the exchange checksum; nothing replayed")
     set_residency(eng, args)
     big = c.get("big_min_ops", 0) if args.big_min_ops < 0 else args.big_min_ops
     if args.residency == "blk" and big:

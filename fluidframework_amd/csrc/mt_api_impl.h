@@ -76,7 +76,10 @@ const char* MT_FN(last_error)(mt_ctx* c) { return c ? c->err.c_str() : "null con
 #ifndef MT_SRC_HASH
 #define MT_SRC_HASH "unhashed"
 #endif
-const char* MT_FN(source_hash)(void) { return MT_SRC_HASH; }
+// The same hash behind a tag, so a build script can read it from the file's bytes without
+// loading the library into its own process (dlopen caches a path's first handle).
+__attribute__((used)) const char MT_FN(source_hash_tag)[] = "mt-src-hash:" MT_SRC_HASH;
+const char* MT_FN(source_hash)(void) { return MT_FN(source_hash_tag) + 12; }
 
 // Pools of every document, laid out back to back with per-document capacities.
 static void mt_caps_default(mt_limits& q) {
@@ -664,6 +667,101 @@ int MT_FN(get_length)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t
     if (rc) return rc;
     mtb_sync(c);
     mtb_d2h(c, out, c->b_tmp3.p, 4ull * n);
+    return MT_OK;
+}
+
+// Position queries (mt_query.h): sorted by document (stable), one wave per document's group,
+// answers back in query order; the found segments' text gathered on the device, their JSON
+// written here from the text and the property-map chunks the kernel copied.
+static int mt_run_queries(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t* pos, const int32_t* ref,
+                          const int32_t* cli, std::vector<MtQueryOut>& res) {
+    res.assign(n, MtQueryOut{});
+    if (n == 0) return MT_OK;
+    for (uint32_t i = 0; i < n; i++) if (docs[i] >= c->S.maxDocs) { c->err = "query document out of range"; return MT_E_INVALID; }
+    std::vector<uint32_t> ord(n);
+    for (uint32_t i = 0; i < n; i++) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return docs[a] < docs[b]; });
+    std::vector<MtQuery> q(n);
+    std::vector<uint32_t> grp;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t i = ord[k];
+        q[k].doc = docs[i]; q[k].pos = pos[i]; q[k].ref = ref ? ref[i] : -1; q[k].client = cli ? cli[i] : -1;
+        if (k == 0 || docs[i] != docs[ord[k - 1]]) grp.push_back(k);
+    }
+    grp.push_back(n);
+    const uint32_t ng = (uint32_t)grp.size() - 1;
+    int rc;
+    if ((rc = mtb_ensure(c, c->b_q, sizeof(MtQuery) * n))) return rc;
+    if ((rc = mtb_ensure(c, c->b_qgrp, 4ull * (ng + 1)))) return rc;
+    if ((rc = mtb_ensure(c, c->b_qout, sizeof(MtQueryOut) * n))) return rc;
+    if ((rc = mtb_sync(c))) return rc;
+    mtb_h2d(c, c->b_q.p, q.data(), sizeof(MtQuery) * n);
+    mtb_h2d(c, c->b_qgrp.p, grp.data(), 4ull * (ng + 1));
+    if ((rc = mtb_launch_query(c, (const MtQuery*)c->b_q.p, (const uint32_t*)c->b_qgrp.p, (MtQueryOut*)c->b_qout.p, ng))) return rc;
+    if ((rc = mtb_sync(c))) return rc;
+    std::vector<MtQueryOut> tmp(n);
+    mtb_d2h(c, tmp.data(), c->b_qout.p, sizeof(MtQueryOut) * n);
+    for (uint32_t k = 0; k < n; k++) res[ord[k]] = tmp[k];
+    return MT_OK;
+}
+
+int MT_FN(get_containing_segment)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t* pos, const int32_t* ref,
+                                  const int32_t* cli, mt_seg_info* out, const char** json_arena, const uint64_t** json_off) {
+    if (!c || (n && (!docs || !pos))) return MT_E_INVALID;
+    std::vector<MtQueryOut> res;
+    int rc = mt_run_queries(c, n, docs, pos, ref, cli, res);
+    if (rc) return rc;
+    if (out) for (uint32_t i = 0; i < n; i++) out[i] = res[i].info;
+    if (!json_arena) return MT_OK;
+    // text of the found text segments, gathered on the device into one arena
+    std::vector<unsigned long long> at, off(1, 0);
+    std::vector<uint32_t> len, which;
+    for (uint32_t i = 0; i < n; i++) {
+        const mt_seg_info& f = res[i].info;
+        if (!f.found || f.marker_ref_type >= 0 || f.len <= 0) continue;
+        at.push_back(res[i].text_at); len.push_back((uint32_t)f.len); which.push_back(i);
+        off.push_back(off.back() + (unsigned long long)f.len);
+    }
+    std::vector<uint16_t> txt(off.back());
+    const uint32_t m = (uint32_t)len.size();
+    if (m) {
+        if ((rc = mtb_ensure(c, c->b_qat, 8ull * m))) return rc;
+        if ((rc = mtb_ensure(c, c->b_qlen, 4ull * m))) return rc;
+        if ((rc = mtb_ensure(c, c->b_qoff, 8ull * m))) return rc;
+        if ((rc = mtb_ensure(c, c->b_qtext, 2ull * off.back()))) return rc;
+        mtb_h2d(c, c->b_qat.p, at.data(), 8ull * m);
+        mtb_h2d(c, c->b_qlen.p, len.data(), 4ull * m);
+        mtb_h2d(c, c->b_qoff.p, off.data(), 8ull * m);
+        if ((rc = mtb_launch_gather_text(c, (const unsigned long long*)c->b_qat.p, (const uint32_t*)c->b_qlen.p,
+                                         (const unsigned long long*)c->b_qoff.p, (uint16_t*)c->b_qtext.p, m))) return rc;
+        if ((rc = mtb_sync(c))) return rc;
+        mtb_d2h(c, txt.data(), c->b_qtext.p, 2ull * off.back());
+    }
+    std::vector<int64_t> slot(n, -1);
+    for (uint32_t k = 0; k < m; k++) slot[which[k]] = k;
+    c->seg_json_arena.clear(); c->seg_json_off.assign(1, 0);
+    for (uint32_t i = 0; i < n; i++) {
+        const mt_seg_info& f = res[i].info;
+        if (f.found) {
+            const bool marker = f.marker_ref_type >= 0;
+            const int64_t k = slot[i];
+            mtsnap::seg_json_of(c->seg_json_arena, marker, f.marker_ref_type, f.prop_set >= 0 ? res[i].ps : nullptr, c->names,
+                                k >= 0 ? txt.data() + off[k] : nullptr, k >= 0 ? (size_t)len[k] : 0);
+        }
+        c->seg_json_off.push_back(c->seg_json_arena.size());
+    }
+    *json_arena = c->seg_json_arena.data();
+    if (json_off) *json_off = c->seg_json_off.data();
+    return MT_OK;
+}
+
+int MT_FN(resolve_remote_position)(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t* pos, const int32_t* ref,
+                                   const int32_t* cli, int32_t* out) {
+    if (!c || (n && (!docs || !pos || !out))) return MT_E_INVALID;
+    std::vector<MtQueryOut> res;
+    int rc = mt_run_queries(c, n, docs, pos, ref, cli, res);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < n; i++) out[i] = res[i].info.resolved;
     return MT_OK;
 }
 

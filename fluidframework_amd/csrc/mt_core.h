@@ -476,6 +476,10 @@ __shared__ MtCold mt_cold_v;
 #else
 static MtCold mt_cold_v;
 #endif
+#if defined(MT_DBG_FAIL) && defined(__HIP_DEVICE_COMPILE__)
+struct MtDbg { int s, n; uint32_t op; };     // diagnostic builds: the last row split
+__shared__ MtDbg mt_dbg_v;
+#endif
 
 // RES: MT_RES_HBM (every pool in HBM), MT_RES_LDS (rows, blocks, heap, window,
 // U set in LDS) or MT_RES_BLK (blocks and heap in LDS).  FULL: the instantiation can
@@ -1437,6 +1441,31 @@ template <int RES, bool FULL = true> struct MtEngT {
             node = B; B = h.parent;
         }
     }
+    // MergeTree.getContainingSegment (MT/mergeTree.ts:1616-1627) by searchBlock (:1786-1815):
+    // each block's first child whose (r, c) length exceeds what is left of pos (no tie rule;
+    // a negative pos takes every block's first child, as `_pos < len` does), down to a row.
+    // Returns the row and sets off = pos - its start; -1 when no child holds pos (segment
+    // undefined).  depth / path: child index per level, root first, 3 bits each.
+    MT_HD int containing(int pos, int r, int c, int& off, int& depth, unsigned long long& path) {
+        if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
+        int B = root, p = pos;
+        depth = 0; path = 0;
+        for (;;) {
+            BlkH h;
+            auto ch = blkLoad(B, h);
+            auto cl = childLens(B, h, ch, r, c);
+            auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
+            auto pre = wave_excl_scan8(lens);
+            const int pp = p;
+            const int j = wave_first(wave_map(h.n, [&](int k) MT_LAM { return pp - own(pre, k) < own(lens, k); }));
+            if (j < 0) return -1;
+            p -= wave_at(pre, j);
+            depth++; path = (path << 3) | (unsigned long long)j;
+            const int child = wave_at(ch, j);
+            if (h.height == 0) { off = p; return child; }
+            B = child;
+        }
+    }
     // posFromRelativePos (MT/mergeTree.ts:1949-1972): the marker's position under (r, c),
     // then past the marker (+ cachedLength 1 + offset) or before it (- offset).  -1: the
     // id was never mapped (getMarkerFromId undefined).  A marker whose row was unlinked
@@ -1688,6 +1717,9 @@ template <int RES, bool FULL = true> struct MtEngT {
         MT_EV2(5, 1);
         const int n = allocRow();
         if (n < 0) return -1;
+#if defined(MT_DBG_FAIL) && defined(__HIP_DEVICE_COMPILE__)
+        mt_dbg_v.s = s; mt_dbg_v.n = n; mt_dbg_v.op = curOp;
+#endif
         const int ls = uni(row(s).len);
         const uint32_t mt = uni(row(s).meta);
         row(n).len = ls - pos; row(s).len = pos;
@@ -1757,6 +1789,38 @@ template <int RES, bool FULL = true> struct MtEngT {
             node = NB; idx = uni(sc->pathJ[L - 1]) + 1; L = L - 1;
         }
     }
+#if defined(MT_DBG_FAIL) && defined(__HIP_DEVICE_COMPILE__)
+    // Diagnostic builds only: a walk found no position.  Prints the walk's view of the
+    // block's children beside fresh (volatile, after a full wait) reloads of the same records.
+    __device__ void dbgWalkFail(int kind, int B, const BlkH& h, int ch, const ChildL& cl, int pos, int p, int total, int L,
+                                int r, int c) {
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        const int lane = wave_lane();
+        if (lane == 0)
+            printf("WALKFAIL op=%u kind=%d B=%d height=%d n=%d hlen=%d L=%d root=%d H=%d pos=%d p=%d total=%d r=%d c=%d "
+                   "minSeq=%d curSeq=%d uValid=%d nU=%d lastSplit(s=%d n=%d op=%u)\n",
+                   curOp, kind, B, h.height, h.n, h.len, L, root, height, pos, p, total, r, c, minSeq, curSeq, (int)uValid, nU,
+                   mt_dbg_v.s, mt_dbg_v.n, mt_dbg_v.op);
+        if (lane < h.n) {
+            if (h.height == 0) {
+                const volatile MtRow* v = (const volatile MtRow*)&row(ch);
+                const int ln = v->len, sq = v->seq, rs = v->rseq, par = v->parent;
+                const uint32_t mt = v->meta, rc = v->rcl;
+                const unsigned long long ov = v->ovl;
+                const bool vis = vis_rc(sq, mt, rs, rc, ov, r, c, ovx, ovxN, ch);
+                printf("  WALKFAIL child %d row=%d used_len=%d tie=%d | fresh len=%d seq=%d rseq=%d meta=%x rcl=%u ovl=%llx "
+                       "parent=%d vis=%d\n", lane, ch, cl.len, (int)cl.tie, ln, sq, rs, mt, rc, ov, par, (int)vis);
+            } else {
+                int corr = 0;
+                if constexpr (BT) corr = mt_ldsb().bcorr[ch];
+                const volatile MtBlk* v = (const volatile MtBlk*)&bk(ch);
+                printf("  WALKFAIL child %d blk=%d used_len=%d | bk.len=%d bcorr=%d n=%d parent=%d height=%d\n", lane, ch, cl.len,
+                       v->len, corr, v->n, v->parent, v->height);
+            }
+        }
+    }
+#endif
     // insertingWalk (MT/mergeTree.ts:2363-2493) for one remote op perspective.  L0 > 0
     // resumes at level L0 of the previous walk's path (pathB/pathJ/pathOff above L0 still
     // valid, U unchanged): the root descent would pick the same children down to there.
@@ -1778,7 +1842,28 @@ template <int RES, bool FULL = true> struct MtEngT {
             const bool kpre = !BLKL && h.height > 0;
             LaneArr<int> r0{}, r1{};
             if (kpre) kidsLoad(ch, h.n, r0, r1);
+#if defined(MT_DBG_WIDE)
+            // diagnostic build: the leaf step loads every row field in one round trip (the
+            // variant that failed on the device in rounds 2 and 3)
+            LaneArr<ChildL> cl;
+            if (h.height == 0) {
+                const int rr = r, cc = c;
+                cl = wave_map(h.n, [&](int j) MT_LAM {
+                    const int s = own(ch, j);
+                    const int fl_ = row(s).len, fs = row(s).seq, fr = row(s).rseq, ft = row(s).toff, fp = row(s).props;
+                    const int fc = row(s).tcap, fmid = row(s).mid, fpar = row(s).parent;
+                    const uint32_t fm = row(s).meta, frc = row(s).rcl;
+                    const unsigned long long fo = row(s).ovl;
+                    mt_keep(ft ^ fp ^ fc ^ fmid ^ fpar);
+                    ChildL o;
+                    o.len = vis_rc(fs, fm, fr, frc, fo, rr, cc, ovx, ovxN, s) ? fl_ : 0;
+                    o.tie = !((fm & MT_M_REMOVED) && fr <= rr);
+                    return o;
+                });
+            } else cl = kpre ? childLens(B, h, ch, r, c, true, kidsLen(r0, r1), lsN) : childLens(B, h, ch, r, c);
+#else
             auto cl = kpre ? childLens(B, h, ch, r, c, true, kidsLen(r0, r1), lsN) : childLens(B, h, ch, r, c);
+#endif
             MT_QE(1, q1);
             auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
             auto pre = wave_excl_scan8(lens);
@@ -1833,6 +1918,9 @@ template <int RES, bool FULL = true> struct MtEngT {
                 uValid = false;
                 return MT_W_OK;
             }
+#if defined(MT_DBG_FAIL) && defined(__HIP_DEVICE_COMPILE__)
+            dbgWalkFail(kind, B, h, ch, cl, pos, p, total, L, r, c);
+#endif
             return MT_W_FAIL;
         }
     }
@@ -2860,8 +2948,10 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (status) return;
         // The end boundary's walk resumes at the deepest block of the start walk's path whose
         // perspective range still holds end (tree and U unchanged unless a block split).
+        // (A start past the perspective length fails at the root and leaves the path of an
+        // earlier walk behind: then both walks start at the root.)
         int L0 = 0;
-        if (MT_PATH_RESUME && !lastSplit && uValid && uRef == r && uCli == c) {
+        if (MT_PATH_RESUME && w != MT_W_FAIL && !lastSplit && uValid && uRef == r && uCli == c) {
             for (int l = lastL; l > 0; l--) {
                 if (end - uni(sc->pathOff[l]) <= uni(sc->pathLen[l])) { L0 = l; break; }
             }
@@ -2869,7 +2959,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         w = walk(MT_WALK_SPLIT, end, r, c, -1, 0, L0);
         if (w == MT_W_OK) c_rows += 2;
         if (status) return;
-        if (lastSplit || !uValid) L0 = 0;
+        if (w == MT_W_FAIL || lastSplit || !uValid) L0 = 0;
         MT_PE(MT_PH_SPLIT, t0);
         MT_PB(t1);
         rangeMap(mode, start, end, r, c, sq, opset, rewrite, L0);

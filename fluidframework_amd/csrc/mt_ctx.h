@@ -6,6 +6,7 @@
 #include "mt_replay.h"
 #include "mt_snapshot.h"
 #include "mt_pack.h"
+#include "mt_query.h"
 
 struct mt_ctx {
     int device = 0;
@@ -24,7 +25,8 @@ struct mt_ctx {
     // device op batch (resident)
     struct DevBuf { void* p = nullptr; size_t cap = 0; };
     DevBuf b_stage, b_pack_docs, b_pack_sz, b_pack_off, b_gencl, b_cursor, b_doc, b_off, b_rec, b_pay, b_rel, b_drec, b_dcount, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3,
-           b_ld_meta, b_ld_seg, b_ld_pay, b_ld_plan, b_ld_poff, b_dtext, b_resume, b_start;
+           b_ld_meta, b_ld_seg, b_ld_pay, b_ld_plan, b_ld_poff, b_dtext, b_resume, b_start,
+           b_q, b_qgrp, b_qout, b_qat, b_qlen, b_qoff, b_qtext;   // position queries (mt_get_containing_segment)
     MtOps ops{};
     uint32_t n_runs = 0;
     std::vector<uint32_t> run_off;     // host copy of the resident batch's op offsets (n_runs + 1)
@@ -59,6 +61,8 @@ struct mt_ctx {
     std::vector<uint32_t> blob_first;
     std::vector<uint16_t> text_arena;
     std::vector<uint64_t> text_off;
+    std::string seg_json_arena;                   // mt_get_containing_segment's segment JSON
+    std::vector<uint64_t> seg_json_off;
     // delta capture (mt_delta_capture / mt_delta_records)
     uint64_t delta_cap = 0, delta_tcap = 0;
     bool delta_valid = false, delta_over = false;

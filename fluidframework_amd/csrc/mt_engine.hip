@@ -46,6 +46,23 @@ __global__ __launch_bounds__(64) void mt_get_length_kernel(MtState S, const uint
     if (__lane_id() == 0) out[blockIdx.x] = l;
 }
 
+// Position queries (mt_query.h): one wave per document group of the sorted queries.
+__global__ __launch_bounds__(64) void mt_query_kernel(MtState S, const MtQuery* q, const uint32_t* grp, MtQueryOut* out) {
+    __shared__ MtScratch sc;
+    const uint32_t q0 = grp[blockIdx.x], q1 = grp[blockIdx.x + 1];
+    MtEngFast e;
+    e.bind(S, q[q0].doc, &sc);
+    mt_query_run(e, S, q, q0, q1, out);
+}
+// Text of found segments into one arena: workgroup i copies len[i] units from text[at[i]].
+__global__ __launch_bounds__(256) void mt_gather_text_kernel(const uint16_t* text, const unsigned long long* at,
+                                                             const uint32_t* len, const unsigned long long* off,
+                                                             uint16_t* dst) {
+    const uint32_t i = blockIdx.x, n = len[i];
+    const unsigned long long a = at[i], o = off[i];
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) dst[o + k] = text[a + k];
+}
+
 // Staging for host-side serialization (mt_pack.h): sizes, then the packed copy.
 __global__ __launch_bounds__(64) void mt_pack_size_kernel(MtState S, const uint32_t* docs, MtPackSize* out) {
     __shared__ MtScratch sc;
@@ -200,6 +217,20 @@ static int mtb_launch_get_length(mt_ctx* c, const uint32_t* docs, const int32_t*
     if (!n) return MT_OK;
     (void)hipGetLastError();
     hipLaunchKernelGGL(mt_get_length_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, ref, cli, out);
+    return mtb_check(c);
+}
+
+static int mtb_launch_query(mt_ctx* c, const MtQuery* q, const uint32_t* grp, MtQueryOut* out, uint32_t n_groups) {
+    if (!n_groups) return MT_OK;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(mt_query_kernel, dim3(n_groups), dim3(64), 0, (hipStream_t)c->stream, c->S, q, grp, out);
+    return mtb_check(c);
+}
+static int mtb_launch_gather_text(mt_ctx* c, const unsigned long long* at, const uint32_t* len, const unsigned long long* off,
+                                  uint16_t* dst, uint32_t n) {
+    if (!n) return MT_OK;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(mt_gather_text_kernel, dim3(n), dim3(256), 0, (hipStream_t)c->stream, c->S.text, at, len, off, dst);
     return mtb_check(c);
 }
 

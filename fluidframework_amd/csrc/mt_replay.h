@@ -78,6 +78,9 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
     // record at the top of each iteration, so it loads in place).
     auto wn = wave_map(8, [&](int q) MT_LAM { return (!g && o0 < o1) ? ((const int*)&ops.rec[o0])[q] : 0; });
     if (!g && Eng::kFull) { e.drec = ops.drec; e.dcount = ops.dcount; e.dcap = ops.dcap; e.dtext = ops.dtext; e.dtcap = ops.dtcap; }
+    // this message's capture reservation (FULL): released after the message, or after the
+    // loop when an error ends the run mid-message
+    unsigned long long resR = 0, resT = 0;
     for (uint32_t i = o0; i < o1; i++) {
         e.curOp = i;
         if (Eng::kLds && !e.ldsHeadroom()) return i;
@@ -103,7 +106,6 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
         const uint32_t w7 = (uint32_t)wave_at(w, 7);
         const int plen = (int)(w7 & 0xFFFF), pid = (int)(int16_t)(w7 >> 16);
         if (ty == MT_OP_UNSUPPORTED) { e.status |= MT_DS_UNSUPPORTED; break; }
-        unsigned long long resR = 0, resT = 0;
         if constexpr (Eng::kFull) {
             if (!g && e.drec) {
                 // capture headroom for this message: a range op emits at most one record per
@@ -172,8 +174,9 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
             e.setMinSeq(ms);
         }
         if (e.status) break;
-        if constexpr (Eng::kFull) { if (resR) e.dRelease(resR, resT); }
+        if constexpr (Eng::kFull) { if (resR) { e.dRelease(resR, resT); resR = resT = 0; } }
     }
+    if constexpr (Eng::kFull) { if (resR) e.dRelease(resR, resT); }
     return o1;
 }
 

@@ -94,19 +94,23 @@ template <class F> void walk_all(const MtSnapView& v, int B, F& f) {
     }
 }
 
-// TextSegment/Marker toJSONObject (textSegment.ts:48-54, mergeTree.ts:649-653)
-inline void seg_json(std::string& o, const MtSnapView& v, const MtNames& nm, int s, const uint16_t* txt, size_t tn) {
-    const bool marker = (v.R[s].meta & MT_M_MARKER) != 0;
-    const int ps = v.R[s].props;
+// TextSegment/Marker toJSONObject (textSegment.ts:48-54, mergeTree.ts:649-653); props: the
+// property map's first chunk, null when properties are undefined.
+inline void seg_json_of(std::string& o, bool marker, int refType, const MtPSet* props, const MtNames& nm,
+                        const uint16_t* txt, size_t tn) {
     if (marker) {
-        o += "{\"marker\":{\"refType\":"; put_int(o, v.R[s].toff); o += "}";
-        if (ps >= 0) { o += ",\"props\":"; props_json(o, v.pset + ps, nm); }
+        o += "{\"marker\":{\"refType\":"; put_int(o, refType); o += "}";
+        if (props) { o += ",\"props\":"; props_json(o, props, nm); }
         o += "}";
-    } else if (ps >= 0) {
-        o += "{\"text\":"; quote16(o, txt, tn); o += ",\"props\":"; props_json(o, v.pset + ps, nm); o += "}";
+    } else if (props) {
+        o += "{\"text\":"; quote16(o, txt, tn); o += ",\"props\":"; props_json(o, props, nm); o += "}";
     } else {
         quote16(o, txt, tn);
     }
+}
+inline void seg_json(std::string& o, const MtSnapView& v, const MtNames& nm, int s, const uint16_t* txt, size_t tn) {
+    const int ps = v.R[s].props;
+    seg_json_of(o, (v.R[s].meta & MT_M_MARKER) != 0, v.R[s].toff, ps >= 0 ? v.pset + ps : nullptr, nm, txt, tn);
 }
 
 inline bool props_match(const MtSnapView& v, const MtNames& nm, int a, int b) {

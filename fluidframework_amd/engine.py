@@ -16,6 +16,7 @@ The product path has no CPU fallback: if ``libmtgpu.so`` (built by
 from __future__ import annotations
 
 import ctypes
+import json
 import os
 from dataclasses import dataclass
 
@@ -110,8 +111,16 @@ def _bind(lib, prefix: str):
         delta_text=f("delta_text", ctypes.c_int, [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_uint64),
                                                   ctypes.POINTER(U32)]),
         doc_pset=f("doc_pset", ctypes.c_int, [P, U32, I32, P, P, ctypes.POINTER(U32)]),
+        get_containing_segment=f("get_containing_segment", ctypes.c_int,
+                                 [P, U32, P, P, P, P, P, ctypes.POINTER(P), ctypes.POINTER(P)]),
+        resolve_remote_position=f("resolve_remote_position", ctypes.c_int, [P, U32, P, P, P, P, P]),
     )
 
+
+SEG_INFO_FIELDS = ("found", "offset", "obs_pos", "len", "seq", "client", "removed_seq", "removed_client", "prop_set",
+                   "marker_ref_type", "depth", "path_lo", "path_hi", "row", "resolved", "pad")
+SEG_INFO_DTYPE = np.dtype([(f, np.uint32 if f.startswith("path") else np.int32) for f in SEG_INFO_FIELDS])
+POS_UNDEFINED = -(1 << 31)              # MT_POS_UNDEFINED
 
 DELTA_DTYPE = np.dtype([("op", np.uint32), ("kind", np.int32), ("pos", np.int32), ("len", np.int32),
                         ("seg", np.int32), ("a", np.int32), ("b", np.int32), ("pad", np.int32)])
@@ -405,6 +414,39 @@ class Engine:
                                           out.ctypes.data), "mt_get_length")
         return out
 
+    def containing_segment(self, docs, pos, ref_seq=None, client=None, json: bool = True):
+        """mt_get_containing_segment: getContainingSegment (MT/mergeTree.ts:1616-1627) of each
+        query under (ref_seq[i], client[i]) (ref_seq < 0 or None: the local view), with
+        resolveRemoteClientPosition in the `resolved` field.  Returns (SEG_INFO_DTYPE records,
+        list of segment JSON texts or None when json is False / not found)."""
+        d, p = _u32(docs), _i32(pos)
+        n = len(d)
+        r = _i32(np.full(n, -1) if ref_seq is None else ref_seq)
+        c = _i32(np.full(n, -1) if client is None else client)
+        out = np.zeros(n, SEG_INFO_DTYPE)
+        arena, off = ctypes.c_void_p(), ctypes.c_void_p()
+        self._check(self.fn["get_containing_segment"](self.h, n, d.ctypes.data, p.ctypes.data, r.ctypes.data,
+                                                      c.ctypes.data, out.ctypes.data,
+                                                      ctypes.byref(arena) if json else None,
+                                                      ctypes.byref(off) if json else None),
+                    "mt_get_containing_segment")
+        texts = [None] * n
+        if json:
+            offs = np.ctypeslib.as_array(ctypes.cast(off, ctypes.POINTER(ctypes.c_uint64)), (n + 1,)).copy()
+            raw = ctypes.string_at(arena, int(offs[-1])) if offs[-1] else b""
+            texts = [raw[offs[i]:offs[i + 1]].decode("utf-8", "surrogatepass") if out["found"][i] else None
+                     for i in range(n)]
+        return out, texts
+
+    def resolve_remote_position(self, docs, pos, ref_seq, client) -> np.ndarray:
+        """mt_resolve_remote_position (MT/mergeTree.ts:2125-2145): local positions,
+        POS_UNDEFINED where the reference returns undefined."""
+        d, p, r, c = _u32(docs), _i32(pos), _i32(ref_seq), _i32(client)
+        out = np.zeros(len(d), np.int32)
+        self._check(self.fn["resolve_remote_position"](self.h, len(d), d.ctypes.data, p.ctypes.data, r.ctypes.data,
+                                                       c.ctypes.data, out.ctypes.data), "mt_resolve_remote_position")
+        return out
+
     def snapshot(self, docs, msn, seq, legacy: bool = False):
         """SnapshotV1 (or, with legacy, SnapshotLegacy header/body) blobs per document:
         list of (list[bytes], digest)."""
@@ -472,6 +514,37 @@ def catchup_ops(blobs: dict, snap) -> list:
     return _json.loads(raw.decode("utf-8") if isinstance(raw, (bytes, bytearray)) else raw)
 
 
+NON_COLLAB_CLIENT = -2                  # NonCollabClient, MT/constants.ts
+
+
+class Segment:
+    """A segment as Client.getContainingSegment hands it out: the ISegment fields
+    (MT/mergeTree.ts:87-122) of a TextSegment or Marker, by value.  The reference hands out
+    the live object; this drop-in returns a copy taken at query time, valid for getPosition
+    until the document next changes (the engine's rows are reused, so no handle stays live)."""
+
+    def __init__(self, info, js: str, client, version: int):
+        self.cachedLength = int(info["len"])
+        self.seq = int(info["seq"])
+        self.clientId = client._short_of(int(info["client"]))
+        rs = int(info["removed_seq"])
+        self.removedSeq = None if rs == POS_UNDEFINED else rs
+        self.removedClientId = client._short_of(int(info["removed_client"])) if self.removedSeq is not None else None
+        j = json.loads(js)
+        self._json = j
+        if isinstance(j, str):
+            self.text, self.properties = j, None
+        elif "marker" in j:
+            self.text, self.refType, self.properties = None, j["marker"]["refType"], j.get("props")
+        else:
+            self.text, self.properties = j["text"], j.get("props")
+        self._obs_pos = int(info["obs_pos"])
+        self._doc, self._version = client.doc_id, version
+
+    def toJSONObject(self):
+        return self._json
+
+
 class MergeTreeClient:
     """Drop-in subset of merge-tree ``Client`` (MT/client.ts:44) for a passive observer.
 
@@ -500,6 +573,7 @@ class MergeTreeClient:
         """Client.updateSeqNumbers (client.ts:843-850): the device window moves, and so
         do the host copies that snapshot() passes back to mt_update_seq."""
         self.group.flush()
+        self.group.version += 1
         self.engine.update_seq([self.doc_id], [min_seq], [seq])
         self.engine.sync()
         self._raise_status()
@@ -548,6 +622,75 @@ class MergeTreeClient:
     def getCurrentSeq(self) -> int:
         return self.current_seq
 
+    # ---- short client ids (client.ts:658-670): the local client is 0, remote clients follow
+    #      in first-seen order (the order of the reference when collaboration starts first)
+    def getOrAddShortClientId(self, longClientId: str) -> int:
+        if self.longClientId is not None and longClientId == self.longClientId:
+            return 0
+        return self.names.index(longClientId) + 1
+
+    def getShortClientId(self, longClientId: str) -> int:
+        if self.longClientId is not None and longClientId == self.longClientId:
+            return 0
+        if longClientId not in self.names.ids:
+            raise MergeTreeError(f"unknown client {longClientId!r}")
+        return self.names.ids[longClientId] + 1
+
+    def getLongClientId(self, shortClientId: int) -> str:
+        if shortClientId == 0:
+            return self.longClientId
+        return self.names.names[shortClientId - 1]
+
+    def _short_of(self, index: int) -> int:
+        """The engine's per-document client index as this Client's short id."""
+        return NON_COLLAB_CLIENT if index < 0 else index + 1
+
+    def _query(self, pos: int, ref_seq: int, short_id: int | None):
+        self.group.flush()
+        self._raise_status()
+        if short_id is None or short_id == 0:
+            ref, cli = -1, -1                         # the local view
+        else:
+            ref, cli = int(ref_seq), int(short_id) - 1
+        info, js = self.engine.containing_segment([self.doc_id], [pos], [ref], [cli])
+        return info[0], js[0]
+
+    def getContainingSegment(self, pos: int) -> dict:
+        """Client.getContainingSegment (client.ts:1040-1043 -> MergeTree.getContainingSegment,
+        mergeTree.ts:1616-1627) under the local view: {"segment": Segment | None, "offset"}."""
+        info, js = self._query(pos, 0, None)
+        if not info["found"]:
+            return {"segment": None, "offset": None}
+        return {"segment": Segment(info, js, self, self.group.version), "offset": int(info["offset"])}
+
+    def getPosition(self, segment: Segment) -> int:
+        """Client.getPosition (client.ts:306-311): the segment's local position."""
+        if segment is None:
+            return -1
+        if segment._doc != self.doc_id or segment._version != self.group.version or self.pending:
+            raise MergeTreeError("segment copy is stale: the document changed since getContainingSegment")
+        return segment._obs_pos
+
+    def resolveRemoteClientPosition(self, remoteClientPosition: int, remoteClientRefSeq: int,
+                                    remoteClientId: int):
+        """MergeTree.resolveRemoteClientPosition (mergeTree.ts:2125-2145): the local position of a
+        remote client's position at its refSeq; None where the reference returns undefined."""
+        info, _ = self._query(remoteClientPosition, remoteClientRefSeq, remoteClientId)
+        v = int(info["resolved"])
+        return None if v == POS_UNDEFINED else v
+
+    def getPropertiesAtPosition(self, pos: int):
+        """Client.getPropertiesAtPosition (client.ts:1045-1057)."""
+        seg = self.getContainingSegment(pos)["segment"]
+        return seg.properties if seg is not None else None
+
+    def getRangeExtentsOfPosition(self, pos: int) -> dict:
+        """Client.getRangeExtentsOfPosition (client.ts:1058-1071)."""
+        seg = self.getContainingSegment(pos)["segment"]
+        if seg is None:
+            return {"posStart": None, "posAfterEnd": None}
+        return {"posStart": seg._obs_pos, "posAfterEnd": seg._obs_pos + seg.cachedLength}
+
     def load(self, blobs: dict, longClientId: str = "snapshot") -> dict:
         """Client.load (MT/client.ts:958) through SnapshotLoader (snapshotLoader.ts:39-222):
         `blobs` maps blob paths (header, body_0.. or body) to contents.  Returns
@@ -558,6 +701,7 @@ class MergeTreeClient:
         snap = parse_snapshot(chunks)
         lb = LoadBatchBuilder(self.engine.props)
         lb.add(self.doc_id, snap, self.names)
+        self.group.version += 1
         self.engine.upload_doc_names(self.doc_id, self.names.json_literals())
         self.names_uploaded = len(self.names.names)
         self.engine.load_snapshot(lb.build())
@@ -574,6 +718,7 @@ class ClientGroup:
     def __init__(self, engine: Engine):
         self.engine = engine
         self.clients: list[MergeTreeClient] = []
+        self.version = 0                 # bumped whenever any document changes (Segment copies)
 
     def new_client(self, options: dict | None = None) -> MergeTreeClient:
         d = len(self.clients)
@@ -605,6 +750,7 @@ class ClientGroup:
                 self.engine.upload_doc_names(c.doc_id, c.names.json_literals())
                 c.names_uploaded = len(c.names.names)
         batch = bb.build()
+        self.version += 1
         self.last_batch = batch          # op indexing of delta records (Engine.delta_records)
         # Capture is armed only around batches with a listener (the other batches run the
         # kernels without capture code).  The capacity is a launch's buffer, not a bound:

@@ -125,6 +125,13 @@ class ShardedReplay:
         return len(self.owned)
 
     def replay(self):
+        # documents whose exchange rows arrived with a checksum other than rank 0's are
+        # corrupt: replaying them would publish wrong results as if they were right
+        bad = int(self.timings.get("exchange_bad_docs", 0))
+        if bad:
+            from .engine import ExchangeError
+            raise ExchangeError(f"refusing to replay: {bad} of {self.n_docs} documents failed the exchange checksum",
+                                np.zeros(0, np.uint32))
         self.engine.open_docs(0, self.n_docs)
         self.engine.replay_resident()
 

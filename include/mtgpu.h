@@ -349,6 +349,44 @@ int  mt_doc_pools(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, int32_t* out
 int  mt_get_length(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
                    const int32_t* ref_seq, const int32_t* client, int32_t* out_len);
 
+/*
+ * Position queries on the current state of replayed documents, batched (one wave per
+ * document, its queries in order).  Query i asks about document doc_ids[i] at pos[i] under
+ * the perspective (ref_seq[i], client[i]), client = per-document client index;
+ * ref_seq[i] < 0 is the local (observer) view, (currentSeq, local client).
+ *   MergeTree.getContainingSegment  MT/mergeTree.ts:1616-1627 (searchBlock :1786-1815;
+ *                                   Client.getContainingSegment client.ts:1040-1043)
+ *   MergeTree.resolveRemoteClientPosition  MT/mergeTree.ts:2125-2145
+ * out[i].found = 0 when the segment is undefined (pos at or past the perspective length).
+ * json_arena (optional): the library-owned toJSONObject text of each found segment
+ * (textSegment.ts:48-54, mergeTree.ts:649-653), query i = bytes [json_off[i], json_off[i+1])
+ * (empty when not found), valid until the next call.
+ */
+#define MT_POS_UNDEFINED INT32_MIN
+typedef struct mt_seg_info {
+    int32_t found;            /* 1: a segment holds pos under the perspective                   */
+    int32_t offset;           /* pos minus the segment's start under the perspective             */
+    int32_t obs_pos;          /* the segment's start in the local view (getPosition, :1578-1596) */
+    int32_t len;              /* cachedLength                                                     */
+    int32_t seq, client;      /* insertion seq; client index (-1: NonCollabClient)               */
+    int32_t removed_seq;      /* INT32_MIN: undefined                                             */
+    int32_t removed_client;   /* -1 when not removed                                              */
+    int32_t prop_set;         /* the document's property-set id (mt_doc_pset), -1: undefined     */
+    int32_t marker_ref_type;  /* -1: text segment                                                 */
+    int32_t depth;            /* tree levels above the segment                                    */
+    uint32_t path_lo, path_hi;/* child index per level, root first, 3 bits each (as mt_dump_segments) */
+    int32_t row;              /* engine row id                                                    */
+    int32_t resolved;         /* resolveRemoteClientPosition: obs_pos + offset; the local length
+                                 when pos == the perspective length; else MT_POS_UNDEFINED      */
+    int32_t pad;
+} mt_seg_info;
+int  mt_get_containing_segment(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, const int32_t* pos,
+                               const int32_t* ref_seq, const int32_t* client, mt_seg_info* out,
+                               const char** json_arena, const uint64_t** json_off);
+/* resolveRemoteClientPosition only: out_pos[i] = mt_seg_info.resolved of the same query. */
+int  mt_resolve_remote_position(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, const int32_t* pos,
+                                const int32_t* ref_seq, const int32_t* client, int32_t* out_pos);
+
 /* Client long-id strings (JSON literals) by per-document client index; used for
  * the snapshot's "client"/"removedClient" fields (snapshotV1.ts:229, :237). */
 int  mt_set_client_names(mt_ctx* ctx, uint32_t n, const char* const* client_json);

@@ -445,6 +445,23 @@ struct Tree {
         }
         return total;
     }
+    // getContainingSegment (:1616-1627) through searchBlock (:1786-1815): the first child with
+    // pos < nodeLength at each level; offset = what is left of pos in the segment.
+    Seg* containingSegment(int pos, int refSeq, int clientId, int& offset) {
+        Block* b = root; int p = pos;
+        for (;;) {
+            Node* hit = nullptr;
+            for (int i = 0; i < b->childCount; i++) {
+                Node* c = b->children[i];
+                const int len = nodeLength(c, refSeq, clientId);
+                if (p < len) { hit = c; break; }
+                p -= len;
+            }
+            if (!hit) return nullptr;
+            if (hit->leaf) { offset = p; return (Seg*)hit; }
+            b = (Block*)hit;
+        }
+    }
     int posFromRelativePos(const JVal& rp, int refSeq, int clientId) {                      // :1949-1972
         int pos = -1;
         const JVal* id = nullptr;
@@ -1801,6 +1818,66 @@ int32_t ora_get_length(ora_doc* o, int32_t ref, int32_t client) {
     else if (client < (int)o->d.streamToShort.size() && o->d.streamToShort[client] >= 0) cl = o->d.streamToShort[client];
     else cl = -1000 - client;
     return o->d.t.getLength(ref, cl);
+}
+// getContainingSegment / resolveRemoteClientPosition (MT/mergeTree.ts:1616-1627, :2125-2145)
+// for stream client `client` at ref (ref < 0: the local client at currentSeq); out16 in
+// mt_seg_info order (prop_set: 1 if properties are defined, else -1; row: -1).
+int ora_containing_segment(ora_doc* o, int32_t pos, int32_t ref, int32_t client, const char* client_literal, int32_t* out,
+                           char** json) {
+    Doc& d = o->d; Tree& t = d.t;
+    int cl, rs;
+    if (ref < 0) { cl = t.cwClientId; rs = t.currentSeq; }
+    else if (client_literal) {                                // a long id (JSON literal) the messages named
+        rs = ref;
+        auto it = d.nameToShort.find(client_literal);
+        cl = it != d.nameToShort.end() ? it->second : -999999;
+    } else {
+        rs = ref;
+        if (client >= 0 && client < (int)d.streamToShort.size() && d.streamToShort[client] >= 0) cl = d.streamToShort[client];
+        else cl = -1000 - (client < 0 ? 0 : client);
+    }
+    int off = 0;
+    Seg* s = t.containingSegment(pos, rs, cl, off);
+    for (int k = 0; k < 16; k++) out[k] = 0;
+    if (json) *json = nullptr;
+    if (!s) {
+        out[1] = -1; out[2] = -1; out[5] = -1; out[6] = INT32_MIN; out[7] = -1; out[8] = -1; out[9] = -1; out[13] = -1;
+        out[14] = pos == t.getLength(rs, cl) ? t.getLength(t.currentSeq, t.cwClientId) : INT32_MIN;
+        return 0;
+    }
+    const int gp = t.getPosition(s, t.currentSeq, t.cwClientId);
+    out[0] = 1; out[1] = off; out[2] = gp; out[3] = s->cachedLength; out[4] = s->seq;
+    // clients as stream indexes (batch streams), or, asked by long id, as the oracle's own short
+    // ids (ora_client_name gives their long ids)
+    auto who = [&](int sid) { return client_literal ? (sid < 0 ? -1 : sid) : (t.collaborating ? d.streamOf(sid) : sid); };
+    out[5] = who(s->clientId);
+    out[6] = s->hasRemoved ? s->removedSeq : INT32_MIN;
+    out[7] = s->hasRemoved ? who(s->removedClientId) : -1;
+    out[8] = s->hasProps ? 1 : -1; out[9] = s->marker ? s->refType : -1;
+    std::vector<int> ix;
+    for (Node* x = s; x->parent; x = x->parent) ix.push_back(x->index);
+    uint64_t path = 0;
+    for (int k = (int)ix.size() - 1; k >= 0; k--) path = (path << 3) | (uint64_t)(ix[k] & 7);
+    out[10] = (int)ix.size(); out[11] = (int32_t)(path & 0xFFFFFFFFu); out[12] = (int32_t)(path >> 32);
+    out[13] = -1; out[14] = gp + off;
+    if (json) {
+        const std::string js = seg_json(s, nullptr);
+        *json = (char*)malloc(js.size() + 1); memcpy(*json, js.c_str(), js.size() + 1);
+    }
+    return 1;
+}
+// Diagnostic: getLength by leaf sums (nodeLength of every segment) instead of partial lengths.
+int32_t ora_get_length_exact(ora_doc* o, int32_t ref, int32_t client) {
+    int cl;
+    if (client < 0) cl = o->d.t.cwClientId;
+    else if (client < (int)o->d.streamToShort.size() && o->d.streamToShort[client] >= 0) cl = o->d.streamToShort[client];
+    else cl = -1000 - client;
+    return o->d.t.exactLength(o->d.t.root, ref, cl);
+}
+// The long id (JSON literal) of one of the document's short client ids; NULL if none.
+const char* ora_client_name(ora_doc* o, int32_t short_id) {
+    Doc& d = o->d;
+    return short_id >= 0 && short_id < (int)d.shortToName.size() ? d.shortToName[short_id].c_str() : nullptr;
 }
 static uint8_t* pack_blobs(const std::vector<std::string>& blobs, uint64_t* digest, uint64_t* total);
 uint8_t* ora_snapshot_v1(ora_doc* o, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total) {

@@ -60,6 +60,17 @@ int      ora_local_annotate(ora_doc* d, int32_t start, int32_t end, int32_t prop
  * reference throws, UNSUPPORTED for aliased loadBody segments / bad specs). */
 int      ora_load_snapshot(ora_doc* d, uint32_t n_blobs, const char* const* blobs);
 int32_t  ora_get_length(ora_doc* d, int32_t ref_seq, int32_t client); /* client -1: observer */
+/* getContainingSegment under stream client `client`'s perspective at ref_seq (ref_seq < 0:
+ * the local client at currentSeq, Client.getContainingSegment; client_literal non-null: the
+ * client with that long id, a JSON string literal), with resolveRemoteClientPosition in
+ * out16[14]; out16 in mt_seg_info order (prop_set 1 = properties defined, row -1); *json
+ * (optional, ora_free_buf) = the segment's toJSONObject.  Returns found. */
+int      ora_containing_segment(ora_doc* d, int32_t pos, int32_t ref_seq, int32_t client, const char* client_literal,
+                                int32_t* out16, char** json);
+/* Diagnostic: getLength as the sum of nodeLength over every segment (no partial lengths). */
+int32_t  ora_get_length_exact(ora_doc* d, int32_t ref_seq, int32_t client);
+/* The long id (JSON literal) of a short client id of the document, NULL if none. */
+const char* ora_client_name(ora_doc* d, int32_t short_id);
 /* Snapshot: returns a malloc'd buffer: u32 n_blobs, then per blob u64 len + bytes. */
 uint8_t* ora_snapshot_v1(ora_doc* d, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total_bytes);
 /* SnapshotLegacy (MT/snapshotlegacy.ts:104-240) blobs "header"[, "body"], same packing. */

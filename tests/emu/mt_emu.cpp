@@ -90,6 +90,18 @@ static int mtb_launch_get_length(mt_ctx* c, const uint32_t* docs, const int32_t*
     }
     return MT_OK;
 }
+static int mtb_launch_query(mt_ctx* c, const MtQuery* q, const uint32_t* grp, MtQueryOut* out, uint32_t n_groups) {
+    for (uint32_t g = 0; g < n_groups; g++) {
+        MtScratch sc; MtEngFast e; e.bind(c->S, q[grp[g]].doc, &sc);
+        mt_query_run(e, c->S, q, grp[g], grp[g + 1], out);
+    }
+    return MT_OK;
+}
+static int mtb_launch_gather_text(mt_ctx* c, const unsigned long long* at, const uint32_t* len, const unsigned long long* off,
+                                  uint16_t* dst, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) memcpy(dst + off[i], c->S.text + at[i], 2ull * len[i]);
+    return MT_OK;
+}
 static int mtb_launch_pack_size(mt_ctx* c, const uint32_t* docs, MtPackSize* out, uint32_t n) {
     for (uint32_t i = 0; i < n; i++) { MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc); out[i] = mt_pack_size(e); }
     return MT_OK;

@@ -82,6 +82,12 @@ def lib():
         L.ora_replay_batch.restype = ctypes.c_double
         L.ora_replay_batch.argtypes = [ctypes.POINTER(MtOpBatch), ctypes.POINTER(MtPropTable), ctypes.c_int, P, P, P]
         L.ora_counters.argtypes = [P, P]
+        L.ora_containing_segment.restype = ctypes.c_int
+        L.ora_get_length_exact.restype = I32
+        L.ora_get_length_exact.argtypes = [P, I32, I32]
+        L.ora_client_name.restype = ctypes.c_char_p
+        L.ora_client_name.argtypes = [P, I32]
+        L.ora_containing_segment.argtypes = [P, I32, I32, I32, ctypes.c_char_p, P, ctypes.POINTER(P)]
         _lib = L
     return _lib
 
@@ -237,6 +243,28 @@ class OracleDoc:
         a = np.frombuffer(ctypes.string_at(buf, n.value * 48), np.int32).reshape(-1, 12).copy()
         self.L.ora_free_buf(buf)
         return a
+
+    def containing_segment(self, pos: int, ref_seq: int = -1, client: int = -1, client_id: str | None = None):
+        """getContainingSegment (+ resolveRemoteClientPosition) under stream client `client`'s
+        perspective at ref_seq (ref_seq < 0: the local client at currentSeq; client_id: the
+        client with that long id instead): (16 int32 in mt_seg_info order, the segment's JSON
+        text or None)."""
+        from fluidframework_amd.jsjson import quote
+        out = np.zeros(16, np.int32)
+        js = ctypes.c_void_p()
+        lit = quote(client_id).encode("utf-8", "surrogatepass") if client_id is not None else None
+        self.L.ora_containing_segment(self.h, pos, ref_seq, client, lit, out.ctypes.data, ctypes.byref(js))
+        txt = None
+        if js.value:
+            txt = ctypes.string_at(js.value).decode("utf-8", "surrogatepass")
+            self.L.ora_free_buf(js.value)
+        return out, txt
+
+    def client_name(self, short_id: int):
+        """The long id of one of the oracle's short client ids (None if none)."""
+        import json
+        v = self.L.ora_client_name(self.h, short_id)
+        return None if v is None else json.loads(v.decode("utf-8", "surrogatepass"))
 
     def counters(self) -> dict:
         """The §8(d) algorithmic counters (mt_doc_counters order) by the oracle's own count."""
