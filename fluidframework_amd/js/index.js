@@ -200,6 +200,22 @@ class Engine {
     syncAsync() { return addon.syncAsync(this.h); }
     status(docs) { return addon.docStatus(this.h, Uint32Array.from(docs)); }
     getLength(docs, refSeq, client) { return addon.getLength(this.h, Uint32Array.from(docs), Int32Array.from(refSeq), Int32Array.from(client)); }
+    /**
+     * mt_get_containing_segment: per query {found, offset, obsPos, len, seq, client, removedSeq,
+     * removedClient, propSet, markerRefType, depth, pathLo, pathHi, row, resolved, json}
+     * (refSeq < 0: the local view; resolved === -2**31: undefined).
+     */
+    containingSegment(docs, pos, refSeq, client) {
+        const { info, json } = addon.getContainingSegment(this.h, Uint32Array.from(docs), Int32Array.from(pos),
+            Int32Array.from(refSeq), Int32Array.from(client));
+        const F = ["found", "offset", "obsPos", "len", "seq", "client", "removedSeq", "removedClient", "propSet",
+            "markerRefType", "depth", "pathLo", "pathHi", "row", "resolved"];
+        return json.map((j, i) => {
+            const o = { json: j };
+            F.forEach((f, k) => { o[f] = info[16 * i + k]; });
+            return o;
+        });
+    }
     updateSeq(docs, msn, seq) { addon.updateSeq(this.h, Uint32Array.from(docs), Int32Array.from(msn), Int32Array.from(seq)); }
     snapshot(docs, msn, seq, legacy = false) {
         return (legacy ? addon.snapshotLegacy : addon.snapshotV1)(this.h, Uint32Array.from(docs), Int32Array.from(msn),
@@ -273,6 +289,7 @@ class MergeTreeClient {
         const snap = parseSnapshot(blobs);
         const lb = new LoadBuilder(this.group.engine.props);
         lb.add(this.docId, snap, this.names);
+        this.group.version++;
         addon.setDocClientNames(this.group.engine.h, this.docId, this.names.names.map((n) => JSON.stringify(n)));
         this.namesUploaded = this.names.names.length;
         this.group.engine.loadSnapshot(lb.build());
@@ -288,6 +305,7 @@ class MergeTreeClient {
     }
     updateSeqNumbers(min, seq) {
         this.group.flush();
+        this.group.version++;
         this.group.engine.updateSeq([this.docId], [min], [seq]);
         this.minSeq = min; this.currentSeq = seq;
         this.checkStatus();
@@ -301,6 +319,60 @@ class MergeTreeClient {
         this.group.flush();
         this.checkStatus();
         return this.group.engine.getText([this.docId])[0];
+    }
+    // Short client ids (client.ts:658-670): the local client 0, remote clients in first-seen order.
+    getOrAddShortClientId(longClientId) {
+        if (this.longClientId !== undefined && longClientId === this.longClientId) return 0;
+        return this.names.index(longClientId) + 1;
+    }
+    getShortClientId(longClientId) {
+        if (this.longClientId !== undefined && longClientId === this.longClientId) return 0;
+        const i = this.names.ids.get(longClientId);
+        if (i === undefined) throw new Error(`unknown client ${longClientId}`);
+        return i + 1;
+    }
+    getLongClientId(shortClientId) { return shortClientId === 0 ? this.longClientId : this.names.names[shortClientId - 1]; }
+    query(pos, refSeq, shortId) {
+        this.group.flush();
+        this.checkStatus();
+        const local = shortId === undefined || shortId === 0;
+        return this.group.engine.containingSegment([this.docId], [pos], [local ? -1 : refSeq], [local ? -1 : shortId - 1])[0];
+    }
+    /**
+     * Client.getContainingSegment (client.ts:1040-1043; MergeTree.getContainingSegment,
+     * mergeTree.ts:1616-1627) in the local view: { segment, offset }.  The segment is a copy
+     * (ISegment fields and toJSONObject) taken now, valid for getPosition until the document
+     * next changes.
+     */
+    getContainingSegment(pos) {
+        const q = this.query(pos, 0, undefined);
+        if (!q.found) return { segment: undefined, offset: undefined };
+        const j = JSON.parse(q.json);
+        const shortOf = (i) => (i < 0 ? -2 : i + 1);                // NonCollabClient = -2
+        const seg = {
+            cachedLength: q.len, seq: q.seq, clientId: shortOf(q.client),
+            removedSeq: q.removedSeq === -(2 ** 31) ? undefined : q.removedSeq,
+            removedClientId: q.removedSeq === -(2 ** 31) ? undefined : shortOf(q.removedClient),
+            properties: typeof j === "string" ? undefined : j.props,
+            toJSONObject: () => j, _obsPos: q.obsPos, _version: this.group.version,
+        };
+        if (typeof j === "string") seg.text = j;
+        else if (j.marker) seg.refType = j.marker.refType;
+        else seg.text = j.text;
+        return { segment: seg, offset: q.offset };
+    }
+    /** Client.getPosition (client.ts:306-311) of a segment copy from getContainingSegment. */
+    getPosition(segment) {
+        if (segment === undefined) return -1;
+        if (segment._version !== this.group.version || this.pending.length) {
+            throw new Error("segment copy is stale: the document changed since getContainingSegment");
+        }
+        return segment._obsPos;
+    }
+    /** MergeTree.resolveRemoteClientPosition (mergeTree.ts:2125-2145); undefined where the reference's is. */
+    resolveRemoteClientPosition(remoteClientPosition, remoteClientRefSeq, remoteClientId) {
+        const q = this.query(remoteClientPosition, remoteClientRefSeq, remoteClientId);
+        return q.resolved === -(2 ** 31) ? undefined : q.resolved;
     }
     /**
      * Client.snapshot (client.ts:923-956) with the reference's signature: the delta
@@ -339,7 +411,7 @@ class MergeTreeClient {
 
 /** Many documents on one engine: `newClient()` per document, `flush()` batches. */
 class ClientGroup {
-    constructor(engine) { this.engine = engine; this.clients = []; }
+    constructor(engine) { this.engine = engine; this.clients = []; this.version = 0; }
     newClient(options) {
         const d = this.clients.length;
         if (d >= this.engine.maxDocs) throw new Error("engine document capacity exhausted");
@@ -365,6 +437,7 @@ class ClientGroup {
             }
         }
         const batch = bb.build();
+        this.version++;                                      // segment copies taken before are stale
         // Capture only around batches with a listener; the capacity is one launch's buffer
         // (a batch that emits more resumes in further launches, mt_delta_capture).
         if (listen.length) this.engine.deltaCapture(Math.max(1 << 16, 512 * listen.length + 16 * batch.type.length));

@@ -392,6 +392,34 @@ napi_value GetLength(napi_env env, napi_callback_info info) {
     return rc ? throw_rc(env, c, rc, "mt_get_length") : make_i32(env, out.data(), n);
 }
 
+// getContainingSegment(ctx, docs, pos, refSeq, client) -> {info: Int32Array (16 per query,
+// mt_seg_info), json: [string | null]} (mt_get_containing_segment)
+napi_value GetContainingSegment(napi_env env, napi_callback_info info) {
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return nullptr;
+    mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
+    const uint32_t* docs; const int32_t* pos; const int32_t* ref; const int32_t* cli; size_t n, n1, n2, n3;
+    if (!typed(env, argv[1], napi_uint32_array, &docs, &n) || !typed(env, argv[2], napi_int32_array, &pos, &n1) ||
+        !typed(env, argv[3], napi_int32_array, &ref, &n2) || !typed(env, argv[4], napi_int32_array, &cli, &n3)) return nullptr;
+    if (n1 < n || n2 < n || n3 < n) { napi_throw_range_error(env, nullptr, "pos/refSeq/client shorter than docs"); return nullptr; }
+    std::vector<mt_seg_info> out(n + 1);
+    const char* arena = nullptr; const uint64_t* off = nullptr;
+    int rc = mt_get_containing_segment(c, (uint32_t)n, docs, pos, ref, cli, out.data(), &arena, &off);
+    if (rc) return throw_rc(env, c, rc, "mt_get_containing_segment");
+    napi_value o, js;
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "info", make_i32(env, (const int32_t*)out.data(), 16 * n));
+    NAPI_OK(napi_create_array_with_length(env, n, &js));
+    for (size_t i = 0; i < n; i++) {
+        napi_value s;
+        if (out[i].found) napi_create_string_utf8(env, arena + off[i], (size_t)(off[i + 1] - off[i]), &s);
+        else napi_get_null(env, &s);
+        napi_set_element(env, js, (uint32_t)i, s);
+    }
+    napi_set_named_property(env, o, "json", js);
+    return o;
+}
+
 // snapshotV1(ctx, docs, msn, seq) -> [{blobs: [header, body_0, ...], digest: BigInt}]
 // snapshotLegacy(ctx, docs, msn, seq) -> [{blobs: [header(, body)], digest: BigInt}]
 static napi_value snapshot_blobs(napi_env env, napi_callback_info info, bool legacy) {
@@ -530,6 +558,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"docStatus", nullptr, DocStatus, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"updateSeq", nullptr, UpdateSeq, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"getLength", nullptr, GetLength, nullptr, nullptr, nullptr, kAttr, nullptr},
+        {"getContainingSegment", nullptr, GetContainingSegment, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"snapshotV1", nullptr, SnapshotV1, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"snapshotLegacy", nullptr, SnapshotLegacy, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"getText", nullptr, GetText, nullptr, nullptr, nullptr, kAttr, nullptr},

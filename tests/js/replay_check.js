@@ -34,6 +34,27 @@ clients.forEach((c, d) => {
         c.options = opts;
     }
 });
+// optional position queries [doc, pos, refSeq (< 0: local view), long client id]: through the
+// Client (getContainingSegment / getPosition / resolveRemoteClientPosition) and the engine
+if (spec.queries) {
+    out.queries = spec.queries.map(([d, pos, ref, who]) => {
+        const c = clients[d];
+        const local = ref < 0;
+        const known = !local && c.names.ids.has(who);
+        const cli = local ? -1 : (known ? c.names.ids.get(who) : 60);
+        const q = eng.containingSegment([c.docId], [pos], [ref], [cli])[0];
+        const name = (i) => (i < 0 ? null : c.names.names[i]);
+        const r = { ...q, client: name(q.client), removedClient: name(q.removedClient) };
+        if (local) {
+            const { segment, offset } = c.getContainingSegment(pos);
+            r.viaClient = segment === undefined ? null : [JSON.stringify(segment.toJSONObject()), offset, c.getPosition(segment)];
+        } else if (known) {
+            r.viaClient = c.resolveRemoteClientPosition(pos, ref, c.getShortClientId(who));
+            if (r.viaClient === undefined) r.viaClient = null;
+        }
+        return r;
+    });
+}
 const snaps = eng.snapshot(clients.map((c) => c.docId), clients.map((c) => c.minSeq), clients.map((c) => c.getCurrentSeq()));
 out.digests = snaps.map((s) => s.digest.toString(16));
 fs.writeFileSync(outPath, JSON.stringify(out));

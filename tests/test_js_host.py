@@ -18,7 +18,8 @@ from test_emu_parity import CONFIGS, ann_props
 
 pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 
-EXPORTS = ["applyBatch", "create", "deltaCapture", "deltaRecords", "deltaText", "destroy", "docPset", "docStatus", "docsOpen", "getLength", "getText", "lastError",
+EXPORTS = ["applyBatch", "create", "deltaCapture", "deltaRecords", "deltaText", "destroy", "docPset", "docStatus", "docsOpen",
+           "getContainingSegment", "getLength", "getText", "lastError",
            "loadSnapshot", "setClientNames", "setDocClientNames", "setProps", "setResidency", "snapshotLegacy", "snapshotV1", "sync",
            "syncAsync",
            "updateSeq"]
@@ -35,9 +36,11 @@ def check(cfg, n_docs, addon, seed=31):
     # under catchUpBlobName (snapshotlegacy.ts:162-172).
     catch_up = [msgs[d][-3:] if d % 2 == 0 else [] for d in range(n_docs)]
     blob_name = "randomNameForCatchUpOps"     # generateSharedStrings.ts:17 renames it the same way
+    queries = position_queries(batch, kept, CONFIGS[cfg]["clients"], seed)
     got = run_node(msgs, addon=addon, limits=dict(rowsPerDoc=20000, windowPerDoc=8192, propsetsPerDoc=8192,
                                                   textPerDoc=1 << 18),
-                   legacy={"options": {"catchUpBlobName": blob_name}, "catchUp": catch_up})
+                   legacy={"options": {"catchUpBlobName": blob_name}, "catchUp": catch_up}, queries=queries)
+    check_queries(queries, got["queries"], kept)
     last = batch.op_offsets[1:] - 1
     for d in range(n_docs):
         od = kept[d]
@@ -52,6 +55,48 @@ def check(cfg, n_docs, addon, seed=31):
         if catch_up[d]:
             want.append((blob_name, json.dumps(catch_up[d], separators=(",", ":"))))
         assert [tuple(x) for x in got["legacy"][d]] == want, f"doc {d} legacy snapshot"
+
+
+def position_queries(batch, kept, n_clients, seed, per_doc=60):
+    """[doc, pos, refSeq, "c<i>"] queries under valid perspectives (refSeq at or above the
+    client's last refSeq and the MSN; -1: the local view) at the end of each stream."""
+    import numpy as np
+    rng = np.random.RandomState(seed)
+    A, out = batch.arrays, []
+    for d in range(len(batch.op_offsets) - 1):
+        o0, o1 = int(batch.op_offsets[d]), int(batch.op_offsets[d + 1])
+        ms, cs = int(A["msn"][o1 - 1]), int(A["seq"][o1 - 1])
+        last_ref = {}
+        for k in range(o0, o1):
+            c = int(A["client"][k])
+            last_ref[c] = max(last_ref.get(c, 0), int(A["ref_seq"][k]))
+        for _ in range(per_doc):
+            if rng.rand() < 0.3:
+                out.append([d, int(rng.randint(-1, kept[d].get_length(cs, -1) + 2)), -1, None])
+                continue
+            c = int(rng.randint(0, n_clients))
+            r = int(rng.randint(max(ms, last_ref.get(c, 0)), cs + 1))
+            out.append([d, int(rng.randint(-1, kept[d].get_length(r, c) + 3)), r, f"c{c}"])
+    return out
+
+
+def check_queries(queries, got, kept):
+    """Node's answers (engine record and the Client method) against the oracle's."""
+    for (d, pos, ref, who), g in zip(queries, got):
+        c = -1 if who is None else int(who[1:])
+        want, wjs = kept[d].containing_segment(pos, ref, c)
+        name = lambda i: None if i < 0 else f"c{i}"  # noqa: E731
+        assert [g["found"], g["offset"], g["obsPos"], g["len"], g["seq"], g["client"], g["removedSeq"],
+                g["removedClient"], g["resolved"]] == [int(want[0]), int(want[1]), int(want[2]), int(want[3]),
+                                                       int(want[4]), name(int(want[5])), int(want[6]),
+                                                       name(int(want[7])), int(want[14])], (d, pos, ref, who, g)
+        assert g["json"] == wjs
+        if who is None:
+            assert g["viaClient"] == (None if wjs is None else [json.dumps(json.loads(wjs), separators=(",", ":"),
+                                                                          ensure_ascii=False), int(want[1]),
+                                                               int(want[2])])
+        elif "viaClient" in g:
+            assert g["viaClient"] == (None if int(want[14]) == -(1 << 31) else int(want[14]))
 
 
 def test_product_addon_loads_and_exports():
