@@ -320,7 +320,8 @@ def run_config4(args, c, world, rank, local):
         "gen_seconds": gen_s,
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"], odg, ost = cpu_baseline_config4(eng, c, pa, pb, min(16, os.cpu_count() or 1))
+        out["cpu_baseline"], odg, ost = cpu_baseline_config4(eng, c, pa, pb, min(16, os.cpu_count() or 1),
+                                                             docs=min(n, args.parity_docs))
         if ok:
             out["parity"] = digest_parity(digs, odg, ost)
     elif world > 1 and ok:
@@ -453,6 +454,8 @@ def run_config5(args, c, world, rank, local):
         "exchange": {"docs_checked": int(bad[2].item()), "checksum_mismatch_docs": int(bad[1].item()),
                      "note": "per-document 64-bit checksums of the exchanged rows: packed by rank 0, verified on "
                              "arrival by the owning rank (mt_generated_pack_rows / mt_upload_rows_dev)"},
+        "snapshot": {"docs": sh.n_docs, "ms": sh.timings.get("snapshot_ms"), "host_threads": min(16, os.cpu_count() or 1),
+                     "note": "rank 0's mt_snapshot_digests (staged download + SnapshotV1 JSON + xxh64), before the gather"},
         "sharding": {"rebalance_ms": sh.timings.get("rebalance_ms"), "rebalance_bytes": sh.timings.get("rebalance_bytes"),
                      "digest_gather_ms": sh.timings.get("digest_ms"), "ingest_generate_s": sh.timings.get("generate_s"),
                      "setup_s": setup_s, "digest_xor": f"{int(np.bitwise_xor.reduce(digs)):016x}",
@@ -469,23 +472,25 @@ def run_config5(args, c, world, rank, local):
     print(json.dumps(out), flush=True)
 
 
-def config5_parity(args, c, sh, digs, k=48):
-    """Oracle replay (its own generator, same seeds and per-document counts) of the
-    smallest-id documents, against the digests gathered to rank 0 (checker only)."""
+def config5_parity(args, c, sh, digs):
+    """Oracle replay (its own generator, same seeds and per-document counts, documents
+    generated on host threads) of the smallest-id documents (--parity-docs, default 4096),
+    against the digests gathered to rank 0 (checker only)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from fluidframework_amd.batch import MtGenParams
     from oracle_lib import generate
-    k = min(k, len(sh.all_ops))
+    k = min(args.parity_docs or 4096, len(sh.all_ops))
     p = MtGenParams(args.seed, k, 0, 2, c["lag"], c["ins"], c["rem"], c["ins_len"], c["rem_len"], c["ann_sets"],
                     c["rewrite"])
     cl = sh.clients_all[:k] if getattr(sh, "clients_all", None) is not None else None
     if cl is None:
         return "status words clean on every rank (no client counts for an oracle check)"
     batch, st, kept = generate(p, ann_props(), docs=range(k), keep=True, ops_per_doc=sh.all_ops[:k],
-                               clients_per_doc=cl)
+                               clients_per_doc=cl, threads=min(16, os.cpu_count() or 1))
     last = batch.op_offsets[1:] - 1
     odg = np.array([kept[d].snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]))[1]
                     for d in range(k)], np.uint64)
+    del kept
     return digest_parity(digs, odg, np.asarray(st)) + ", all ranks clean"
 
 
@@ -660,6 +665,8 @@ def _main(argv=None):
     ap.add_argument("--seed", type=int, default=20241015)
     ap.add_argument("--prebuild", type=int, default=0, help="config4: override pre-build appends per document")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--parity-docs", type=int, default=0,
+                    help="documents the oracle checks (config 4: default one per host thread; config 5: 4096)")
     ap.add_argument("--no-ingest", action="store_true", help="skip the host ingest leg (packers, H2D)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--residency", default="auto", choices=["auto", "lds", "hbm", "blk", "big"],
@@ -772,7 +779,10 @@ def _main(argv=None):
     handover = None
     if args.residency != "hbm":
         cur = eng.last_cursors(c["docs"]).astype(np.int64)
-        handover = int((cur < (np.arange(c["docs"]) + 1) * c["ops"]).sum())
+        ends = (np.arange(c["docs"]) + 1) * c["ops"]
+        ho = np.nonzero(cur < ends)[0]
+        # where each hand-over happened: the op index within its run (the rest ran from HBM)
+        handover = {"docs": int(len(ho)), "at_op": [int(cur[d] - d * c["ops"]) for d in ho[:16]]}
     # SnapshotV1 of every document at its current window (reported, not timed as ops)
     t1 = time.perf_counter()
     sthreads = min(16, os.cpu_count() or 1)

@@ -745,7 +745,9 @@ int MT_FN(get_containing_segment)(mt_ctx* c, uint32_t n, const uint32_t* docs, c
         if (f.found) {
             const bool marker = f.marker_ref_type >= 0;
             const int64_t k = slot[i];
-            mtsnap::seg_json_of(c->seg_json_arena, marker, f.marker_ref_type, f.prop_set >= 0 ? res[i].ps : nullptr, c->names,
+            std::string pj;
+            if (f.prop_set >= 0) mtsnap::props_json(pj, res[i].ps, c->names);
+            mtsnap::seg_json_of(c->seg_json_arena, marker, f.marker_ref_type, f.prop_set >= 0 ? &pj : nullptr,
                                 k >= 0 ? txt.data() + off[k] : nullptr, k >= 0 ? (size_t)len[k] : 0);
         }
         c->seg_json_off.push_back(c->seg_json_arena.size());
@@ -793,9 +795,8 @@ static int mt_download_doc(mt_ctx* c, uint32_t d, MtHostDoc& h) {
 
 // Gather documents' live state into host memory with two kernels and one copy
 // (mt_pack.h); views[i] points into `host`.
-static int mt_stage_docs(mt_ctx* c, uint32_t n, const uint32_t* docs, std::vector<uint8_t>& host,
-                         std::vector<MtSnapView>& views) {
-    views.clear(); host.clear();
+static int mt_stage_docs(mt_ctx* c, uint32_t n, const uint32_t* docs, std::vector<MtSnapView>& views) {
+    views.clear();
     if (n == 0) return MT_OK;
     for (uint32_t i = 0; i < n; i++) if (docs[i] >= c->S.maxDocs) { c->err = "doc id out of range"; return MT_E_INVALID; }
     int rc;
@@ -803,20 +804,23 @@ static int mt_stage_docs(mt_ctx* c, uint32_t n, const uint32_t* docs, std::vecto
     if ((rc = mtb_ensure(c, c->b_pack_sz, sizeof(MtPackSize) * n))) return rc;
     if ((rc = mtb_ensure(c, c->b_pack_off, 8ull * n))) return rc;
     mtb_h2d(c, c->b_pack_docs.p, docs, 4ull * n);
-    if ((rc = mtb_launch_pack_size(c, (const uint32_t*)c->b_pack_docs.p, (MtPackSize*)c->b_pack_sz.p, n))) return rc;
+    const uint32_t epoch = ++c->stage_epoch;
+    if ((rc = mtb_launch_pack_size(c, (const uint32_t*)c->b_pack_docs.p, (MtPackSize*)c->b_pack_sz.p, n, epoch))) return rc;
     std::vector<MtPackSize> sz(n);
     mtb_d2h(c, sz.data(), c->b_pack_sz.p, sizeof(MtPackSize) * n);
     std::vector<uint64_t> off(n + 1, 0);
     for (uint32_t i = 0; i < n; i++) off[i + 1] = off[i] + mt_pack_bytes(sz[i]);
     if ((rc = mtb_ensure(c, c->b_stage, off[n] + 16))) return rc;
     mtb_h2d(c, c->b_pack_off.p, off.data(), 8ull * n);
-    if ((rc = mtb_launch_pack(c, (const uint32_t*)c->b_pack_docs.p, (const uint64_t*)c->b_pack_off.p, (uint8_t*)c->b_stage.p, n))) return rc;
+    if ((rc = mtb_launch_pack(c, (const uint32_t*)c->b_pack_docs.p, (const uint64_t*)c->b_pack_off.p, (uint8_t*)c->b_stage.p, n,
+                              epoch))) return rc;
     if ((rc = mtb_sync(c))) return rc;
-    host.resize(off[n] + 16);
-    mtb_d2h(c, host.data(), c->b_stage.p, off[n]);
+    uint8_t* host = mtb_host_stage(c, off[n] + 16);
+    if (!host) { c->err = "pinned staging allocation failed"; return MT_E_OOM; }
+    mtb_d2h(c, host, c->b_stage.p, off[n]);
     views.resize(n);
     for (uint32_t i = 0; i < n; i++) {
-        const MtStagedDoc sd = MtStagedDoc::at(host.data() + off[i]);
+        const MtStagedDoc sd = MtStagedDoc::at(host + off[i]);
         MtSnapView& v = views[i];
         v.hdr = sd.hdr; v.R = sd.R; v.blk = sd.blk; v.text = sd.text; v.pset = sd.pset;
     }
@@ -843,8 +847,8 @@ static int mt_snapshot_blobs(mt_ctx* c, uint32_t n, const uint32_t* docs, const 
     if (!c) return MT_E_INVALID;
     int rc = MT_FN(update_seq)(c, n, docs, msn, seq);       // Client.snapshot: updateSeqNumbers first (client.ts:936)
     if (rc) return rc;
-    std::vector<uint8_t> host; std::vector<MtSnapView> views;
-    if ((rc = mt_stage_docs(c, n, docs, host, views))) return rc;
+    std::vector<MtSnapView> views;
+    if ((rc = mt_stage_docs(c, n, docs, views))) return rc;
     if ((rc = mt_check_staged_status(c, n, docs, views))) return rc;
     c->snap_arena.clear(); c->blob_off.assign(1, 0); c->blob_first.assign(1, 0);
     for (uint32_t i = 0; i < n; i++) {
@@ -878,22 +882,28 @@ int MT_FN(snapshot_digests)(mt_ctx* c, uint32_t n, const uint32_t* docs, const i
     if (!c || (n && (!docs || !msn || !seq || !digest))) return MT_E_INVALID;
     int rc = MT_FN(update_seq)(c, n, docs, msn, seq);
     if (rc) return rc;
-    std::vector<uint8_t> host; std::vector<MtSnapView> views;
-    if ((rc = mt_stage_docs(c, n, docs, host, views))) return rc;
-    if ((rc = mt_check_staged_status(c, n, docs, views))) return rc;
     if (threads < 1) threads = 1;
-    if ((uint32_t)threads > n) threads = (int)(n ? n : 1);
-    auto work = [&](int t) {
-        for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)threads) {
-            auto dn = c->doc_clients.find(docs[i]);
-            digest[i] = mtsnap::blobs_digest(mtsnap::snapshot_blobs(views[i], c->names,
-                                                                    dn == c->doc_clients.end() ? nullptr : &dn->second));
-        }
-    };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < threads; t++) pool.emplace_back(work, t);
-    work(0);
-    for (auto& th : pool) th.join();
+    // chunks of documents, so the staging buffers stay bounded however many documents
+    // (a million Zipf documents stage ~20 GB)
+    const uint32_t CH = 32768;
+    for (uint32_t a = 0; a < n; a += CH) {
+        const uint32_t m = (n - a) < CH ? (n - a) : CH;
+        std::vector<MtSnapView> views;
+        if ((rc = mt_stage_docs(c, m, docs + a, views))) return rc;
+        if ((rc = mt_check_staged_status(c, m, docs + a, views))) return rc;
+        const int th = (uint32_t)threads > m ? (int)m : threads;
+        auto work = [&](int t) {
+            for (uint32_t i = (uint32_t)t; i < m; i += (uint32_t)th) {
+                auto dn = c->doc_clients.find(docs[a + i]);
+                digest[a + i] = mtsnap::blobs_digest(mtsnap::snapshot_blobs(views[i], c->names,
+                                                                            dn == c->doc_clients.end() ? nullptr : &dn->second));
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < th; t++) pool.emplace_back(work, t);
+        work(0);
+        for (auto& t : pool) t.join();
+    }
     return MT_OK;
 }
 
@@ -901,8 +911,8 @@ int MT_FN(get_text)(mt_ctx* c, uint32_t n, const uint32_t* docs, const uint16_t*
     if (!c) return MT_E_INVALID;
     int rc = mtb_sync(c);
     if (rc) return rc;
-    std::vector<uint8_t> host; std::vector<MtSnapView> views;
-    if ((rc = mt_stage_docs(c, n, docs, host, views))) return rc;
+    std::vector<MtSnapView> views;
+    if ((rc = mt_stage_docs(c, n, docs, views))) return rc;
     c->text_arena.clear(); c->text_off.assign(1, 0);
     for (uint32_t i = 0; i < n; i++) {
         mtsnap::observer_text(views[i], c->text_arena);

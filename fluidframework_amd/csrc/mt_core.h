@@ -470,6 +470,7 @@ struct MtCold {
     uint16_t* dtext; unsigned long long dtcap;
     uint32_t dused, tused; int dstop;
     int* regr; int regTop, regHalf, regCap;   // register row arena (this document's)
+    int pcKey[4], pcVal[4];                   // newMap: property maps made from an op's set alone
 };
 #if defined(__HIP_DEVICE_COMPILE__)
 __shared__ MtCold mt_cold_v;
@@ -661,6 +662,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         nU = 0; uValid = false; uRef = -1; uCli = -1;
         heapTop = heapN > 0 ? uni(heap[1].maxSeq) : 0x7FFFFFFF;     // HBM home: bind precedes toLds
         lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0; bcOn = false; htOk = false; hlistN = 0; htOn = pfOn = false; mwSeq = 0;
+        for (int i = 0; i < 4; i++) mt_cold_v.pcKey[i] = -1;
         rfHbm = st.hold + (size_t)d * MT_RFL; rfN = uni(h.rfN); blkFreeN = uni(h.blkFreeN);
         heapHW = uni(h.heapHW); winHW = uni(h.winHW); ovxN = uni(h.ovxN);
         regTop = uni(h.regTop); regHalf = uni(h.regHalf) & 1;
@@ -697,6 +699,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     MT_HD void open() {
         root = 0; height = 0; minSeq = 0; curSeq = 0; rowTop = 0; blkTop = 1; blkFree = -1;
         heapN = 0; winN = 0; textTop = 0; psetTop = 0; status = 0; textHalf = 0; heapTop = 0x7FFFFFFF; rfN = 0;
+        for (int i = 0; i < 4; i++) mt_cold_v.pcKey[i] = -1;    // the memo's maps are gone with the pool
         blkFreeN = 0; heapHW = 0; winHW = 0; ovxN = 0;
         text = S.textBase;
         c_ops = c_msgs = c_ins = c_rows = c_depth = c_scour = 0;
@@ -1847,6 +1850,10 @@ template <int RES, bool FULL = true> struct MtEngT {
             // variant that failed on the device in rounds 2 and 3)
             LaneArr<ChildL> cl;
             if (h.height == 0) {
+#if defined(MT_DBG_FENCE) && defined(__HIP_DEVICE_COMPILE__)
+                __builtin_amdgcn_s_waitcnt(0);                   // every earlier access complete first
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+#endif
                 const int rr = r, cc = c;
                 cl = wave_map(h.n, [&](int j) MT_LAM {
                     const int s = own(ch, j);
@@ -2449,6 +2456,19 @@ template <int RES, bool FULL = true> struct MtEngT {
         return id;
     }
 
+    // The property map of a new segment made from op prop set `opset` alone (TextSegment.make /
+    // Marker.make -> addProperties on undefined properties).  Maps are immutable and never freed,
+    // so segments made from the same set share one: a direct-mapped memo of the last maps made
+    // (per bind) instead of a new map per insert.
+    MT_HD int newPropMap(int opset) {
+        const int k = opset & 3;
+        if (mt_cold_v.pcKey[k] == opset) return mt_cold_v.pcVal[k];
+        const int id = applyPropSet(-1, opset, false);
+        if (status) return id;
+        mt_cold_v.pcKey[k] = opset; mt_cold_v.pcVal[k] = id;
+        return id;
+    }
+
     /* ----------------------------------------------------- range walks -- */
     // nodeMap over [start, end) under (r, c) with the remove / annotate leaf
     // action and post-order length maintenance (MT/mergeTree.ts:2626-2739,
@@ -2656,7 +2676,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         wave_sync();
         for (int i = 0; i < nh; i++) {                        // TextSegment.make / Marker.make: addProperties(props)
             const int pid = uni((int)G[i].prop);
-            if (pid >= 0) { const int ps = applyPropSet(-1, pid, false); row(i).props = ps; }
+            if (pid >= 0) { const int ps = newPropMap(pid); row(i).props = ps; }
         }
         if (status) return;
         for (int base = 0; base < nh; base += MT_WAVE) {      // collab window
@@ -2742,7 +2762,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             c_ins += (uint64_t)plen;
         }
         const int pid = uni((int)g->prop);
-        if (pid >= 0) { const int ps = applyPropSet(-1, pid, false); row(n).props = ps; }
+        if (pid >= 0) { const int ps = newPropMap(pid); row(n).props = ps; }
         wave_sync();
         if (status) return 0;
         const int w = walk(MT_WALK_INSERT, pos, 0, cli, n, rm ? 0 : L);
@@ -2772,7 +2792,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                 if (markerId >= midCap) { status |= MT_DS_UNSUPPORTED; return; }
                 midt[markerId] = n;
             }
-            row(n).props = segProps >= 0 ? applyPropSet(-1, segProps, false) : -1;
+            row(n).props = segProps >= 0 ? newPropMap(segProps) : -1;
             row(n).tcap = marker ? 0 : plen;
             if (marker) row(n).toff = refType;
             else {

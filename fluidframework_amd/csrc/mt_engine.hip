@@ -64,18 +64,19 @@ __global__ __launch_bounds__(256) void mt_gather_text_kernel(const uint16_t* tex
 }
 
 // Staging for host-side serialization (mt_pack.h): sizes, then the packed copy.
-__global__ __launch_bounds__(64) void mt_pack_size_kernel(MtState S, const uint32_t* docs, MtPackSize* out) {
+__global__ __launch_bounds__(64) void mt_pack_size_kernel(MtState S, const uint32_t* docs, MtPackSize* out, uint32_t epoch) {
     __shared__ MtScratch sc;
     MtEng e;
     e.bind(S, docs[blockIdx.x], &sc);
-    const MtPackSize z = mt_pack_size(e);
+    const MtPackSize z = mt_pack_size(e, epoch);
     if (__lane_id() == 0) out[blockIdx.x] = z;
 }
-__global__ __launch_bounds__(64) void mt_pack_kernel(MtState S, const uint32_t* docs, const uint64_t* off, uint8_t* stage) {
+__global__ __launch_bounds__(64) void mt_pack_kernel(MtState S, const uint32_t* docs, const uint64_t* off, uint8_t* stage,
+                                                     uint32_t epoch) {
     __shared__ MtScratch sc;
     MtEng e;
     e.bind(S, docs[blockIdx.x], &sc);
-    mt_pack_doc(e, stage + off[blockIdx.x]);
+    mt_pack_doc(e, stage + off[blockIdx.x], epoch);
 }
 
 // Document exchange rows (mt_shard.h): one wave per document run.
@@ -105,6 +106,7 @@ static void mtb_fini(mt_ctx* c) {
         if (st.ev) (void)hipEventDestroy((hipEvent_t)st.ev);
         if (st.p) (void)hipHostFree(st.p);
     }
+    if (c->dl_host) (void)hipHostFree(c->dl_host);
     if (c->ev0) (void)hipEventDestroy((hipEvent_t)c->ev0);
     if (c->ev1) (void)hipEventDestroy((hipEvent_t)c->ev1);
     if (c->stream2) { (void)hipStreamSynchronize((hipStream_t)c->stream2); (void)hipStreamDestroy((hipStream_t)c->stream2); }
@@ -137,6 +139,17 @@ static void mtb_stage_send(mt_ctx* c, void* dev, size_t n) {
     (void)hipMemcpyAsync(dev, st.p, n, hipMemcpyHostToDevice, (hipStream_t)c->stream);
     (void)hipEventRecord((hipEvent_t)st.ev, (hipStream_t)c->stream);
     c->stage_k ^= 1;
+}
+// Pinned host buffer the document staging downloads into (reused, grown on demand).
+static uint8_t* mtb_host_stage(mt_ctx* c, size_t n) {
+    if (c->dl_cap < n) {
+        if (c->dl_host) (void)hipHostFree(c->dl_host);
+        c->dl_host = nullptr; c->dl_cap = 0;
+        const size_t cap = n + n / 4 + 4096;
+        if (hipHostMalloc(&c->dl_host, cap, hipHostMallocDefault) != hipSuccess) { c->dl_host = nullptr; return nullptr; }
+        c->dl_cap = cap;
+    }
+    return (uint8_t*)c->dl_host;
 }
 static int mtb_sync(mt_ctx* c) {
     hipError_t e = hipStreamSynchronize((hipStream_t)c->stream);
@@ -242,16 +255,16 @@ static int mtb_launch_rows(mt_ctx* c, bool pack, uint32_t first, uint32_t n, uin
                        (unsigned long long*)rows, cs);
     return mtb_check(c);
 }
-static int mtb_launch_pack_size(mt_ctx* c, const uint32_t* docs, MtPackSize* out, uint32_t n) {
+static int mtb_launch_pack_size(mt_ctx* c, const uint32_t* docs, MtPackSize* out, uint32_t n, uint32_t epoch) {
     if (!n) return MT_OK;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(mt_pack_size_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, out);
+    hipLaunchKernelGGL(mt_pack_size_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, out, epoch);
     return mtb_check(c);
 }
-static int mtb_launch_pack(mt_ctx* c, const uint32_t* docs, const uint64_t* off, uint8_t* stage, uint32_t n) {
+static int mtb_launch_pack(mt_ctx* c, const uint32_t* docs, const uint64_t* off, uint8_t* stage, uint32_t n, uint32_t epoch) {
     if (!n) return MT_OK;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(mt_pack_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, off, stage);
+    hipLaunchKernelGGL(mt_pack_kernel, dim3(n), dim3(64), 0, (hipStream_t)c->stream, c->S, docs, off, stage, epoch);
     return mtb_check(c);
 }
 

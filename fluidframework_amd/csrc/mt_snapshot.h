@@ -95,22 +95,41 @@ template <class F> void walk_all(const MtSnapView& v, int B, F& f) {
 }
 
 // TextSegment/Marker toJSONObject (textSegment.ts:48-54, mergeTree.ts:649-653); props: the
-// property map's first chunk, null when properties are undefined.
-inline void seg_json_of(std::string& o, bool marker, int refType, const MtPSet* props, const MtNames& nm,
-                        const uint16_t* txt, size_t tn) {
+// property map's JSON, null when properties are undefined.
+inline void seg_json_of(std::string& o, bool marker, int refType, const std::string* props, const uint16_t* txt, size_t tn) {
     if (marker) {
         o += "{\"marker\":{\"refType\":"; put_int(o, refType); o += "}";
-        if (props) { o += ",\"props\":"; props_json(o, props, nm); }
+        if (props) { o += ",\"props\":"; o += *props; }
         o += "}";
     } else if (props) {
-        o += "{\"text\":"; quote16(o, txt, tn); o += ",\"props\":"; props_json(o, props, nm); o += "}";
+        o += "{\"text\":"; quote16(o, txt, tn); o += ",\"props\":"; o += *props; o += "}";
     } else {
         quote16(o, txt, tn);
     }
 }
-inline void seg_json(std::string& o, const MtSnapView& v, const MtNames& nm, int s, const uint16_t* txt, size_t tn) {
-    const int ps = v.R[s].props;
-    seg_json_of(o, (v.R[s].meta & MT_M_MARKER) != 0, v.R[s].toff, ps >= 0 ? v.pset + ps : nullptr, nm, txt, tn);
+// The JSON of a document's property maps, each written once (an annotate-heavy document
+// repeats a few maps over thousands of segments).
+struct PropsJson {
+    const MtSnapView& v; const MtNames& nm;
+    std::vector<std::string> js; std::vector<uint8_t> have;
+    PropsJson(const MtSnapView& v_, const MtNames& nm_) : v(v_), nm(nm_), js(v_.hdr.psetTop), have(v_.hdr.psetTop, 0) {}
+    const std::string* get(int ps) {
+        if (ps < 0) return nullptr;
+        if (ps >= (int)have.size()) { js.resize(ps + 1); have.resize(ps + 1, 0); }
+        if (!have[ps]) { props_json(js[ps], v.pset + ps, nm); have[ps] = 1; }
+        return &js[ps];
+    }
+};
+// Segment JSON texts back to back (one buffer, not one allocation per segment).
+struct SegList {
+    std::string buf; std::vector<size_t> off{0};
+    size_t size() const { return off.size() - 1; }
+    void end() { off.push_back(buf.size()); }
+    void put(std::string& o, size_t i) const { o.append(buf, off[i], off[i + 1] - off[i]); }
+    size_t bytes(size_t a, size_t n) const { return off[a + n] - off[a]; }
+};
+inline void seg_json(std::string& o, const MtSnapView& v, PropsJson& pj, int s, const uint16_t* txt, size_t tn) {
+    seg_json_of(o, (v.R[s].meta & MT_M_MARKER) != 0, v.R[s].toff, pj.get(v.R[s].props), txt, tn);
 }
 
 inline bool props_match(const MtSnapView& v, const MtNames& nm, int a, int b) {
@@ -127,11 +146,28 @@ inline bool props_match(const MtSnapView& v, const MtNames& nm, int a, int b) {
     return true;
 }
 
+// matchProperties of two staged maps, memoized by id pair (a document alternates a few maps).
+struct PropsMatch {
+    const MtSnapView& v; const MtNames& nm;
+    long long key[16]; bool val[16];
+    PropsMatch(const MtSnapView& v_, const MtNames& nm_) : v(v_), nm(nm_) { for (auto& k : key) k = -1; }
+    bool operator()(int a, int b) {
+        if (a == b) return true;
+        if (a < 0 || b < 0) return false;
+        const long long k = ((long long)a << 32) | (unsigned)b;
+        const int h = (int)(((unsigned)a * 31u + (unsigned)b) & 15u);
+        if (key[h] == k) return val[h];
+        key[h] = k; val[h] = props_match(v, nm, a, b);
+        return val[h];
+    }
+};
 inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtNames& nm,
                                                const std::vector<std::string>* doc_clients = nullptr) {
     const std::vector<std::string>& cj = doc_clients ? *doc_clients : nm.client_json;
     const int minSeq = v.hdr.minSeq, curSeq = v.hdr.curSeq;
-    std::vector<std::string> segs; std::vector<long long> lens;
+    PropsJson pj(v, nm);
+    PropsMatch pm_(v, nm);
+    SegList segs; std::vector<long long> lens;
     int prev = -1; std::vector<uint16_t> ptext; bool pcloned = false;
     auto client = [&](int c) -> const std::string& {
         static const std::string orig = "\"original\"";
@@ -139,10 +175,10 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
     };
     auto pushPrev = [&]() {
         if (prev < 0) return;
-        std::string o;
-        if (pcloned) { seg_json(o, v, nm, prev, ptext.data(), ptext.size()); lens.push_back((long long)ptext.size()); }
-        else { seg_json(o, v, nm, prev, v.text + v.R[prev].toff, (size_t)v.R[prev].len); lens.push_back(v.R[prev].len); }
-        segs.push_back(std::move(o));
+        std::string& o = segs.buf;
+        if (pcloned) { seg_json(o, v, pj, prev, ptext.data(), ptext.size()); lens.push_back((long long)ptext.size()); }
+        else { seg_json(o, v, pj, prev, v.text + v.R[prev].toff, (size_t)v.R[prev].len); lens.push_back(v.R[prev].len); }
+        segs.end();
     };
     auto extract = [&](int s) {
         const bool removed = (v.R[s].meta & MT_M_REMOVED) != 0;
@@ -156,20 +192,21 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
                 const size_t pl = pcloned ? ptext.size() : (size_t)v.R[prev].len;
                 ok = !(pl > 0 && pt[pl - 1] == '\n') && ((long long)pl <= MT_GRAN || v.R[s].len <= MT_GRAN);
             }
-            if (ok && props_match(v, nm, v.R[prev].props, v.R[s].props)) {
+            if (ok && pm_(v.R[prev].props, v.R[s].props)) {
                 if (!pcloned) { ptext.assign(v.text + v.R[prev].toff, v.text + v.R[prev].toff + v.R[prev].len); pcloned = true; }
                 ptext.insert(ptext.end(), v.text + v.R[s].toff, v.text + v.R[s].toff + v.R[s].len);
             } else { pushPrev(); prev = s; pcloned = false; }
             return;
         }
         pushPrev(); prev = -1; pcloned = false;
-        std::string o = "{\"json\":";
+        std::string& o = segs.buf;
+        o += "{\"json\":";
         const bool marker = (v.R[s].meta & MT_M_MARKER) != 0;
-        seg_json(o, v, nm, s, marker ? nullptr : v.text + v.R[s].toff, marker ? 0 : (size_t)v.R[s].len);
+        seg_json(o, v, pj, s, marker ? nullptr : v.text + v.R[s].toff, marker ? 0 : (size_t)v.R[s].len);
         if (v.R[s].seq > minSeq) { o += ",\"seq\":"; put_int(o, v.R[s].seq); o += ",\"client\":"; o += client((int)(v.R[s].meta & MT_M_CLIENT)); }
         if (removed) { o += ",\"removedSeq\":"; put_int(o, v.R[s].rseq); o += ",\"removedClient\":"; o += client((int)v.R[s].rcl); }
         o += "}";
-        segs.push_back(std::move(o)); lens.push_back(v.R[s].len);
+        segs.end(); lens.push_back(v.R[s].len);
     };
     walk_all(v, v.hdr.root, extract);
     pushPrev();
@@ -183,9 +220,11 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
     std::vector<std::string> blobs;
     for (size_t k = 0; k < chunks.size(); k++) {
         const Chunk& c = chunks[k];
-        std::string o = "{\"version\":\"1\",\"segmentCount\":"; put_int(o, (long long)c.count);
+        std::string o;
+        o.reserve(segs.bytes(c.start, c.count) + c.count + 256 + 16 * chunks.size());
+        o += "{\"version\":\"1\",\"segmentCount\":"; put_int(o, (long long)c.count);
         o += ",\"length\":"; put_int(o, c.length); o += ",\"segments\":[";
-        for (size_t i = 0; i < c.count; i++) { if (i) o.push_back(','); o += segs[c.start + i]; }
+        for (size_t i = 0; i < c.count; i++) { if (i) o.push_back(','); segs.put(o, c.start + i); }
         o += "],\"startIndex\":"; put_int(o, (long long)c.start);
         if (k == 0) {
             o += ",\"headerMetadata\":{\"minSequenceNumber\":"; put_int(o, minSeq);
@@ -209,18 +248,20 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
 // Blob 0 is "header"; blob 1, if any, is "body".
 inline std::vector<std::string> snapshot_legacy_blobs(const MtSnapView& v, const MtNames& nm) {
     const int minSeq = v.hdr.minSeq;
-    std::vector<std::string> segs; std::vector<long long> lens;
+    PropsJson pj(v, nm);
+    PropsMatch pm_(v, nm);
+    SegList segs; std::vector<long long> lens;
     int prev = -1; std::vector<uint16_t> ptext; bool pcloned = false;
     auto pushPrev = [&]() {
         if (prev < 0) return;
-        std::string o;
+        std::string& o = segs.buf;
         const bool pm = (v.R[prev].meta & MT_M_MARKER) != 0;
-        if (pcloned) { seg_json(o, v, nm, prev, ptext.data(), ptext.size()); lens.push_back((long long)ptext.size()); }
+        if (pcloned) { seg_json(o, v, pj, prev, ptext.data(), ptext.size()); lens.push_back((long long)ptext.size()); }
         else {
-            seg_json(o, v, nm, prev, pm ? nullptr : v.text + v.R[prev].toff, pm ? 0 : (size_t)v.R[prev].len);
+            seg_json(o, v, pj, prev, pm ? nullptr : v.text + v.R[prev].toff, pm ? 0 : (size_t)v.R[prev].len);
             lens.push_back(v.R[prev].len);
         }
-        segs.push_back(std::move(o));
+        segs.end();
     };
     auto extract = [&](int s) {                                         // snapshotlegacy.ts:190-209
         const bool removed = (v.R[s].meta & MT_M_REMOVED) != 0;
@@ -233,7 +274,7 @@ inline std::vector<std::string> snapshot_legacy_blobs(const MtSnapView& v, const
                 const size_t pl = pcloned ? ptext.size() : (size_t)v.R[prev].len;
                 ok = !(pl > 0 && pt[pl - 1] == '\n') && ((long long)pl <= MT_GRAN || v.R[s].len <= MT_GRAN);
             }
-            if (ok && props_match(v, nm, v.R[prev].props, v.R[s].props)) {
+            if (ok && pm_(v.R[prev].props, v.R[s].props)) {
                 if (!pcloned) { ptext.assign(v.text + v.R[prev].toff, v.text + v.R[prev].toff + v.R[prev].len); pcloned = true; }
                 ptext.insert(ptext.end(), v.text + v.R[s].toff, v.text + v.R[s].toff + v.R[s].len);
                 return;
@@ -260,7 +301,8 @@ inline std::vector<std::string> snapshot_legacy_blobs(const MtSnapView& v, const
         o += ",\"totalSegmentCount\":"; put_int(o, (long long)segs.size());
         o += ",\"chunkSequenceNumber\":"; put_int(o, minSeq);
         o += ",\"segmentTexts\":[";
-        for (size_t i = 0; i < c.count; i++) { if (i) o.push_back(','); o += segs[c.start + i]; }
+        o.reserve(o.size() + segs.bytes(c.start, c.count) + c.count + 256);
+        for (size_t i = 0; i < c.count; i++) { if (i) o.push_back(','); segs.put(o, c.start + i); }
         o += "]";
         if (header) {                                                   // buildHeaderMetadataForLegecyChunk
             o += ",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}";

@@ -157,15 +157,14 @@ class Engine:
                        window_per_doc, markers_per_doc, register_rows_per_doc)
         h = ctypes.c_void_p()
         if per_doc:
-            arr = (MtLimits * max_docs)()
+            # one mt_limits record per document, filled column by column (a million documents)
             scal = dict(rows_per_doc=rows_per_doc, blocks_per_doc=blocks_per_doc, text_per_doc=text_per_doc,
                         propsets_per_doc=propsets_per_doc, heap_per_doc=heap_per_doc, window_per_doc=window_per_doc,
                         markers_per_doc=markers_per_doc, register_rows_per_doc=register_rows_per_doc)
-            cols = {k: (np.asarray(per_doc[k], np.uint32) if k in per_doc else None) for k in scal}
-            for i in range(max_docs):
-                for k, v in scal.items():
-                    setattr(arr[i], k, int(cols[k][i]) if cols[k] is not None else v)
-            rc = self.fn["create_docs"](device, max_docs, ctypes.cast(arr, ctypes.c_void_p), ctypes.byref(h))
+            arr = np.zeros(max_docs, np.dtype([(n, np.uint32) for n, _ in MtLimits._fields_]))
+            for k, v in scal.items():
+                arr[k] = np.asarray(per_doc[k], np.uint32)[:max_docs] if k in per_doc else v
+            rc = self.fn["create_docs"](device, max_docs, arr.ctypes.data, ctypes.byref(h))
         else:
             rc = self.fn["create"](device, ctypes.byref(lim), ctypes.byref(h))
         self.h = h

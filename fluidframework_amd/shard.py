@@ -143,6 +143,7 @@ class ShardedReplay:
         n = self.n_docs
         neg = np.full(n, -1, np.int32)
         dig = self.engine.snapshot_digests(range(n), neg, neg, threads=threads) if n else np.zeros(0, np.uint64)
+        self.timings["snapshot_ms"] = (time.perf_counter() - t0) * 1e3     # this rank's SnapshotV1 digests
         self.local_digests = dig           # engine slot order (owned[i]): each rank's own parity sample
         world, rank = dist.get_world_size(), dist.get_rank()
         counts = np.bincount(self.owner, minlength=world)

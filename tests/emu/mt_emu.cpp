@@ -12,7 +12,7 @@
 #include "../../fluidframework_amd/csrc/mt_shard.h"
 
 static int mtb_init(mt_ctx*) { return 0; }
-static void mtb_fini(mt_ctx* c) { for (auto& st : c->stage) free(st.p); }
+static void mtb_fini(mt_ctx* c) { for (auto& st : c->stage) free(st.p); free(c->dl_host); }
 static int mtb_malloc(void** p, size_t n) { *p = calloc(1, n ? n : 16); return *p ? 0 : 1; }
 static void mtb_free(void* p) { free(p); }
 static void mtb_memset(void* p, int v, size_t n) { memset(p, v, n); }
@@ -20,6 +20,10 @@ static void mtb_h2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n)
 static void mtb_d2h(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static void mtb_d2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static int mtb_sync(mt_ctx*) { return MT_OK; }
+static uint8_t* mtb_host_stage(mt_ctx* c, size_t n) {
+    if (c->dl_cap < n) { free(c->dl_host); c->dl_host = malloc(n); c->dl_cap = c->dl_host ? n : 0; }
+    return (uint8_t*)c->dl_host;
+}
 static void* mtb_stage_get(mt_ctx* c, size_t n) {
     mt_ctx::Stage& st = c->stage[c->stage_k];
     if (st.cap < n) { free(st.p); st.p = malloc(n); st.cap = st.p ? n : 0; }
@@ -102,12 +106,12 @@ static int mtb_launch_gather_text(mt_ctx* c, const unsigned long long* at, const
     for (uint32_t i = 0; i < n; i++) memcpy(dst + off[i], c->S.text + at[i], 2ull * len[i]);
     return MT_OK;
 }
-static int mtb_launch_pack_size(mt_ctx* c, const uint32_t* docs, MtPackSize* out, uint32_t n) {
-    for (uint32_t i = 0; i < n; i++) { MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc); out[i] = mt_pack_size(e); }
+static int mtb_launch_pack_size(mt_ctx* c, const uint32_t* docs, MtPackSize* out, uint32_t n, uint32_t epoch) {
+    for (uint32_t i = 0; i < n; i++) { MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc); out[i] = mt_pack_size(e, epoch); }
     return MT_OK;
 }
-static int mtb_launch_pack(mt_ctx* c, const uint32_t* docs, const uint64_t* off, uint8_t* stage, uint32_t n) {
-    for (uint32_t i = 0; i < n; i++) { MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc); mt_pack_doc(e, stage + off[i]); }
+static int mtb_launch_pack(mt_ctx* c, const uint32_t* docs, const uint64_t* off, uint8_t* stage, uint32_t n, uint32_t epoch) {
+    for (uint32_t i = 0; i < n; i++) { MtScratch sc; MtEng e; e.bind(c->S, docs[i], &sc); mt_pack_doc(e, stage + off[i], epoch); }
     return MT_OK;
 }
 static int mtb_launch_rows(mt_ctx* c, bool pack, uint32_t first, uint32_t n, uint32_t L, const uint64_t* dst, uint64_t* rows,

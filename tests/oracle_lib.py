@@ -283,12 +283,16 @@ def gen_params(seed=1, n_docs=1, ops=1000, clients=2, lag=8, ins=55, rem=45, ins
     return MtGenParams(seed, n_docs, ops, clients, lag, ins, rem, ins_len, rem_len, ann_sets, rewrite)
 
 
-def generate(params: MtGenParams, props: PropTable, docs=None, keep=False, ops_per_doc=None, clients_per_doc=None):
+def generate(params: MtGenParams, props: PropTable, docs=None, keep=False, ops_per_doc=None, clients_per_doc=None,
+             threads: int = 1):
     """Generate streams with the oracle as sequencer+observer; returns (OpBatch, [status], [OracleDoc]).
     ops_per_doc / clients_per_doc: per-document counts (indexed by position in docs),
-    as mt_generate_docs takes them."""
+    as mt_generate_docs takes them.  threads > 1: documents are generated concurrently
+    (each document's stream is independent; ctypes releases the GIL)."""
     L = lib()
     docs = list(range(params.n_docs)) if docs is None else list(docs)
+    if threads > 1 and len(docs) > 1:
+        return _generate_threaded(params, props, docs, keep, ops_per_doc, clients_per_doc, threads)
     cols = {k: [] for k in ("type", "flags", "client", "seq", "ref_seq", "msn", "pos1", "pos2",
                             "payload_off", "payload_len", "prop_id")}
     payloads, offs, stats, kept = [], [0], [], []
@@ -325,6 +329,30 @@ def generate(params: MtGenParams, props: PropTable, docs=None, keep=False, ops_p
                                 np.concatenate(payloads) if payloads else np.zeros(1, np.uint16),
                                 **{k: np.concatenate(v) for k, v in cols.items()})
     return batch, stats, kept
+
+
+def _generate_threaded(params, props, docs, keep, ops_per_doc, clients_per_doc, threads):
+    """generate() over a thread pool: each document generated alone (payload base 0), then
+    the runs concatenated with their payload offsets rebased."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(j):
+        return generate(params, props, docs=[docs[j]], keep=keep,
+                        ops_per_doc=None if ops_per_doc is None else [ops_per_doc[j]],
+                        clients_per_doc=None if clients_per_doc is None else [clients_per_doc[j]])
+
+    with ThreadPoolExecutor(threads) as ex:
+        parts = list(ex.map(one, range(len(docs))))
+    bs = [p[0] for p in parts]
+    pay_base = np.concatenate(([0], np.cumsum([len(b.payload) for b in bs])[:-1])).astype(np.int64)
+    cols = {}
+    for k in bs[0].arrays:
+        cols[k] = np.concatenate([b.arrays[k] for b in bs])
+    cols["payload_off"] = np.concatenate([b.arrays["payload_off"].astype(np.int64) + o
+                                          for b, o in zip(bs, pay_base)]).astype(np.uint32)
+    offs = np.concatenate(([0], np.cumsum([int(b.op_offsets[-1]) for b in bs]))).astype(np.uint32)
+    batch = OpBatch.from_arrays(np.asarray(docs, np.uint32), offs, np.concatenate([b.payload for b in bs]), **cols)
+    return batch, [p[1][0] for p in parts], [p[2][0] for p in parts] if keep else []
 
 
 def replay(batch: OpBatch, props: PropTable, names: list[str] | None = None):

@@ -96,12 +96,31 @@ def test_sharded_replay_gloo_world2_matches_oracle(tmp_path):
     assert [int(x) for x in d2] == want
 
 
-def test_exchange_rows_checksum_catches_corruption():
-    """mt_generated_pack_rows / mt_upload_rows_dev on the host emulation (device pointers are
-    host pointers there): rows round-trip into a resident batch that replays exactly like the
-    generated one, and any flipped bit or zeroed row of a document is reported for that
-    document only (MT_E_EXCHANGE)."""
-    from emu_lib import emu_engine
+class HostRows:
+    """Exchange-row buffers in host memory (the emulation's "device" pointers)."""
+
+    @staticmethod
+    def zeros(n, w):
+        return np.zeros((n, w), np.uint64)
+
+    @staticmethod
+    def ptr(a):
+        return a.ctypes.data
+
+    @staticmethod
+    def corrupt(a, r, w, how):
+        b = a.copy()
+        if how == "bit":
+            b[r, w] ^= np.uint64(1 << 17)
+        else:
+            b[r, :] = 0
+        return b
+
+
+def check_exchange_rows(factory, buf):
+    """mt_generated_pack_rows / mt_upload_rows_dev: rows round-trip into a resident batch that
+    replays exactly like the generated one, and any flipped bit or zeroed row of a document is
+    reported for that document only (MT_E_EXCHANGE)."""
     from fluidframework_amd.batch import MtGenParams, PropTable
     from fluidframework_amd.engine import ExchangeError
     from fluidframework_amd.shard import generation_caps
@@ -109,7 +128,7 @@ def test_exchange_rows_checksum_catches_corruption():
     clients = np.array([3, 2, 9, 4], np.uint32)
     L = GEN["ins_len_max"]
     caps = generation_caps(counts, L)
-    src = emu_engine(4, per_doc=caps)
+    src = factory(4, per_doc=caps)
     src.upload_props(PropTable())
     src.upload_names(NAMES)
     src.generate(MtGenParams(**{**GEN, "seed": 5, "n_docs": 4, "ops_per_doc": 0, "clients": 2}),
@@ -119,13 +138,13 @@ def test_exchange_rows_checksum_catches_corruption():
     order = np.array([2, 0, 3, 1])                         # a plan: send order differs from generation order
     row_of = np.empty(4, np.int64)
     row_of[order] = np.concatenate(([0], np.cumsum(counts[order].astype(np.int64))[:-1]))
-    rows = np.zeros((int(counts.sum()), W), np.uint64)
-    sums = src.generated_pack_rows(0, 4, row_of.astype(np.uint64), rows.ctypes.data)
+    rows = buf.zeros(int(counts.sum()), W)
+    sums = src.generated_pack_rows(0, 4, row_of.astype(np.uint64), buf.ptr(rows))
     off = np.concatenate(([0], np.cumsum(counts[order]))).astype(np.uint32)
-    dst = emu_engine(4, per_doc={k: np.asarray(v)[order] for k, v in caps.items()})
+    dst = factory(4, per_doc={k: np.asarray(v)[order] for k, v in caps.items()})
     dst.upload_props(PropTable())
     dst.upload_names(NAMES)
-    assert not dst.upload_rows_dev(range(4), off, rows.ctypes.data, L, sums[order]).any()
+    assert not dst.upload_rows_dev(range(4), off, buf.ptr(rows), L, sums[order]).any()
     dst.open_docs(0, 4)
     dst.replay_resident()
     dst.sync()
@@ -134,12 +153,12 @@ def test_exchange_rows_checksum_catches_corruption():
     want = src.snapshot_digests(range(4), neg, neg, threads=1)
     assert np.array_equal(dst.snapshot_digests(range(4), neg, neg, threads=1), want[order])
     for how in ("bit", "zero"):                             # corrupt the third document of the plan (doc 3)
-        bad = rows.copy()
-        r = int(row_of[3]) + 5
-        if how == "bit":
-            bad[r, W - 1] ^= np.uint64(1 << 17)
-        else:
-            bad[r, :] = 0
+        bad = buf.corrupt(rows, int(row_of[3]) + 5, W - 1, how)
         with pytest.raises(ExchangeError) as ei:
-            dst.upload_rows_dev(range(4), off, bad.ctypes.data, L, sums[order])
+            dst.upload_rows_dev(range(4), off, buf.ptr(bad), L, sums[order])
         assert list(ei.value.bad_runs) == [0, 0, 1, 0]
+
+
+def test_exchange_rows_checksum_catches_corruption():
+    from emu_lib import emu_engine
+    check_exchange_rows(emu_engine, HostRows)
