@@ -384,6 +384,18 @@ struct MtScratch {
     int corr[MT_MAXN];                // per-child perspective corrections (childLens)
 };
 
+// A row or block record read or written as dwords (lane k: dword k); may_alias keeps those
+// accesses ordered with the field accesses of the same record.
+typedef int __attribute__((may_alias)) mt_ai;
+#ifndef MT_LEAF_ONCE
+#define MT_LEAF_ONCE 1                // walk: leaf rows loaded whole once, splits from registers
+#endif
+MT_INLINE int pick16(const int* c, int j) {         // c[j] for a lane index j (no private-array indexing)
+    int v = c[0];
+#pragma unroll
+    for (int i = 1; i < 16; i++) v = (j == i) ? c[i] : v;
+    return v;
+}
 MT_INLINE int pick8(const int* c, int j) {
     int v = c[0];
 #pragma unroll
@@ -392,24 +404,30 @@ MT_INLINE int pick8(const int* c, int j) {
 }
 // Is client c in row s's removedClientOverlap?  Clients < 63 are bits of the mask; the
 // rest live in the document's side list (bit 63 set), scanned only in that rare case.
+// c is wave-uniform, so the c < 63 test is a scalar branch; the side-list scan runs every
+// entry in every lane (no per-lane exits: see vis_rc).
 MT_INLINE bool ovl_has(const MtOvx* ox, int n, unsigned long long ovl, int s, int rseq, int c) {
     if (c < 63) return ((ovl >> c) & 1ull) != 0;
-    if (!(ovl >> 63)) return false;
+    const bool more = (ovl >> 63) != 0;
+    bool f = false;
     for (int i = 0; i < n; i++) {
         const MtOvx e = ox[i];
-        if (e.row == s && e.client == c && e.rseq == rseq) return true;
+        f = f | (more & (e.row == s) & (e.client == c) & (e.rseq == rseq));
     }
-    return false;
+    return f;
 }
 // nodeLength's visibility of segment row s under perspective (r, c), MT/mergeTree.ts:1652-1692.
+// Evaluated without short circuits, so per-lane conditions stay lane masks instead of nested
+// divergent branches: with the short-circuit form the gfx950 backend merged a caller's
+// `vis ? len : 0` wrongly across those branches (removed rows whose removal the perspective
+// has not seen came out as length 0; round 4, DESIGN.md §4 "Device-only INSERT_FAILED").
 MT_INLINE bool vis_rc(int seq, uint32_t meta, int rseq, uint32_t rcl, unsigned long long ovl, int r, int c,
                       const MtOvx* ox, int nox, int s) {
     const int cl = (int)(meta & MT_M_CLIENT);
-    if (!(cl == c || seq <= r)) return false;
-    if (meta & MT_M_REMOVED) {
-        if ((int)rcl == c || rseq <= r || ovl_has(ox, nox, ovl, s, rseq, c)) return false;
-    }
-    return true;
+    const bool seen = (cl == c) | (seq <= r);
+    const bool removed = (meta & MT_M_REMOVED) != 0;
+    const bool gone = ((int)rcl == c) | (rseq <= r) | ovl_has(ox, nox, ovl, s, rseq, c);
+    return seen & !(removed & gone);
 }
 
 struct BlkH { int len, parent, n, height, scour; };
@@ -1735,6 +1753,43 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (mt & MT_M_INWIN) winAddKnown(n, mt & ~(MT_M_INWIN | MT_M_HREF));   // n's meta as just written
         return n;
     }
+    // splitRow with row s already loaded (lane j of lf, the walk's leaf step): the right half is
+    // written by twelve lanes in one store (one dword each) and nothing of s is read again.
+    // dword k of a row held in registers (k a compile-time constant after unrolling: no address
+    // is taken, so the record stays in VGPRs)
+    MT_HD static int rowDword(const MtRow& f, int k) {
+        switch (k) {
+            case 0: return f.len; case 1: return f.seq; case 2: return f.rseq; case 3: return (int)f.meta;
+            case 4: return f.toff; case 5: return f.props; case 6: return f.parent; case 7: return f.tcap;
+            case 8: return (int)(uint32_t)f.ovl; case 9: return (int)(uint32_t)(f.ovl >> 32);
+            case 10: return (int)f.rcl; default: return f.mid;
+        }
+    }
+    MT_HD static LaneArr<int> leafField(const LaneArr<MtRow>& lf, int j, int k) {
+        (void)j;
+        return wave_map(MT_WAVE, [&](int t) MT_LAM { return rowDword(own(lf, t), k); });
+    }
+    MT_HD int splitRowKnown(int s, int pos, const LaneArr<MtRow>& lf, int j) {
+        MT_EV2(5, 1);
+        const int n = allocRow();
+        if (n < 0) return -1;
+#if defined(MT_DBG_FAIL) && defined(__HIP_DEVICE_COMPILE__)
+        mt_dbg_v.s = s; mt_dbg_v.n = n; mt_dbg_v.op = curOp;
+#endif
+        const uint32_t mt = (uint32_t)wave_at(leafField(lf, j, 3), j);
+        const uint32_t ovh = (uint32_t)wave_at(leafField(lf, j, 9), j);
+        // lane j holds row s: it writes the right half whole (three 16-byte stores)
+        wave_for(MT_WAVE, [&](int t) MT_LAM {
+            if (t != j) return;
+            MtRow q = own(lf, t);
+            q.len -= pos; q.meta &= ~(MT_M_INWIN | MT_M_HREF); q.toff += pos; q.tcap -= pos; q.mid = 0;
+            row(n) = q;
+        });
+        row(s).len = pos; row(s).tcap = pos;                   // each row owns [toff, toff+tcap) of the arena
+        if (ovh >> 31) ovxCopy(s, n);
+        if (mt & MT_M_INWIN) winAddKnown(n, mt & ~(MT_M_INWIN | MT_M_HREF));   // n's meta as just written
+        return n;
+    }
     // Insert `node` at child index idx of path level L, splitting full blocks
     // 4/4 upward (insertingWalk :2465-2489, split :2495-2508, updateRoot :1868).
     // `delta` = observer length added under the path (0 for a row split).
@@ -1845,32 +1900,21 @@ template <int RES, bool FULL = true> struct MtEngT {
             const bool kpre = !BLKL && h.height > 0;
             LaneArr<int> r0{}, r1{};
             if (kpre) kidsLoad(ch, h.n, r0, r1);
-#if defined(MT_DBG_WIDE)
-            // diagnostic build: the leaf step loads every row field in one round trip (the
-            // variant that failed on the device in rounds 2 and 3)
+            // Leaf rows: every field in one round trip (MtRow is three 16-byte loads per lane), so a
+            // split that follows needs no second load of the row (splitRowKnown).
+            LaneArr<MtRow> lf{};
             LaneArr<ChildL> cl;
-            if (h.height == 0) {
-#if defined(MT_DBG_FENCE) && defined(__HIP_DEVICE_COMPILE__)
-                __builtin_amdgcn_s_waitcnt(0);                   // every earlier access complete first
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-#endif
+            if (MT_LEAF_ONCE && h.height == 0) {
                 const int rr = r, cc = c;
+                lf = wave_map(h.n, [&](int j) MT_LAM { return row(own(ch, j)); });
                 cl = wave_map(h.n, [&](int j) MT_LAM {
-                    const int s = own(ch, j);
-                    const int fl_ = row(s).len, fs = row(s).seq, fr = row(s).rseq, ft = row(s).toff, fp = row(s).props;
-                    const int fc = row(s).tcap, fmid = row(s).mid, fpar = row(s).parent;
-                    const uint32_t fm = row(s).meta, frc = row(s).rcl;
-                    const unsigned long long fo = row(s).ovl;
-                    mt_keep(ft ^ fp ^ fc ^ fmid ^ fpar);
+                    const MtRow f = own(lf, j);
                     ChildL o;
-                    o.len = vis_rc(fs, fm, fr, frc, fo, rr, cc, ovx, ovxN, s) ? fl_ : 0;
-                    o.tie = !((fm & MT_M_REMOVED) && fr <= rr);
+                    o.len = vis_rc(f.seq, f.meta, f.rseq, f.rcl, f.ovl, rr, cc, ovx, ovxN, own(ch, j)) ? f.len : 0;
+                    o.tie = !((f.meta & MT_M_REMOVED) && f.rseq <= rr);     // breakTie, as leafLens
                     return o;
                 });
             } else cl = kpre ? childLens(B, h, ch, r, c, true, kidsLen(r0, r1), lsN) : childLens(B, h, ch, r, c);
-#else
-            auto cl = kpre ? childLens(B, h, ch, r, c, true, kidsLen(r0, r1), lsN) : childLens(B, h, ch, r, c);
-#endif
             MT_QE(1, q1);
             auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
             auto pre = wave_excl_scan8(lens);
@@ -1894,8 +1938,9 @@ template <int RES, bool FULL = true> struct MtEngT {
                 const int s = wave_at(ch, j);
                 lastL = L; lastSplit = false;
                 if (kind == MT_WALK_SPLIT) {
-                    if (pj > 0 && !(uni(row(s).meta) & MT_M_MARKER)) {
-                        const int n = splitRow(s, pj);
+                    const uint32_t sm = MT_LEAF_ONCE ? (uint32_t)wave_at(leafField(lf, j, 3), j) : uni(row(s).meta);
+                    if (pj > 0 && !(sm & MT_M_MARKER)) {
+                        const int n = MT_LEAF_ONCE ? splitRowKnown(s, pj, lf, j) : splitRow(s, pj);
                         if (n < 0) return MT_W_FAIL;
                         insertAtPath(L, j + 1, n, 0);
                         if (FULL && drec) {                     // SPLIT, splitLeafSegment (mergeTree.ts:2243-2258)

@@ -18,12 +18,6 @@ struct __attribute__((aligned(16))) MtQueryOut {
     MtPSet ps[MT_PKEYS / MT_PSK];
 };
 static_assert(sizeof(mt_seg_info) == 64, "mt_seg_info is 16 dwords");
-MT_INLINE int pick16(const int* c, int j) {         // c[j] for a lane index j (no private-array indexing)
-    int v = c[0];
-#pragma unroll
-    for (int i = 1; i < 16; i++) v = (j == i) ? c[i] : v;
-    return v;
-}
 
 template <class Eng>
 MT_HD void mt_query_run(Eng& e, const MtState& S, const MtQuery* q, uint32_t q0, uint32_t q1, MtQueryOut* out) {

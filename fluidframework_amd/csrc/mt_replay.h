@@ -180,6 +180,9 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
     return o1;
 }
 
+#ifndef MT_BLK_NO_CONT
+#define MT_BLK_NO_CONT 0
+#endif
 // One document run of a replay launch (every replay kernel and the host emulation run this).
 // The run starts at ops.start[run] (a capture resume) or op_off[run]; RES is the residency it
 // starts in: MT_RES_LDS hands the rest to a second, all-HBM launch (the returned op index goes
@@ -201,7 +204,7 @@ MT_HD uint32_t mt_replay_doc(const MtState& S, const MtOps& ops, uint32_t run, M
         const bool stopped = e.dStop != 0;
         e.store(doc);
         if (stopped) { stop = cur; cur = o1; }                   // no hand-over: the host resumes it
-        else if (RES != MT_RES_LDS && cur < o1) {
+        else if (RES != MT_RES_LDS && !(RES == MT_RES_BLK && MT_BLK_NO_CONT) && cur < o1) {
             // A document that outgrew LDS continues here with its pools in HBM (no second
             // launch: long documents, which outgrow it first, keep their head start).
             MtEngT<MT_RES_HBM, FULL> h;

@@ -8,7 +8,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "emu", "mt_emu.cpp")
 LIB = os.path.join(ROOT, "tests", "emu", "libmtemu.so")
 DEPS = [SRC, os.path.join(ROOT, "include", "mtgpu.h")] + [os.path.join(ROOT, "fluidframework_amd", "csrc", f) for f in
-                ("mt_core.h", "mt_replay.h", "mt_snapshot.h", "mt_pack.h", "mt_api_impl.h", "mt_ctx.h", "wave.h", "mt_shard.h")]
+                ("mt_core.h", "mt_replay.h", "mt_snapshot.h", "mt_pack.h", "mt_api_impl.h", "mt_ctx.h", "wave.h", "mt_shard.h",
+                 "mt_query.h")]
 
 
 def _atomic_build(cmd, out):

@@ -465,3 +465,27 @@ def test_snapshot_legacy_known_answers_on_emulation(n):
 @pytest.mark.parametrize("n", [10000, 10010])
 def test_snapshot_legacy_known_answers_on_gpu(n):
     check_snapshot_legacy(GPU, n)
+
+
+# ---- regression: rows whose removal the author has not seen (round 4) ----------------------
+def check_unseen_removal_split(factory):
+    """A leaf that a walk splits holds removed rows whose removal the op's author has not
+    seen: they count at their full length (nodeLength, mergeTree.ts:1671-1683).  With the
+    short-circuit visibility test, the gfx950 backend once merged `vis ? len : 0` wrongly for
+    such rows (length 0), and the walk lost the position (INSERT_FAILED) or landed late.  B
+    removes "lo " at seq 1; A, still at refSeq 0, inserts "X" at 5 of "hello world" (between
+    "hello" and " "), then at 8 of its view ("wo|rld"), then removes [1, 4) of its view."""
+    msgs = [msg("B", 1, 0, 0, rem(3, 6)), msg("A", 2, 0, 0, ins(5, "X")), msg("A", 3, 0, 0, ins(9, "Y")),
+            msg("A", 4, 0, 0, rem(1, 4))]
+    od, c = run_both(factory, msgs, load_first=HW_CHARS)
+    assert c.getText() == od.get_text() == "hXwoYrld"
+    header_now(od, c)
+
+
+def test_unseen_removal_split_on_emulation():
+    check_unseen_removal_split(emu_engine)
+
+
+@pytest.mark.gpu
+def test_unseen_removal_split_on_gpu():
+    check_unseen_removal_split(GPU)
