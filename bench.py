@@ -454,6 +454,8 @@ def run_config5(args, c, world, rank, local):
         "exchange": {"docs_checked": int(bad[2].item()), "checksum_mismatch_docs": int(bad[1].item()),
                      "note": "per-document 64-bit checksums of the exchanged rows: packed by rank 0, verified on "
                              "arrival by the owning rank (mt_generated_pack_rows / mt_upload_rows_dev)"},
+        "memory": {"engine_pools_gb": eng.pool_bytes() / 1e9,
+                   "exchange_buffers_peak_gb": (torch.cuda.max_memory_allocated(device) / 1e9) if device.type == "cuda" else None},
         "snapshot": {"docs": sh.n_docs, "ms": sh.timings.get("snapshot_ms"), "host_threads": min(16, os.cpu_count() or 1),
                      "note": "rank 0's mt_snapshot_digests (staged download + SnapshotV1 JSON + xxh64), before the gather"},
         "sharding": {"rebalance_ms": sh.timings.get("rebalance_ms"), "rebalance_bytes": sh.timings.get("rebalance_bytes"),

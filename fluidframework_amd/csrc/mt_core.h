@@ -180,6 +180,7 @@ enum { MT_PH_U = 0, MT_PH_SPLIT, MT_PH_INSERT, MT_PH_RANGE, MT_PH_ZAMBONI, MT_PH
 #define MT_M_MARKER 0x00020000u
 #define MT_M_INWIN 0x00040000u
 #define MT_M_REG 0x00080000u          // a clone held by a register (not linked; its text survives compaction)
+#define MT_M_NONL 0x00100000u         // the text holds no "\n" (canAppend's trailing-newline test loads nothing)
 #define MT_M_HREF1 0x01000000u        // heap-entry reference count, bits 24..31 (saturating)
 #define MT_M_HREF 0xFF000000u
 
@@ -387,6 +388,9 @@ struct MtScratch {
 // A row or block record read or written as dwords (lane k: dword k); may_alias keeps those
 // accesses ordered with the field accesses of the same record.
 typedef int __attribute__((may_alias)) mt_ai;
+#ifndef MT_NONL
+#define MT_NONL 1                     // rows flag text without a newline (MT_M_NONL)
+#endif
 #ifndef MT_LEAF_ONCE
 #define MT_LEAF_ONCE 1                // walk: leaf rows loaded whole once, splits from registers
 #endif
@@ -2251,7 +2255,8 @@ template <int RES, bool FULL = true> struct MtEngT {
             // prev's last unit (canAppend: no trailing "\n") for lanes followed by a pair
             const uint64_t needLast = pm >> 1;
             auto lastNL = wave_map(span, [&](int t) MT_LAM {
-                return ((needLast >> t) & 1ull) ? (text[own(ft, t) + own(fl, t) - 1] == (uint16_t)'\n' ? 1 : 0) : 0;
+                const bool need = ((needLast >> t) & 1ull) && !((uint32_t)own(fm, t) & MT_M_NONL);
+                return need ? (text[own(ft, t) + own(fl, t) - 1] == (uint16_t)'\n' ? 1 : 0) : 0;
             });
             const auto lastNL1 = wave_from8<-1>(lastNL);
             // matchProperties: equal ids match; a missing map never matches a present one;
@@ -2290,6 +2295,14 @@ template <int RES, bool FULL = true> struct MtEngT {
                 while ((m >> i1) & 1ull) i1++;
                 m &= ~((i1 >= 64 ? ~0ull : ((1ull << i1) - 1ull)));
                 mergeRun(f, ft, fc, fl, i0 - 1, i0, i1);
+                {   // the appended text may carry a newline: the head keeps the flag only if all did
+                    const uint32_t hm = (uint32_t)wave_at(fm, i0 - 1);
+                    if (hm & MT_M_NONL) {
+                        bool all = true;
+                        for (int i = i0; i < i1; i++) all = all && ((uint32_t)wave_at(fm, i) & MT_M_NONL);
+                        if (!all) row(wave_at(f, i0 - 1)).meta = hm & ~MT_M_NONL;
+                    }
+                }
             }
         }
         if (FULL && drec) { // maintenance callbacks in child order: UNLINK (:1299-1305), APPEND (:1325-1331)
@@ -2829,8 +2842,12 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (L > 0) {
             const int n = allocRow();
             if (n < 0) return;
+            // payloads up to 64 units are already in lanes: flag text without a newline
+            const bool nonl = MT_NONL && !marker && plen <= MT_WAVE &&
+                              wave_count(wave_map(plen, [&](int k) MT_LAM { return own(pay, k) == (int)'\n'; })) == 0;
+            const uint32_t m0 = (uint32_t)c | (marker ? MT_M_MARKER : 0u) | (nonl ? MT_M_NONL : 0u);
             row(n).len = L; row(n).seq = sq; row(n).rseq = MT_NOREM;
-            row(n).meta = (uint32_t)c | (marker ? MT_M_MARKER : 0u);
+            row(n).meta = m0;
             row(n).ovl = 0ull; row(n).parent = -1; row(n).rcl = 0u;
             row(n).mid = markerId >= 0 ? markerId + 1 : 0;
             if (markerId >= 0) {                       // mapIdToSegment before the walk (MT/mergeTree.ts:2218-2222)
@@ -2871,7 +2888,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             MT_PE(MT_PH_INSERT, t1);
             if (w != MT_W_OK || landB < 0) { status |= MT_DS_INSERT_FAILED; return; }
             c_rows += 2;
-            const uint32_t m1 = winAddKnown(n, (uint32_t)c | (marker ? MT_M_MARKER : 0u));
+            const uint32_t m1 = winAddKnown(n, m0);
             if (sq > minSeq) addToLRUSetKnown(n, sq, landB, m1);
             if (FULL && drec) emitDelta(MT_DK_INSERT, obsPosition(n), L, n, uni(row(n).props), -1, -1);   // insertSegments callback
         }
@@ -2918,7 +2935,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                 const int d = i < f0 ? sc->rfree[f0 - 1 - i] : t0 + (i - f0);
                 const uint32_t mt = row(s).meta;
                 row(d).len = row(s).len; row(d).seq = row(s).seq; row(d).rseq = row(s).rseq;
-                row(d).meta = (mt & (MT_M_CLIENT | MT_M_REMOVED | MT_M_MARKER)) | MT_M_REG;
+                row(d).meta = (mt & (MT_M_CLIENT | MT_M_REMOVED | MT_M_MARKER | MT_M_NONL)) | MT_M_REG;
                 row(d).rcl = row(s).rcl; row(d).props = row(s).props; row(d).mid = row(s).mid;
                 row(d).toff = row(s).toff; row(d).tcap = (mt & MT_M_MARKER) ? 0 : row(s).len;
                 row(d).ovl = 0ull; row(d).parent = -1;
