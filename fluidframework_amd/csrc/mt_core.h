@@ -103,6 +103,9 @@
 #ifndef MT_G_MWMIN
 #define MT_G_MWMIN 512                 // windows up to this many entries are scanned by wave 0 alone
 #endif
+#ifndef MT_G_ALLCH
+#define MT_G_ALLCH 0                   // 1: ... with every chunk's rows loaded in one round trip
+#endif
 enum { MT_MW_EXIT = 0, MT_MW_SCAN = 1, MT_MW_CHAIN = 2, MT_MW_PREFETCH = 3 };
 // Jobs alternate between two LDS slots, so wave 0 can post an asynchronous job (PREFETCH: no
 // completion barrier) and write the next one while helpers still read the last.
@@ -1168,12 +1171,32 @@ template <int RES, bool FULL = true> struct MtEngT {
         int newWin = 0; nU = 0;
         const int wN0 = winN;
         if (wN0 <= MT_G_MWMIN) {                    // a few chunks: wave 0 alone, no barriers
+#if MT_G_ALLCH
+            // every chunk's rows in one round trip (one wave per SIMD here: registers to spare),
+            // then placed in order (placement writes only entries below the chunk it places)
+            constexpr int NC = MT_G_MWMIN / MT_WAVE;
+            LaneArr<WinI> wis[NC];
+#pragma unroll
+            for (int q = 0; q < NC; q++) {
+                const int base = q * MT_WAVE;
+                const int m = base >= wN0 ? 0 : ((wN0 - base) < MT_WAVE ? (wN0 - base) : MT_WAVE);
+                const auto ids = wave_map(m, [&](int k) MT_LAM { return wn(base + k); });
+                wis[q] = wave_map(m, [&](int k) MT_LAM { return winEntry(own(ids, k), r, c); });
+            }
+#pragma unroll
+            for (int q = 0; q < NC; q++) {
+                const int base = q * MT_WAVE;
+                if (base >= wN0) break;
+                placeChunk(wis[q], base, (wN0 - base) < MT_WAVE ? (wN0 - base) : MT_WAVE, prune, newWin);
+            }
+#else
             for (int base = 0; base < wN0; base += MT_WAVE) {
                 const int m = (wN0 - base) < MT_WAVE ? (wN0 - base) : MT_WAVE;
                 const auto ids = wave_map(m, [&](int k) MT_LAM { return wn(base + k); });
                 const auto wi = wave_map(m, [&](int k) MT_LAM { return winEntry(own(ids, k), r, c); });
                 placeChunk(wi, base, m, prune, newWin);
             }
+#endif
         }
         for (int r0 = 0; wN0 > MT_G_MWMIN && r0 < wN0; r0 += MT_G_STG) {
             const int n = (wN0 - r0) < MT_G_STG ? (wN0 - r0) : MT_G_STG;

@@ -489,3 +489,26 @@ def test_unseen_removal_split_on_emulation():
 @pytest.mark.gpu
 def test_unseen_removal_split_on_gpu():
     check_unseen_removal_split(GPU)
+
+
+# ---- canAppend's trailing newline through zamboni merges (textSegment.ts:63-68) ------------
+def check_newline_merge(factory):
+    """"ab" takes "c\\n" (no trailing newline on "ab"), but the merged "abc\\n" must not take "d";
+    "x\\ny" (newline inside, not trailing) still takes "z".  The engine flags newline-free rows
+    (MT_M_NONL) and a merge clears the head's flag when a follower had a newline."""
+    msgs = [msg("A", 1, 0, 0, ins(0, "ab")), msg("A", 2, 1, 1, ins(2, "c\n")), msg("A", 3, 2, 2, ins(4, "d")),
+            msg("A", 4, 3, 3, ins(5, "x\ny")), msg("A", 5, 4, 4, ins(8, "z")),
+            msg("A", 6, 5, 5, None, type="noop"), msg("A", 7, 6, 6, None, type="noop")]
+    od, c = run_both(factory, msgs)
+    assert c.getText() == "abc\ndx\nyz"
+    hdr = json.loads(header_now(od, c))
+    assert hdr["segments"] == ["abc\n", "dx\nyz"], hdr["segments"]
+
+
+def test_newline_merge_on_emulation():
+    check_newline_merge(emu_engine)
+
+
+@pytest.mark.gpu
+def test_newline_merge_on_gpu():
+    check_newline_merge(GPU)
