@@ -678,7 +678,7 @@ def _main(argv=None):
     ap.add_argument("--caps", default="", help="override pool caps, e.g. rows_per_doc=400,text_per_doc=16384")
     ap.add_argument("--big-flags", type=int, default=0,
                     help="big residency A/B switches (MT_BIGF_*): 1 block cache off, 2 zamboni prefetch off, "
-                         "4 corrections table off")
+                         "4 corrections table off, 8 parent cache off")
     ap.add_argument("--big-min-ops", type=int, default=-1,
                     help="size classes under blk residency: runs of at least this many messages replay in the "
                          "long-document kernel on a second stream (0: off; default: the config's)")

@@ -574,11 +574,11 @@ int MT_FN(set_residency)(mt_ctx* c, int use_lds, int rows, int blocks, int heap)
     const int maxHeap = use_lds == 3 ? MT_G_HEAP : (use_lds == 2 ? MT_B_HEAP : MT_L_HEAP);
     if (!c || use_lds < 0 || use_lds > 3 || rows < 0 || blocks < 0 || heap < 0 ||
         rows > (use_lds == 3 ? MT_G_WIN : MT_L_ROWS) ||
-        blocks > (use_lds == 2 ? MT_B_BLKS : (use_lds == 3 ? 7 : MT_L_BLKS)) || heap > maxHeap)
+        blocks > (use_lds == 2 ? MT_B_BLKS : (use_lds == 3 ? 15 : MT_L_BLKS)) || heap > maxHeap)
         return MT_E_INVALID;
     c->use_lds = use_lds;
     c->lds_rows = rows ? rows : (use_lds == 3 ? MT_G_WIN : MT_L_ROWS);   // 3: window entries in LDS
-    // 3: blocks = MT_BIGF_* switches (block cache, zamboni prefetch, corrections table off; A/B)
+    // 3: blocks = MT_BIGF_* switches (block cache, zamboni prefetch, corrections table, parent cache off; A/B)
     c->lds_blks = use_lds == 3 ? blocks : (blocks ? blocks : (use_lds == 2 ? MT_B_BLKS : MT_L_BLKS));
     c->lds_heap = heap ? heap : maxHeap;
     return MT_OK;

@@ -110,7 +110,7 @@ enum { MT_MW_EXIT = 0, MT_MW_SCAN = 1, MT_MW_CHAIN = 2, MT_MW_PREFETCH = 3 };
 // Jobs alternate between two LDS slots, so wave 0 can post an asynchronous job (PREFETCH: no
 // completion barrier) and write the next one while helpers still read the last.
 // Runtime switches of the long-document residency (mt_set_residency(ctx, 3, rows, flags, heap)):
-enum { MT_BIGF_NO_BCACHE = 1, MT_BIGF_NO_PREFETCH = 2, MT_BIGF_NO_TABLE = 4 };
+enum { MT_BIGF_NO_BCACHE = 1, MT_BIGF_NO_PREFETCH = 2, MT_BIGF_NO_TABLE = 4, MT_BIGF_NO_BPC = 8 };
 // Per-block perspective corrections of the long-document residency: an LDS hash table
 // block id -> Σ delta of the U rows under the block, built bottom-up once per U set (each
 // distinct block's parent is loaded once), so a descent level looks its children up instead
@@ -119,11 +119,22 @@ enum { MT_BIGF_NO_BCACHE = 1, MT_BIGF_NO_PREFETCH = 2, MT_BIGF_NO_TABLE = 4 };
 #ifndef MT_G_HT
 #define MT_G_HT 4096
 #endif
+// Parent cache of the long-document residency: block id -> parent in LDS, direct-mapped, one
+// dword per entry (tag = id >> MT_G_BPL in bits 20..31, parent + 1 in bits 0..19), so htBuild's
+// bottom-up passes read the parents of the blocks it saw for the last U sets from LDS instead
+// of HBM.  Every write of a block's parent field updates it (bpPut / bpDrop); documents with
+// 2^20 blocks or more run without it.
+#ifndef MT_G_BPC
+#define MT_G_BPC 1
+#endif
+#define MT_G_BPL 11
+#define MT_G_BP (1 << MT_G_BPL)
+#define MT_BP_EMPTY 0xFFFFFFFFu
 #define MT_G_HTN (MT_G_HT * 3 / 4)
 enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2, MT_RES_BIG = 3 };
 // Diagnostic builds keep per-document phase/event counters (prof[]) across binds;
 // product builds never load or store them (8 SGPR pairs fewer live in the replay loop).
-#if defined(MT_PROFILE) || defined(MT_PROFILE2) || defined(MT_PROFILE3) || defined(MT_EVCOUNT) || defined(MT_EVCOUNT2)
+#if defined(MT_PROFILE) || defined(MT_PROFILE2) || defined(MT_PROFILE3) || defined(MT_PROFILE4) || defined(MT_BPC_STATS) || defined(MT_EVCOUNT) || defined(MT_EVCOUNT2)
 #define MT_KEEP_PROF 1
 #else
 #define MT_KEEP_PROF 0
@@ -165,7 +176,7 @@ enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2, MT_RES_BIG = 3 };
 #define MT_QC(i)
 #endif
 // Zamboni breakdown probes (device diagnostic builds only, -DMT_PROFILE3): 0 zamboni
-// total, 1 scourLeaf, 2 appendText, 3 packParent, 4 updatePathLens, 5 heapGet,
+// total, 1 scourLeaf, 2 appendText, 3 packParent, 4 packParent's leaf scour, 5 heapGet,
 // 6 path after scour (child rewrite + pack/update), 7 pops.
 #if defined(MT_PROFILE3) && defined(__HIP_DEVICE_COMPILE__)
 #define MT_ZB(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
@@ -175,6 +186,26 @@ enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2, MT_RES_BIG = 3 };
 #define MT_ZB(v)
 #define MT_ZE(i, v)
 #define MT_ZC(i)
+#endif
+// Parent-cache statistics (host-emulation diagnostic builds only, -DMT_BPC_STATS): 0 lookups,
+// 1 hits, 2 misses on an empty slot, 3 misses on another block's entry, 4 puts over another
+// block's entry, 5 drops of a live entry.
+#if defined(MT_BPC_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+#define MT_BS(i) prof[i] += 1
+#else
+#define MT_BS(i)
+#endif
+// computeU probes of the long-document residency (device diagnostic builds only, -DMT_PROFILE4):
+// 0 window scan cyc, 1 htBuild cyc, 2 htBuild levels, 3 U entries, 4 window entries, 5 calls,
+// 6 parent lookups, 7 parent-cache misses.
+#if defined(MT_PROFILE4) && defined(__HIP_DEVICE_COMPILE__)
+#define MT_UB(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define MT_UE(i, v) prof[i] += __builtin_amdgcn_s_memtime() - (v)
+#define MT_UC(i, x) prof[i] += (unsigned long long)(x)
+#else
+#define MT_UB(v)
+#define MT_UE(i, v)
+#define MT_UC(i, x)
 #endif
 enum { MT_PH_U = 0, MT_PH_SPLIT, MT_PH_INSERT, MT_PH_RANGE, MT_PH_ZAMBONI, MT_PH_OP, MT_PH_GEN, MT_PH_TEXT };
 
@@ -371,6 +402,7 @@ struct __attribute__((aligned(16))) MtLdsBig {
     int sid[MT_G_STG], sdel[MT_G_STG], spf[MT_G_STG];
     int htk[MT_G_HT], htv[MT_G_HT];   // corrections table: block id (MT_BC_EMPTY: free), Σ delta
     uint16_t hlist[MT_G_HT];          // occupied slots in insertion (level) order
+    uint32_t bpc[MT_G_BP];            // parent cache (MT_G_BPC)
     struct Job {                      // a job wave 0 posts to the workgroup (mwRun / mwPost)
         int op, r, c, r0, n, H, minSeq, heapN;
         MtRow* R; int* win; MtBlk* blk; int* uanc; uint16_t* text;
@@ -388,14 +420,17 @@ struct MtScratch {
     int corr[MT_MAXN];                // per-child perspective corrections (childLens)
 };
 
-// A row or block record read or written as dwords (lane k: dword k); may_alias keeps those
-// accesses ordered with the field accesses of the same record.
-typedef int __attribute__((may_alias)) mt_ai;
+// A row record read as 16-byte quads (one wide load per quad); may_alias keeps those accesses
+// ordered with the field accesses of the same record.
+struct __attribute__((aligned(16), may_alias)) MtQ16a { uint32_t x, y, z, w; };
 #ifndef MT_NONL
 #define MT_NONL 1                     // rows flag text without a newline (MT_M_NONL)
 #endif
 #ifndef MT_LEAF_ONCE
 #define MT_LEAF_ONCE 1                // walk: leaf rows loaded whole once, splits from registers
+#endif
+#ifndef MT_SCOUR_QUADS
+#define MT_SCOUR_QUADS 1              // scourLeaves: rows' first two quads in two wide loads
 #endif
 MT_INLINE int pick16(const int* c, int j) {         // c[j] for a lane index j (no private-array indexing)
     int v = c[0];
@@ -642,6 +677,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     bool bcOn;                          // MT_RES_BIG: descents fill the LDS block cache
     bool htOk; int hlistN;              // MT_RES_BIG: the corrections table is built for U; occupied slots
     bool htOn, pfOn; int mwSeq;         // MT_RES_BIG: table / zamboni prefetch enabled; jobs posted so far
+    bool bpOn;                          // MT_RES_BIG: the LDS parent cache is kept (MT_G_BPC)
     int& nCol = mt_cold_v.ncol;         // rows gathered by rangeMap(MT_MAP_COLLECT) at the register arena's tail
     int landB;                          // leaf block the last insertAtPath linked its node under
     int rfN; int*& rfHbm = mt_cold_v.rfhbm;   // recycled-row stack: depth, HBM home between runs
@@ -686,7 +722,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         c_ops = c_msgs = c_ins = c_rows = c_depth = c_scour = 0;
         nU = 0; uValid = false; uRef = -1; uCli = -1;
         heapTop = heapN > 0 ? uni(heap[1].maxSeq) : 0x7FFFFFFF;     // HBM home: bind precedes toLds
-        lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0; bcOn = false; htOk = false; hlistN = 0; htOn = pfOn = false; mwSeq = 0;
+        lastL = 0; lastIdx = 0; lastSplit = false; gcEpoch = 0; bcOn = false; htOk = false; hlistN = 0; htOn = pfOn = false; mwSeq = 0; bpOn = false;
         for (int i = 0; i < 4; i++) mt_cold_v.pcKey[i] = -1;
         rfHbm = st.hold + (size_t)d * MT_RFL; rfN = uni(h.rfN); blkFreeN = uni(h.blkFreeN);
         heapHW = uni(h.heapHW); winHW = uni(h.winHW); ovxN = uni(h.ovxN);
@@ -735,6 +771,7 @@ template <int RES, bool FULL = true> struct MtEngT {
 #endif
         wave_for(8, [&](int i) MT_LAM { bk(0).c[i] = -1; });
         bk(0).len = 0; bk(0).parent = -1; bk(0).n = 0; bk(0).height = 0; bk(0).scour = -1;
+        bpReset();
         wave_for(MT_REG_CAP, [&](int i) MT_LAM { regs[i].client = -1; regs[i].n = 0; regs[i].flags = 0; regs[i].off = 0; });
         regTop = 0; regHalf = 0;
         // idToSegment entries are not reset: an entry is read only for an id the host
@@ -756,7 +793,59 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (blkTop >= (int)blkCap) { status |= MT_DS_OOM_BLOCKS; return -1; }
         return blkTop++;
     }
-    MT_HD void freeBlock(int id) { bk(id).parent = blkFree; bk(id).n = -1; blkFree = id; blkFreeN++; }
+    MT_HD void freeBlock(int id) { bk(id).parent = blkFree; bk(id).n = -1; blkFree = id; blkFreeN++; bpDrop(id); }
+    // The parent cache (MT_RES_BIG, MT_G_BPC): bpPut after every write of a block's parent field,
+    // bpDrop when the field stops being a parent (free list), bpReset when block ids are reassigned.
+    MT_HD static uint32_t bpPack(int b, int p) { return ((uint32_t)(b >> MT_G_BPL) << 20) | (uint32_t)(p + 1); }
+    MT_HD void bpPut(int b, int p) {
+        if constexpr (BIG) {
+            if (MT_G_BPC && bpOn) {
+                uint32_t& e = mt_ldsg().bpc[b & (MT_G_BP - 1)];
+                if (e != MT_BP_EMPTY && (e >> 20) != (uint32_t)(b >> MT_G_BPL)) MT_BS(4);
+                e = bpPack(b, p);
+            }
+        }
+    }
+    MT_HD void bpDrop(int b) {
+        if constexpr (BIG) {
+            if (MT_G_BPC && bpOn) {
+                uint32_t& e = mt_ldsg().bpc[b & (MT_G_BP - 1)];
+                if ((e >> 20) == (uint32_t)(b >> MT_G_BPL)) MT_BS(5);
+                e = MT_BP_EMPTY;
+            }
+        }
+    }
+    MT_HD void bpReset() {
+        if constexpr (BIG) {
+            if (MT_G_BPC && bpOn) {
+                for (int base = 0; base < MT_G_BP; base += MT_WAVE)
+                    wave_for(MT_WAVE, [&](int k) MT_LAM { mt_ldsg().bpc[base + k] = MT_BP_EMPTY; });
+                wave_sync();
+            }
+        }
+    }
+    // bk(b).parent, through the parent cache when it is kept (a miss fills the entry).
+    MT_HD int bkParent(int b) {
+        if constexpr (BIG) {
+            if (MT_G_BPC && bpOn) {
+                uint32_t& e = mt_ldsg().bpc[b & (MT_G_BP - 1)];
+                const uint32_t v = e;
+                MT_BS(0);
+                if ((v >> 20) == (uint32_t)(b >> MT_G_BPL)) {
+                    MT_BS(1);
+#if defined(MT_BPC_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
+                    if ((int)(v & 0xFFFFFu) - 1 != bk(b).parent) abort();     // host emulation: a stale entry
+#endif
+                    return (int)(v & 0xFFFFFu) - 1;
+                }
+                if (v == MT_BP_EMPTY) MT_BS(2); else MT_BS(3);
+                const int p = bk(b).parent;
+                e = bpPack(b, p);
+                return p;
+            }
+        }
+        return bk(b).parent;
+    }
 
     /* ---------------------------------------------------- LDS residency -- */
     // Lane-parallel copy of n 16-byte quads.
@@ -792,6 +881,8 @@ template <int RES, bool FULL = true> struct MtEngT {
             bcOn = MT_G_BCACHE && !(lb & MT_BIGF_NO_BCACHE);    // lb: MT_BIGF_* switches (A/B)
             pfOn = MT_G_NW > 1 && !(lb & MT_BIGF_NO_PREFETCH);
             htOn = !(lb & MT_BIGF_NO_TABLE);
+            bpOn = MT_G_BPC && !(lb & MT_BIGF_NO_BPC) && blkCap < (1u << 20);
+            bpReset();
             wave_sync();
             gRowCap = S.rowCap; gBlkCap = blkCap; gHeapCap = S.heapCap; gWinCap = S.winCap;
             S.heapCap = gHeapCap < (uint32_t)lh ? gHeapCap : (uint32_t)lh;
@@ -989,7 +1080,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         return wave_sum8(v);
     }
     MT_HD void setChildParent(int h, int id, int p) {
-        if (h == 0) row(id).parent = p; else bk(id).parent = p;
+        if (h == 0) row(id).parent = p; else { bk(id).parent = p; bpPut(id, p); }
     }
 
     /* ------------------------------------- perspective window (U set) -- */
@@ -1170,6 +1261,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         MtLdsBig& G = mt_ldsg();
         int newWin = 0; nU = 0;
         const int wN0 = winN;
+        MT_UB(u0); MT_UC(4, wN0); MT_UC(5, 1);
         if (wN0 <= MT_G_MWMIN) {                    // a few chunks: wave 0 alone, no barriers
 #if MT_G_ALLCH
             // every chunk's rows in one round trip (one wave per SIMD here: registers to spare),
@@ -1213,8 +1305,11 @@ template <int RES, bool FULL = true> struct MtEngT {
             }
         }
         wave_sync();
+        MT_UE(0, u0); MT_UC(3, nU);
+        MT_UB(u1);
         htOk = false;
         if (nU > 0 && height > 0 && !(htOn && htBuild())) mwRun(MT_MW_CHAIN, r, c, 0, nU);
+        MT_UE(1, u1);
         if (prune) winN = newWin;
         wave_sync();
         uValid = true; uRef = r; uCli = c;
@@ -1289,7 +1384,14 @@ template <int RES, bool FULL = true> struct MtEngT {
             for (int base = l0; base < l1; base += MT_WAVE) {
                 const int m = (l1 - base) < MT_WAVE ? (l1 - base) : MT_WAVE;
                 const auto ch = wave_map(m, [&](int k) MT_LAM { return (int)G.hlist[base + k]; });
-                const auto par = wave_map(m, [&](int k) MT_LAM { return bk(G.htk[own(ch, k)]).parent; });
+#if defined(MT_PROFILE4)
+                MT_UC(6, m);
+                if (bpOn) MT_UC(7, wave_count(wave_map(m, [&](int k) MT_LAM {
+                    const int b = G.htk[own(ch, k)];
+                    return (G.bpc[b & (MT_G_BP - 1)] >> 20) != (uint32_t)(b >> MT_G_BPL);
+                })));
+#endif
+                const auto par = wave_map(m, [&](int k) MT_LAM { return bkParent(G.htk[own(ch, k)]); });
                 const auto val = wave_map(m, [&](int k) MT_LAM { return G.htv[own(ch, k)]; });
                 const auto a = wave_map(m, [&](int k) MT_LAM {
                     const int p = own(par, k);
@@ -1302,6 +1404,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             }
             wave_sync();
             l0 = l1; l1 = hlistN;
+            MT_UC(2, 1);
         }
         htOk = true;
         return true;
@@ -1855,6 +1958,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                 bk(B).c[i] = i < 4 ? own(nc, i) : -1;
             });
             bk(NB).n = 4; bk(NB).height = h.height; bk(NB).scour = -1; bk(NB).parent = h.parent;
+            bpPut(NB, h.parent);
             bk(B).n = 4;
             wave_for(4, [&](int i) MT_LAM { setChildParent(h.height, own(hi, i), NB); });
             if (first && ix >= 4) landB = NB;
@@ -1868,6 +1972,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                 wave_for(8, [&](int i) MT_LAM { bk(R).c[i] = i == 0 ? B : (i == 1 ? NB : -1); });
                 bk(R).n = 2; bk(R).height = h.height + 1; bk(R).parent = -1; bk(R).scour = -1; bk(R).len = bLen + nbLen;
                 bk(B).parent = R; bk(NB).parent = R;
+                bpPut(R, -1); bpPut(B, R); bpPut(NB, R);
                 root = R; height = h.height + 1;
                 return;
             }
@@ -2249,6 +2354,25 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int b = own(bsel, t);
             return (t & 7) < bk(b).n ? bk(b).c[t & 7] : -1;
         });
+#if MT_SCOUR_QUADS
+        // the fields below are the row's first two quads (len seq rseq meta | toff props parent
+        // tcap): two 16-byte loads per lane instead of seven dword loads
+        const auto q0 = wave_map(span, [&](int j) MT_LAM {
+            const int g = own(f, j);
+            return g >= 0 ? ((const MtQ16a*)&row(g))[0] : MtQ16a{0u, 0u, 0u, 0u};
+        });
+        const auto q1 = wave_map(span, [&](int j) MT_LAM {
+            const int g = own(f, j);
+            return g >= 0 ? ((const MtQ16a*)&row(g))[1] : MtQ16a{0u, 0u, 0u, 0u};
+        });
+        auto fl = wave_map(span, [&](int j) MT_LAM { return (int)own(q0, j).x; });
+        auto fs = wave_map(span, [&](int j) MT_LAM { return (int)own(q0, j).y; });
+        auto fr = wave_map(span, [&](int j) MT_LAM { return (int)own(q0, j).z; });
+        auto fm = wave_map(span, [&](int j) MT_LAM { return (int)own(q0, j).w; });
+        auto ft = wave_map(span, [&](int j) MT_LAM { return (int)own(q1, j).x; });
+        auto fp = wave_map(span, [&](int j) MT_LAM { return (int)own(q1, j).y; });
+        auto fc = wave_map(span, [&](int j) MT_LAM { return (int)own(q1, j).w; });
+#else
         auto fm = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? (int)row(g).meta : 0; });
         auto fs = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).seq : 0; });
         auto fr = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).rseq : 0; });
@@ -2256,6 +2380,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         auto fp = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).props : 0; });
         auto ft = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).toff : 0; });
         auto fc = wave_map(span, [&](int j) MT_LAM { const int g = own(f, j); return g >= 0 ? row(g).tcap : 0; });
+#endif
         const int ms = minSeq;
         // class: 0 empty, 1 unlink, 2 held removed, 3 held above the MSN, 4 candidate
         auto cls = wave_map(span, [&](int t) MT_LAM {
@@ -2385,7 +2510,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             auto pch = blkLoad(P, ph);
             int nh = 0;
             const int chh = ph.height - 1;                       // children of P are blocks of this height
-            if (chh == 0) nh = scourLeaves(pch, ph.n, 0);
+            if (chh == 0) { MT_ZB(z4); nh = scourLeaves(pch, ph.n, 0); MT_ZE(4, z4); }
             else {
                 for (int i = 0; i < ph.n; i++) {
                     const int cb = wave_at(pch, i);
@@ -2401,23 +2526,36 @@ template <int RES, bool FULL = true> struct MtEngT {
             // then allocating, without a dependent LDS load per allocation).
             const int reuse = cc < ph.n ? cc : ph.n;
             for (int i = 0; i < ph.n - reuse; i++) freeBlock(wave_at(pch, i));
-            wave_sync();
-            const int base = nh / cc; int extra = nh % cc; int rd = 0;
-            auto packed = wave_map(8, [&](int i) MT_LAM { return -1; });
-            for (int ni = 0; ni < cc; ni++) {
-                int cntc = base; if (extra > 0) { cntc++; extra--; }
-                const int NB = ni < reuse ? wave_at(pch, ph.n - 1 - ni) : allocBlock();
+            const int pn = ph.n;
+            auto nbid = wave_shfl(pch, [=](int ni) MT_LAM { return ni < reuse ? pn - 1 - ni : 0; });
+            for (int ni = reuse; ni < cc; ni++) {            // more blocks than P had (rare)
+                const int NB = allocBlock();
                 if (NB < 0) return;
-                const int r0 = rd;
-                wave_for(8, [&](int i) MT_LAM { bk(NB).c[i] = i < cntc ? sc->hold[r0 + i] : -1; });
-                wave_for(cntc, [&](int i) MT_LAM { setChildParent(chh, sc->hold[r0 + i], NB); });
-                rd += cntc;
-                bk(NB).n = cntc; bk(NB).height = chh; bk(NB).parent = P; bk(NB).scour = -1;
-                bk(NB).len = wave_sum8(wave_map(cntc, [&](int i) MT_LAM { return sc->holdLen[r0 + i]; }));
-                wave_sync();
-                packed = wave_map(8, [&](int i) MT_LAM { return i == ni ? NB : own(packed, i); });
+                nbid = wave_set(nbid, ni, NB);
             }
-            wave_for(8, [&](int i) MT_LAM { bk(P).c[i] = own(packed, i); });
+            wave_sync();
+            // New block ni takes hold[st(ni), st(ni) + cnt(ni)): the first `extra` blocks one child
+            // more than `base`.  All blocks at once: lane t writes slot t & 7 of block t >> 3 (and
+            // its child's parent), then lane ni block ni's header.
+            const int base = nh / cc, extra = nh % cc;
+            const auto nb8 = wave_gather8(nbid);
+            wave_for(8 * cc, [&](int t) MT_LAM {
+                const int ni = t >> 3, slot = t & 7;
+                const int cnt = base + (ni < extra ? 1 : 0), st = ni * base + (ni < extra ? ni : extra);
+                const int ch = slot < cnt ? sc->hold[st + slot] : -1;
+                const int NB = own(nb8, t);
+                bk(NB).c[slot] = ch;
+                if (ch >= 0) setChildParent(chh, ch, NB);
+            });
+            wave_for(cc, [&](int ni) MT_LAM {
+                const int cnt = base + (ni < extra ? 1 : 0), st = ni * base + (ni < extra ? ni : extra);
+                const int NB = own(nbid, ni);
+                int len = 0;
+                for (int k = 0; k < MT_MAXN; k++) len += k < cnt ? sc->holdLen[st + k] : 0;
+                bk(NB).n = cnt; bk(NB).height = chh; bk(NB).parent = P; bk(NB).scour = -1; bk(NB).len = len;
+                bpPut(NB, P);
+            });
+            wave_for(8, [&](int i) MT_LAM { bk(P).c[i] = i < cc ? own(nbid, i) : -1; });
             bk(P).n = cc;
             wave_sync();
             if (cc < MT_MAXN / 2 && ph.parent >= 0) { P = ph.parent; continue; }
@@ -2778,6 +2916,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (winN > winHW) winHW = winN;
         // reloadFromSegments: level h groups the nodes of level h-1 seven at a time
         blkTop = 0; blkFree = -1; blkFreeN = 0;
+        bpReset();                                  // nothing reads parents before the build ends
         int first = 0, count = nh, h = 0;
         for (;;) {
             const int nb = (count + MT_MAXN - 2) / (MT_MAXN - 1);

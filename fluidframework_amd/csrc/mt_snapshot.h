@@ -40,8 +40,21 @@ inline void put_utf8(std::string& o, uint32_t cp) {
 // JSON.stringify string quoting over UTF-16 code units (well-formed stringify).
 inline void quote16(std::string& o, const uint16_t* s, size_t n) {
     static const char hx[] = "0123456789abcdef";
-    o.push_back('"');
-    for (size_t i = 0; i < n; i++) {
+    // the plain prefix (printable ASCII other than '"' and '\\') is written byte by byte into
+    // place; the general loop takes over at the first unit that needs more
+    const size_t o0 = o.size();
+    o.resize(o0 + n + 2);
+    char* d = &o[o0];
+    *d++ = '"';
+    size_t i = 0;
+    for (; i < n; i++) {
+        const uint16_t c = s[i];
+        if (c < 0x20 || c >= 0x7F || c == '"' || c == '\\') break;
+        *d++ = (char)c;
+    }
+    if (i == n) { *d = '"'; return; }
+    o.resize(o0 + 1 + i);
+    for (; i < n; i++) {
         const uint16_t c = s[i];
         if (c == '"') { o += "\\\""; continue; }
         if (c == '\\') { o += "\\\\"; continue; }
@@ -120,12 +133,13 @@ struct PropsJson {
         return &js[ps];
     }
 };
-// Segment JSON texts back to back (one buffer, not one allocation per segment).
+// Segment JSON texts back to back, each followed by its separator (one buffer, not one
+// allocation per segment; a chunk's segments are one append).
 struct SegList {
     std::string buf; std::vector<size_t> off{0};
     size_t size() const { return off.size() - 1; }
-    void end() { off.push_back(buf.size()); }
-    void put(std::string& o, size_t i) const { o.append(buf, off[i], off[i + 1] - off[i]); }
+    void end() { buf.push_back(','); off.push_back(buf.size()); }
+    void putRange(std::string& o, size_t a, size_t n) const { if (n) o.append(buf, off[a], off[a + n] - off[a] - 1); }
     size_t bytes(size_t a, size_t n) const { return off[a + n] - off[a]; }
 };
 inline void seg_json(std::string& o, const MtSnapView& v, PropsJson& pj, int s, const uint16_t* txt, size_t tn) {
@@ -168,6 +182,7 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
     PropsJson pj(v, nm);
     PropsMatch pm_(v, nm);
     SegList segs; std::vector<long long> lens;
+    segs.buf.reserve((size_t)v.hdr.rowTop * 48); segs.off.reserve((size_t)v.hdr.rowTop + 1); lens.reserve(v.hdr.rowTop);
     int prev = -1; std::vector<uint16_t> ptext; bool pcloned = false;
     auto client = [&](int c) -> const std::string& {
         static const std::string orig = "\"original\"";
@@ -221,10 +236,10 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
     for (size_t k = 0; k < chunks.size(); k++) {
         const Chunk& c = chunks[k];
         std::string o;
-        o.reserve(segs.bytes(c.start, c.count) + c.count + 256 + 16 * chunks.size());
+        o.reserve(segs.bytes(c.start, c.count) + 256 + 16 * chunks.size());
         o += "{\"version\":\"1\",\"segmentCount\":"; put_int(o, (long long)c.count);
         o += ",\"length\":"; put_int(o, c.length); o += ",\"segments\":[";
-        for (size_t i = 0; i < c.count; i++) { if (i) o.push_back(','); segs.put(o, c.start + i); }
+        segs.putRange(o, c.start, c.count);
         o += "],\"startIndex\":"; put_int(o, (long long)c.start);
         if (k == 0) {
             o += ",\"headerMetadata\":{\"minSequenceNumber\":"; put_int(o, minSeq);
@@ -301,8 +316,8 @@ inline std::vector<std::string> snapshot_legacy_blobs(const MtSnapView& v, const
         o += ",\"totalSegmentCount\":"; put_int(o, (long long)segs.size());
         o += ",\"chunkSequenceNumber\":"; put_int(o, minSeq);
         o += ",\"segmentTexts\":[";
-        o.reserve(o.size() + segs.bytes(c.start, c.count) + c.count + 256);
-        for (size_t i = 0; i < c.count; i++) { if (i) o.push_back(','); segs.put(o, c.start + i); }
+        o.reserve(o.size() + segs.bytes(c.start, c.count) + 256);
+        segs.putRange(o, c.start, c.count);
         o += "]";
         if (header) {                                                   // buildHeaderMetadataForLegecyChunk
             o += ",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}";
@@ -342,10 +357,47 @@ inline uint64_t xxh64(const uint8_t* p, size_t len, uint64_t seed) {
     h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
     return h;
 }
+// xxh64 fed in pieces (the same value as xxh64 of the pieces back to back).
+struct Xxh64 {
+    static constexpr uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL, P3 = 1609587929392839161ULL,
+                              P4 = 9650029242287828579ULL, P5 = 2870177450012600261ULL;
+    uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1, total = 0;
+    uint8_t tail[32]; size_t tn = 0;
+    static uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+    static uint64_t rd64(const uint8_t* q) { uint64_t x; memcpy(&x, q, 8); return x; }
+    static uint64_t rnd(uint64_t acc, uint64_t in) { acc += in * P2; acc = rotl(acc, 31); return acc * P1; }
+    void stripe(const uint8_t* p) { v1 = rnd(v1, rd64(p)); v2 = rnd(v2, rd64(p + 8)); v3 = rnd(v3, rd64(p + 16)); v4 = rnd(v4, rd64(p + 24)); }
+    void update(const uint8_t* p, size_t len) {
+        total += len;
+        if (tn) {
+            const size_t k = (32 - tn) < len ? (32 - tn) : len;
+            memcpy(tail + tn, p, k); tn += k; p += k; len -= k;
+            if (tn < 32) return;
+            stripe(tail); tn = 0;
+        }
+        for (; len >= 32; p += 32, len -= 32) stripe(p);
+        memcpy(tail, p, len); tn = len;
+    }
+    uint64_t digest() const {
+        uint64_t h;
+        if (total >= 32) {
+            h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+            for (uint64_t vv : {v1, v2, v3, v4}) { h ^= rnd(0, vv); h = h * P1 + P4; }
+        } else h = P5;
+        h += total;
+        const uint8_t* p = tail; const uint8_t* e = tail + tn;
+        while (p + 8 <= e) { h ^= rnd(0, rd64(p)); h = rotl(h, 27) * P1 + P4; p += 8; }
+        if (p + 4 <= e) { uint32_t x; memcpy(&x, p, 4); h ^= (uint64_t)x * P1; h = rotl(h, 23) * P2 + P3; p += 4; }
+        while (p < e) { h ^= (*p) * P5; h = rotl(h, 11) * P1; p++; }
+        h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+        return h;
+    }
+};
+// xxh64 (seed 0) of the blobs each preceded by its 8-byte little-endian length.
 inline uint64_t blobs_digest(const std::vector<std::string>& blobs) {
-    std::string buf;
-    for (const auto& b : blobs) { uint64_t n = b.size(); buf.append((const char*)&n, 8); buf += b; }
-    return xxh64((const uint8_t*)buf.data(), buf.size(), 0);
+    Xxh64 x;
+    for (const auto& b : blobs) { const uint64_t n = b.size(); x.update((const uint8_t*)&n, 8); x.update((const uint8_t*)b.data(), n); }
+    return x.digest();
 }
 
 inline void observer_text(const MtSnapView& v, std::vector<uint16_t>& out) {

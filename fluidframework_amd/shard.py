@@ -60,10 +60,12 @@ def lpt_assign(costs: np.ndarray, world: int) -> np.ndarray:
 
 
 def generation_caps(ops: np.ndarray, ins_len: int) -> dict:
-    """Generous per-document pools for the generating context."""
+    """Generous per-document pools for the generating context.  The window is bounded by the
+    MSN's lag behind the current seq, not by the stream length; 1,048,576 Zipf documents hold
+    one whose window passes 1,024 entries (a client silent for a long stretch holds the MSN)."""
     o = np.asarray(ops, np.int64)
     return dict(rows_per_doc=3 * o + 64, blocks_per_doc=o + 64, heap_per_doc=2 * o + 64,
-                window_per_doc=np.minimum(o + 64, 1024), text_per_doc=ins_len * o + 4096,
+                window_per_doc=np.minimum(2 * o + 64, 8192), text_per_doc=ins_len * o + 4096,
                 propsets_per_doc=np.full(len(o), 64))
 
 

@@ -310,9 +310,11 @@ int  mt_replay_resident(mt_ctx* ctx);
  * and a document that outgrows the LDS blocks continues from HBM in the same
  * wave at the exact op it reached; 0: every pool in HBM; 1: rows, blocks, heap
  * and window all in LDS (finished by a second HBM launch when outgrown); 3: long
- * documents (blocks beyond LDS): zamboni heap, collab window and U set in LDS
- * (~68 KB, two documents per CU), blocks/rows/text in HBM, same in-wave hand-over
- * (rows = window entries kept in LDS, the rest stay in HBM).
+ * documents (blocks beyond LDS): zamboni heap, collab window, U set, per-block
+ * corrections table and parent cache in LDS (one four-wave workgroup per CU),
+ * blocks/rows/text in HBM, same in-wave hand-over (rows = window entries kept in
+ * LDS, the rest stay in HBM; blocks = A/B switches, bits 1 block cache, 2 zamboni
+ * prefetch, 4 corrections table, 8 parent cache: off).
  * rows/blocks/heap (0 = compiled maximum) may only lower the caps; tests use
  * small caps to force the hand-over. */
 int  mt_set_residency(mt_ctx* ctx, int use_lds, int rows, int blocks, int heap);

@@ -23,9 +23,10 @@ def _atomic_build(cmd, out):
 def build_emu(force=False):
     if force or not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(d) for d in DEPS):
         # long-document residency: windows above 64 entries take the multi-wave scan (the device
-        # scans up to 512 in wave 0 alone), so the CPU tests' small windows run both paths
+        # scans up to 512 in wave 0 alone), so the CPU tests' small windows run both paths; every
+        # parent-cache hit is checked against the block's parent field (abort on a stale entry)
         _atomic_build(["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wno-unknown-pragmas",
-                       "-DMT_G_MWMIN=64", "-o", None, SRC], LIB)
+                       "-DMT_G_MWMIN=64", "-DMT_BPC_CHECK=1", "-o", None, SRC], LIB)
     return LIB
 
 

@@ -79,8 +79,9 @@ def check_deep_window(factory, n, pre, ops, lag, rows, window, text, psets=8192,
 # residency: (2) blk (blocks outgrow LDS: HBM continuation), (3) long-document mode with
 # the compiled LDS caps, with a 64-entry LDS window (the rest in HBM) and an 8-entry heap
 # cap that forces the in-wave hand-over (block cache written back mid-run), and with the
-# block cache, zamboni prefetch and corrections table off (blocks = MT_BIGF_* switches).
-@pytest.mark.parametrize("res", [(2, 0, 0, 0), (3, 0, 0, 0), (3, 64, 0, 8), (3, 0, 7, 0)])
+# block cache, zamboni prefetch, corrections table and parent cache off (blocks = MT_BIGF_*
+# switches).
+@pytest.mark.parametrize("res", [(2, 0, 0, 0), (3, 0, 0, 0), (3, 64, 0, 8), (3, 0, 7, 0), (3, 0, 8, 0)])
 @pytest.mark.parametrize("lag", [64, 512])
 def test_deep_window_on_checkpoint_matches_oracle(lag, res):
     check_deep_window(emu_engine, 2, 3000, 1500, lag, rows=12000, window=8192, text=1 << 16, residency=res)

@@ -1,5 +1,5 @@
 """Diagnostic: per-message event counts of config 4's measured stream (host emulation,
--DMT_EVCOUNT or EVFLAG=MT_EVCOUNT2), documents pre-built as bench.py does.  Not the product."""
+-DMT_EVCOUNT or EVFLAG=MT_EVCOUNT2 / MT_BPC_STATS), documents pre-built as bench.py does.  Not the product."""
 import ctypes as C, os, subprocess, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -33,6 +33,9 @@ if flag == "MT_EVCOUNT":
     print(f"config4 pre={pre} ops={ops} res={res}: computeU/msg {tot[0]/msgs:.2f}  |U|/call {tot[1]/max(tot[0],1):.1f}  "
           f"win/call {tot[2]/max(tot[0],1):.1f}  heapGet/msg {tot[3]/msgs:.3f}  siftLevels/get {tot[4]/max(tot[3],1):.2f}  "
           f"walkLevels/msg {tot[5]/msgs:.2f}  blockSplits/msg {tot[6]/msgs:.3f}  heapN/get {tot[7]/max(tot[3],1):.0f}")
+elif flag == "MT_BPC_STATS":
+    names = ["lookups", "hits", "miss empty", "miss other", "put evicts", "drops live"]
+    print(" ".join(f"{nm}={tot[i]/msgs:.2f}" for i, nm in enumerate(names)))
 else:
     names = ["packParent", "updatePathLens levels", "copyText units", "copyText calls", "textGC", "splitRow",
              "zamboni pops", "rangeMap leaf blocks"]

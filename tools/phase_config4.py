@@ -35,6 +35,9 @@ tot = (raw - base).sum(axis=0).astype(float)
 names = ["computeU", "split-walks", "insert-walk", "rangeMap", "zamboni", "op-total", "gen", "textGC"]
 if flag == "MT_PROFILE2":
     names = ["walk blkLoad", "walk childLens", "walk levels(n)", "computeU", "computeU(n)", "heapGet", "heapGet(n)", "scourLeaf"]
+if flag == "MT_PROFILE4":
+    names = ["U scan", "htBuild", "ht levels(n)", "U entries(n)", "window(n)", "computeU(n)", "parent lookups(n)",
+             "parent misses(n)"]
 print(f"{flag} residency={res} config4 docs={n} prebuild={pre} ops={ops} replay wall {dt*1e3:.1f} ms; per-doc mean cycles per msg:")
 for i, nm in enumerate(names):
     print(f"  {nm:16s} {tot[i]/n/ops:10.0f}")

@@ -41,7 +41,7 @@ fn(eng.h, docs, raw.ctypes.data)
 tot = raw.sum(axis=0).astype(float)
 names = ["computeU", "split-walks", "insert-walk", "rangeMap", "zamboni", "op-total", "gen", "textGC"]
 if flag == "MT_PROFILE3":
-    names = ["zamboni", "scourLeaf", "appendText", "packParent", "updatePathLens", "heapGet", "after-scour", "pops(n)"]
+    names = ["zamboni", "scourLeaf", "appendText", "packParent", "pack's scour", "heapGet", "after-scour", "pops(n)"]
 if flag == "MT_PROFILE2":
     names = ["walk blkLoad", "walk childLens", "walk levels(n)", "computeU", "computeU(n)", "heapGet", "heapGet(n)", "scourLeaf"]
 print(f"{flag} residency={res} ops={c['ops']}")
