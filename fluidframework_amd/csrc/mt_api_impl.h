@@ -291,7 +291,7 @@ static int mt_upload_ops(mt_ctx* c, const mt_op_batch* B) {
     uint8_t* d = (uint8_t*)c->b_batch.p;
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)(d + o_doc); o.op_off = (const uint32_t*)(d + o_off); o.rec = (MtOpRec*)(d + o_rec);
-    o.payload = (uint16_t*)(d + o_pay); o.n_runs = B->n_runs; o.payload_units = B->payload_units;
+    o.payload = (uint16_t*)(d + o_pay); o.n_runs = B->n_runs; o.payload_units = B->payload_units; o.pay_base = nullptr;
     o.rel = (const MtRelPos*)(d + o_rel); o.n_rel = B->rel ? B->n_rel : 0;
     c->n_runs = B->n_runs;
     c->run_off.assign(B->op_offsets, B->op_offsets + R + 1); c->batch_gen++;
@@ -978,7 +978,7 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     mtb_h2d(c, c->b_gencl.p, cl.data(), 4ull * P->n_docs);
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
-    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs; o.payload_units = PU;
+    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = P->n_docs; o.payload_units = PU; o.pay_base = nullptr;
     o.rel = nullptr; o.n_rel = 0; o.drec = nullptr; o.dcount = nullptr; o.dcap = 0;
     o.dtext = nullptr; o.dtcap = 0; o.resume = nullptr; o.start = nullptr;
     c->n_runs = P->n_docs;
@@ -1054,7 +1054,7 @@ int MT_FN(upload_batch_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids,
     if (payload_units) mtb_d2d(c, c->b_pay.p, payload, 2 * payload_units);
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
-    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs; o.payload_units = payload_units;
+    o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs; o.payload_units = payload_units; o.pay_base = nullptr;
     o.rel = nullptr; o.n_rel = 0;
     c->n_runs = n_runs;
     c->run_off.assign(op_offsets, op_offsets + n_runs + 1); c->batch_gen++;
@@ -1092,17 +1092,28 @@ int MT_FN(upload_rows_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids, 
     }
     const uint64_t N = op_offsets[n_runs], L = payload_stride;
     if (N && !rows_dev) return MT_E_INVALID;
-    if (N * L >= 0xFFFFFFFFull) { c->err = "payload slots exceed 2^32 units"; return MT_E_INVALID; }
+    // payload_off is relative to the run's base (op_off[run] * L, 64-bit), so only a run's own
+    // slots must stay below 2^32 units
+    for (uint32_t r = 0; r < n_runs; r++)
+        if ((uint64_t)(op_offsets[r + 1] - op_offsets[r]) * L >= 0xFFFFFFFFull) {
+            c->err = "one document's payload slots exceed 2^32 units"; return MT_E_INVALID;
+        }
     int rc;
 #define UP(buf, bytes) if ((rc = mtb_ensure(c, c->buf, (bytes)))) return rc;
     UP(b_doc, 4ull * n_runs + 4) UP(b_off, 4ull * (n_runs + 1)) UP(b_rec, sizeof(MtOpRec) * N + 32) UP(b_pay, 2 * N * L + 2)
-    UP(b_tmp1, 8ull * n_runs + 8)
+    UP(b_tmp1, 8ull * n_runs + 8) UP(b_pbase, 8ull * n_runs + 8)
 #undef UP
     mtb_h2d(c, c->b_doc.p, doc_ids, 4ull * n_runs);
     mtb_h2d(c, c->b_off.p, op_offsets, 4ull * (n_runs + 1));
+    {
+        std::vector<unsigned long long> pbase(n_runs);
+        for (uint32_t r = 0; r < n_runs; r++) pbase[r] = (unsigned long long)op_offsets[r] * L;
+        if (n_runs) mtb_h2d(c, c->b_pbase.p, pbase.data(), 8ull * n_runs);
+    }
     MtOps& o = c->ops;
     o.doc_ids = (const uint32_t*)c->b_doc.p; o.op_off = (const uint32_t*)c->b_off.p; o.rec = (MtOpRec*)c->b_rec.p;
     o.payload = (uint16_t*)c->b_pay.p; o.n_runs = n_runs; o.payload_units = N * L;
+    o.pay_base = (const unsigned long long*)c->b_pbase.p;
     o.rel = nullptr; o.n_rel = 0;
     c->n_runs = n_runs;
     c->run_off.assign(op_offsets, op_offsets + n_runs + 1); c->batch_gen++;

@@ -321,6 +321,10 @@ struct MtOps {                                // device copy of an mt_op_batch
     const uint32_t* start;                    // capture resume: first op of each run (null: op_off)
     uint32_t n_runs;
     uint64_t payload_units;                   // records are bounds-checked against it on the device
+    // Per-run payload bases in units (null: payload_off is absolute).  An exchanged batch of a
+    // million documents holds more than 2^32 payload units; its records' payload_off is then
+    // relative to the run's base (mt_upload_rows_dev).
+    const unsigned long long* pay_base;
 };
 enum { MT_DC_REC = 0, MT_DC_RECRES = 1, MT_DC_TXT = 2, MT_DC_TXTRES = 3 };
 // Records one message can emit at most, beyond its own range or paste: 2 ensureIntervalBoundary
@@ -428,6 +432,9 @@ struct __attribute__((aligned(16), may_alias)) MtQ16a { uint32_t x, y, z, w; };
 #endif
 #ifndef MT_LEAF_ONCE
 #define MT_LEAF_ONCE 1                // walk: leaf rows loaded whole once, splits from registers
+#endif
+#ifndef MT_GT_CH
+#define MT_GT_CH 4                    // gatherText: 64-unit chunks loaded before any is stored
 #endif
 #ifndef MT_SCOUR_QUADS
 #define MT_SCOUR_QUADS 1              // scourLeaves: rows' first two quads in two wide loads
@@ -2269,9 +2276,8 @@ template <int RES, bool FULL = true> struct MtEngT {
         int n = hlen;
         for (int i = i0; i < i1; i++) n += wave_at(len, i);
         MT_EV2(2, n); MT_EV2(3, 1);
-        for (int base = 0; base < n; base += MT_WAVE) {
-            const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
-            // piece of unit base+k: scan the (<= 9) piece prefixes, all scalar
+        // piece of unit q: scan the (<= 9) piece prefixes, all scalar
+        auto srcOf = [&](int base, int m) MT_LAM {
             auto from = wave_map(m, [&](int k) MT_LAM { const int q = base + k; return q < hlen ? hsrc + q : -1; });
             int pre = hlen;
             for (int i = i0; i < i1; i++) {
@@ -2282,9 +2288,27 @@ template <int RES, bool FULL = true> struct MtEngT {
                 });
                 pre += pl;
             }
-            auto v = wave_map(m, [&](int k) MT_LAM { return (int)text[own(from, k)]; });
+            return from;
+        };
+        // The destination never overlaps a source (a new region, or the head's slack past its
+        // text), so MT_GT_CH chunks of 64 units are loaded before any is stored: one round trip
+        // per MT_GT_CH * 64 units instead of one per 64.
+        for (int base = 0; base < n; base += MT_GT_CH * MT_WAVE) {
+            LaneArr<int> v[MT_GT_CH];
+#pragma unroll
+            for (int u = 0; u < MT_GT_CH; u++) {
+                const int b = base + u * MT_WAVE;
+                const int m = b >= n ? 0 : ((n - b) < MT_WAVE ? (n - b) : MT_WAVE);
+                const auto from = srcOf(b, m);
+                v[u] = wave_map(m, [&](int k) MT_LAM { return (int)text[own(from, k)]; });
+            }
             wave_sync();
-            wave_for(m, [&](int k) MT_LAM { text[dst + base + k] = (uint16_t)own(v, k); });
+#pragma unroll
+            for (int u = 0; u < MT_GT_CH; u++) {
+                const int b = base + u * MT_WAVE;
+                const int m = b >= n ? 0 : ((n - b) < MT_WAVE ? (n - b) : MT_WAVE);
+                wave_for(m, [&](int k) MT_LAM { text[dst + b + k] = (uint16_t)own(v[u], k); });
+            }
         }
         wave_sync();
     }
@@ -2423,19 +2447,41 @@ template <int RES, bool FULL = true> struct MtEngT {
             }
             pm &= propOk & ~wave_ballot(wave_map(span, [&](int t) MT_LAM { return own(lastNL1, t) != 0; }));
             // the granularity rule: prev.len <= 256 || seg.len <= 256 on the accumulated run
-            uint64_t walk = pm | (pm >> 1);
-            int P = 0, head = -1;
-            while (walk) {
-                const int k = __builtin_ctzll(walk);
-                walk &= walk - 1;
-                const int lk = wave_at(fl, k);
-                if (((pm >> k) & 1ull) && (P <= MT_GRAN || lk <= MT_GRAN)) { merged |= 1ull << k; P += lk; }
-                else {
-                    if (head >= 0) runLen = wave_set(runLen, head, P);
-                    head = k; P = lk;
+            const uint64_t bigF = wave_ballot(wave_map(span, [&](int t) MT_LAM {
+                return ((pm >> t) & 1ull) && own(fl, t) > MT_GRAN;
+            }));
+            if (!bigF) {
+                // every follower is short, so every pair merges whatever the run's length: the
+                // runs are the pairs' chains, and a head's length is a prefix-sum difference
+                merged = pm;
+                const uint64_t heads = (pm | (pm >> 1)) & ~pm;
+                const auto fl0 = wave_map(MT_WAVE, [&](int t) MT_LAM { return t < span ? own(fl, t) : 0; });
+                const auto S = wave_excl_scan(fl0);                      // units before lane t
+                const uint64_t mg = merged;
+                // S at the first lane past the run (runs end inside the span, 8 * nb <= 56 lanes)
+                const auto Se = wave_shfl(S, [mg](int t) MT_LAM {
+                    const uint64_t after = t < 63 ? (mg >> (t + 1)) : 0ull;
+                    const int e = t + 1 + __builtin_ctzll(~after);
+                    return e < 64 ? e : 63;
+                });
+                runLen = wave_map(span, [&](int t) MT_LAM {
+                    return ((heads >> t) & 1ull) ? own(Se, t) - own(S, t) : own(fl, t);
+                });
+            } else {
+                uint64_t walk = pm | (pm >> 1);
+                int P = 0, head = -1;
+                while (walk) {
+                    const int k = __builtin_ctzll(walk);
+                    walk &= walk - 1;
+                    const int lk = wave_at(fl, k);
+                    if (((pm >> k) & 1ull) && (P <= MT_GRAN || lk <= MT_GRAN)) { merged |= 1ull << k; P += lk; }
+                    else {
+                        if (head >= 0) runLen = wave_set(runLen, head, P);
+                        head = k; P = lk;
+                    }
                 }
+                if (head >= 0) runLen = wave_set(runLen, head, P);
             }
-            if (head >= 0) runLen = wave_set(runLen, head, P);
             // move the text, one run at a time (followers still linked: compaction keeps their text)
             for (uint64_t m = merged; m;) {
                 const int i0 = __builtin_ctzll(m);

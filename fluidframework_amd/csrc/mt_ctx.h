@@ -24,7 +24,7 @@ struct mt_ctx {
     std::string err;
     // device op batch (resident)
     struct DevBuf { void* p = nullptr; size_t cap = 0; };
-    DevBuf b_stage, b_pack_docs, b_pack_sz, b_pack_off, b_gencl, b_cursor, b_doc, b_off, b_rec, b_pay, b_rel, b_drec, b_dcount, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3,
+    DevBuf b_stage, b_pack_docs, b_pack_sz, b_pack_off, b_gencl, b_cursor, b_doc, b_off, b_rec, b_pay, b_pbase, b_rel, b_drec, b_dcount, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3,
            b_ld_meta, b_ld_seg, b_ld_pay, b_ld_plan, b_ld_poff, b_dtext, b_resume, b_start,
            b_q, b_qgrp, b_qout, b_qat, b_qlen, b_qoff, b_qtext;   // position queries (mt_get_containing_segment)
     MtOps ops{};

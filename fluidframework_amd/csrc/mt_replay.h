@@ -68,6 +68,8 @@ template <class Eng>
 MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t doc,
                                 const MtGen* g, int* lastRef, uint32_t o0) {
     const uint32_t o1 = ops.op_off[run + 1];
+    const unsigned long long pb = ops.pay_base ? uni64(ops.pay_base[run]) : 0ull;
+    const uint16_t* payR = ops.payload + pb;                  // this run's payload (pay_base: relative offsets)
     MtRng rng; rng.s = 0;
     const uint32_t nc = g ? (g->clients_per_run ? g->clients_per_run[run] : g->clients) : 0;
     if (g) {
@@ -127,11 +129,11 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
             if (e.curSeq >= sq) e.status |= MT_DS_ASSERT_SEQ;       // completeAndLogOp, MT/client.ts:482
             if (e.minSeq > ms) e.status |= MT_DS_ASSERT_MSN;        // MT/client.ts:484
             if (r < e.minSeq) e.status |= MT_DS_REFSEQ_BELOW_MSN;   // nacked by deli (deli/lambda.ts:302-318)
-            if (ty == MT_OP_INSERT && !(fl & MT_OPF_MARKER) && (uint64_t)poff + (uint64_t)plen > ops.payload_units)
+            if (ty == MT_OP_INSERT && !(fl & MT_OPF_MARKER) && pb + (uint64_t)poff + (uint64_t)plen > ops.payload_units)
                 e.status |= MT_DS_BAD_OP;
             if (e.status) break;
             const bool pre = ty == MT_OP_INSERT && !(fl & MT_OPF_MARKER) && plen <= MT_WAVE;
-            const auto pay = wave_map(pre ? plen : 0, [&](int k) MT_LAM { return (int)ops.payload[poff + (uint32_t)k]; });
+            const auto pay = wave_map(pre ? plen : 0, [&](int k) MT_LAM { return (int)payR[poff + (uint32_t)k]; });
             if (!(e.uValid && e.uRef == r && e.uCli == c)) e.computeU(r, c, true);
             e.mwPrefetch();                                      // long documents: warm zamboni's rows
             int q1 = p1, q2 = p2;
@@ -144,7 +146,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
             }
             if (ty == MT_OP_INSERT) {
                 const bool marker = (fl & MT_OPF_MARKER) != 0;
-                e.opInsert(q1, r, c, sq, ops.payload + poff, plen, marker, p2, (fl & MT_OPF_SEG_PROPS) ? pid : -1,
+                e.opInsert(q1, r, c, sq, payR + poff, plen, marker, p2, (fl & MT_OPF_SEG_PROPS) ? pid : -1,
                            (marker && (fl & MT_OPF_MARKER_ID)) ? (int)poff : -1, pay);
             } else if (ty == MT_OP_REMOVE) {
                 e.opRange(MT_MAP_REMOVE, q1, q2, r, c, sq, -1, false);

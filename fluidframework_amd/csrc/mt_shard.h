@@ -48,8 +48,8 @@ MT_HD unsigned long long mt_pack_rows_doc(const MtOps& ops, uint32_t run, uint32
 }
 
 // Receiver: rows [op_off[run], op_off[run+1]) into the resident batch (records and
-// payload slots; payload_off rewritten to the op's slot in this batch); returns the
-// checksum of the rows as received.
+// payload slots; payload_off rewritten to the op's slot relative to the run's payload base,
+// op_off[run] * L, which ops.pay_base holds); returns the checksum of the rows as received.
 MT_HD unsigned long long mt_unpack_rows_doc(const MtOps& ops, uint32_t run, uint32_t L, const unsigned long long* rows) {
     const unsigned long long o0 = ops.op_off[run], n = (unsigned long long)ops.op_off[run + 1] - o0;
     const unsigned long long W = 4 + L / 4;
@@ -73,7 +73,7 @@ MT_HD unsigned long long mt_unpack_rows_doc(const MtOps& ops, uint32_t run, uint
                         const unsigned long long w0 = in[j * W];
                         const uint32_t ty = (uint32_t)(w0 & 0xFF), fl = (uint32_t)((w0 >> 8) & 0xFF);
                         if (ty == MT_OP_INSERT && !(fl & MT_OPF_MARKER))
-                            w = (w & 0xFFFFFFFF00000000ULL) | (unsigned long long)(uint32_t)((o0 + j) * L);
+                            w = (w & 0xFFFFFFFF00000000ULL) | (unsigned long long)(uint32_t)(j * L);
                     }
                     rec[(o0 + j) * 4 + t] = w;
                 } else pay[(o0 + j) * (L / 4) + (t - 4)] = w;
