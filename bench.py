@@ -301,6 +301,7 @@ def run_config4(args, c, world, rank, local):
         return
     kern_s = float(np.mean(kms)) / 1e3
     achieved = bytes_per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
+    traffic = measured_traffic("config4", {"docs": n, "ops": ops}, REPLAY_KERNEL[args.residency])
     out = {
         "metric": "sequenced merge-tree ops applied/sec (whole node) + achieved HBM GB/s",
         "value": msgs * world * args.steps / dt, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
@@ -313,7 +314,8 @@ def run_config4(args, c, world, rank, local):
                    "parallelism": f"doc-sharded x{world}", "residency": args.residency,
                    "step": "mt_restore (device copy of the pre-built documents) + replay"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": REPLAY_KERNEL[args.residency],
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic[0] if traffic else None,
+                     "traffic_source": traffic[1] if traffic else None, "kernel": REPLAY_KERNEL[args.residency],
                      "kernel_ms": kern_s * 1e3, "bytes_per_launch": bytes_per_launch},
         "parity": "status words clean" if ok else "STATUS ERROR",
         "snapshot": {"docs": n, "ms": snap_ms, "digest_xor": f"{int(np.bitwise_xor.reduce(digs)):016x}"},
@@ -437,18 +439,22 @@ def run_config5(args, c, world, rank, local):
     total_msgs = int(sh.all_ops.sum())
     kern_s = float(np.mean(kms)) / 1e3
     achieved = bytes_per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
+    # the PMC passes run at N = 1 (rank 0 replays every document): per launch of that workload
+    traffic = measured_traffic("config5", {"docs": c["docs"], "ops": 0}, REPLAY_KERNEL[args.residency]) if world == 1 else None
     out = {
         "metric": "sequenced merge-tree ops applied/sec (whole node) + achieved HBM GB/s",
         "value": total_msgs * args.steps / dt, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int32",
         "data": "synthetic (device-generated sequenced op streams, SURVEY.md §8(d) config-5 rules)",
-        "config": {"workload": f"config5: {c['desc']}", "docs_per_gpu": c["docs"], "docs_total": total_docs,
+        "config": {"workload": f"config5: {c['desc']}".replace("131072 docs per GPU", f"{c['docs']} docs per GPU"),
+                   "docs_per_gpu": c["docs"], "docs_total": total_docs,
                    "msgs_total": total_msgs, "msgs_mean": total_msgs / total_docs,
                    "msgs_max": int(sh.all_ops.max()), "parallelism": f"doc-sharded x{world} (LPT)",
                    "residency": args.residency, "big_min_ops": big if args.residency == "blk" else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": REPLAY_KERNEL[args.residency] + " (rank 0)",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic[0] if traffic else None,
+                     "traffic_source": traffic[1] if traffic else None, "kernel": REPLAY_KERNEL[args.residency] + " (rank 0)",
                      "kernel_ms": kern_s * 1e3, "bytes_per_launch": bytes_per_launch},
         "parity": "status words clean on every rank" if int(bad[0].item()) == 0 else "STATUS ERROR",
         "exchange": {"docs_checked": int(bad[2].item()), "checksum_mismatch_docs": int(bad[1].item()),

@@ -58,6 +58,9 @@
 #ifndef MT_B_BLKS
 #define MT_B_BLKS 104
 #endif
+#ifndef MT_B_SLACK
+#define MT_B_SLACK 10                 // block residency: free blocks kept beyond 2 * height before each message
+#endif
 #define MT_B_BT 128                   // corrections-table slots (block ids < MT_B_BLKS)
 #define MT_B_U 64                     // U-set entries kept in LDS (the rest, if any, in HBM)
 #ifndef MT_B_HEAP
@@ -134,7 +137,7 @@ enum { MT_BIGF_NO_BCACHE = 1, MT_BIGF_NO_PREFETCH = 2, MT_BIGF_NO_TABLE = 4, MT_
 enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2, MT_RES_BIG = 3 };
 // Diagnostic builds keep per-document phase/event counters (prof[]) across binds;
 // product builds never load or store them (8 SGPR pairs fewer live in the replay loop).
-#if defined(MT_PROFILE) || defined(MT_PROFILE2) || defined(MT_PROFILE3) || defined(MT_PROFILE4) || defined(MT_BPC_STATS) || defined(MT_EVCOUNT) || defined(MT_EVCOUNT2)
+#if defined(MT_PROFILE) || defined(MT_PROFILE2) || defined(MT_PROFILE3) || defined(MT_PROFILE4) || defined(MT_BPC_STATS) || defined(MT_EVCOUNT3) || defined(MT_EVCOUNT) || defined(MT_EVCOUNT2)
 #define MT_KEEP_PROF 1
 #else
 #define MT_KEEP_PROF 0
@@ -977,11 +980,13 @@ template <int RES, bool FULL = true> struct MtEngT {
         if constexpr (BIG) return (lHeap - heapN) >= 4 && height + 3 <= MT_G_H;
         if constexpr (!BLKL) return true;
         // Block budget per message: the split + insert cascades allocate at most
-        // 2*height + 5 blocks; packParent regrowth (+2 per level at most, and rare)
-        // gets a fixed 12.  The largest growth measured over configs 2-3 in the host
-        // emulation was 2*height + 2.  Exceeding it would set MT_DS_OOM_BLOCKS (never
-        // silently wrong); mt_set_residency(ctx, 0, ...) avoids LDS entirely.
-        if constexpr (!LDS) return (lBlks - blkTop + blkFreeN) >= 2 * height + 17 && (lHeap - heapN) >= 4 &&
+        // 2*height + 5 blocks; packParent regrowth (+2 per level at most, and rare) gets
+        // MT_B_SLACK - 5 more.  The largest growth of a message (op and both zamboni calls)
+        // measured in the host emulation is 2*height + 2, on every one of 704 documents of
+        // configs 2 and 3 and lag-256/1,024 variants (tools/micro/block_growth.py,
+        // MT_EVCOUNT3).  Exceeding the budget would set MT_DS_OOM_BLOCKS (never silently
+        // wrong); mt_set_residency(ctx, 0, ...) avoids LDS entirely.
+        if constexpr (!LDS) return (lBlks - blkTop + blkFreeN) >= 2 * height + MT_B_SLACK && (lHeap - heapN) >= 4 &&
                                    height + 3 <= MT_L_H;
         return (lRows - rowTop + rfN) >= 4 && (lBlks - blkTop + blkFreeN) >= 6 * (height + 2) + 8 &&
                (lHeap - heapN) >= 4 && height + 3 <= MT_L_H;

@@ -83,6 +83,10 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
     // this message's capture reservation (FULL): released after the message, or after the
     // loop when an error ends the run mid-message
     unsigned long long resR = 0, resT = 0;
+#if defined(MT_EVCOUNT3) && !defined(__HIP_DEVICE_COMPILE__)
+    if (e.prof[0] == 0) e.prof[0] = 1000000 - 100;          // max growth - 2 * height, offset by 1e6
+    e.prof[3] = (unsigned long long)(e.blkTop - e.blkFreeN); e.prof[4] = (unsigned long long)e.height;
+#endif
     for (uint32_t i = o0; i < o1; i++) {
         e.curOp = i;
         if (Eng::kLds && !e.ldsHeadroom()) return i;
@@ -174,6 +178,14 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
             if (e.curSeq > sq) { e.status |= MT_DS_ASSERT_SEQ; break; }
             e.curSeq = sq;
             e.setMinSeq(ms);
+#if defined(MT_EVCOUNT3) && !defined(__HIP_DEVICE_COMPILE__)
+            {   // host emulation: blocks a message added (op and zamboni) beyond 2 * height at its start
+                const int used = e.blkTop - e.blkFreeN;
+                const long long g = (long long)used - (long long)e.prof[3] - 2ll * (long long)e.prof[4];
+                if (g > (long long)e.prof[0] - 1000000) e.prof[0] = (unsigned long long)(g + 1000000);
+                e.prof[3] = (unsigned long long)used; e.prof[4] = (unsigned long long)e.height;
+            }
+#endif
         }
         if (e.status) break;
         if constexpr (Eng::kFull) { if (resR) { e.dRelease(resR, resT); resR = resT = 0; } }
