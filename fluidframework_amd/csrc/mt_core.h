@@ -2303,7 +2303,8 @@ template <int RES, bool FULL = true> struct MtEngT {
 #pragma unroll
             for (int u = 0; u < MT_GT_CH; u++) {
                 const int b = base + u * MT_WAVE;
-                const int m = b >= n ? 0 : ((n - b) < MT_WAVE ? (n - b) : MT_WAVE);
+                if (b >= n) break;                                   // uniform: skips the piece scan too
+                const int m = (n - b) < MT_WAVE ? (n - b) : MT_WAVE;
                 const auto from = srcOf(b, m);
                 v[u] = wave_map(m, [&](int k) MT_LAM { return (int)text[own(from, k)]; });
             }
@@ -2311,7 +2312,8 @@ template <int RES, bool FULL = true> struct MtEngT {
 #pragma unroll
             for (int u = 0; u < MT_GT_CH; u++) {
                 const int b = base + u * MT_WAVE;
-                const int m = b >= n ? 0 : ((n - b) < MT_WAVE ? (n - b) : MT_WAVE);
+                if (b >= n) break;
+                const int m = (n - b) < MT_WAVE ? (n - b) : MT_WAVE;
                 wave_for(m, [&](int k) MT_LAM { text[dst + b + k] = (uint16_t)own(v[u], k); });
             }
         }
