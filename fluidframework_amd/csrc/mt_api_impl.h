@@ -16,6 +16,7 @@
 //   mtb_event_start / mtb_event_stop_ms
 #pragma once
 #include <algorithm>
+#include <chrono>
 #include <thread>
 #include <stdio.h>
 #include <stdlib.h>
@@ -814,10 +815,16 @@ static int mt_stage_docs(mt_ctx* c, uint32_t n, const uint32_t* docs, std::vecto
     mtb_h2d(c, c->b_pack_off.p, off.data(), 8ull * n);
     if ((rc = mtb_launch_pack(c, (const uint32_t*)c->b_pack_docs.p, (const uint64_t*)c->b_pack_off.p, (uint8_t*)c->b_stage.p, n,
                               epoch))) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
     if ((rc = mtb_sync(c))) return rc;
+    const auto t1 = std::chrono::steady_clock::now();
     uint8_t* host = mtb_host_stage(c, off[n] + 16);
     if (!host) { c->err = "pinned staging allocation failed"; return MT_E_OOM; }
     mtb_d2h(c, host, c->b_stage.p, off[n]);
+    if (getenv("MT_SNAP_TIMING"))
+        fprintf(stderr, "mt_stage_docs: %u docs, %.1f MB staged, pack kernel wait %.1f ms, host buffer + download %.1f ms\n", n,
+                off[n] / 1e6, std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
     views.resize(n);
     for (uint32_t i = 0; i < n; i++) {
         const MtStagedDoc sd = MtStagedDoc::at(host + off[i]);
@@ -886,11 +893,15 @@ int MT_FN(snapshot_digests)(mt_ctx* c, uint32_t n, const uint32_t* docs, const i
     // chunks of documents, so the staging buffers stay bounded however many documents
     // (a million Zipf documents stage ~20 GB)
     const uint32_t CH = 32768;
+    // MT_SNAP_TIMING=1: per-chunk stage / emit times on stderr (diagnostic)
+    static const bool timing = getenv("MT_SNAP_TIMING") != nullptr;
     for (uint32_t a = 0; a < n; a += CH) {
         const uint32_t m = (n - a) < CH ? (n - a) : CH;
         std::vector<MtSnapView> views;
+        const auto t0 = std::chrono::steady_clock::now();
         if ((rc = mt_stage_docs(c, m, docs + a, views))) return rc;
         if ((rc = mt_check_staged_status(c, m, docs + a, views))) return rc;
+        const auto t1 = std::chrono::steady_clock::now();
         const int th = (uint32_t)threads > m ? (int)m : threads;
         auto work = [&](int t) {
             for (uint32_t i = (uint32_t)t; i < m; i += (uint32_t)th) {
@@ -903,6 +914,12 @@ int MT_FN(snapshot_digests)(mt_ctx* c, uint32_t n, const uint32_t* docs, const i
         for (int t = 1; t < th; t++) pool.emplace_back(work, t);
         work(0);
         for (auto& t : pool) t.join();
+        if (timing) {
+            const auto t2 = std::chrono::steady_clock::now();
+            fprintf(stderr, "mt_snapshot_digests: docs %u..%u stage %.1f ms, emit+digest %.1f ms on %d threads\n", a, a + m,
+                    std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                    std::chrono::duration<double, std::milli>(t2 - t1).count(), th);
+        }
     }
     return MT_OK;
 }
