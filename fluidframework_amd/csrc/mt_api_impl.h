@@ -17,6 +17,7 @@
 #pragma once
 #include <algorithm>
 #include <chrono>
+#include <functional>
 #include <thread>
 #include <stdio.h>
 #include <stdlib.h>
@@ -796,7 +797,7 @@ static int mt_download_doc(mt_ctx* c, uint32_t d, MtHostDoc& h) {
 
 // Gather documents' live state into host memory with two kernels and one copy
 // (mt_pack.h); views[i] points into `host`.
-static int mt_stage_docs(mt_ctx* c, uint32_t n, const uint32_t* docs, std::vector<MtSnapView>& views) {
+static int mt_stage_docs(mt_ctx* c, uint32_t n, const uint32_t* docs, std::vector<MtSnapView>& views, int buf = 0) {
     views.clear();
     if (n == 0) return MT_OK;
     for (uint32_t i = 0; i < n; i++) if (docs[i] >= c->S.maxDocs) { c->err = "doc id out of range"; return MT_E_INVALID; }
@@ -818,7 +819,7 @@ static int mt_stage_docs(mt_ctx* c, uint32_t n, const uint32_t* docs, std::vecto
     const auto t0 = std::chrono::steady_clock::now();
     if ((rc = mtb_sync(c))) return rc;
     const auto t1 = std::chrono::steady_clock::now();
-    uint8_t* host = mtb_host_stage(c, off[n] + 16);
+    uint8_t* host = mtb_host_stage(c, off[n] + 16, buf);
     if (!host) { c->err = "pinned staging allocation failed"; return MT_E_OOM; }
     mtb_d2h(c, host, c->b_stage.p, off[n]);
     if (getenv("MT_SNAP_TIMING"))
@@ -847,6 +848,59 @@ static int mt_check_staged_status(mt_ctx* c, uint32_t n, const uint32_t* docs, c
         }
     return MT_OK;
 }
+// Documents staged in groups of at most MT_STAGE_BUDGET bytes (estimated from their headers:
+// every row, block, text unit and property set, an upper bound of the packed size), so the
+// pinned download buffers stay small (pinning a multi-GB buffer costs more than the copy) and
+// are reused group after group; fn(first, count, views) consumes each group while the next is
+// staged; a group holds a multiple of `mult` documents (whole rounds of the emitting threads).
+#define MT_STAGE_BUDGET (384ull << 20)
+typedef std::function<int(uint32_t, uint32_t, const std::vector<MtSnapView>&)> MtGroupFn;
+static int mt_staged_groups(mt_ctx* c, uint32_t n, const uint32_t* docs, const MtGroupFn& fn, uint32_t mult = 1) {
+    std::vector<MtDocHdr> h;
+    int rc = mt_read_hdrs(c, n, docs, h);
+    if (rc) return rc;
+    const char* bs = getenv("MT_STAGE_BUDGET");             // bytes per group (tests force small groups)
+    const uint64_t budget = bs ? strtoull(bs, nullptr, 10) : MT_STAGE_BUDGET;
+    auto groupEnd = [&](uint32_t a) {
+        uint64_t bytes = 0; uint32_t m = 0;
+        while (a + m < n && m < 32768) {
+            const MtDocHdr& d = h[a + m];
+            const uint64_t b = 48ull * (uint64_t)(d.rowTop > 0 ? d.rowTop : 0) + 64ull * (uint64_t)(d.blkTop > 0 ? d.blkTop : 0) +
+                               2ull * (uint64_t)(d.textTop > 0 ? d.textTop : 0) +
+                               (uint64_t)sizeof(MtPSet) * (uint64_t)(d.psetTop > 0 ? d.psetTop : 0) + 1024;
+            if (m > 0 && bytes + b > budget) break;
+            bytes += b; m++;
+        }
+        if (a + m < n && m > mult) m -= m % mult;             // whole rounds of the emitting threads
+        return a + m;
+    };
+    const bool timing = getenv("MT_SNAP_TIMING") != nullptr;
+    // double-buffered: group g+1 is staged (device pack + download into the other pinned
+    // buffer) while group g is emitted on the host threads
+    std::vector<MtSnapView> cur, nxt;
+    uint32_t a = 0, b = n ? groupEnd(0) : 0;
+    if (n && ((rc = mt_stage_docs(c, b - a, docs + a, cur, 0)) || (rc = mt_check_staged_status(c, b - a, docs + a, cur))))
+        return rc;
+    for (int buf = 0; a < n; buf ^= 1) {
+        const auto t0 = std::chrono::steady_clock::now();
+        int erc = MT_OK;
+        std::thread emit([&] { erc = fn(a, b - a, cur); });
+        const uint32_t b2 = b < n ? groupEnd(b) : b;
+        int src = MT_OK;
+        if (b < n && !(src = mt_stage_docs(c, b2 - b, docs + b, nxt, buf ^ 1))) src = mt_check_staged_status(c, b2 - b, docs + b, nxt);
+        const auto t1 = std::chrono::steady_clock::now();
+        emit.join();
+        if (timing)
+            fprintf(stderr, "mt_staged_groups: docs %u..%u emitted in %.1f ms beside staging the next %u in %.1f ms\n", a, b,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), b2 - b,
+                    std::chrono::duration<double, std::milli>(t1 - t0).count());
+        if (erc) return erc;
+        if (src) return src;
+        std::swap(cur, nxt);
+        a = b; b = b2;
+    }
+    return MT_OK;
+}
 // Client.snapshot (client.ts:923-956): SnapshotV1 or, with legacy set, SnapshotLegacy.
 static int mt_snapshot_blobs(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t* msn, const int32_t* seq,
                              uint64_t* digest, const char** arena, const uint64_t** blob_off,
@@ -854,19 +908,21 @@ static int mt_snapshot_blobs(mt_ctx* c, uint32_t n, const uint32_t* docs, const 
     if (!c) return MT_E_INVALID;
     int rc = MT_FN(update_seq)(c, n, docs, msn, seq);       // Client.snapshot: updateSeqNumbers first (client.ts:936)
     if (rc) return rc;
-    std::vector<MtSnapView> views;
-    if ((rc = mt_stage_docs(c, n, docs, views))) return rc;
-    if ((rc = mt_check_staged_status(c, n, docs, views))) return rc;
     c->snap_arena.clear(); c->blob_off.assign(1, 0); c->blob_first.assign(1, 0);
-    for (uint32_t i = 0; i < n; i++) {
-        auto dn = c->doc_clients.find(docs[i]);
-        std::vector<std::string> blobs = legacy ? mtsnap::snapshot_legacy_blobs(views[i], c->names)
-                                                : mtsnap::snapshot_blobs(views[i], c->names,
-                                                                         dn == c->doc_clients.end() ? nullptr : &dn->second);
-        if (digest) digest[i] = mtsnap::blobs_digest(blobs);
-        for (auto& b : blobs) { c->snap_arena += b; c->blob_off.push_back(c->snap_arena.size()); }
-        c->blob_first.push_back((uint32_t)(c->blob_off.size() - 1));
-    }
+    rc = mt_staged_groups(c, n, docs, [&](uint32_t a, uint32_t m, const std::vector<MtSnapView>& views) {
+        for (uint32_t j = 0; j < m; j++) {
+            const uint32_t i = a + j;
+            auto dn = c->doc_clients.find(docs[i]);
+            std::vector<std::string> blobs = legacy ? mtsnap::snapshot_legacy_blobs(views[j], c->names)
+                                                    : mtsnap::snapshot_blobs(views[j], c->names,
+                                                                             dn == c->doc_clients.end() ? nullptr : &dn->second);
+            if (digest) digest[i] = mtsnap::blobs_digest(blobs);
+            for (auto& b : blobs) { c->snap_arena += b; c->blob_off.push_back(c->snap_arena.size()); }
+            c->blob_first.push_back((uint32_t)(c->blob_off.size() - 1));
+        }
+        return (int)MT_OK;
+    });
+    if (rc) return rc;
     if (arena) *arena = c->snap_arena.data();
     if (blob_off) *blob_off = c->blob_off.data();
     if (blob_first) *blob_first = c->blob_first.data();
@@ -890,18 +946,9 @@ int MT_FN(snapshot_digests)(mt_ctx* c, uint32_t n, const uint32_t* docs, const i
     int rc = MT_FN(update_seq)(c, n, docs, msn, seq);
     if (rc) return rc;
     if (threads < 1) threads = 1;
-    // chunks of documents, so the staging buffers stay bounded however many documents
-    // (a million Zipf documents stage ~20 GB)
-    const uint32_t CH = 32768;
-    // MT_SNAP_TIMING=1: per-chunk stage / emit times on stderr (diagnostic)
-    static const bool timing = getenv("MT_SNAP_TIMING") != nullptr;
-    for (uint32_t a = 0; a < n; a += CH) {
-        const uint32_t m = (n - a) < CH ? (n - a) : CH;
-        std::vector<MtSnapView> views;
-        const auto t0 = std::chrono::steady_clock::now();
-        if ((rc = mt_stage_docs(c, m, docs + a, views))) return rc;
-        if ((rc = mt_check_staged_status(c, m, docs + a, views))) return rc;
-        const auto t1 = std::chrono::steady_clock::now();
+    // groups of documents (mt_staged_groups), so the staging buffers stay bounded however many
+    // documents (a million Zipf documents stage ~20 GB)
+    return mt_staged_groups(c, n, docs, [&](uint32_t a, uint32_t m, const std::vector<MtSnapView>& views) {
         const int th = (uint32_t)threads > m ? (int)m : threads;
         auto work = [&](int t) {
             for (uint32_t i = (uint32_t)t; i < m; i += (uint32_t)th) {
@@ -914,14 +961,8 @@ int MT_FN(snapshot_digests)(mt_ctx* c, uint32_t n, const uint32_t* docs, const i
         for (int t = 1; t < th; t++) pool.emplace_back(work, t);
         work(0);
         for (auto& t : pool) t.join();
-        if (timing) {
-            const auto t2 = std::chrono::steady_clock::now();
-            fprintf(stderr, "mt_snapshot_digests: docs %u..%u stage %.1f ms, emit+digest %.1f ms on %d threads\n", a, a + m,
-                    std::chrono::duration<double, std::milli>(t1 - t0).count(),
-                    std::chrono::duration<double, std::milli>(t2 - t1).count(), th);
-        }
-    }
-    return MT_OK;
+        return (int)MT_OK;
+    }, (uint32_t)threads);
 }
 
 int MT_FN(get_text)(mt_ctx* c, uint32_t n, const uint32_t* docs, const uint16_t** arena, const uint64_t** off) {

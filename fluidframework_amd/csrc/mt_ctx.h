@@ -43,7 +43,7 @@ struct mt_ctx {
     struct Stage { void* p = nullptr; size_t cap = 0; void* ev = nullptr; };
     Stage stage[2];
     int stage_k = 0;
-    void* dl_host = nullptr; size_t dl_cap = 0;   // pinned host buffer of document staging (downloads)
+    void* dl_host[2] = {nullptr, nullptr}; size_t dl_cap[2] = {0, 0};   // pinned host buffers of document staging (downloads)
     uint32_t stage_epoch = 0x7E000000u;            // marks of a staging's referenced property maps
     DevBuf b_batch;
     MtGen gen{};

@@ -106,7 +106,7 @@ static void mtb_fini(mt_ctx* c) {
         if (st.ev) (void)hipEventDestroy((hipEvent_t)st.ev);
         if (st.p) (void)hipHostFree(st.p);
     }
-    if (c->dl_host) (void)hipHostFree(c->dl_host);
+    for (int b = 0; b < 2; b++) if (c->dl_host[b]) (void)hipHostFree(c->dl_host[b]);
     if (c->ev0) (void)hipEventDestroy((hipEvent_t)c->ev0);
     if (c->ev1) (void)hipEventDestroy((hipEvent_t)c->ev1);
     if (c->stream2) { (void)hipStreamSynchronize((hipStream_t)c->stream2); (void)hipStreamDestroy((hipStream_t)c->stream2); }
@@ -141,15 +141,15 @@ static void mtb_stage_send(mt_ctx* c, void* dev, size_t n) {
     c->stage_k ^= 1;
 }
 // Pinned host buffer the document staging downloads into (reused, grown on demand).
-static uint8_t* mtb_host_stage(mt_ctx* c, size_t n) {
-    if (c->dl_cap < n) {
-        if (c->dl_host) (void)hipHostFree(c->dl_host);
-        c->dl_host = nullptr; c->dl_cap = 0;
+static uint8_t* mtb_host_stage(mt_ctx* c, size_t n, int buf) {
+    if (c->dl_cap[buf] < n) {
+        if (c->dl_host[buf]) (void)hipHostFree(c->dl_host[buf]);
+        c->dl_host[buf] = nullptr; c->dl_cap[buf] = 0;
         const size_t cap = n + n / 4 + 4096;
-        if (hipHostMalloc(&c->dl_host, cap, hipHostMallocDefault) != hipSuccess) { c->dl_host = nullptr; return nullptr; }
-        c->dl_cap = cap;
+        if (hipHostMalloc(&c->dl_host[buf], cap, hipHostMallocDefault) != hipSuccess) { c->dl_host[buf] = nullptr; return nullptr; }
+        c->dl_cap[buf] = cap;
     }
-    return (uint8_t*)c->dl_host;
+    return (uint8_t*)c->dl_host[buf];
 }
 static int mtb_sync(mt_ctx* c) {
     hipError_t e = hipStreamSynchronize((hipStream_t)c->stream);

@@ -12,7 +12,7 @@
 #include "../../fluidframework_amd/csrc/mt_shard.h"
 
 static int mtb_init(mt_ctx*) { return 0; }
-static void mtb_fini(mt_ctx* c) { for (auto& st : c->stage) free(st.p); free(c->dl_host); }
+static void mtb_fini(mt_ctx* c) { for (auto& st : c->stage) free(st.p); free(c->dl_host[0]); free(c->dl_host[1]); }
 static int mtb_malloc(void** p, size_t n) { *p = calloc(1, n ? n : 16); return *p ? 0 : 1; }
 static void mtb_free(void* p) { free(p); }
 static void mtb_memset(void* p, int v, size_t n) { memset(p, v, n); }
@@ -20,9 +20,9 @@ static void mtb_h2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n)
 static void mtb_d2h(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static void mtb_d2d(mt_ctx*, void* d, const void* s, size_t n) { memcpy(d, s, n); }
 static int mtb_sync(mt_ctx*) { return MT_OK; }
-static uint8_t* mtb_host_stage(mt_ctx* c, size_t n) {
-    if (c->dl_cap < n) { free(c->dl_host); c->dl_host = malloc(n); c->dl_cap = c->dl_host ? n : 0; }
-    return (uint8_t*)c->dl_host;
+static uint8_t* mtb_host_stage(mt_ctx* c, size_t n, int buf) {
+    if (c->dl_cap[buf] < n) { free(c->dl_host[buf]); c->dl_host[buf] = malloc(n); c->dl_cap[buf] = c->dl_host[buf] ? n : 0; }
+    return (uint8_t*)c->dl_host[buf];
 }
 static void* mtb_stage_get(mt_ctx* c, size_t n) {
     mt_ctx::Stage& st = c->stage[c->stage_k];

@@ -85,6 +85,17 @@ def test_emu_matches_oracle(cfg):
     compare(batch, props, 4)
 
 
+def test_emu_snapshots_in_staging_groups_match_oracle(monkeypatch):
+    """Snapshots staged one document per group (MT_STAGE_BUDGET=1: every group is staged into
+    the other pinned buffer while the last one is emitted) equal the oracle's."""
+    monkeypatch.setenv("MT_STAGE_BUDGET", "1")
+    props = ann_props()
+    p = gen_params(seed=12, n_docs=5, **CONFIGS["cfg3"])
+    batch, st, _ = generate(p, props)
+    assert st == [0] * 5
+    compare(batch, props, 5)
+
+
 # LDS residency hand-over: tiny LDS caps make documents leave LDS mid-run (at
 # different ops, with different pools the binding one) and finish from HBM;
 # (0, ...) runs the HBM-pool kernel alone.  Results must not change.
