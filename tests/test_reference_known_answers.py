@@ -512,3 +512,30 @@ def test_newline_merge_on_emulation():
 @pytest.mark.gpu
 def test_newline_merge_on_gpu():
     check_newline_merge(GPU)
+
+
+# ---- a range op that starts past the end of its author's view (round-3 advisor item) --------
+def check_range_past_end(factory, residency):
+    """A remove and an annotate whose start lies past the length in the author's view map no
+    segment (mapRange finds none: the op is a no-op); the range walk's path resume must not
+    reuse the previous op's path for the end then.  Under block (2) and all-HBM (0) residency."""
+    def fac(n, **kw):
+        e = factory(n, **kw)
+        e.set_residency(residency)
+        return e
+    msgs = [msg("A", 1, 0, 0, ins(3, "XY")), msg("B", 2, 1, 0, rem(1, 4)),
+            msg("A", 3, 2, 1, rem(20, 24)), msg("B", 4, 3, 2, ann(40, 44, {"k": 1})),
+            msg("A", 5, 4, 3, rem(12, 15)), msg("B", 6, 5, 4, ins(2, "z")), msg("A", 7, 6, 5, rem(0, 2))]
+    od, c = run_both(fac, msgs, load_first=HW_CHARS)
+    header_now(od, c)
+
+
+@pytest.mark.parametrize("residency", [2, 0])
+def test_range_past_end_on_emulation(residency):
+    check_range_past_end(emu_engine, residency)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("residency", [2, 0])
+def test_range_past_end_on_gpu(residency):
+    check_range_past_end(GPU, residency)
