@@ -71,7 +71,7 @@
 // MT_G_U U-set entries with their ancestor chains in LDS (~68 KB: two documents per CU),
 // rows and blocks in HBM.  Meant for launches with few documents per CU.
 #ifndef MT_G_U
-#define MT_G_U 640
+#define MT_G_U 768
 #endif
 #ifndef MT_G_HEAP
 #define MT_G_HEAP 2046
@@ -122,17 +122,17 @@ enum { MT_BIGF_NO_BCACHE = 1, MT_BIGF_NO_PREFETCH = 2, MT_BIGF_NO_TABLE = 4, MT_
 #ifndef MT_G_HT
 #define MT_G_HT 4096
 #endif
-// Parent table of the long-document residency: block id -> parent in LDS, open addressing
-// (linear probing, 2,048 slots, cleared when 3/4 full), so htBuild's bottom-up passes read the
-// parents of the blocks it saw for earlier U sets, and of the blocks the last walks passed
-// through, from LDS instead of HBM.  Every write of a block's parent field updates the entry
-// (bpPut); a freed block's entry says "unknown" (bpDrop); bind, open and snapshot load clear it.
+// Parent cache of the long-document residency: block id -> parent in LDS, direct-mapped, one
+// dword per entry (tag = id >> MT_G_BPL in bits 20..31, parent + 1 in bits 0..19), so htBuild's
+// bottom-up passes read the parents of the blocks it saw for the last U sets from LDS instead
+// of HBM.  Every write of a block's parent field updates it (bpPut / bpDrop); documents with
+// 2^20 blocks or more run without it.
 #ifndef MT_G_BPC
 #define MT_G_BPC 1
 #endif
 #define MT_G_BPL 11
 #define MT_G_BP (1 << MT_G_BPL)
-#define MT_BP_UNKNOWN ((int)0x80000001)
+#define MT_BP_EMPTY 0xFFFFFFFFu
 #define MT_G_HTN (MT_G_HT * 3 / 4)
 enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2, MT_RES_BIG = 3 };
 // Diagnostic builds keep per-document phase/event counters (prof[]) across binds;
@@ -190,8 +190,9 @@ enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2, MT_RES_BIG = 3 };
 #define MT_ZE(i, v)
 #define MT_ZC(i)
 #endif
-// Parent-table statistics (host-emulation diagnostic builds only, -DMT_BPC_STATS): 0 lookups,
-// 1 hits, 2 misses (absent), 3 misses (entry unknown), 4 slots claimed, 5 entries dropped.
+// Parent-cache statistics (host-emulation diagnostic builds only, -DMT_BPC_STATS): 0 lookups,
+// 1 hits, 2 misses on an empty slot, 3 misses on another block's entry, 4 puts over another
+// block's entry, 5 drops of a live entry.
 #if defined(MT_BPC_STATS) && !defined(__HIP_DEVICE_COMPILE__)
 #define MT_BS(i) prof[i] += 1
 #else
@@ -408,8 +409,7 @@ struct __attribute__((aligned(16))) MtLdsBig {
     int sid[MT_G_STG], sdel[MT_G_STG], spf[MT_G_STG];
     int htk[MT_G_HT], htv[MT_G_HT];   // corrections table: block id (MT_BC_EMPTY: free), Σ delta
     uint16_t hlist[MT_G_HT];          // occupied slots in insertion (level) order
-    int bpk[MT_G_BP], bpv[MT_G_BP];   // parent table (MT_G_BPC): block id (MT_BC_EMPTY: free), parent
-    int bpN;                          // claimed slots
+    uint32_t bpc[MT_G_BP];            // parent cache (MT_G_BPC)
     struct Job {                      // a job wave 0 posts to the workgroup (mwRun / mwPost)
         int op, r, c, r0, n, H, minSeq, heapN;
         MtRow* R; int* win; MtBlk* blk; int* uanc; uint16_t* text;
@@ -804,80 +804,53 @@ template <int RES, bool FULL = true> struct MtEngT {
         return blkTop++;
     }
     MT_HD void freeBlock(int id) { bk(id).parent = blkFree; bk(id).n = -1; blkFree = id; blkFreeN++; bpDrop(id); }
-    // The parent table (MT_RES_BIG, MT_G_BPC): bpPut after every write of a block's parent field,
+    // The parent cache (MT_RES_BIG, MT_G_BPC): bpPut after every write of a block's parent field,
     // bpDrop when the field stops being a parent (free list), bpReset when block ids are reassigned.
-    MT_HD static unsigned bpHash(int b) { return ((unsigned)b * 2654435761u) >> (32 - MT_G_BPL); }
-    // Lane-level: the slot holding b, or the empty slot where it would go (found = false).
-    MT_HD int bpFind(int b, bool& found) const {
-        const MtLdsBig& G = mt_ldsg();
-        unsigned sl = bpHash(b);
-        for (int i = 0; i < MT_G_BP; i++) {
-            const int k = G.bpk[sl];
-            if (k == b) { found = true; return (int)sl; }
-            if (k == MT_BC_EMPTY) { found = false; return (int)sl; }
-            sl = (sl + 1) & (MT_G_BP - 1);
-        }
-        found = false; return -1;
-    }
-    // Lane-level insert or update (lanes may race on one key: they write the same parent).
-    MT_HD void bpSet(int b, int p) {
-        MtLdsBig& G = mt_ldsg();
-        unsigned sl = bpHash(b);
-        for (int i = 0; i < MT_G_BP; i++) {
-            const int old = lds_cas(&G.bpk[sl], MT_BC_EMPTY, b);
-            if (old == MT_BC_EMPTY || old == b) {
-                G.bpv[sl] = p;
-                if (old == MT_BC_EMPTY) { MT_BS(4); lds_add(&G.bpN, 1); }
-                return;
-            }
-            sl = (sl + 1) & (MT_G_BP - 1);
-        }
-    }
+    MT_HD static uint32_t bpPack(int b, int p) { return ((uint32_t)(b >> MT_G_BPL) << 20) | (uint32_t)(p + 1); }
     MT_HD void bpPut(int b, int p) {
-        if constexpr (BIG) { if (MT_G_BPC && bpOn) bpSet(b, p); }
+        if constexpr (BIG) {
+            if (MT_G_BPC && bpOn) {
+                uint32_t& e = mt_ldsg().bpc[b & (MT_G_BP - 1)];
+                if (e != MT_BP_EMPTY && (e >> 20) != (uint32_t)(b >> MT_G_BPL)) MT_BS(4);
+                e = bpPack(b, p);
+            }
+        }
     }
     MT_HD void bpDrop(int b) {
         if constexpr (BIG) {
             if (MT_G_BPC && bpOn) {
-                bool f; const int sl = bpFind(b, f);
-                if (f) { MT_BS(5); mt_ldsg().bpv[sl] = MT_BP_UNKNOWN; }
+                uint32_t& e = mt_ldsg().bpc[b & (MT_G_BP - 1)];
+                if ((e >> 20) == (uint32_t)(b >> MT_G_BPL)) MT_BS(5);
+                e = MT_BP_EMPTY;
             }
         }
     }
     MT_HD void bpReset() {
         if constexpr (BIG) {
             if (MT_G_BPC && bpOn) {
-                MtLdsBig& G = mt_ldsg();
                 for (int base = 0; base < MT_G_BP; base += MT_WAVE)
-                    wave_for(MT_WAVE, [&](int k) MT_LAM { G.bpk[base + k] = MT_BC_EMPTY; });
-                G.bpN = 0;
+                    wave_for(MT_WAVE, [&](int k) MT_LAM { mt_ldsg().bpc[base + k] = MT_BP_EMPTY; });
                 wave_sync();
             }
         }
     }
-    // Clears the table once it is 3/4 full (linear probing stays short); the next lookups refill it.
-    MT_HD void bpTrim() {
-        if constexpr (BIG) { if (MT_G_BPC && bpOn && uni(mt_ldsg().bpN) > MT_G_BP * 3 / 4) bpReset(); }
-    }
-    // bk(b).parent, through the parent table when it is kept (a miss fills the entry).
+    // bk(b).parent, through the parent cache when it is kept (a miss fills the entry).
     MT_HD int bkParent(int b) {
         if constexpr (BIG) {
             if (MT_G_BPC && bpOn) {
+                uint32_t& e = mt_ldsg().bpc[b & (MT_G_BP - 1)];
+                const uint32_t v = e;
                 MT_BS(0);
-                bool f; const int sl = bpFind(b, f);
-                if (f) {
-                    const int v = mt_ldsg().bpv[sl];
-                    if (v != MT_BP_UNKNOWN) {
-                        MT_BS(1);
+                if ((v >> 20) == (uint32_t)(b >> MT_G_BPL)) {
+                    MT_BS(1);
 #if defined(MT_BPC_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
-                        if (v != bk(b).parent) abort();                    // host emulation: a stale entry
+                    if ((int)(v & 0xFFFFFu) - 1 != bk(b).parent) abort();     // host emulation: a stale entry
 #endif
-                        return v;
-                    }
+                    return (int)(v & 0xFFFFFu) - 1;
                 }
-                if (f) MT_BS(3); else MT_BS(2);
+                if (v == MT_BP_EMPTY) MT_BS(2); else MT_BS(3);
                 const int p = bk(b).parent;
-                bpSet(b, p);
+                e = bpPack(b, p);
                 return p;
             }
         }
@@ -1398,7 +1371,6 @@ template <int RES, bool FULL = true> struct MtEngT {
         }
         hlistN = 0;
         wave_sync();
-        bpTrim();
         if (nU > MT_G_HTN) return false;
         forU([&](auto inL, int base, int m) MT_LAM {
             constexpr bool L = decltype(inL)::value;
@@ -1427,18 +1399,9 @@ template <int RES, bool FULL = true> struct MtEngT {
 #if defined(MT_PROFILE4)
                 MT_UC(6, m);
                 if (bpOn) MT_UC(7, wave_count(wave_map(m, [&](int k) MT_LAM {
-                    bool f; const int sl = bpFind(G.htk[own(ch, k)], f);
-                    return !f || G.bpv[sl] == MT_BP_UNKNOWN;
+                    const int b = G.htk[own(ch, k)];
+                    return (G.bpc[b & (MT_G_BP - 1)] >> 20) != (uint32_t)(b >> MT_G_BPL);
                 })));
-#endif
-#if defined(MT_BPC_STATS) && !defined(__HIP_DEVICE_COMPILE__)
-                if (bpOn) {                                   // levels, and levels where some lookup misses
-                    MT_BS(7);
-                    if (wave_count(wave_map(m, [&](int k) MT_LAM {
-                            bool f; const int sl = bpFind(G.htk[own(ch, k)], f);
-                            return !f || G.bpv[sl] == MT_BP_UNKNOWN;
-                        }))) MT_BS(6);
-                }
 #endif
                 const auto par = wave_map(m, [&](int k) MT_LAM { return bkParent(G.htk[own(ch, k)]); });
                 const auto val = wave_map(m, [&](int k) MT_LAM { return G.htv[own(ch, k)]; });
@@ -2111,12 +2074,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             if (j >= 0) {
                 const int pj = p - wave_at(pre, j);
                 if (interior) {
-                    sc->pathJ[L] = j; L++;
-                    const int pb = B;
-                    B = wave_at(ch, j); p = pj;
-                    // every block a walk passes: the rows it reaches join the window, and htBuild asks
-                    // for their ancestors soon
-                    if constexpr (BIG) wave_for(1, [&](int) MT_LAM { bpPut(B, pb); });
+                    sc->pathJ[L] = j; L++; B = wave_at(ch, j); p = pj;
                     if (narrow && h.height > 1) lsN = narrowU(lsN, h.height - 1, B);
                     if (kpre) ch = kidRec(r0, r1, j, h, B); else ch = blkLoad(B, h);
                     continue;

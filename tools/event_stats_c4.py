@@ -34,7 +34,7 @@ if flag == "MT_EVCOUNT":
           f"win/call {tot[2]/max(tot[0],1):.1f}  heapGet/msg {tot[3]/msgs:.3f}  siftLevels/get {tot[4]/max(tot[3],1):.2f}  "
           f"walkLevels/msg {tot[5]/msgs:.2f}  blockSplits/msg {tot[6]/msgs:.3f}  heapN/get {tot[7]/max(tot[3],1):.0f}")
 elif flag == "MT_BPC_STATS":
-    names = ["lookups", "hits", "miss absent", "miss unknown", "slots claimed", "drops", "levels missing", "levels"]
+    names = ["lookups", "hits", "miss empty", "miss other", "put evicts", "drops live"]
     print(" ".join(f"{nm}={tot[i]/msgs:.2f}" for i, nm in enumerate(names)))
 else:
     names = ["packParent", "updatePathLens levels", "copyText units", "copyText calls", "textGC", "splitRow",
