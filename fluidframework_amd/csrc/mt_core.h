@@ -1100,16 +1100,28 @@ template <int RES, bool FULL = true> struct MtEngT {
     // and its U delta (perspective length - observer length).
     MT_HD WinI winEntry(int s, int r, int c) const {
         WinI w; w.id = s;
+#if MT_SCOUR_QUADS
+        // the row as three 16-byte loads (len seq rseq meta | toff props parent tcap | ovl rcl mid)
+        const MtQ16a q0 = ((const MtQ16a*)&row(s))[0], q1 = ((const MtQ16a*)&row(s))[1], q2 = ((const MtQ16a*)&row(s))[2];
+        const uint32_t mt = q0.w;
+        const int sq = (int)q0.y, rs = (int)q0.z, ln = (int)q0.x;
+        w.parent = (int)q1.z;
+        const unsigned long long ovl = (unsigned long long)q2.x | ((unsigned long long)q2.y << 32);
+        const uint32_t rcl = q2.z;
+#else
         const uint32_t mt = row(s).meta;
-        const bool removed = (mt & MT_M_REMOVED) != 0;
-        const int sq = row(s).seq, rs = row(s).rseq;
+        const int sq = row(s).seq, rs = row(s).rseq, ln = row(s).len;
         w.parent = row(s).parent;
+        const unsigned long long ovl = row(s).ovl;
+        const uint32_t rcl = row(s).rcl;
+#endif
+        const bool removed = (mt & MT_M_REMOVED) != 0;
         const bool linked = w.parent >= 0;
         w.live = linked && (sq > minSeq || (removed && rs > minSeq));
         w.recycle = !linked && !(mt & MT_M_HREF);
-        const bool vr = vis_rc(sq, mt, rs, row(s).rcl, row(s).ovl, r, c, ovx, ovxN, s);
+        const bool vr = vis_rc(sq, mt, rs, rcl, ovl, r, c, ovx, ovxN, s);
         const bool vo = !removed;
-        w.delta = w.live ? ((vr ? row(s).len : 0) - (vo ? row(s).len : 0)) : 0;
+        w.delta = w.live ? ((vr ? ln : 0) - (vo ? ln : 0)) : 0;
         return w;
     }
     // One 64-entry chunk of the window scan, in order: compaction of live entries (prune),
