@@ -1734,10 +1734,32 @@ template <int RES, bool FULL = true> struct MtEngT {
             node = B; B = h.parent; leaf = false;
         }
     }
-    // A leaf's rows under (r, c); their meta and props come back from the same round trip.
-    MT_HD LaneArr<ChildL> leafLens(const LaneArr<int>& ch, int n, int r, int c, LaneArr<uint32_t>& lm, LaneArr<int>& lp) {
+    // A leaf's rows under (r, c); their meta, props and cachedLength come back from the same
+    // round trip.
+    MT_HD LaneArr<ChildL> leafLens(const LaneArr<int>& ch, int n, int r, int c, LaneArr<uint32_t>& lm, LaneArr<int>& lp,
+                                   LaneArr<int>& lr) {
+#if MT_SCOUR_QUADS
+        // each row as three 16-byte loads (len seq rseq meta | toff props parent tcap | ovl rcl mid)
+        const auto q0 = wave_map(n, [&](int j) MT_LAM { return ((const MtQ16a*)&row(own(ch, j)))[0]; });
+        const auto q1 = wave_map(n, [&](int j) MT_LAM { return ((const MtQ16a*)&row(own(ch, j)))[1]; });
+        const auto q2 = wave_map(n, [&](int j) MT_LAM { return ((const MtQ16a*)&row(own(ch, j)))[2]; });
+        lm = wave_map(n, [&](int j) MT_LAM { return own(q0, j).w; });
+        lp = wave_map(n, [&](int j) MT_LAM { return (int)own(q1, j).y; });
+        lr = wave_map(n, [&](int j) MT_LAM { return (int)own(q0, j).x; });
+        return wave_map(n, [&](int j) MT_LAM {
+            const MtQ16a a = own(q0, j), x = own(q2, j);
+            const uint32_t mt = a.w;
+            const int rs = (int)a.z;
+            const unsigned long long ovl = (unsigned long long)x.x | ((unsigned long long)x.y << 32);
+            ChildL o;
+            o.len = vis_rc((int)a.y, mt, rs, x.z, ovl, r, c, ovx, ovxN, own(ch, j)) ? (int)a.x : 0;
+            o.tie = !((mt & MT_M_REMOVED) && rs <= r);     // breakTie (MT/mergeTree.ts:2270-2292)
+            return o;
+        });
+#else
         lm = wave_map(n, [&](int j) MT_LAM { return row(own(ch, j)).meta; });
         lp = wave_map(n, [&](int j) MT_LAM { return row(own(ch, j)).props; });
+        lr = wave_map(n, [&](int j) MT_LAM { return row(own(ch, j)).len; });
         return wave_map(n, [&](int j) MT_LAM {
             const int s = own(ch, j);
             const uint32_t mt = own(lm, j);
@@ -1750,14 +1772,15 @@ template <int RES, bool FULL = true> struct MtEngT {
             o.tie = !((mt & MT_M_REMOVED) && rs <= r);
             return o;
         });
+#endif
     }
     // Perspective lengths of block B's children (nodeLength, MT/mergeTree.ts:1652-1692).
     // lsN >= 0 (MT_RES_BIG descents): only the lsN U entries listed in ulist lie under B.
     MT_HD LaneArr<ChildL> childLens(int B, const BlkH& h, const LaneArr<int>& ch, int r, int c,
                                     bool haveLen = false, const LaneArr<int>& kl = LaneArr<int>{}, int lsN = -1) {
         if (h.height == 0) {
-            LaneArr<uint32_t> lm; LaneArr<int> lp;
-            return leafLens(ch, h.n, r, c, lm, lp);
+            LaneArr<uint32_t> lm; LaneArr<int> lp, lr;
+            return leafLens(ch, h.n, r, c, lm, lp, lr);
         }
         if constexpr (BT) {                              // the children's corrections from the table
             return wave_map(h.n, [&](int j) MT_LAM {
@@ -2779,8 +2802,8 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int B = wave_at(fB, L);
             BlkH h;
             auto ch = blkLoad(B, h);
-            LaneArr<uint32_t> lm{}; LaneArr<int> lp{};
-            auto cl = h.height == 0 ? leafLens(ch, h.n, r, c, lm, lp) : childLens(B, h, ch, r, c);
+            LaneArr<uint32_t> lm{}; LaneArr<int> lp{}, lr{};
+            auto cl = h.height == 0 ? leafLens(ch, h.n, r, c, lm, lp, lr) : childLens(B, h, ch, r, c);
             auto lens = wave_map(h.n, [&](int j) MT_LAM { return own(cl, j).len; });
             const int j0 = wave_at(fJ, L);
             auto lensFrom = wave_map(h.n, [&](int j) MT_LAM { return j >= j0 ? own(lens, j) : 0; });
@@ -2816,7 +2839,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                             row(s).meta = mt | MT_M_REMOVED;
                             row(s).rcl = (uint32_t)c;
                             row(s).rseq = sq;
-                            return row(s).len;
+                            return own(lr, j);
                         });
                         obsDelta = -wave_sum8(nd);
                         wave_sync();

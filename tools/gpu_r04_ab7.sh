@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 4 pass 7: the GPU suite, then configs 2-5 (window entries read as row quads; the
+# Round 4 pass 7: the GPU suite, then configs 2-5 (window entries and leaf lengths read as row quads; the
 # direct-mapped parent cache back; snapshot staging groups in whole thread rounds).
 set -o pipefail
-OUT=gpurun_out/r04_ab7; mkdir -p $OUT
+OUT=gpurun_out/${OUTDIR:-r04_ab7}; mkdir -p $OUT
 export PYTHONUNBUFFERED=1
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/gpu_suite.log 2>&1
 rc=$?; echo "suite rc=$rc"; tail -2 $OUT/gpu_suite.log; [ $rc -eq 0 ] || exit $rc
