@@ -3090,12 +3090,28 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (status) return;
         const int L = marker ? 1 : plen;
         if (L > 0) {
-            // the text first: compaction (textGC, inside textAlloc) scans rows up to rowTop, so
-            // the new row is allocated after it and written whole, in one pass
-            int t0 = refType;
-            if (!marker) {
-                t0 = textAlloc(plen);
+            const int n = allocRow();
+            if (n < 0) return;
+            // payloads up to 64 units are already in lanes: flag text without a newline
+            const bool nonl = MT_NONL && !marker && plen <= MT_WAVE &&
+                              wave_count(wave_map(plen, [&](int k) MT_LAM { return own(pay, k) == (int)'\n'; })) == 0;
+            const uint32_t m0 = (uint32_t)c | (marker ? MT_M_MARKER : 0u) | (nonl ? MT_M_NONL : 0u);
+            row(n).len = L; row(n).seq = sq; row(n).rseq = MT_NOREM;
+            row(n).meta = m0;
+            row(n).ovl = 0ull; row(n).parent = -1; row(n).rcl = 0u;
+            row(n).mid = markerId >= 0 ? markerId + 1 : 0;
+            if (markerId >= 0) {                       // mapIdToSegment before the walk (MT/mergeTree.ts:2218-2222)
+                if (markerId >= midCap) { status |= MT_DS_UNSUPPORTED; return; }
+                midt[markerId] = n;
+            }
+            row(n).props = segProps >= 0 ? newPropMap(segProps) : -1;
+            row(n).tcap = marker ? 0 : plen;
+            if (marker) row(n).toff = refType;
+            else {
+                row(n).parent = -1;                                  // not yet linked: excluded from compaction
+                const int t0 = textAlloc(plen);
                 if (t0 < 0) return;
+                row(n).toff = t0;
                 if (plen <= MT_WAVE) wave_for(plen, [&](int k) MT_LAM { text[t0 + k] = (uint16_t)own(pay, k); });
                 else {
                     for (int base = 0; base < plen; base += MT_WAVE) {
@@ -3105,28 +3121,6 @@ template <int RES, bool FULL = true> struct MtEngT {
                 }
                 c_ins += (uint64_t)plen;
             }
-            const int n = allocRow();
-            if (n < 0) return;
-            // payloads up to 64 units are already in lanes: flag text without a newline
-            const bool nonl = MT_NONL && !marker && plen <= MT_WAVE &&
-                              wave_count(wave_map(plen, [&](int k) MT_LAM { return own(pay, k) == (int)'\n'; })) == 0;
-            const uint32_t m0 = (uint32_t)c | (marker ? MT_M_MARKER : 0u) | (nonl ? MT_M_NONL : 0u);
-            if (markerId >= 0) {                       // mapIdToSegment before the walk (MT/mergeTree.ts:2218-2222)
-                if (markerId >= midCap) { status |= MT_DS_UNSUPPORTED; return; }
-                midt[markerId] = n;
-            }
-            const int props = segProps >= 0 ? newPropMap(segProps) : -1;
-            // the row in one pass, lane k storing quad k: len seq rseq meta | toff props parent
-            // tcap | ovl rcl mid (parent -1: not yet linked, excluded from compaction)
-            const uint32_t mid = markerId >= 0 ? (uint32_t)(markerId + 1) : 0u, tcap = marker ? 0u : (uint32_t)plen;
-            wave_for(3, [&](int k) MT_LAM {
-                MtQ16a v;
-                v.x = k == 0 ? (uint32_t)L : (k == 1 ? (uint32_t)t0 : 0u);
-                v.y = k == 0 ? (uint32_t)sq : (k == 1 ? (uint32_t)props : 0u);
-                v.z = k == 0 ? (uint32_t)MT_NOREM : (k == 1 ? 0xFFFFFFFFu : 0u);
-                v.w = k == 0 ? m0 : (k == 1 ? tcap : mid);
-                ((MtQ16a*)&row(n))[k] = v;
-            });
             wave_sync();
             MT_PB(t1);
             landB = -1;
