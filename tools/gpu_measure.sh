@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 4 measurement: bench lines with the CPU baseline and the widened oracle parity samples
+# Measurement pass: bench lines with the CPU baseline and the widened oracle parity samples
 # (config 4: all 256 documents; config 5: 4096 documents) and the snapshot times.
-# usage: tools/gpu_r04_measure.sh <outdir under gpurun_out> [configs...]
+# usage: tools/gpu_measure.sh <outdir under gpurun_out> [configs...]
 set -o pipefail
 O=gpurun_out/${1:-r04m}; shift
 CFGS=${@:-config3 config4 config5}
