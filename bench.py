@@ -122,6 +122,15 @@ def measured_traffic(cfg_name, c, kernel):
     return best
 
 
+def partition_of(args, c):
+    """(min_ops, cus) of --partition MIN:CUS (or the config's default), None when off."""
+    spec = args.partition if args.partition else c.get("partition", "")
+    if not spec or spec == "off":
+        return None
+    a, b = spec.split(":")
+    return int(a), int(b)
+
+
 def caps_for(c):
     ops = c["ops"]
     return dict(rows_per_doc=3 * ops + 64, blocks_per_doc=ops + 64, heap_per_doc=2 * ops + 64,
@@ -403,6 +412,9 @@ def run_config5(args, c, world, rank, local):
     big = c.get("big_min_ops", 0) if args.big_min_ops < 0 else args.big_min_ops
     if args.residency == "blk" and big:
         eng.set_size_class(big)
+    part = partition_of(args, c)
+    if args.residency == "blk" and part:
+        eng.set_partition(*part)
     my_msgs = int(sh.ops.sum())
     for _ in range(args.warmup):
         sh.replay()
@@ -451,7 +463,8 @@ def run_config5(args, c, world, rank, local):
                    "docs_per_gpu": c["docs"], "docs_total": total_docs,
                    "msgs_total": total_msgs, "msgs_mean": total_msgs / total_docs,
                    "msgs_max": int(sh.all_ops.max()), "parallelism": f"doc-sharded x{world} (LPT)",
-                   "residency": args.residency, "big_min_ops": big if args.residency == "blk" else None},
+                   "residency": args.residency, "big_min_ops": big if args.residency == "blk" else None,
+                   "partition": {"min_msgs": part[0], "cus": part[1]} if args.residency == "blk" and part else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic[0] if traffic else None,
                      "traffic_source": traffic[1] if traffic else None, "kernel": REPLAY_KERNEL[args.residency] + " (rank 0)",
@@ -685,6 +698,9 @@ def _main(argv=None):
     ap.add_argument("--big-flags", type=int, default=0,
                     help="big residency A/B switches (MT_BIGF_*): 1 block cache off, 2 zamboni prefetch off, "
                          "4 corrections table off, 8 parent cache off")
+    ap.add_argument("--partition", default="",
+                    help="partitioned size classes under blk residency, MIN_MSGS:CUS (runs of at least MIN_MSGS "
+                         "messages on CUS reserved CUs, one per SIMD; 'off' to disable the config's default)")
     ap.add_argument("--big-min-ops", type=int, default=-1,
                     help="size classes under blk residency: runs of at least this many messages replay in the "
                          "long-document kernel on a second stream (0: off; default: the config's)")

@@ -570,6 +570,13 @@ int MT_FN(doc_pset)(mt_ctx* c, uint32_t doc, int32_t id, uint16_t* keys, int32_t
 int MT_FN(set_size_class)(mt_ctx* c, uint32_t big_min_ops) {
     if (!c) return MT_E_INVALID;
     c->big_min_ops = big_min_ops;
+    c->part_cus = 0;
+    return MT_OK;
+}
+int MT_FN(set_partition)(mt_ctx* c, uint32_t min_ops, uint32_t cus) {
+    if (!c) return MT_E_INVALID;
+    c->big_min_ops = min_ops;
+    c->part_cus = min_ops ? cus : 0;
     return MT_OK;
 }
 int MT_FN(set_residency)(mt_ctx* c, int use_lds, int rows, int blocks, int heap) {

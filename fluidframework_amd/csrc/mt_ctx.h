@@ -38,6 +38,11 @@ struct mt_ctx {
     uint64_t runs_gen = ~0ull; uint32_t runs_min = 0, n_long = 0, n_short = 0;
     DevBuf b_runs;
     void* stream2 = nullptr; void* ev_fork = nullptr; void* ev_join = nullptr;
+    // Partitioned size classes (mt_set_partition): part_cus > 0 sends the long runs to the
+    // block-residency kernel on a stream masked to part_cus CUs, one document per SIMD (the
+    // launch pads each workgroup's LDS to a quarter of the CU's), and the rest to the other CUs.
+    uint32_t part_cus = 0, part_made = 0;
+    void* streamA = nullptr; void* streamB = nullptr; void* ev_joinB = nullptr;
     // mt_apply_batch / mt_upload_batch staging: two pinned host slots used alternately, each
     // with the event of its last H2D, and one device region the batch lands in
     struct Stage { void* p = nullptr; size_t cap = 0; void* ev = nullptr; };

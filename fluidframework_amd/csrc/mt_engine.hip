@@ -110,6 +110,9 @@ static void mtb_fini(mt_ctx* c) {
     if (c->ev0) (void)hipEventDestroy((hipEvent_t)c->ev0);
     if (c->ev1) (void)hipEventDestroy((hipEvent_t)c->ev1);
     if (c->stream2) { (void)hipStreamSynchronize((hipStream_t)c->stream2); (void)hipStreamDestroy((hipStream_t)c->stream2); }
+    if (c->streamA) { (void)hipStreamSynchronize((hipStream_t)c->streamA); (void)hipStreamDestroy((hipStream_t)c->streamA); }
+    if (c->streamB) { (void)hipStreamSynchronize((hipStream_t)c->streamB); (void)hipStreamDestroy((hipStream_t)c->streamB); }
+    if (c->ev_joinB) (void)hipEventDestroy((hipEvent_t)c->ev_joinB);
     if (c->ev_fork) (void)hipEventDestroy((hipEvent_t)c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy((hipEvent_t)c->ev_join);
 }
@@ -167,8 +170,54 @@ static int mtb_check(mt_ctx* c) {
     if (e != hipSuccess) { c->err = hipGetErrorString(e); return MT_E_HIP; }
     return MT_OK;
 }
+// The two CU-masked streams of partitioned size classes: A holds part_cus CUs spread evenly
+// over the device (every k-th CU, so every XCD gives its share), B the rest.
+static int mtb_partition_streams(mt_ctx* c) {
+    if (c->part_made == c->part_cus && c->streamA) return 0;
+    if (c->streamA) { (void)hipStreamSynchronize((hipStream_t)c->streamA); (void)hipStreamDestroy((hipStream_t)c->streamA); c->streamA = nullptr; }
+    if (c->streamB) { (void)hipStreamSynchronize((hipStream_t)c->streamB); (void)hipStreamDestroy((hipStream_t)c->streamB); c->streamB = nullptr; }
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu <= 0) return 1;
+    const uint32_t want = c->part_cus < (uint32_t)ncu ? c->part_cus : (uint32_t)ncu - 1;
+    std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
+    uint32_t got = 0;
+    for (int i = 0; i < ncu; i++) {
+        const bool inA = got < want && (uint64_t)i * want / (uint64_t)ncu != (uint64_t)(i + 1) * want / (uint64_t)ncu;
+        if (inA) { ma[i / 32] |= 1u << (i % 32); got++; } else mb[i / 32] |= 1u << (i % 32);
+    }
+    hipStream_t a, b;
+    if (hipExtStreamCreateWithCUMask(&a, (uint32_t)ma.size(), ma.data()) != hipSuccess) return 1;
+    if (hipExtStreamCreateWithCUMask(&b, (uint32_t)mb.size(), mb.data()) != hipSuccess) { (void)hipStreamDestroy(a); return 1; }
+    c->streamA = a; c->streamB = b;
+    if (!c->ev_joinB) { hipEvent_t e; (void)hipEventCreateWithFlags(&e, hipEventDisableTiming); c->ev_joinB = e; }
+    c->part_made = c->part_cus;
+    return 0;
+}
 static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) {
     uint32_t* cur = (uint32_t*)c->b_cursor.p;
+    if (c->use_lds == 2 && c->big_min_ops && c->n_long && c->part_cus && !mtb_partition_streams(c)) {
+        // partitioned size classes: long runs on stream A's CUs, one workgroup per SIMD (each
+        // padded to a quarter of the CU's 160 KB of LDS), the rest on stream B's CUs; joined
+        const uint32_t* runs = (const uint32_t*)c->b_runs.p;
+        hipStream_t sa = (hipStream_t)c->streamA, sb = (hipStream_t)c->streamB;
+        // any workgroup total in (160 KB / 5, 160 KB / 4] leaves four per CU; the kernels'
+        // static LDS is ~10-13 KB
+        const uint32_t pad = 27u << 10;
+        (void)hipEventRecord((hipEvent_t)c->ev_fork, s);
+        (void)hipStreamWaitEvent(sa, (hipEvent_t)c->ev_fork, 0);
+        (void)hipStreamWaitEvent(sb, (hipEvent_t)c->ev_fork, 0);
+        if (full) mtk_blk_full(sa, c->n_long, c->S, c->ops, runs, cur, c->lds_blks, c->lds_heap, pad);
+        else mtk_blk_fast(sa, c->n_long, c->S, c->ops, runs, cur, c->lds_blks, c->lds_heap, pad);
+        if (c->n_short) {
+            if (full) mtk_blk_full(sb, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);
+            else mtk_blk_fast(sb, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);
+        }
+        (void)hipEventRecord((hipEvent_t)c->ev_join, sa);
+        (void)hipEventRecord((hipEvent_t)c->ev_joinB, sb);
+        (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_join, 0);
+        (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_joinB, 0);
+        return;
+    }
     if (c->use_lds == 2 && c->big_min_ops && c->n_long) {
         // size classes: long runs on stream2 in the long-document kernel, the rest here, joined
         const uint32_t* runs = (const uint32_t*)c->b_runs.p;

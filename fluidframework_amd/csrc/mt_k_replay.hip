@@ -100,13 +100,13 @@ __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_generate_kernel(MtSt
 // ------------------------------------------------------------- launchers ----
 #if MT_KSET == 0
 void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
-                  int lh) {
-    hipLaunchKernelGGL(mt_replay_blk_kernel<false>, dim3(n), dim3(64), 0, s, S, o, runs, cur, lb, lh);
+                  int lh, uint32_t pad) {
+    hipLaunchKernelGGL(mt_replay_blk_kernel<false>, dim3(n), dim3(64), pad, s, S, o, runs, cur, lb, lh);
 }
 #elif MT_KSET == 1
 void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
-                  int lh) {
-    hipLaunchKernelGGL(mt_replay_blk_kernel<true>, dim3(n), dim3(64), 0, s, S, o, runs, cur, lb, lh);
+                  int lh, uint32_t pad) {
+    hipLaunchKernelGGL(mt_replay_blk_kernel<true>, dim3(n), dim3(64), pad, s, S, o, runs, cur, lb, lh);
 }
 #elif MT_KSET == 2
 void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,

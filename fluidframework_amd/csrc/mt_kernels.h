@@ -3,11 +3,12 @@
 #include <hip/hip_runtime.h>
 #include "mt_core.h"
 
-// runs: the run each workgroup replays (size classes), or null for run = blockIdx.x
+// runs: the run each workgroup replays (size classes), or null for run = blockIdx.x;
+// pad: dynamic LDS bytes added to each workgroup (fewer workgroups per CU; unused by the kernel)
 void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
-                  int lh);
+                  int lh, uint32_t pad = 0);
 void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
-                  int lh);
+                  int lh, uint32_t pad = 0);
 void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,
              int lw, int lb, int lh);
 void mtk_lds(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lr, int lb, int lh);

@@ -75,6 +75,7 @@ def _bind(lib, prefix: str):
         doc_pools=f("doc_pools", ctypes.c_int, [P, U32, P, P]),
         set_residency=f("set_residency", ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
         set_size_class=f("set_size_class", ctypes.c_int, [P, U32]),
+        set_partition=f("set_partition", ctypes.c_int, [P, U32, U32]),
         set_props=f("set_props", ctypes.c_int, [P, ctypes.POINTER(MtPropTable)]),
         set_client_names=f("set_client_names", ctypes.c_int, [P, U32, P]),
         set_doc_client_names=f("set_doc_client_names", ctypes.c_int, [P, U32, U32, P]),
@@ -338,6 +339,11 @@ class Engine:
         """mt_set_size_class: under block residency, runs of at least big_min_ops op records
         replay in the long-document kernel on a second stream (0: off)."""
         self._check(self.fn["set_size_class"](self.h, int(big_min_ops)), "mt_set_size_class")
+
+    def set_partition(self, min_ops: int, cus: int):
+        """mt_set_partition: under block residency, runs of at least min_ops op records replay on
+        `cus` CUs reserved for them, one document per SIMD; the rest on the other CUs (0: off)."""
+        self._check(self.fn["set_partition"](self.h, int(min_ops), int(cus)), "mt_set_partition")
 
     def checkpoint(self):
         """mt_checkpoint: device copy of every document's state."""

@@ -323,6 +323,13 @@ int  mt_set_residency(mt_ctx* ctx, int use_lds, int rows, int blocks, int heap);
  * in HBM, one wave per SIMD) on a second stream, concurrently with the block-residency kernel
  * for the other runs; 0 (the default) turns it off.  Results are identical either way. */
 int  mt_set_size_class(mt_ctx* ctx, uint32_t big_min_ops);
+/* Partitioned size classes under block residency (mt_set_residency 2): runs of at least
+ * min_ops op records replay in the block-residency kernel on `cus` CUs reserved for them, one
+ * document per SIMD (their workgroups' LDS is padded so four fit a CU), concurrently with the
+ * other runs on the remaining CUs (CU-masked streams, joined before the call returns its
+ * event).  A long run then shares its SIMD with no other document: the step of a batch whose
+ * longest documents set it shortens.  cus = 0 or min_ops = 0: off. */
+int  mt_set_partition(mt_ctx* ctx, uint32_t min_ops, uint32_t cus);
 /* Per run of the last LDS-resident replay: the op index where it handed over to
  * the HBM kernel (== the run's end when it finished in LDS).  Diagnostic. */
 int  mt_last_cursors(mt_ctx* ctx, uint32_t n_runs, uint32_t* out);

@@ -98,7 +98,7 @@ def test_gpu_config4_downscaled_matches_oracle(lag, res):
                       rows=40000, window=16384, text=1 << 18, psets=40000, residency=res)
 
 
-def check_size_classes(factory, counts, big_min_ops):
+def check_size_classes(factory, counts, big_min_ops, partition_cus=0):
     """mt_set_size_class: the longer runs of a batch go to the long-document kernel (LDS heap,
     window and U set) while the rest stay under block residency; every document must still
     match the oracle."""
@@ -113,7 +113,10 @@ def check_size_classes(factory, counts, big_min_ops):
     eng.upload_props(props)
     eng.upload_names(NAMES)
     eng.set_residency(2)
-    eng.set_size_class(big_min_ops)
+    if partition_cus:
+        eng.set_partition(big_min_ops, partition_cus)   # long runs on reserved CUs, one per SIMD
+    else:
+        eng.set_size_class(big_min_ops)
     eng.open_docs(0, n)
     eng.apply(batch)
     eng.sync()
@@ -135,3 +138,14 @@ def test_size_classes_match_oracle_on_emulation():
 @pytest.mark.gpu
 def test_size_classes_match_oracle_on_gpu():
     check_size_classes(lambda n, **kw: Engine(n, device=0, **kw), [300, 2500, 80, 1200, 40, 3000, 9000, 700] * 4, 1000)
+
+
+def test_partition_classes_match_oracle_on_emulation():
+    check_size_classes(emu_engine, [300, 2500, 80, 1200, 40, 3000], 1000, partition_cus=8)
+
+
+@pytest.mark.gpu
+def test_partition_classes_match_oracle_on_gpu():
+    """mt_set_partition: the long runs on CU-masked stream A with padded LDS, the rest on B."""
+    check_size_classes(lambda n, **kw: Engine(n, device=0, **kw), [300, 2500, 80, 1200, 40, 3000, 9000, 700] * 4, 1000,
+                       partition_cus=32)
