@@ -216,6 +216,7 @@ static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) 
         (void)hipEventRecord((hipEvent_t)c->ev_joinB, sb);
         (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_join, 0);
         (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_joinB, 0);
+        if (MT_BLK_NO_CONT) mtk_hbm(full, s, n_runs, c->S, c->ops, cur);     // documents that outgrew LDS
         return;
     }
     if (c->use_lds == 2 && c->big_min_ops && c->n_long) {
@@ -231,12 +232,14 @@ static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) 
         }
         (void)hipEventRecord((hipEvent_t)c->ev_join, s2);
         (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_join, 0);
+        if (MT_BLK_NO_CONT && c->n_short) mtk_hbm(full, s, n_runs, c->S, c->ops, cur);   // documents that outgrew LDS
         return;
     }
     if (c->use_lds == 3) mtk_big(full, s, n_runs, c->S, c->ops, nullptr, cur, c->lds_rows, c->lds_blks, c->lds_heap);
     else if (c->use_lds == 2) {
         if (full) mtk_blk_full(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);
         else mtk_blk_fast(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);
+        if (MT_BLK_NO_CONT) mtk_hbm(full, s, n_runs, c->S, c->ops, cur);     // documents that outgrew LDS
     } else if (c->use_lds) {
         mtk_lds(full, s, n_runs, c->S, c->ops, cur, c->lds_rows, c->lds_blks, c->lds_heap);
         mtk_hbm(full, s, n_runs, c->S, c->ops, cur);

@@ -195,12 +195,13 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
 }
 
 #ifndef MT_BLK_NO_CONT
-#define MT_BLK_NO_CONT 0
+#define MT_BLK_NO_CONT 1
 #endif
 // One document run of a replay launch (every replay kernel and the host emulation run this).
 // The run starts at ops.start[run] (a capture resume) or op_off[run]; RES is the residency it
-// starts in: MT_RES_LDS hands the rest to a second, all-HBM launch (the returned op index goes
-// to cursor[]), MT_RES_BLK / MT_RES_BIG continue in HBM in the same wave.  Capture launches
+// starts in: MT_RES_LDS and MT_RES_BLK hand the rest to a second, all-HBM launch (the returned
+// op index goes to cursor[]; the block-residency kernel then carries no second engine, so it
+// runs without scratch), MT_RES_BIG continues in HBM in the same wave.  Capture launches
 // record in ops.resume[run] where the run stopped for headroom (op_off[run + 1]: finished).
 template <int RES, bool FULL>
 MT_HD uint32_t mt_replay_doc(const MtState& S, const MtOps& ops, uint32_t run, MtScratch* sc, int l0, int l1, int l2) {
@@ -228,10 +229,12 @@ MT_HD uint32_t mt_replay_doc(const MtState& S, const MtOps& ops, uint32_t run, M
             h.store(doc);
         }
     }
-    if (FULL && ops.resume && !(RES == MT_RES_LDS && cur < o1)) wave_for(1, [&](int) MT_LAM { ops.resume[run] = stop; });
+    constexpr bool handsOver = RES == MT_RES_LDS || (RES == MT_RES_BLK && MT_BLK_NO_CONT);
+    if (FULL && ops.resume && !(handsOver && cur < o1)) wave_for(1, [&](int) MT_LAM { ops.resume[run] = stop; });
     return cur;
 }
-// The all-HBM pass after an MT_RES_LDS launch: the rest of each run from its hand-over point.
+// The all-HBM pass after an MT_RES_LDS or MT_RES_BLK launch: the rest of each run from its
+// hand-over point.
 template <bool FULL>
 MT_HD void mt_replay_doc_rest(const MtState& S, const MtOps& ops, uint32_t run, MtScratch* sc, uint32_t o0) {
     const uint32_t o1 = ops.op_off[run + 1];

@@ -45,7 +45,7 @@ static void replay_runs(mt_ctx* c, uint32_t n_runs) {
         else if (c->use_lds) cursor[run] = mt_replay_doc<MT_RES_LDS, FULL>(c->S, c->ops, run, &sc, c->lds_rows, c->lds_blks, c->lds_heap);
         else (void)mt_replay_doc<MT_RES_HBM, FULL>(c->S, c->ops, run, &sc, 0, 0, 0);
     }
-    for (uint32_t run = 0; run < n_runs && c->use_lds == 1; run++) {
+    for (uint32_t run = 0; run < n_runs && (c->use_lds == 1 || (c->use_lds == 2 && MT_BLK_NO_CONT)); run++) {
         MtScratch sc;
         mt_replay_doc_rest<FULL>(c->S, c->ops, run, &sc, cursor[run]);
     }
