@@ -802,7 +802,7 @@ def _main(argv=None):
     cnt2 = eng.counters(range(c["docs"]))
     handover = None
     if args.residency != "hbm":
-        cur = eng.last_cursors(c["docs"]).astype(np.int64)
+        cur = eng.last_cursors(c["docs"]).astype(np.int64) & 0x7FFFFFFF   # high bit: finished in-wave
         ends = (np.arange(c["docs"]) + 1) * c["ops"]
         ho = np.nonzero(cur < ends)[0]
         # where each hand-over happened: the op index within its run (the rest ran from HBM)

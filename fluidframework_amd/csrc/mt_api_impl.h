@@ -56,6 +56,25 @@ static int mt_size_class_lists(mt_ctx* c) {
     return MT_OK;
 }
 
+// The continuation classes of block residency for the resident batch: runs of at least
+// cont_min_ops op records in [0, n_cont), the rest after them.
+static int mt_cont_lists(mt_ctx* c) {
+    if (c->cont_gen == c->batch_gen && c->cont_min_made == c->cont_min_ops) return MT_OK;
+    const uint32_t R = c->n_runs;
+    std::vector<uint32_t> lst; lst.reserve(R);
+    const bool ok = c->run_off.size() == R + 1;
+    for (uint32_t r = 0; r < R && ok; r++) if (c->run_off[r + 1] - c->run_off[r] >= c->cont_min_ops) lst.push_back(r);
+    c->n_cont = (uint32_t)lst.size();
+    for (uint32_t r = 0; r < R && ok; r++) if (c->run_off[r + 1] - c->run_off[r] < c->cont_min_ops) lst.push_back(r);
+    c->n_nocont = (uint32_t)lst.size() - c->n_cont;
+    if (!ok) { c->n_cont = 0; c->n_nocont = 0; }
+    int rc;
+    if ((rc = mtb_ensure(c, c->b_cruns, 4ull * lst.size() + 4))) return rc;
+    if (!lst.empty()) mtb_h2d(c, c->b_cruns.p, lst.data(), 4ull * lst.size());
+    c->cont_gen = c->batch_gen; c->cont_min_made = c->cont_min_ops;
+    return MT_OK;
+}
+
 // Host loops over a batch's ops run on up to 16 threads once a batch is large enough to pay
 // for them (ingest: validation and the SoA -> 32-byte record packing).
 template <class F> static void mt_par_for(size_t n, F f) {
@@ -571,6 +590,11 @@ int MT_FN(set_size_class)(mt_ctx* c, uint32_t big_min_ops) {
     if (!c) return MT_E_INVALID;
     c->big_min_ops = big_min_ops;
     c->part_cus = 0;
+    return MT_OK;
+}
+int MT_FN(set_continuation)(mt_ctx* c, uint32_t min_ops) {
+    if (!c) return MT_E_INVALID;
+    c->cont_min_ops = min_ops;
     return MT_OK;
 }
 int MT_FN(set_partition)(mt_ctx* c, uint32_t min_ops, uint32_t cus) {

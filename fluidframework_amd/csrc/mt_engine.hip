@@ -207,7 +207,7 @@ static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) 
         (void)hipStreamWaitEvent(sa, (hipEvent_t)c->ev_fork, 0);
         (void)hipStreamWaitEvent(sb, (hipEvent_t)c->ev_fork, 0);
         if (full) mtk_blk_full(sa, c->n_long, c->S, c->ops, runs, cur, c->lds_blks, c->lds_heap, pad);
-        else mtk_blk_fast(sa, c->n_long, c->S, c->ops, runs, cur, c->lds_blks, c->lds_heap, pad);
+        else mtk_blk_fast_cont(sa, c->n_long, c->S, c->ops, runs, cur, c->lds_blks, c->lds_heap, pad);
         if (c->n_short) {
             if (full) mtk_blk_full(sb, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);
             else mtk_blk_fast(sb, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);
@@ -216,7 +216,7 @@ static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) 
         (void)hipEventRecord((hipEvent_t)c->ev_joinB, sb);
         (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_join, 0);
         (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_joinB, 0);
-        if (MT_BLK_NO_CONT) mtk_hbm(full, s, n_runs, c->S, c->ops, cur);     // documents that outgrew LDS
+        if (!full && c->n_short) mtk_hbm(full, s, n_runs, c->S, c->ops, cur);   // documents that outgrew LDS
         return;
     }
     if (c->use_lds == 2 && c->big_min_ops && c->n_long) {
@@ -232,22 +232,40 @@ static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) 
         }
         (void)hipEventRecord((hipEvent_t)c->ev_join, s2);
         (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_join, 0);
-        if (MT_BLK_NO_CONT && c->n_short) mtk_hbm(full, s, n_runs, c->S, c->ops, cur);   // documents that outgrew LDS
+        if (!full && c->n_short) mtk_hbm(full, s, n_runs, c->S, c->ops, cur);   // documents that outgrew LDS
         return;
     }
     if (c->use_lds == 3) mtk_big(full, s, n_runs, c->S, c->ops, nullptr, cur, c->lds_rows, c->lds_blks, c->lds_heap);
     else if (c->use_lds == 2) {
-        if (full) mtk_blk_full(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);
-        else mtk_blk_fast(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);
-        if (MT_BLK_NO_CONT) mtk_hbm(full, s, n_runs, c->S, c->ops, cur);     // documents that outgrew LDS
+        if (full) mtk_blk_full(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);   // continues in-wave
+        else if (c->n_cont == 0) {
+            mtk_blk_fast(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);
+            mtk_hbm(full, s, n_runs, c->S, c->ops, cur);                        // documents that outgrew LDS
+        } else {
+            // long runs in the kernel with the in-wave continuation on stream2, the rest here
+            const uint32_t* runs = (const uint32_t*)c->b_cruns.p;
+            hipStream_t s2 = (hipStream_t)c->stream2;
+            (void)hipEventRecord((hipEvent_t)c->ev_fork, s);
+            (void)hipStreamWaitEvent(s2, (hipEvent_t)c->ev_fork, 0);
+            mtk_blk_fast_cont(s2, c->n_cont, c->S, c->ops, runs, cur, c->lds_blks, c->lds_heap);
+            if (c->n_nocont) mtk_blk_fast(s, c->n_nocont, c->S, c->ops, runs + c->n_cont, cur, c->lds_blks, c->lds_heap);
+            (void)hipEventRecord((hipEvent_t)c->ev_join, s2);
+            (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_join, 0);
+            if (c->n_nocont) mtk_hbm(full, s, n_runs, c->S, c->ops, cur);       // documents that outgrew LDS
+        }
     } else if (c->use_lds) {
         mtk_lds(full, s, n_runs, c->S, c->ops, cur, c->lds_rows, c->lds_blks, c->lds_heap);
         mtk_hbm(full, s, n_runs, c->S, c->ops, cur);
     } else mtk_hbm(full, s, n_runs, c->S, c->ops, nullptr);
 }
 static int mt_size_class_lists(mt_ctx* c);
+static int mt_cont_lists(mt_ctx* c);
 static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     if (n_runs == 0) return MT_OK;
+    if (!g.enabled && c->use_lds == 2 && !c->big_min_ops) {
+        int rc = mt_cont_lists(c);
+        if (rc) return rc;
+    }
     hipStream_t s = (hipStream_t)c->stream;
     if (!g.enabled && c->use_lds == 2 && c->big_min_ops) {
         int rc = mt_size_class_lists(c);

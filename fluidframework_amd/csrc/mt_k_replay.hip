@@ -3,8 +3,9 @@
 // Built several times with -DMT_KSET=<n> (see __graft_entry__.build_engine): each object
 // holds one group of template instantiations, so the groups compile in parallel, and
 // mt_engine.hip launches them through the mtk_* functions declared in mt_kernels.h.
-//   MT_KSET 0: mt_replay_blk_kernel<false> (the hot path)   1: mt_replay_blk_kernel<true>
-//   MT_KSET 2: mt_replay_big_kernel<false / true>             3: mt_replay_lds_kernel<false / true>
+//   MT_KSET 0: mt_replay_blk_kernel<false, false> (the hot path: no in-wave continuation)
+//   MT_KSET 1: mt_replay_blk_kernel<true, true>   5: mt_replay_blk_kernel<false, true> (long runs)
+//   MT_KSET 2: mt_replay_big_kernel<false / true>  3: mt_replay_lds_kernel<false / true>
 //   MT_KSET 4: the all-HBM kernels and the generator
 #include <hip/hip_runtime.h>
 #include "mt_ctx.h"
@@ -31,13 +32,14 @@ __global__ __launch_bounds__(64, MT_LDS_WAVES_PER_SIMD) void mt_replay_lds_kerne
     if (__lane_id() == 0) cursor[blockIdx.x] = cur;
 }
 // Blocks + heap in LDS (~9.5 KB per workgroup, 4 waves per SIMD), rows/window in HBM; a
-// document that outgrows LDS continues in HBM in the same wave.
-template <bool FULL>
+// document that outgrows LDS continues in HBM in the same wave (CONT) or stops for the
+// all-HBM launch that follows.
+template <bool FULL, bool CONT>
 __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(MtState S, MtOps ops, const uint32_t* runs,
                                                                                uint32_t* cursor, int lb, int lh) {
     __shared__ MtScratch sc;
     const uint32_t run = runs ? runs[blockIdx.x] : blockIdx.x;          // size classes: a run list
-    const uint32_t cur = mt_replay_doc<MT_RES_BLK, FULL>(S, ops, run, &sc, 0, lb, lh);
+    const uint32_t cur = mt_replay_doc<MT_RES_BLK, FULL, CONT>(S, ops, run, &sc, 0, lb, lh);
     if (__lane_id() == 0) cursor[run] = cur;
 }
 // Long documents (MT_RES_BIG): heap, window, U set and a block cache of the tree's upper
@@ -101,12 +103,17 @@ __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_generate_kernel(MtSt
 #if MT_KSET == 0
 void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
                   int lh, uint32_t pad) {
-    hipLaunchKernelGGL(mt_replay_blk_kernel<false>, dim3(n), dim3(64), pad, s, S, o, runs, cur, lb, lh);
+    hipLaunchKernelGGL((mt_replay_blk_kernel<false, false>), dim3(n), dim3(64), pad, s, S, o, runs, cur, lb, lh);
+}
+#elif MT_KSET == 5
+void mtk_blk_fast_cont(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,
+                       int lb, int lh, uint32_t pad) {
+    hipLaunchKernelGGL((mt_replay_blk_kernel<false, true>), dim3(n), dim3(64), pad, s, S, o, runs, cur, lb, lh);
 }
 #elif MT_KSET == 1
 void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
                   int lh, uint32_t pad) {
-    hipLaunchKernelGGL(mt_replay_blk_kernel<true>, dim3(n), dim3(64), pad, s, S, o, runs, cur, lb, lh);
+    hipLaunchKernelGGL((mt_replay_blk_kernel<true, true>), dim3(n), dim3(64), pad, s, S, o, runs, cur, lb, lh);
 }
 #elif MT_KSET == 2
 void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,

@@ -9,6 +9,9 @@ void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, c
                   int lh, uint32_t pad = 0);
 void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
                   int lh, uint32_t pad = 0);
+// the block-residency kernel with the in-wave HBM continuation (long runs)
+void mtk_blk_fast_cont(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,
+                       int lb, int lh, uint32_t pad = 0);
 void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,
              int lw, int lb, int lh);
 void mtk_lds(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lr, int lb, int lh);

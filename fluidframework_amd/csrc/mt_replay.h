@@ -194,16 +194,18 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
     return o1;
 }
 
-#ifndef MT_BLK_NO_CONT
-#define MT_BLK_NO_CONT 1
-#endif
+// cursor[] flag: the run left LDS at the op index in the low bits and finished in HBM in the same
+// wave (the all-HBM launch that follows skips it; mt_last_cursors reports the hand-over op).
+#define MT_CUR_DONE 0x80000000u
 // One document run of a replay launch (every replay kernel and the host emulation run this).
 // The run starts at ops.start[run] (a capture resume) or op_off[run]; RES is the residency it
-// starts in: MT_RES_LDS and MT_RES_BLK hand the rest to a second, all-HBM launch (the returned
-// op index goes to cursor[]; the block-residency kernel then carries no second engine, so it
-// runs without scratch), MT_RES_BIG continues in HBM in the same wave.  Capture launches
-// record in ops.resume[run] where the run stopped for headroom (op_off[run + 1]: finished).
-template <int RES, bool FULL>
+// starts in.  A document that outgrows the LDS pools continues in HBM in the same wave when
+// CONT (MT_RES_BIG, and MT_RES_BLK for long runs), or else stops there and hands the rest to a
+// second, all-HBM launch (the returned op index goes to cursor[]): MT_RES_LDS, and MT_RES_BLK
+// for the runs shorter than the context's continuation threshold, whose kernel then carries no
+// second engine and runs without scratch.  Capture launches record in ops.resume[run] where the
+// run stopped for headroom (op_off[run + 1]: finished).
+template <int RES, bool FULL, bool CONT = true>
 MT_HD uint32_t mt_replay_doc(const MtState& S, const MtOps& ops, uint32_t run, MtScratch* sc, int l0, int l1, int l2) {
     const uint32_t doc = ops.doc_ids[run], o1 = ops.op_off[run + 1];
     const uint32_t o0 = ops.start ? ops.start[run] : ops.op_off[run];
@@ -219,7 +221,7 @@ MT_HD uint32_t mt_replay_doc(const MtState& S, const MtOps& ops, uint32_t run, M
         const bool stopped = e.dStop != 0;
         e.store(doc);
         if (stopped) { stop = cur; cur = o1; }                   // no hand-over: the host resumes it
-        else if (RES != MT_RES_LDS && !(RES == MT_RES_BLK && MT_BLK_NO_CONT) && cur < o1) {
+        else if (RES != MT_RES_LDS && CONT && cur < o1) {
             // A document that outgrew LDS continues here with its pools in HBM (no second
             // launch: long documents, which outgrow it first, keep their head start).
             MtEngT<MT_RES_HBM, FULL> h;
@@ -227,9 +229,10 @@ MT_HD uint32_t mt_replay_doc(const MtState& S, const MtOps& ops, uint32_t run, M
             const uint32_t c2 = mt_replay_run(h, ops, run, doc, nullptr, nullptr, cur);
             if (h.dStop) stop = c2;
             h.store(doc);
+            cur |= MT_CUR_DONE;                              // finished here: no second launch
         }
     }
-    constexpr bool handsOver = RES == MT_RES_LDS || (RES == MT_RES_BLK && MT_BLK_NO_CONT);
+    constexpr bool handsOver = RES == MT_RES_LDS || !CONT;
     if (FULL && ops.resume && !(handsOver && cur < o1)) wave_for(1, [&](int) MT_LAM { ops.resume[run] = stop; });
     return cur;
 }

@@ -76,6 +76,7 @@ def _bind(lib, prefix: str):
         set_residency=f("set_residency", ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
         set_size_class=f("set_size_class", ctypes.c_int, [P, U32]),
         set_partition=f("set_partition", ctypes.c_int, [P, U32, U32]),
+        set_continuation=f("set_continuation", ctypes.c_int, [P, U32]),
         set_props=f("set_props", ctypes.c_int, [P, ctypes.POINTER(MtPropTable)]),
         set_client_names=f("set_client_names", ctypes.c_int, [P, U32, P]),
         set_doc_client_names=f("set_doc_client_names", ctypes.c_int, [P, U32, U32, P]),
@@ -232,7 +233,8 @@ class Engine:
         self._check(self.fn["replay_resident"](self.h), "mt_replay_resident")
 
     def last_cursors(self, n_runs: int) -> np.ndarray:
-        """mt_last_cursors: op index where each run left LDS in the last replay."""
+        """mt_last_cursors: op index where each run left LDS in the last replay (bit 31 set: it
+        finished in HBM in the same wave)."""
         out = np.zeros(n_runs, np.uint32)
         self._check(self.fn["last_cursors"](self.h, n_runs, out.ctypes.data), "mt_last_cursors")
         return out
@@ -339,6 +341,11 @@ class Engine:
         """mt_set_size_class: under block residency, runs of at least big_min_ops op records
         replay in the long-document kernel on a second stream (0: off)."""
         self._check(self.fn["set_size_class"](self.h, int(big_min_ops)), "mt_set_size_class")
+
+    def set_continuation(self, min_ops: int):
+        """mt_set_continuation: block-residency runs of at least min_ops op records continue an
+        outgrown document in HBM in the same wave; shorter ones hand it to a second launch."""
+        self._check(self.fn["set_continuation"](self.h, int(min_ops)), "mt_set_continuation")
 
     def set_partition(self, min_ops: int, cus: int):
         """mt_set_partition: under block residency, runs of at least min_ops op records replay on

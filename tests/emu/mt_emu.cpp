@@ -41,11 +41,16 @@ static void replay_runs(mt_ctx* c, uint32_t n_runs) {
         else if (c->use_lds == 2 && c->big_min_ops && !c->part_cus && c->run_off.size() == n_runs + 1 &&
                  c->run_off[run + 1] - c->run_off[run] >= c->big_min_ops)      // size classes (mt_set_size_class)
             cursor[run] = mt_replay_doc<MT_RES_BIG, FULL>(c->S, c->ops, run, &sc, MT_G_WIN, 0, MT_G_HEAP);
-        else if (c->use_lds == 2) cursor[run] = mt_replay_doc<MT_RES_BLK, FULL>(c->S, c->ops, run, &sc, 0, c->lds_blks, c->lds_heap);
+        else if (c->use_lds == 2) {                       // long runs (and FULL) continue in-wave, as on the device
+            const bool cont = FULL || c->part_cus || c->big_min_ops || c->run_off.size() != n_runs + 1 ||
+                              c->run_off[run + 1] - c->run_off[run] >= c->cont_min_ops;
+            cursor[run] = cont ? mt_replay_doc<MT_RES_BLK, FULL, true>(c->S, c->ops, run, &sc, 0, c->lds_blks, c->lds_heap)
+                               : mt_replay_doc<MT_RES_BLK, FULL, false>(c->S, c->ops, run, &sc, 0, c->lds_blks, c->lds_heap);
+        }
         else if (c->use_lds) cursor[run] = mt_replay_doc<MT_RES_LDS, FULL>(c->S, c->ops, run, &sc, c->lds_rows, c->lds_blks, c->lds_heap);
         else (void)mt_replay_doc<MT_RES_HBM, FULL>(c->S, c->ops, run, &sc, 0, 0, 0);
     }
-    for (uint32_t run = 0; run < n_runs && (c->use_lds == 1 || (c->use_lds == 2 && MT_BLK_NO_CONT)); run++) {
+    for (uint32_t run = 0; run < n_runs && (c->use_lds == 1 || (c->use_lds == 2 && !FULL)); run++) {
         MtScratch sc;
         mt_replay_doc_rest<FULL>(c->S, c->ops, run, &sc, cursor[run]);
     }

@@ -36,6 +36,8 @@ def compare(batch, props, n_docs, factory=None, **cap):
                      propsets_per_doc=cap.get("psets", 8192), text_per_doc=cap.get("text", 1 << 18))
     if "residency" in cap:
         eng.set_residency(*cap["residency"])
+    if "cont" in cap:
+        eng.set_continuation(cap["cont"])
     eng.upload_props(props)
     eng.upload_names(NAMES)
     eng.open_docs(0, n_docs)
@@ -108,6 +110,17 @@ def test_emu_residency_handover_matches_oracle(cfg, res):
     batch, st, _ = generate(p, props)
     assert st == [0] * 3
     compare(batch, props, 3, residency=res)
+
+
+# Block residency with tiny caps: every run in the kernel with the in-wave continuation
+# (mt_set_continuation(0)) and every run in the one that hands over to a second launch.
+@pytest.mark.parametrize("cont", [0, 1 << 30])
+def test_emu_block_continuation_classes_match_oracle(cont):
+    props = ann_props()
+    p = gen_params(seed=23, n_docs=3, **CONFIGS["grow"])
+    batch, st, _ = generate(p, props)
+    assert st == [0] * 3
+    compare(batch, props, 3, residency=(2, 0, 40, 12), cont=cont)
 
 
 @pytest.mark.parametrize("cfg", ["cfg1", "cfg3"])

@@ -36,6 +36,18 @@ def test_gpu_residency_handover_matches_oracle(res):
     compare(batch, props, 6, factory=gpu_engine, residency=res)
 
 
+@pytest.mark.parametrize("cont", [0, 1 << 30])
+def test_gpu_block_continuation_classes_match_oracle(cont):
+    # Block residency with tiny caps: every run in the kernel with the in-wave continuation
+    # (cont 0), then every run in the one without it (outgrown documents finish in the
+    # all-HBM launch that follows).
+    props = ann_props()
+    p = gen_params(seed=23, n_docs=6, **CONFIGS["grow"])
+    batch, st, _ = generate(p, props)
+    assert st == [0] * 6
+    compare(batch, props, 6, factory=gpu_engine, residency=(2, 0, 40, 12), cont=cont)
+
+
 def test_gpu_deep_tree_matches_oracle():
     props = ann_props()
     cfg = dict(clients=8, lag=32, ins=70, rem=20, ins_len=8, rem_len=8, ops=20000, ann_sets=24, rewrite=5)
