@@ -415,6 +415,8 @@ def run_config5(args, c, world, rank, local):
     part = partition_of(args, c)
     if args.residency == "blk" and part:
         eng.set_partition(*part)
+    if args.cont_min >= 0:
+        eng.set_continuation(args.cont_min)
     my_msgs = int(sh.ops.sum())
     for _ in range(args.warmup):
         sh.replay()
@@ -698,6 +700,9 @@ def _main(argv=None):
     ap.add_argument("--big-flags", type=int, default=0,
                     help="big residency A/B switches (MT_BIGF_*): 1 block cache off, 2 zamboni prefetch off, "
                          "4 corrections table off, 8 parent cache off")
+    ap.add_argument("--cont-min", type=int, default=-1,
+                    help="block residency: runs of at least this many messages keep the in-wave HBM "
+                         "continuation (mt_set_continuation; -1: the library default)")
     ap.add_argument("--partition", default="",
                     help="partitioned size classes under blk residency, MIN_MSGS:CUS (runs of at least MIN_MSGS "
                          "messages on CUS reserved CUs, one per SIMD; 'off' to disable the config's default)")
@@ -753,6 +758,8 @@ def _main(argv=None):
     big = c.get("big_min_ops", 0) if args.big_min_ops < 0 else args.big_min_ops
     if args.residency == "blk" and big:
         eng.set_size_class(big)
+    if args.cont_min >= 0:
+        eng.set_continuation(args.cont_min)
     eng.upload_props(ann_props())
     eng.upload_names(['"c%d"' % i for i in range(64)])
     seed = args.seed ^ (rank * 0x9E3779B1)

@@ -42,9 +42,10 @@ struct mt_ctx {
     // block-residency kernel on a stream masked to part_cus CUs, one document per SIMD (the
     // launch pads each workgroup's LDS to a quarter of the CU's), and the rest to the other CUs.
     uint32_t part_cus = 0, part_made = 0;
-    // Block residency: runs of at least cont_min_ops op records replay in the kernel with the
-    // in-wave HBM continuation (a long document that outgrows LDS keeps its head start), the
-    // rest in the one without it (no scratch; an outgrown document finishes in a second launch).
+    // Block residency: a batch with a run of at least cont_min_ops op records replays in the
+    // kernel with the in-wave HBM continuation (a long document that outgrows LDS keeps its head
+    // start); other batches in the one without it (no scratch; an outgrown document finishes
+    // in a second, all-HBM launch).
     uint32_t cont_min_ops = 16384, n_cont = 0, n_nocont = 0, cont_min_made = 0;
     uint64_t cont_gen = ~0ull;
     DevBuf b_cruns;

@@ -239,19 +239,14 @@ static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) 
     else if (c->use_lds == 2) {
         if (full) mtk_blk_full(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);   // continues in-wave
         else if (c->n_cont == 0) {
+            // no run reaches the continuation threshold: the kernel without the second engine
             mtk_blk_fast(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);
             mtk_hbm(full, s, n_runs, c->S, c->ops, cur);                        // documents that outgrew LDS
         } else {
-            // long runs in the kernel with the in-wave continuation on stream2, the rest here
-            const uint32_t* runs = (const uint32_t*)c->b_cruns.p;
-            hipStream_t s2 = (hipStream_t)c->stream2;
-            (void)hipEventRecord((hipEvent_t)c->ev_fork, s);
-            (void)hipStreamWaitEvent(s2, (hipEvent_t)c->ev_fork, 0);
-            mtk_blk_fast_cont(s2, c->n_cont, c->S, c->ops, runs, cur, c->lds_blks, c->lds_heap);
-            if (c->n_nocont) mtk_blk_fast(s, c->n_nocont, c->S, c->ops, runs + c->n_cont, cur, c->lds_blks, c->lds_heap);
-            (void)hipEventRecord((hipEvent_t)c->ev_join, s2);
-            (void)hipStreamWaitEvent(s, (hipEvent_t)c->ev_join, 0);
-            if (c->n_nocont) mtk_hbm(full, s, n_runs, c->S, c->ops, cur);       // documents that outgrew LDS
+            // a long run is in the batch: one launch of the kernel with the in-wave continuation
+            // (the runs start in batch order, longest first under LPT; two kernels on two streams
+            // let short runs take the slots first and measured slower)
+            mtk_blk_fast_cont(s, n_runs, c->S, c->ops, nullptr, cur, c->lds_blks, c->lds_heap);
         }
     } else if (c->use_lds) {
         mtk_lds(full, s, n_runs, c->S, c->ops, cur, c->lds_rows, c->lds_blks, c->lds_heap);

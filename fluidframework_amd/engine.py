@@ -343,8 +343,9 @@ class Engine:
         self._check(self.fn["set_size_class"](self.h, int(big_min_ops)), "mt_set_size_class")
 
     def set_continuation(self, min_ops: int):
-        """mt_set_continuation: block-residency runs of at least min_ops op records continue an
-        outgrown document in HBM in the same wave; shorter ones hand it to a second launch."""
+        """mt_set_continuation: a block-residency batch holding a run of at least min_ops op records
+        continues outgrown documents in HBM in the same wave; other batches hand them to a
+        second launch."""
         self._check(self.fn["set_continuation"](self.h, int(min_ops)), "mt_set_continuation")
 
     def set_partition(self, min_ops: int, cus: int):

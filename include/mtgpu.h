@@ -330,10 +330,10 @@ int  mt_set_size_class(mt_ctx* ctx, uint32_t big_min_ops);
  * event).  A long run then shares its SIMD with no other document: the step of a batch whose
  * longest documents set it shortens.  cus = 0 or min_ops = 0: off. */
 int  mt_set_partition(mt_ctx* ctx, uint32_t min_ops, uint32_t cus);
-/* Block residency: runs of at least min_ops op records (default 16,384) replay in the kernel
- * that continues an outgrown document in HBM in the same wave; shorter runs in the kernel
- * without that second engine (no scratch), an outgrown one finishing in a second, all-HBM
- * launch.  0: every run continues in-wave. */
+/* Block residency: a batch holding a run of at least min_ops op records (default 16,384)
+ * replays in the kernel that continues an outgrown document in HBM in the same wave; other
+ * batches in the kernel without that second engine (no scratch), an outgrown document
+ * finishing in a second, all-HBM launch.  0: always the continuing kernel. */
 int  mt_set_continuation(mt_ctx* ctx, uint32_t min_ops);
 /* Per run of the last LDS-resident replay: the op index where it handed over to
  * the HBM kernel (== the run's end when it finished in LDS).  Diagnostic. */

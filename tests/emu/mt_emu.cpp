@@ -42,8 +42,9 @@ static void replay_runs(mt_ctx* c, uint32_t n_runs) {
                  c->run_off[run + 1] - c->run_off[run] >= c->big_min_ops)      // size classes (mt_set_size_class)
             cursor[run] = mt_replay_doc<MT_RES_BIG, FULL>(c->S, c->ops, run, &sc, MT_G_WIN, 0, MT_G_HEAP);
         else if (c->use_lds == 2) {                       // long runs (and FULL) continue in-wave, as on the device
-            const bool cont = FULL || c->part_cus || c->big_min_ops || c->run_off.size() != n_runs + 1 ||
-                              c->run_off[run + 1] - c->run_off[run] >= c->cont_min_ops;
+            bool anyLong = c->run_off.size() != n_runs + 1;
+            for (uint32_t q = 0; q < n_runs && !anyLong; q++) anyLong = c->run_off[q + 1] - c->run_off[q] >= c->cont_min_ops;
+            const bool cont = FULL || c->part_cus || c->big_min_ops || anyLong;
             cursor[run] = cont ? mt_replay_doc<MT_RES_BLK, FULL, true>(c->S, c->ops, run, &sc, 0, c->lds_blks, c->lds_heap)
                                : mt_replay_doc<MT_RES_BLK, FULL, false>(c->S, c->ops, run, &sc, 0, c->lds_blks, c->lds_heap);
         }
