@@ -24,6 +24,38 @@ MT_OPF_END_OF_MSG, MT_OPF_MARKER, MT_OPF_REWRITE, MT_OPF_SEG_PROPS, MT_OPF_COMBI
 MT_OP_CUT, MT_OP_COPY, MT_OP_PASTE = 5, 6, 7      # register ops (include/mtgpu.h)
 MT_OPF_REL1, MT_OPF_REL2, MT_OPF_MARKER_ID = 0x20, 0x40, 0x80
 MARKER_ID_KEY = "markerId"            # reservedMarkerIdKey, MT/mergeTree.ts:591
+# property values other than interned ids (include/mtgpu.h MT_VAL_*, MT_VK_*)
+MT_VAL_NULL, MT_VAL_NAN, MT_VAL_UNSUP, MT_VAL_CFRESH, MT_VAL_UNDEF, MT_VAL_CONS_BASE = -1, -2, -3, -4, -5, -16
+MT_VK_NUM, MT_VK_SEQM1 = 1, 2
+
+
+def _is_number(v) -> bool:            # typeof v === "number" || typeof v === "boolean" (x + undefined is NaN)
+    return isinstance(v, (int, float))
+
+
+def _seq_minus1(v) -> bool:           # `cv.seq === -1` on a (non-array) object, properties.ts:52
+    s = v.get("seq") if isinstance(v, dict) else None
+    return isinstance(s, (int, float)) and not isinstance(s, bool) and s == -1
+
+
+def value_kind(v) -> int:
+    return (MT_VK_NUM if _is_number(v) else 0) | (MT_VK_SEQM1 if _seq_minus1(v) else 0)
+
+
+def decode_value(v: int, values_json: list):
+    """A stored property value id (mt_doc_pset) as a Python JSON value: interned ids through
+    the table; NaN; JS undefined (jsjson.UNDEFINED); a fresh consensus object
+    {value: undefined, seq} (properties.ts:43-47)."""
+    import json as _json
+    if v >= 0:
+        return _json.loads(values_json[v])
+    if v == MT_VAL_NAN:
+        return float("nan")
+    if v == MT_VAL_UNDEF:
+        return jsjson.UNDEFINED
+    if v <= MT_VAL_CONS_BASE:
+        return {"value": jsjson.UNDEFINED, "seq": MT_VAL_CONS_BASE - v}
+    raise ValueError(f"not a stored property value: {v}")
 
 MT_DS_NAMES = {
     0x01: "ASSERT_SEQ", 0x02: "ASSERT_MSN", 0x04: "INSERT_FAILED", 0x08: "UNSUPPORTED",
@@ -54,7 +86,7 @@ class MtPropTable(ctypes.Structure):
         ("n_sets", ctypes.c_uint32), ("set_off", ctypes.c_void_p), ("key", ctypes.c_void_p),
         ("value", ctypes.c_void_p), ("n_keys", ctypes.c_uint32), ("key_json", ctypes.c_void_p),
         ("key_index", ctypes.c_void_p), ("n_values", ctypes.c_uint32), ("value_json", ctypes.c_void_p),
-        ("value_falsy", ctypes.c_void_p), ("value_class", ctypes.c_void_p),
+        ("value_falsy", ctypes.c_void_p), ("value_class", ctypes.c_void_p), ("value_kind", ctypes.c_void_p),
     ]
 
 
@@ -87,6 +119,7 @@ class PropTable:
         self.values_json: list[str] = []
         self.values_falsy: list[int] = []
         self.values_class: list[int] = []
+        self.values_kind: list[int] = []
         self._class_ids: dict[Any, int] = {}
         self.set_ids: dict[tuple, int] = {}
         self.sets: list[tuple] = []
@@ -112,11 +145,40 @@ class PropTable:
             ck = jsjson.match_class_key(v)
             c = self._class_ids.setdefault(ck, len(self._class_ids))
             self.values_class.append(c)
+            self.values_kind.append(value_kind(v))
             self._c = None
         return i
 
     def intern(self, props: dict) -> int:
         pairs = tuple((self.key_id(k), self.value_id(props[k])) for k in jsjson.js_key_order(list(props.keys())))
+        return self._intern_pairs(pairs)
+
+    def intern_combine(self, props: dict, cop, seq: int) -> tuple[int, int]:
+        """(combine set, MT_OPF_* flags) of a remote annotate with a combining op other than
+        rewrite (include/mtgpu.h): the op's keys, each valued with what
+        combine(op, undefined, undefined, seq) yields (properties.ts:24-62 through
+        segmentPropertiesManager.ts:98-103), i.e. for a key the segment does not hold."""
+        name = cop.get("name") if isinstance(cop, dict) else None
+        has_def = isinstance(cop, dict) and "defaultValue" in cop
+        d = cop.get("defaultValue") if has_def else None
+        if name == "incr":                  # x + undefined: NaN, or a string for strings / objects
+            code = MT_VAL_NAN if (not has_def or d is None or _is_number(d)) else MT_VAL_UNSUP
+            fl = MT_OPF_COMBINE
+        elif name == "consensus":           # {value: undefined, seq}; null.seq throws; seq -1 is set
+            if not has_def:
+                code = MT_VAL_CFRESH
+            elif d is None:
+                code = MT_VAL_UNSUP
+            else:
+                code = self.value_id({**d, "seq": seq} if _seq_minus1(d) else d)
+            fl = MT_OPF_COMBINE | MT_OPF_REWRITE
+        else:                               # no case in combine's switch: the (default) value
+            code = MT_VAL_UNDEF if not has_def else (MT_VAL_NULL if d is None else self.value_id(d))
+            fl = MT_OPF_COMBINE | MT_OPF_REWRITE
+        pairs = tuple((self.key_id(k), code) for k in jsjson.js_key_order(list(props.keys())))
+        return self._intern_pairs(pairs), fl
+
+    def _intern_pairs(self, pairs: tuple) -> int:
         i = self.set_ids.get(pairs)
         if i is None:
             i = self.set_ids[pairs] = len(self.sets)
@@ -142,10 +204,11 @@ class PropTable:
         vj, vk = _cstr_array(self.values_json)
         vf = np.asarray(self.values_falsy or [0], np.uint8)
         vc = np.asarray(self.values_class or [0], np.uint32)
+        vkd = np.asarray(self.values_kind or [0], np.uint8)
         t = MtPropTable(len(self.sets), _ptr(off), _ptr(keys), _ptr(vals), len(self.keys),
                         ctypes.cast(kj, ctypes.c_void_p).value, _ptr(kidx), len(self.values_json),
-                        ctypes.cast(vj, ctypes.c_void_p).value, _ptr(vf), _ptr(vc))
-        self._c = (t, [off, keys, vals, kj, kk, kidx, vj, vk, vf, vc])
+                        ctypes.cast(vj, ctypes.c_void_p).value, _ptr(vf), _ptr(vc), _ptr(vkd))
+        self._c = (t, [off, keys, vals, kj, kk, kidx, vj, vk, vf, vc, vkd])
         return t
 
 
@@ -346,14 +409,21 @@ class BatchBuilder:
                 return
             pid = -1
             if t == MT_OP_ANNOTATE:
+                # segmentPropertiesManager.ts:55-56: rewrite = op && op.name === "rewrite", any other
+                # truthy combiningOp combines (properties.ts:24-62)
                 cop = op.get("combiningOp")
-                if cop is not None:
-                    fl |= MT_OPF_REWRITE if cop.get("name") == "rewrite" else MT_OPF_COMBINE
+                combine = jsjson.js_truthy(cop) and not (isinstance(cop, dict) and cop.get("name") == "rewrite")
+                if jsjson.js_truthy(cop) and not combine:
+                    fl |= MT_OPF_REWRITE
                 if isinstance(op.get("props"), dict) and MARKER_ID_KEY in op["props"]:
                     # re-keying a marker changes idToSegment only at later block updates
                     self._emit(type=MT_OP_UNSUPPORTED, flags=fl, **common)
                     return
-                pid = self.props.intern(op["props"])
+                if combine:
+                    pid, cfl = self.props.intern_combine(op["props"], cop, seq)
+                    fl |= cfl
+                else:
+                    pid = self.props.intern(op["props"])
             if jsjson.js_truthy(reg):                   # cut: Client.copy, then markRangeRemoved (:347-350)
                 if not isinstance(reg, str):
                     self._emit(type=MT_OP_UNSUPPORTED, flags=fl, **common)

@@ -56,21 +56,15 @@ static int mt_size_class_lists(mt_ctx* c) {
     return MT_OK;
 }
 
-// The continuation classes of block residency for the resident batch: runs of at least
-// cont_min_ops op records in [0, n_cont), the rest after them.
+// The continuation class of block residency for the resident batch: whether any run has at
+// least cont_min_ops op records (n_cont > 0 launches the kernel with the in-wave continuation).
 static int mt_cont_lists(mt_ctx* c) {
     if (c->cont_gen == c->batch_gen && c->cont_min_made == c->cont_min_ops) return MT_OK;
     const uint32_t R = c->n_runs;
-    std::vector<uint32_t> lst; lst.reserve(R);
     const bool ok = c->run_off.size() == R + 1;
-    for (uint32_t r = 0; r < R && ok; r++) if (c->run_off[r + 1] - c->run_off[r] >= c->cont_min_ops) lst.push_back(r);
-    c->n_cont = (uint32_t)lst.size();
-    for (uint32_t r = 0; r < R && ok; r++) if (c->run_off[r + 1] - c->run_off[r] < c->cont_min_ops) lst.push_back(r);
-    c->n_nocont = (uint32_t)lst.size() - c->n_cont;
-    if (!ok) { c->n_cont = 0; c->n_nocont = 0; }
-    int rc;
-    if ((rc = mtb_ensure(c, c->b_cruns, 4ull * lst.size() + 4))) return rc;
-    if (!lst.empty()) mtb_h2d(c, c->b_cruns.p, lst.data(), 4ull * lst.size());
+    uint32_t nc = 0;
+    for (uint32_t r = 0; r < R && ok; r++) nc += c->run_off[r + 1] - c->run_off[r] >= c->cont_min_ops;
+    c->n_cont = ok ? nc : 0; c->n_nocont = ok ? R - nc : 0;
     c->cont_gen = c->batch_gen; c->cont_min_made = c->cont_min_ops;
     return MT_OK;
 }
@@ -219,12 +213,7 @@ void MT_FN(destroy)(mt_ctx* c) {
                   S.ovx, S.mid, S.reg, c->ck_rows, c->ck_blk, c->ck_heap, c->ck_win, c->ck_text, c->ck_pset, c->ck_hdr,
                   c->ck_hold, c->ck_ovx, c->ck_mid, c->ck_reg, c->ck_regr, S.regr};
     for (void* p : ps) if (p) mtb_free(p);
-    mt_ctx::DevBuf* bs[] = {&c->b_gencl, &c->b_cursor, &c->b_doc, &c->b_off, &c->b_rec, &c->b_pay, &c->b_rel, &c->b_drec,
-                            &c->b_dcount, &c->b_pset_off,
-                            &c->b_pkey, &c->b_pval, &c->b_pfalsy, &c->b_pclass, &c->b_tmp0, &c->b_tmp1, &c->b_tmp2, &c->b_tmp3,
-                            &c->b_ld_meta, &c->b_ld_seg, &c->b_ld_pay, &c->b_ld_plan, &c->b_ld_poff, &c->b_dtext,
-                            &c->b_resume, &c->b_start, &c->b_batch, &c->b_runs};
-    for (auto* b : bs) if (b->p) mtb_free(b->p);
+    for (auto* b : c->dev_bufs()) if (b->p) mtb_free(b->p);
     mtb_fini(c);
     delete c;
 }
@@ -232,7 +221,15 @@ void MT_FN(destroy)(mt_ctx* c) {
 int MT_FN(docs_open)(mt_ctx* c, uint32_t first, uint32_t n) {
     if (!c || (uint64_t)first + n > c->S.maxDocs) return MT_E_INVALID;
     if (n == 0) return MT_OK;
+    for (uint32_t d = first; d < first + n && d < c->snap_chunk.size(); d++) c->snap_chunk[d] = 0;   // a new Client's options
     return mtb_launch_open(c, first, n);
+}
+int MT_FN(set_doc_snapshot_chunk)(mt_ctx* c, uint32_t n, const uint32_t* docs, const uint64_t* chunk) {
+    if (!c || (n && (!docs || !chunk))) return MT_E_INVALID;
+    for (uint32_t i = 0; i < n; i++) if (docs[i] >= c->S.maxDocs) { c->err = "doc id out of range"; return MT_E_INVALID; }
+    if (c->snap_chunk.size() < c->S.maxDocs) c->snap_chunk.resize(c->S.maxDocs, 0);
+    for (uint32_t i = 0; i < n; i++) c->snap_chunk[docs[i]] = chunk[i];
+    return MT_OK;
 }
 
 int MT_FN(set_props)(mt_ctx* c, const mt_prop_table* P) {
@@ -244,13 +241,16 @@ int MT_FN(set_props)(mt_ctx* c, const mt_prop_table* P) {
     if ((rc = mtb_ensure(c, c->b_pval, 4ull * npairs + 4))) return rc;
     if ((rc = mtb_ensure(c, c->b_pfalsy, 1ull * P->n_values + 1))) return rc;
     if ((rc = mtb_ensure(c, c->b_pclass, 4ull * P->n_values + 4))) return rc;
+    if ((rc = mtb_ensure(c, c->b_pkind, 1ull * P->n_values + 1))) return rc;
     mtb_h2d(c, c->b_pset_off.p, P->set_off, 4ull * (P->n_sets + 1));
     if (npairs) { mtb_h2d(c, c->b_pkey.p, P->key, 2ull * npairs); mtb_h2d(c, c->b_pval.p, P->value, 4ull * npairs); }
     if (P->n_values) { mtb_h2d(c, c->b_pfalsy.p, P->value_falsy, P->n_values); mtb_h2d(c, c->b_pclass.p, P->value_class, 4ull * P->n_values); }
+    if (P->n_values && P->value_kind) mtb_h2d(c, c->b_pkind.p, P->value_kind, P->n_values);
     mtb_sync(c);
     c->S.p_off = (const uint32_t*)c->b_pset_off.p; c->S.p_key = (const uint16_t*)c->b_pkey.p;
     c->S.p_val = (const int32_t*)c->b_pval.p; c->S.p_falsy = (const uint8_t*)c->b_pfalsy.p;
     c->S.p_class = (const uint32_t*)c->b_pclass.p; c->S.p_nsets = P->n_sets;
+    c->S.p_kind = (P->value_kind || !P->n_values) ? (const uint8_t*)c->b_pkind.p : nullptr;
     c->names.key_json.assign(P->key_json, P->key_json + P->n_keys);
     c->names.key_index.assign(P->key_index, P->key_index + P->n_keys);
     c->names.value_json.assign(P->value_json, P->value_json + P->n_values);
@@ -946,7 +946,8 @@ static int mt_snapshot_blobs(mt_ctx* c, uint32_t n, const uint32_t* docs, const 
             auto dn = c->doc_clients.find(docs[i]);
             std::vector<std::string> blobs = legacy ? mtsnap::snapshot_legacy_blobs(views[j], c->names)
                                                     : mtsnap::snapshot_blobs(views[j], c->names,
-                                                                             dn == c->doc_clients.end() ? nullptr : &dn->second);
+                                                                             dn == c->doc_clients.end() ? nullptr : &dn->second,
+                                                                             c->chunk_of(docs[i]));
             if (digest) digest[i] = mtsnap::blobs_digest(blobs);
             for (auto& b : blobs) { c->snap_arena += b; c->blob_off.push_back(c->snap_arena.size()); }
             c->blob_first.push_back((uint32_t)(c->blob_off.size() - 1));
@@ -985,7 +986,8 @@ int MT_FN(snapshot_digests)(mt_ctx* c, uint32_t n, const uint32_t* docs, const i
             for (uint32_t i = (uint32_t)t; i < m; i += (uint32_t)th) {
                 auto dn = c->doc_clients.find(docs[a + i]);
                 digest[a + i] = mtsnap::blobs_digest(mtsnap::snapshot_blobs(views[i], c->names,
-                                                                            dn == c->doc_clients.end() ? nullptr : &dn->second));
+                                                                            dn == c->doc_clients.end() ? nullptr : &dn->second,
+                                                                            c->chunk_of(docs[a + i])));
             }
         };
         std::vector<std::thread> pool;

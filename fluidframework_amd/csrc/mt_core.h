@@ -274,6 +274,7 @@ struct __attribute__((aligned(16))) MtDocHdr {
     int heapHW, winHW;                       // high-water marks (pool sizing, mt_doc_pools)
     int ovxN;                                // overlap side-list entries
     int regTop, regHalf;                     // register row arena: used ids, live half
+    int pNever;                              // a property map holding a never-equal value exists
     unsigned long long prof[8];              // MT_PROFILE builds: s_memtime cycles per phase
 };
 
@@ -298,6 +299,7 @@ struct MtState {                              // device pools, doc-major
     // interned op property sets (mt_prop_table)
     const uint32_t* p_off; const uint16_t* p_key; const int32_t* p_val;
     const uint8_t* p_falsy; const uint32_t* p_class; uint32_t p_nsets;
+    const uint8_t* p_kind;                    // MT_VK_* per value (null: combine sets unsupported)
 };
 
 struct __attribute__((aligned(16))) MtOpRec {  // one 32-byte op record (mt_op_batch member, packed)
@@ -489,6 +491,12 @@ struct WinI { int id; int delta; int parent; bool live; bool recycle; };
 enum { MT_WALK_SPLIT = 0, MT_WALK_INSERT = 1 };
 enum { MT_W_OK = 0, MT_W_NOCHANGE = 1, MT_W_FAIL = 2 };
 enum { MT_MAP_REMOVE = 0, MT_MAP_ANNOTATE = 1, MT_MAP_COLLECT = 2 };
+// How an annotate's prop set applies (applyPropSet): plain, rewrite, or a combining op
+// (MT_OPF_COMBINE: incr; MT_OPF_COMBINE | MT_OPF_REWRITE: consensus and other names).
+enum { MT_PM_SET = 0, MT_PM_REWRITE = 1, MT_PM_INCR = 2, MT_PM_KEEP = 3 };
+MT_INLINE int mt_prop_mode(uint32_t fl) {
+    return (fl & MT_OPF_COMBINE) ? ((fl & MT_OPF_REWRITE) ? MT_PM_KEEP : MT_PM_INCR) : ((fl & MT_OPF_REWRITE) ? MT_PM_REWRITE : MT_PM_SET);
+}
 
 // The wave's view of one document: doc-local pool pointers and the few global
 // parameters it needs (kept small: every field is wave-uniform and lives in SGPRs).
@@ -496,7 +504,7 @@ struct MtEngParams {
     uint32_t rowCap, heapCap, winCap, textCap, psetCap, p_nsets;
     uint16_t* textBase;
     const uint32_t* p_off; const uint16_t* p_key; const int32_t* p_val;
-    const uint8_t* p_falsy; const uint32_t* p_class;
+    const uint8_t* p_falsy; const uint32_t* p_class; const uint8_t* p_kind;
 };
 // The LDS pools live in one file-scope __shared__ object, so every access of
 // the LDS-resident engine (MtEngT<MT_RES_LDS / MT_RES_BLK>) is a ds_* instruction; the host
@@ -541,6 +549,7 @@ struct MtCold {
     uint32_t dused, tused; int dstop;
     int* regr; int regTop, regHalf, regCap;   // register row arena (this document's)
     int pcKey[4], pcVal[4];                   // newMap: property maps made from an op's set alone
+    int pNever;                               // MtDocHdr::pNever
 };
 #if defined(__HIP_DEVICE_COMPILE__)
 __shared__ MtCold mt_cold_v;
@@ -707,7 +716,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         };
         S.rowCap = uni(Ly->rowCap); S.heapCap = uni(Ly->heapCap); S.winCap = uni(Ly->winCap); S.textCap = uni(Ly->textCap);
         S.psetCap = uni(Ly->psetCap); S.p_nsets = st.p_nsets; S.p_off = st.p_off; S.p_key = st.p_key; S.p_val = st.p_val;
-        S.p_falsy = st.p_falsy; S.p_class = st.p_class; S.textBase = st.text + off(&Ly->text);
+        S.p_falsy = st.p_falsy; S.p_class = st.p_class; S.p_kind = st.p_kind; S.textBase = st.text + off(&Ly->text);
         blkCap = uni(Ly->blkCap); hdrp = st.hdr + d;
         R = st.rows + off(&Ly->row);
         blk = st.blk + off(&Ly->blk); heap = st.heap + off(&Ly->heap);
@@ -736,7 +745,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         for (int i = 0; i < 4; i++) mt_cold_v.pcKey[i] = -1;
         rfHbm = st.hold + (size_t)d * MT_RFL; rfN = uni(h.rfN); blkFreeN = uni(h.blkFreeN);
         heapHW = uni(h.heapHW); winHW = uni(h.winHW); ovxN = uni(h.ovxN);
-        regTop = uni(h.regTop); regHalf = uni(h.regHalf) & 1;
+        regTop = uni(h.regTop); regHalf = uni(h.regHalf) & 1; mt_cold_v.pNever = uni(h.pNever);
         if (regTop < 0 || regTop > regCap) regTop = 0;
         if (ovxN < 0 || ovxN > MT_OVX_CAP) ovxN = 0;
         lRows = lBlks = lHeap = 0; gRowCap = gBlkCap = gHeapCap = gWinCap = 0;
@@ -754,6 +763,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         h.blkTop = blkTop; h.blkFree = blkFree; h.heapN = heapN; h.winN = winN; h.textTop = textTop;
         h.psetTop = psetTop; h.status = status; h.textHalf = textHalf; h.rfN = rfN; h.blkFreeN = blkFreeN;
         h.heapHW = heapHW; h.winHW = winHW; h.ovxN = ovxN; h.regTop = regTop; h.regHalf = regHalf;
+        h.pNever = mt_cold_v.pNever;
         { const int n = rfN; int* dst = rfHbm;
           for (int base = 0; base < n; base += MT_WAVE) {
               const int m = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
@@ -783,7 +793,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         bk(0).len = 0; bk(0).parent = -1; bk(0).n = 0; bk(0).height = 0; bk(0).scour = -1;
         bpReset();
         wave_for(MT_REG_CAP, [&](int i) MT_LAM { regs[i].client = -1; regs[i].n = 0; regs[i].flags = 0; regs[i].off = 0; });
-        regTop = 0; regHalf = 0;
+        regTop = 0; regHalf = 0; mt_cold_v.pNever = 0;
         // idToSegment entries are not reset: an entry is read only for an id the host
         // already saw mapped in this document (mt_rel_pos.marker >= 0), and relPos
         // checks that the row still carries that id.
@@ -2259,17 +2269,23 @@ template <int RES, bool FULL = true> struct MtEngT {
     }
     MT_HD int pkey(int id, int i) const { return (int)pset[id + (i >> 4)].key[i & 15]; }
     MT_HD int pval(int id, int i) const { return pset[id + (i >> 4)].val[i & 15]; }
+    // matchProperties class of a stored value: NaN, undefined and fresh consensus objects
+    // (the values below 0) equal nothing, themselves included (MT_VAL_*, include/mtgpu.h).
+    MT_HD uint32_t pclass(int v) const { return v >= 0 ? S.p_class[v] : 0xFFFFFFFFu; }
+    // A map holding such a value matches no map, itself included (pset[id].pad[2], written
+    // only while the document has one: MtCold::pNever).
+    MT_HD bool pNeverMap(int a) const { return mt_cold_v.pNever && a >= 0 && uni(pset[a].pad[2]) != 0; }
     MT_HD bool propsMatch(int a, int b) {                      // matchProperties, MT/properties.ts:64-95
-        if (a == b) return true;
+        if (a == b) return !pNeverMap(a);
         if (a < 0 || b < 0) return false;
         const int na = uni(pset[a].n), nb = uni(pset[b].n);
         if (na != nb) return false;
         auto ok = wave_map(na, [&](int k) MT_LAM {
             const int key = pkey(a, k);
-            const uint32_t ca = S.p_class[pval(a, k)];
+            const uint32_t ca = pclass(pval(a, k));
             bool f = false;
-            for (int i = 0; i < nb; i++) if (pkey(b, i) == key && S.p_class[pval(b, i)] == ca) f = true;
-            return f;
+            for (int i = 0; i < nb; i++) f |= (pkey(b, i) == key) & (pclass(pval(b, i)) == ca);
+            return (f & (ca != 0xFFFFFFFFu)) != 0;
         });
         return wave_count(ok) == na;
     }
@@ -2483,6 +2499,11 @@ template <int RES, bool FULL = true> struct MtEngT {
                 const int a = own(fp1, t), b = own(fp, t);
                 return a == b;
             }));
+            if (mt_cold_v.pNever)                        // a shared map holding NaN / undefined
+                propOk &= ~wave_ballot(wave_map(span, [&](int t) MT_LAM {
+                    const int a = own(fp1, t), b = own(fp, t);
+                    return ((pm >> t) & 1ull) && a == b && a >= 0 && pset[a].pad[2] != 0;
+                }));
             for (uint64_t sb = slow; sb; sb &= sb - 1) {
                 const int k = __builtin_ctzll(sb);
                 if (propsMatch(wave_at(fp1, k), wave_at(fp, k))) propOk |= 1ull << k;
@@ -2708,13 +2729,17 @@ template <int RES, bool FULL = true> struct MtEngT {
     // first deletes keys whose new value is falsy or absent; then each key in
     // Object.keys order is deleted (null) or set (existing keys keep position).
     // Keys live one per lane (insertion order).
-    MT_HD int applyPropSet(int old, int opset, bool rewrite) {
+    // pm: MT_PM_SET / MT_PM_REWRITE, or a combining op (MT_PM_INCR; MT_PM_KEEP for consensus
+    // and other names): opset is then a combine set whose values are what combine yields
+    // for a key the segment does not hold (include/mtgpu.h), and a held key's new value
+    // follows from its old one (segmentPropertiesManager.ts:98-109, properties.ts:24-62).
+    MT_HD int applyPropSet(int old, int opset, int pm, int sq = 0) {
         if (opset < 0 || opset >= (int)S.p_nsets) { status |= MT_DS_UNSUPPORTED; return old; }
         int n = old >= 0 ? uni(pset[old].n) : 0;
         auto kk = wave_map(n, [&](int i) MT_LAM { return pkey(old, i); });
         auto vv = wave_map(n, [&](int i) MT_LAM { return pval(old, i); });
         const int o0 = uni((int)S.p_off[opset]), o1 = uni((int)S.p_off[opset + 1]);
-        if (rewrite && n > 0) {
+        if (pm == MT_PM_REWRITE && n > 0) {
             auto keep = wave_map(n, [&](int i) MT_LAM {
                 const int key = own(kk, i);
                 bool kp = false;
@@ -2731,10 +2756,26 @@ template <int RES, bool FULL = true> struct MtEngT {
             vv = wave_map(n, [&](int i) MT_LAM { return sc->holdLen[i]; });
             wave_sync();
         }
+        if (pm >= MT_PM_INCR && !S.p_kind) { status |= MT_DS_UNSUPPORTED; return old; }
         for (int q = o0; q < o1; q++) {
-            const int key = uni((int)S.p_key[q]), nv = uni((int)S.p_val[q]);
+            const int key = uni((int)S.p_key[q]);
+            int nv = uni((int)S.p_val[q]);
             const int at = wave_first(wave_map(n, [&](int i) MT_LAM { return own(kk, i) == key; }));
-            if (nv < 0) {
+            if (pm >= MT_PM_INCR) {
+                // combine(op, previousValue, undefined, seq): a held value undefined counts as
+                // not held; incr of a number / boolean / NaN is NaN, of anything else a string
+                // (off the path); consensus keeps the value unless it is an object whose seq
+                // is -1 (shared by every segment split from the one it was set on)
+                const int pv = at >= 0 ? wave_at(vv, at) : MT_VAL_UNDEF;
+                if (pv != MT_VAL_UNDEF) {
+                    const uint32_t kd = pv >= 0 ? (uint32_t)uni((int)S.p_kind[pv]) : (pv == MT_VAL_NAN ? MT_VK_NUM : 0u);
+                    if (pm == MT_PM_INCR) nv = (kd & MT_VK_NUM) ? MT_VAL_NAN : MT_VAL_UNSUP;
+                    else nv = (kd & MT_VK_SEQM1) ? MT_VAL_UNSUP : pv;
+                }
+                if (nv == MT_VAL_CFRESH) nv = sq >= 0 ? MT_VAL_CONS(sq) : MT_VAL_UNSUP;
+                if (nv == MT_VAL_UNSUP) { status |= MT_DS_UNSUPPORTED; return old; }
+            }
+            if (nv == MT_VAL_NULL) {
                 if (at >= 0) {
                     auto k1 = wave_from(kk, 1), v1 = wave_from(vv, 1);
                     kk = wave_map(MT_PKEYS, [&](int i) MT_LAM { const int a = own(kk, i), b = own(k1, i); return i < at ? a : b; });
@@ -2755,11 +2796,15 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (psetTop + nch > (int)S.psetCap) { status |= MT_DS_OOM_PROPS; return old; }
         const int id = psetTop;
         psetTop += nch;
+        // never-equal values (NaN, undefined, fresh consensus objects; made by a combining op
+        // or kept from the old map) mark the map
+        const int never = wave_ballot(wave_map(nn, [&](int i) MT_LAM { return own(vv, i) < 0; })) ? 1 : 0;
+        if (never) mt_cold_v.pNever = 1;
         wave_for(nch * MT_PSK, [&](int i) MT_LAM {
             pset[id + (i >> 4)].key[i & 15] = (uint16_t)(i < nn ? own(kk, i) : 0);
             pset[id + (i >> 4)].val[i & 15] = i < nn ? own(vv, i) : 0;
         });
-        wave_for(nch, [&](int k) MT_LAM { pset[id + k].n = nn; });
+        wave_for(nch, [&](int k) MT_LAM { pset[id + k].n = nn; pset[id + k].pad[2] = never; });
         return id;
     }
 
@@ -2770,7 +2815,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     MT_HD int newPropMap(int opset) {
         const int k = opset & 3;
         if (mt_cold_v.pcKey[k] == opset) return mt_cold_v.pcVal[k];
-        const int id = applyPropSet(-1, opset, false);
+        const int id = applyPropSet(-1, opset, MT_PM_SET);
         if (status) return id;
         mt_cold_v.pcKey[k] = opset; mt_cold_v.pcVal[k] = id;
         return id;
@@ -2788,7 +2833,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     // both boundary walks passed through, tree unchanged since): the root walk would visit
     // only that branch above it, so the walk starts there and the observer-length change is
     // added to the ancestors above.  Delta capture starts at the root (observer offsets).
-    MT_HD void rangeMap(int mode, int start, int end, int r, int c, int sq, int opset, bool rewrite, int L0 = 0) {
+    MT_HD void rangeMap(int mode, int start, int end, int r, int c, int sq, int opset, int pm, int L0 = 0) {
         if (!(uValid && uRef == r && uCli == c)) { computeU(r, c, false); L0 = 0; }
         const bool rec = FULL && drec != nullptr;
         if (rec) L0 = 0;
@@ -2880,7 +2925,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                             const int old = wave_at(lp, j);
                             int nw;
                             if (old == lastOld) nw = lastNew;
-                            else { nw = applyPropSet(old, opset, rewrite); lastOld = old; lastNew = nw; }
+                            else { nw = applyPropSet(old, opset, pm, sq); lastOld = old; lastNew = nw; }
                             row(s).props = nw;
                             if (rec) emitDelta(MT_DK_ANNOTATE, base + wave_at(opre, j), uni(row(s).len), s, old, nw);
                         }
@@ -3164,13 +3209,13 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (e < 0) { status |= MT_DS_UNSUPPORTED; return; }          // MT_REG_CAP registers in use
         nCol = 0;
         const uint32_t cr0 = c_rows;
-        rangeMap(MT_MAP_COLLECT, start, end, r, c, 0, -1, false);   // sources into the arena's tail
+        rangeMap(MT_MAP_COLLECT, start, end, r, c, 0, -1, MT_PM_SET);   // sources into the arena's tail
         if (status) return;
         if (regTop + nCol > regCap) {                               // compact, then collect again
             regCompact();
             if (regTop + nCol > regCap) { status |= MT_DS_UNSUPPORTED; return; }
             nCol = 0; c_rows = cr0;                                 // (counted once)
-            rangeMap(MT_MAP_COLLECT, start, end, r, c, 0, -1, false);
+            rangeMap(MT_MAP_COLLECT, start, end, r, c, 0, -1, MT_PM_SET);
             if (status) return;
         }
         const int n = nCol, base = regTop;
@@ -3273,7 +3318,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         wave_sync();
         zamboni();
     }
-    MT_HD void opRange(int mode, int start, int end, int r, int c, int sq, int opset, bool rewrite) {
+    MT_HD void opRange(int mode, int start, int end, int r, int c, int sq, int opset, int pm) {
         MT_PB(t0);
         int w = walk(MT_WALK_SPLIT, start, r, c, -1, 0);
         if (w == MT_W_OK) c_rows += 2;
@@ -3294,7 +3339,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (w == MT_W_FAIL || lastSplit || !uValid) L0 = 0;
         MT_PE(MT_PH_SPLIT, t0);
         MT_PB(t1);
-        rangeMap(mode, start, end, r, c, sq, opset, rewrite, L0);
+        rangeMap(mode, start, end, r, c, sq, opset, pm, L0);
         MT_PE(MT_PH_RANGE, t1);
         if (status) return;
         zamboni();

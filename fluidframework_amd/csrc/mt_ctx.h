@@ -24,9 +24,20 @@ struct mt_ctx {
     std::string err;
     // device op batch (resident)
     struct DevBuf { void* p = nullptr; size_t cap = 0; };
-    DevBuf b_stage, b_pack_docs, b_pack_sz, b_pack_off, b_gencl, b_cursor, b_doc, b_off, b_rec, b_pay, b_pbase, b_rel, b_drec, b_dcount, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_tmp0, b_tmp1, b_tmp2, b_tmp3,
+    DevBuf b_stage, b_pack_docs, b_pack_sz, b_pack_off, b_gencl, b_cursor, b_doc, b_off, b_rec, b_pay, b_pbase, b_rel, b_drec, b_dcount, b_pset_off, b_pkey, b_pval, b_pfalsy, b_pclass, b_pkind, b_tmp0, b_tmp1, b_tmp2, b_tmp3,
            b_ld_meta, b_ld_seg, b_ld_pay, b_ld_plan, b_ld_poff, b_dtext, b_resume, b_start,
            b_q, b_qgrp, b_qout, b_qat, b_qlen, b_qoff, b_qtext;   // position queries (mt_get_containing_segment)
+    DevBuf b_runs, b_batch;
+    // Every device buffer above, for mt_destroy (one list beside the declarations).
+    std::vector<DevBuf*> dev_bufs() {
+        return {&b_stage, &b_pack_docs, &b_pack_sz, &b_pack_off, &b_gencl, &b_cursor, &b_doc, &b_off, &b_rec, &b_pay, &b_pbase,
+                &b_rel, &b_drec, &b_dcount, &b_pset_off, &b_pkey, &b_pval, &b_pfalsy, &b_pclass, &b_pkind, &b_tmp0, &b_tmp1,
+                &b_tmp2, &b_tmp3, &b_ld_meta, &b_ld_seg, &b_ld_pay, &b_ld_plan, &b_ld_poff, &b_dtext, &b_resume, &b_start, &b_q,
+                &b_qgrp, &b_qout, &b_qat, &b_qlen, &b_qoff, &b_qtext, &b_runs, &b_batch};
+    }
+    // options.mergeTreeSnapshotChunkSize per document (mt_set_doc_snapshot_chunk; 0 = 10,000)
+    std::vector<uint64_t> snap_chunk;
+    uint64_t chunk_of(uint32_t d) const { return d < snap_chunk.size() ? snap_chunk[d] : 0; }
     MtOps ops{};
     uint32_t n_runs = 0;
     std::vector<uint32_t> run_off;     // host copy of the resident batch's op offsets (n_runs + 1)
@@ -36,7 +47,6 @@ struct mt_ctx {
     // rest; the run lists live in b_runs (long runs first), rebuilt per resident batch.
     uint32_t big_min_ops = 0;
     uint64_t runs_gen = ~0ull; uint32_t runs_min = 0, n_long = 0, n_short = 0;
-    DevBuf b_runs;
     void* stream2 = nullptr; void* ev_fork = nullptr; void* ev_join = nullptr;
     // Partitioned size classes (mt_set_partition): part_cus > 0 sends the long runs to the
     // block-residency kernel on a stream masked to part_cus CUs, one document per SIMD (the
@@ -48,7 +58,6 @@ struct mt_ctx {
     // in a second, all-HBM launch).
     uint32_t cont_min_ops = 16384, n_cont = 0, n_nocont = 0, cont_min_made = 0;
     uint64_t cont_gen = ~0ull;
-    DevBuf b_cruns;
     void* streamA = nullptr; void* streamB = nullptr; void* ev_joinB = nullptr;
     // mt_apply_batch / mt_upload_batch staging: two pinned host slots used alternately, each
     // with the event of its last H2D, and one device region the batch lands in
@@ -57,7 +66,6 @@ struct mt_ctx {
     int stage_k = 0;
     void* dl_host[2] = {nullptr, nullptr}; size_t dl_cap[2] = {0, 0};   // pinned host buffers of document staging (downloads)
     uint32_t stage_epoch = 0x7E000000u;            // marks of a staging's referenced property maps
-    DevBuf b_batch;
     MtGen gen{};
     uint32_t gen_docs = 0;
     std::vector<uint32_t> gen_off;     // op offsets of the generated runs

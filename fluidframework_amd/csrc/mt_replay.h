@@ -153,16 +153,15 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
                 e.opInsert(q1, r, c, sq, payR + poff, plen, marker, p2, (fl & MT_OPF_SEG_PROPS) ? pid : -1,
                            (marker && (fl & MT_OPF_MARKER_ID)) ? (int)poff : -1, pay);
             } else if (ty == MT_OP_REMOVE) {
-                e.opRange(MT_MAP_REMOVE, q1, q2, r, c, sq, -1, false);
+                e.opRange(MT_MAP_REMOVE, q1, q2, r, c, sq, -1, MT_PM_SET);
             } else if (ty == MT_OP_ANNOTATE) {
-                if (fl & MT_OPF_COMBINE) { e.status |= MT_DS_UNSUPPORTED; break; }
-                e.opRange(MT_MAP_ANNOTATE, q1, q2, r, c, sq, pid, (fl & MT_OPF_REWRITE) != 0);
+                e.opRange(MT_MAP_ANNOTATE, q1, q2, r, c, sq, pid, mt_prop_mode(fl));
             } else if (ty >= MT_OP_CUT && ty <= MT_OP_PASTE) {
                 if constexpr (Eng::kFull) {
                     if (ty == MT_OP_PASTE) e.opPaste(q1, r, c, sq, (int)poff);
                     else {
                         e.opCopy(q1, q2, r, c, (int)poff);                   // CUT: copy, then markRangeRemoved
-                        if (ty == MT_OP_CUT && !e.status) e.opRange(MT_MAP_REMOVE, q1, q2, r, c, sq, -1, false);
+                        if (ty == MT_OP_CUT && !e.status) e.opRange(MT_MAP_REMOVE, q1, q2, r, c, sq, -1, MT_PM_SET);
                     }
                 } else { e.status |= MT_DS_UNSUPPORTED; break; }            // launched without register support
             } else { e.status |= MT_DS_BAD_OP; break; }
@@ -196,7 +195,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
 
 // cursor[] flag: the run left LDS at the op index in the low bits and finished in HBM in the same
 // wave (the all-HBM launch that follows skips it; mt_last_cursors reports the hand-over op).
-#define MT_CUR_DONE 0x80000000u
+#define MT_CUR_DONE MT_CURSOR_DONE          // include/mtgpu.h
 // One document run of a replay launch (every replay kernel and the host emulation run this).
 // The run starts at ops.start[run] (a capture resume) or op_off[run]; RES is the residency it
 // starts in.  A document that outgrows the LDS pools continues in HBM in the same wave when

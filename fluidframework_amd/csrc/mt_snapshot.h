@@ -6,8 +6,9 @@
 // for the passive-observer path: walk segments in tree order
 // (walkAllSegments, mergeTree.ts:2998), elide rows removed at or below the MSN,
 // greedily coalesce rows at or below the MSN (TextSegment.canAppend +
-// matchProperties on clones), keep merge info for the rest, chunk at 10,000
-// characters, and serialize exactly as JSON.stringify does.
+// matchProperties on clones), keep merge info for the rest, chunk at
+// options.mergeTreeSnapshotChunkSize (default 10,000) characters, and serialize exactly as
+// JSON.stringify does.
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -91,10 +92,16 @@ inline void props_json(std::string& o, const MtPSet* p, const MtNames& nm) {
     for (int i = 0; i < ni; i++) order[m++] = idx[i];
     for (int i = 0; i < n; i++) if (nm.key_index[pset_key(p, i)] == 0xFFFFFFFFu) order[m++] = i;
     o.push_back('{');
+    bool first = true;
     for (int q = 0; q < m; q++) {
-        if (q) o.push_back(',');
-        const int i = order[q];
-        o += nm.key_json[pset_key(p, i)]; o.push_back(':'); o += nm.value_json[pset_val(p, i)];
+        const int i = order[q], v = pset_val(p, i);
+        if (v == MT_VAL_UNDEF) continue;                       // JSON.stringify skips undefined members
+        if (!first) o.push_back(',');
+        first = false;
+        o += nm.key_json[pset_key(p, i)]; o.push_back(':');
+        if (v >= 0) o += nm.value_json[v];
+        else if (v <= MT_VAL_CONS_BASE) { o += "{\"seq\":"; put_int(o, (long long)MT_VAL_CONS_BASE - v); o.push_back('}'); }
+        else o += "null";                                       // NaN
     }
     o.push_back('}');
 }
@@ -146,15 +153,18 @@ inline void seg_json(std::string& o, const MtSnapView& v, PropsJson& pj, int s, 
     seg_json_of(o, (v.R[s].meta & MT_M_MARKER) != 0, v.R[s].toff, pj.get(v.R[s].props), txt, tn);
 }
 
+// matchProperties class of a stored value; NaN, undefined and fresh consensus objects (< 0)
+// equal nothing, and a map holding one (pad[2]) matches no map, itself included.
+inline uint32_t value_class_of(const MtNames& nm, int v) { return v >= 0 ? nm.value_class[v] : 0xFFFFFFFFu; }
 inline bool props_match(const MtSnapView& v, const MtNames& nm, int a, int b) {
-    if (a == b) return true;
+    if (a == b) return a < 0 || v.pset[a].pad[2] == 0;
     if (a < 0 || b < 0) return false;
     const MtPSet* pa = v.pset + a; const MtPSet* pb = v.pset + b;
-    if (pa->n != pb->n) return false;
+    if (pa->n != pb->n || pa->pad[2] || pb->pad[2]) return false;
     for (int i = 0; i < pa->n; i++) {
         bool f = false;
         for (int j = 0; j < pb->n; j++)
-            if (pset_key(pb, j) == pset_key(pa, i) && nm.value_class[pset_val(pb, j)] == nm.value_class[pset_val(pa, i)]) f = true;
+            if (pset_key(pb, j) == pset_key(pa, i) && value_class_of(nm, pset_val(pb, j)) == value_class_of(nm, pset_val(pa, i))) f = true;
         if (!f) return false;
     }
     return true;
@@ -166,7 +176,7 @@ struct PropsMatch {
     long long key[16]; bool val[16];
     PropsMatch(const MtSnapView& v_, const MtNames& nm_) : v(v_), nm(nm_) { for (auto& k : key) k = -1; }
     bool operator()(int a, int b) {
-        if (a == b) return true;
+        if (a == b) return a < 0 || v.pset[a].pad[2] == 0;
         if (a < 0 || b < 0) return false;
         const long long k = ((long long)a << 32) | (unsigned)b;
         const int h = (int)(((unsigned)a * 31u + (unsigned)b) & 15u);
@@ -175,8 +185,11 @@ struct PropsMatch {
         return val[h];
     }
 };
+// chunk: options.mergeTreeSnapshotChunkSize (snapshotV1.ts:55; 0: SnapshotV1.chunkSize).
 inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtNames& nm,
-                                               const std::vector<std::string>* doc_clients = nullptr) {
+                                               const std::vector<std::string>* doc_clients = nullptr,
+                                               uint64_t chunk = 0) {
+    const unsigned long long chunkLen = chunk ? (unsigned long long)chunk : 10000ull;
     const std::vector<std::string>& cj = doc_clients ? *doc_clients : nm.client_json;
     const int minSeq = v.hdr.minSeq, curSeq = v.hdr.curSeq;
     PropsJson pj(v, nm);
@@ -229,7 +242,7 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
     std::vector<Chunk> chunks; size_t total = 0; long long totalLen = 0;
     do {
         Chunk c{total, 0, 0};
-        while (c.length < 10000 && c.start + c.count < segs.size()) { c.length += lens[c.start + c.count]; c.count++; }
+        while ((unsigned long long)c.length < chunkLen && c.start + c.count < segs.size()) { c.length += lens[c.start + c.count]; c.count++; }
         chunks.push_back(c); total += c.count; totalLen += c.length;
     } while (total < segs.size());
     std::vector<std::string> blobs;

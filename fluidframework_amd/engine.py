@@ -116,6 +116,7 @@ def _bind(lib, prefix: str):
         get_containing_segment=f("get_containing_segment", ctypes.c_int,
                                  [P, U32, P, P, P, P, P, ctypes.POINTER(P), ctypes.POINTER(P)]),
         resolve_remote_position=f("resolve_remote_position", ctypes.c_int, [P, U32, P, P, P, P, P]),
+        set_doc_snapshot_chunk=f("set_doc_snapshot_chunk", ctypes.c_int, [P, U32, P, P]),
     )
 
 
@@ -408,12 +409,21 @@ class Engine:
         return k[:n.value].copy(), v[:n.value].copy()
 
     def pset_dict(self, doc: int, pset_id: int):
-        """A device property set as a Python dict (None for -1: properties undefined)."""
-        import json as _json
+        """A device property set as a Python dict (None for -1: properties undefined); NaN,
+        undefined and fresh consensus values decoded as batch.decode_value does."""
+        from .batch import decode_value
         if pset_id < 0:
             return None
         keys, vals = self.doc_pset(doc, pset_id)
-        return {self.props.keys[int(k)]: _json.loads(self.props.values_json[int(v)]) for k, v in zip(keys, vals)}
+        return {self.props.keys[int(k)]: decode_value(int(v), self.props.values_json) for k, v in zip(keys, vals)}
+
+    def set_snapshot_chunk(self, docs, chunk_size):
+        """mt_set_doc_snapshot_chunk: options.mergeTreeSnapshotChunkSize per document (0: the
+        default 10,000)."""
+        d = _u32(docs)
+        c = np.ascontiguousarray(chunk_size, np.uint64)
+        self._check(self.fn["set_doc_snapshot_chunk"](self.h, len(d), d.ctypes.data, c.ctypes.data),
+                    "mt_set_doc_snapshot_chunk")
 
     def update_seq(self, docs, msn, seq):
         d, m, s = _u32(docs), _i32(msn), _i32(seq)
@@ -530,6 +540,27 @@ def catchup_ops(blobs: dict, snap) -> list:
 NON_COLLAB_CLIENT = -2                  # NonCollabClient, MT/constants.ts
 
 
+def snapshot_chunk_option(options: dict | None) -> int:
+    """options.mergeTreeSnapshotChunkSize as mt_set_doc_snapshot_chunk takes it (snapshotV1.ts:55:
+    `?? SnapshotV1.chunkSize`): 0 for the default, the size rounded up (lengths are integers,
+    `length < chunkSize`), 2**64-1 for Infinity.  The reference's chunk loop never ends for a
+    size that is not a positive number (NaN, 0, negative, a non-numeric value), so those raise."""
+    import math
+    v = (options or {}).get("mergeTreeSnapshotChunkSize")
+    if v is None:
+        return 0
+    if isinstance(v, str):               # `length < "100"` compares numerically
+        try:
+            v = float(v.strip()) if v.strip() else 0.0
+        except ValueError:
+            v = float("nan")
+    if isinstance(v, bool) or not isinstance(v, (int, float)) or not (v > 0):
+        raise MergeTreeError(f"mergeTreeSnapshotChunkSize {v!r}: the reference's chunk loop would not end")
+    if math.isinf(v):
+        return (1 << 64) - 1
+    return min(int(math.ceil(v)), (1 << 64) - 2)
+
+
 class Segment:
     """A segment as Client.getContainingSegment hands it out: the ISegment fields
     (MT/mergeTree.ts:87-122) of a TextSegment or Marker, by value.  The reference hands out
@@ -545,12 +576,15 @@ class Segment:
         self.removedClientId = client._short_of(int(info["removed_client"])) if self.removedSeq is not None else None
         j = json.loads(js)
         self._json = j
+        # properties from the device map (NaN / undefined / consensus values as the reference
+        # holds them; the JSON text has them as JSON.stringify writes them)
+        props = client.engine.pset_dict(client.doc_id, int(info["prop_set"])) if int(info["prop_set"]) >= 0 else None
         if isinstance(j, str):
             self.text, self.properties = j, None
         elif "marker" in j:
-            self.text, self.refType, self.properties = None, j["marker"]["refType"], j.get("props")
+            self.text, self.refType, self.properties = None, j["marker"]["refType"], props
         else:
-            self.text, self.properties = j["text"], j.get("props")
+            self.text, self.properties = j["text"], props
         self._obs_pos = int(info["obs_pos"])
         self._doc, self._version = client.doc_id, version
 
@@ -737,7 +771,10 @@ class ClientGroup:
         d = len(self.clients)
         if d >= self.engine.max_docs:
             raise MergeTreeError("engine document capacity exhausted")
+        cs = snapshot_chunk_option(options)
         self.engine.open_docs(d, 1)
+        if cs:
+            self.engine.set_snapshot_chunk([d], [cs])
         c = MergeTreeClient(self.engine, d, self, options)
         self.clients.append(c)
         return c

@@ -12,6 +12,11 @@ const OP_CUT = 5, OP_COPY = 6, OP_PASTE = 7;          // register ops (include/m
 const F_END = 1, F_MARKER = 2, F_REWRITE = 4, F_SEG_PROPS = 8, F_COMBINE = 16, F_REL1 = 0x20, F_REL2 = 0x40,
     F_MARKER_ID = 0x80;
 const MARKER_ID_KEY = "markerId";   // reservedMarkerIdKey, MT/mergeTree.ts:591
+// property values other than interned ids, and value kinds (include/mtgpu.h MT_VAL_*, MT_VK_*)
+const VAL_NULL = -1, VAL_NAN = -2, VAL_UNSUP = -3, VAL_CFRESH = -4, VAL_UNDEF = -5, VAL_CONS_BASE = -16;
+const VK_NUM = 1, VK_SEQM1 = 2;
+const isNumberLike = (v) => typeof v === "number" || typeof v === "boolean";      // x + undefined is NaN
+const seqMinus1 = (v) => v !== null && typeof v === "object" && !Array.isArray(v) && v.seq === -1;   // properties.ts:52
 function arrayIndex(k) {
     // canonical array index (OrdinaryOwnPropertyKeys orders these first)
     if (!/^(0|[1-9][0-9]{0,9})$/.test(k)) return undefined;
@@ -34,7 +39,7 @@ function matchClassKey(v) {
 class PropTable {
     constructor() {
         this.keyIds = new Map(); this.keys = [];
-        this.valueIds = new Map(); this.valueJson = []; this.valueFalsy = []; this.valueClass = [];
+        this.valueIds = new Map(); this.valueJson = []; this.valueFalsy = []; this.valueClass = []; this.valueKind = [];
         this.classIds = new Map();
         this.setIds = new Map(); this.sets = [];
     }
@@ -56,11 +61,34 @@ class PropTable {
             let c = this.classIds.get(ck);
             if (c === undefined) { c = this.classIds.size; this.classIds.set(ck, c); }
             this.valueClass.push(c);
+            this.valueKind.push((isNumberLike(v) ? VK_NUM : 0) | (seqMinus1(v) ? VK_SEQM1 : 0));
         }
         return i;
     }
     intern(props) {
-        const pairs = Object.keys(props).map((k) => [this.keyId(k), this.valueId(props[k])]);
+        return this.internPairs(Object.keys(props).map((k) => [this.keyId(k), this.valueId(props[k])]));
+    }
+    /**
+     * [combine set, flags] of a remote annotate with a combining op other than "rewrite"
+     * (include/mtgpu.h): the op's keys, each valued with what combine(op, undefined, undefined,
+     * seq) yields (properties.ts:24-62 via segmentPropertiesManager.ts:98-103).
+     */
+    internCombine(props, cop, seq) {
+        const d = cop.defaultValue;
+        let code, fl;
+        if (cop.name === "incr") {                          // x + undefined: NaN, or a string
+            code = (d === undefined || d === null || isNumberLike(d)) ? VAL_NAN : VAL_UNSUP;
+            fl = F_COMBINE;
+        } else if (cop.name === "consensus") {              // {value: undefined, seq}; null.seq throws
+            code = d === undefined ? VAL_CFRESH : (d === null ? VAL_UNSUP : this.valueId(seqMinus1(d) ? { ...d, seq } : d));
+            fl = F_COMBINE | F_REWRITE;
+        } else {                                            // no case in combine's switch
+            code = d === undefined ? VAL_UNDEF : (d === null ? VAL_NULL : this.valueId(d));
+            fl = F_COMBINE | F_REWRITE;
+        }
+        return [this.internPairs(Object.keys(props).map((k) => [this.keyId(k), code])), fl];
+    }
+    internPairs(pairs) {
         const sig = pairs.map((p) => p.join(":")).join(",");
         let i = this.setIds.get(sig);
         if (i === undefined) { i = this.sets.length; this.setIds.set(sig, i); this.sets.push(pairs); }
@@ -77,6 +105,7 @@ class PropTable {
             valueJson: this.valueJson,
             valueFalsy: Uint8Array.from(this.valueFalsy.length ? this.valueFalsy : [0]),
             valueClass: Uint32Array.from(this.valueClass.length ? this.valueClass : [0]),
+            valueKind: Uint8Array.from(this.valueKind.length ? this.valueKind : [0]),
         };
     }
 }
@@ -196,9 +225,15 @@ class BatchBuilder {
             if (pos1 === undefined || pos2 === undefined) { bad(); return; }
             let pid = -1;
             if (op.type === OP_ANNOTATE) {
-                if (op.combiningOp) fl |= op.combiningOp.name === "rewrite" ? F_REWRITE : F_COMBINE;
+                // segmentPropertiesManager.ts:55-56: rewrite = op && op.name === "rewrite"; any other
+                // truthy combiningOp combines (properties.ts:24-62)
+                const cop = op.combiningOp, combine = !!cop && cop.name !== "rewrite";
+                if (cop && !combine) fl |= F_REWRITE;
                 if (op.props && typeof op.props === "object" && MARKER_ID_KEY in op.props) { bad(); return; }   // re-keyed marker ids
-                pid = this.props.intern(op.props);
+                if (combine) {
+                    const [id, cfl] = this.props.internCombine(op.props, cop, seq);
+                    pid = id; fl |= cfl;
+                } else pid = this.props.intern(op.props);
             }
             if (op.type === OP_REMOVE && op.register) {     // cut: Client.copy, then markRangeRemoved (:347-350)
                 if (typeof op.register !== "string") { bad(); return; }
@@ -248,6 +283,7 @@ class BatchBuilder {
 }
 
 
-module.exports = { OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_GROUP, OP_UNSUPPORTED, OP_CUT, OP_COPY, OP_PASTE,
+module.exports = { VAL_NULL, VAL_NAN, VAL_UNSUP, VAL_CFRESH, VAL_UNDEF, VAL_CONS_BASE, VK_NUM, VK_SEQM1,
+    OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_GROUP, OP_UNSUPPORTED, OP_CUT, OP_COPY, OP_PASTE,
     F_END, F_MARKER, F_REWRITE, F_SEG_PROPS, F_COMBINE, F_REL1, F_REL2, F_MARKER_ID, MARKER_ID_KEY, arrayIndex,
     matchClassKey, PropTable, ClientNames, mergeTreeMembers, COLS, Col, BatchBuilder };

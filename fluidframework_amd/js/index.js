@@ -26,7 +26,7 @@ const path = require("path");
 // MTGPU_NAPI: an alternate build of this addon (the tests' host-emulation build)
 const addon = require(process.env.MTGPU_NAPI || path.join(__dirname, "mtgpu.node"));
 
-const { OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_GROUP, OP_UNSUPPORTED, OP_CUT, OP_COPY, OP_PASTE,
+const { VAL_NAN, VAL_UNDEF, VAL_CONS_BASE, OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_GROUP, OP_UNSUPPORTED, OP_CUT, OP_COPY, OP_PASTE,
     F_END, F_MARKER, F_REWRITE, F_SEG_PROPS, F_COMBINE, F_REL1, F_REL2, F_MARKER_ID, MARKER_ID_KEY, arrayIndex,
     matchClassKey, PropTable, ClientNames, mergeTreeMembers, BatchBuilder } = require("./builder.js");
 const STATUS = {
@@ -171,6 +171,30 @@ class LoadBuilder {
 
 const DEFAULT_LIMITS = { rowsPerDoc: 8192, windowPerDoc: 4096, propsetsPerDoc: 8192, textPerDoc: 1 << 16, markersPerDoc: 4096 };
 
+/** A stored property value id (mt_doc_pset) as a JS value (include/mtgpu.h MT_VAL_*). */
+function decodeValue(v, valueJson) {
+    if (v >= 0) return JSON.parse(valueJson[v]);
+    if (v === VAL_NAN) return NaN;
+    if (v === VAL_UNDEF) return undefined;
+    if (v <= VAL_CONS_BASE) return { value: undefined, seq: VAL_CONS_BASE - v };
+    throw new Error(`not a stored property value: ${v}`);
+}
+
+/**
+ * options.mergeTreeSnapshotChunkSize as mt_set_doc_snapshot_chunk takes it
+ * (`options?.mergeTreeSnapshotChunkSize ?? SnapshotV1.chunkSize`, snapshotV1.ts:55): 0 for the
+ * default; the reference's chunk loop (`length < chunkSize`) never ends for NaN or a size <= 0.
+ */
+function snapshotChunkOption(options) {
+    const v = options ? options.mergeTreeSnapshotChunkSize : undefined;
+    if (v === undefined || v === null) return 0;
+    const x = Number(v);
+    if (typeof v === "object" || typeof v === "boolean" || !(x > 0)) {
+        throw new Error(`mergeTreeSnapshotChunkSize ${String(v)}: the reference's chunk loop would not end`);
+    }
+    return x;
+}
+
 /** One engine context (one GPU) and the documents it holds. */
 class Engine {
     constructor(maxDocs, limits = {}, device = 0) {
@@ -228,14 +252,17 @@ class Engine {
     deltaRecords() { return addon.deltaRecords(this.h); }
     /** The last batch's pasted text (mt_delta_text): INSERT records with b === 0 index it. */
     deltaText() { return addon.deltaText(this.h); }
-    /** A document's device property set as a plain object (undefined for -1). */
+    /** A document's device property set as a plain object (undefined for -1); NaN, undefined and
+     * fresh consensus objects ({value: undefined, seq}, properties.ts:43-47) as the reference holds them. */
     psetObject(doc, id) {
         if (id < 0) return undefined;
         const { keys, values } = addon.docPset(this.h, doc, id);
         const o = {};
-        keys.forEach((k, i) => { o[this.props.keys[k]] = JSON.parse(this.props.valueJson[values[i]]); });
+        keys.forEach((k, i) => { o[this.props.keys[k]] = decodeValue(values[i], this.props.valueJson); });
         return o;
     }
+    /** options.mergeTreeSnapshotChunkSize of documents (snapshotV1.ts:55; 0: the default). */
+    setSnapshotChunk(docs, sizes) { addon.setDocSnapshotChunk(this.h, Uint32Array.from(docs), Float64Array.from(sizes)); }
 }
 
 /**
@@ -353,7 +380,7 @@ class MergeTreeClient {
             cachedLength: q.len, seq: q.seq, clientId: shortOf(q.client),
             removedSeq: q.removedSeq === -(2 ** 31) ? undefined : q.removedSeq,
             removedClientId: q.removedSeq === -(2 ** 31) ? undefined : shortOf(q.removedClient),
-            properties: typeof j === "string" ? undefined : j.props,
+            properties: q.propSet >= 0 ? this.group.engine.psetObject(this.docId, q.propSet) : undefined,
             toJSONObject: () => j, _obsPos: q.obsPos, _version: this.group.version,
         };
         if (typeof j === "string") seg.text = j;
@@ -415,7 +442,9 @@ class ClientGroup {
     newClient(options) {
         const d = this.clients.length;
         if (d >= this.engine.maxDocs) throw new Error("engine document capacity exhausted");
+        const cs = snapshotChunkOption(options);
         this.engine.openDocs(d, 1);
+        if (cs) this.engine.setSnapshotChunk([d], [cs]);
         const c = new MergeTreeClient(this, d, options);
         this.clients.push(c);
         return c;

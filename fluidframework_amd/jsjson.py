@@ -19,6 +19,18 @@ from __future__ import annotations
 import math
 from typing import Any
 
+class _Undefined:
+    """JS `undefined` as a property value (a key that is present with value undefined, e.g. what a
+    combining op with an unknown name and no defaultValue stores): JSON.stringify skips such
+    object members and writes null for such array elements."""
+    __slots__ = ()
+
+    def __repr__(self):
+        return "undefined"
+
+
+UNDEFINED = _Undefined()
+
 _SHORT = {0x22: '\\"', 0x5C: "\\\\", 0x08: "\\b", 0x0C: "\\f", 0x0A: "\\n", 0x0D: "\\r", 0x09: "\\t"}
 
 
@@ -123,14 +135,15 @@ def stringify(v: Any) -> str:
     if isinstance(v, str):
         return quote(v)
     if isinstance(v, (list, tuple)):
-        return "[" + ",".join(stringify(x) for x in v) + "]"
+        return "[" + ",".join("null" if x is UNDEFINED else stringify(x) for x in v) + "]"
     if isinstance(v, dict):
-        return "{" + ",".join(quote(k) + ":" + stringify(v[k]) for k in js_key_order(list(v.keys()))) + "}"
+        return "{" + ",".join(quote(k) + ":" + stringify(v[k]) for k in js_key_order(list(v.keys()))
+                              if v[k] is not UNDEFINED) + "}"
     raise TypeError(f"not a JSON value: {type(v)}")
 
 
 def js_truthy(v: Any) -> bool:
-    if v is None or v is False:
+    if v is None or v is False or v is UNDEFINED:
         return False
     if isinstance(v, (int, float)) and not isinstance(v, bool):
         return not (v == 0 or (isinstance(v, float) and math.isnan(v)))

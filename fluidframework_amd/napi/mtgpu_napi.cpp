@@ -10,6 +10,7 @@
 #define NAPI_VERSION 8
 #include <node_api.h>
 
+#include <math.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -173,7 +174,7 @@ napi_value SetResidency(napi_env env, napi_callback_info info) {
     return rc ? throw_rc(env, c, rc, "mt_set_residency") : undefined(env);
 }
 
-// setProps(ctx, {setOff, key, value, keyJson[], keyIndex, valueJson[], valueFalsy, valueClass})
+// setProps(ctx, {setOff, key, value, keyJson[], keyIndex, valueJson[], valueFalsy, valueClass, valueKind})
 napi_value SetProps(napi_env env, napi_callback_info info) {
     napi_value argv[2];
     if (!get_args(env, info, 2, argv)) return nullptr;
@@ -184,12 +185,14 @@ napi_value SetProps(napi_env env, napi_callback_info info) {
         !field(env, argv[1], "value", napi_int32_array, &val, &nv) || !field(env, argv[1], "keyIndex", napi_uint32_array, &kidx, &nki) ||
         !field(env, argv[1], "valueFalsy", napi_uint8_array, &vf, &nvf) || !field(env, argv[1], "valueClass", napi_uint32_array, &vc, &nvc))
         return nullptr;
+    const uint8_t* vk; size_t nvk;
+    if (!field(env, argv[1], "valueKind", napi_uint8_array, &vk, &nvk)) return nullptr;
     napi_value kj, vj;
     napi_get_named_property(env, argv[1], "keyJson", &kj);
     napi_get_named_property(env, argv[1], "valueJson", &vj);
     std::vector<std::string> ks, vs;
     if (!strings(env, kj, ks) || !strings(env, vj, vs)) return nullptr;
-    if (noff == 0 || nk < off[noff - 1] || nv < off[noff - 1] || nki < ks.size() || nvf < vs.size() || nvc < vs.size()) {
+    if (noff == 0 || nk < off[noff - 1] || nv < off[noff - 1] || nki < ks.size() || nvf < vs.size() || nvc < vs.size() || nvk < vs.size()) {
         napi_throw_range_error(env, nullptr, "property table arrays are inconsistent");
         return nullptr;
     }
@@ -199,7 +202,7 @@ napi_value SetProps(napi_env env, napi_callback_info info) {
     mt_prop_table P{};
     P.n_sets = (uint32_t)(noff - 1); P.set_off = off; P.key = key; P.value = val;
     P.n_keys = (uint32_t)ks.size(); P.key_json = kp.data(); P.key_index = kidx;
-    P.n_values = (uint32_t)vs.size(); P.value_json = vp.data(); P.value_falsy = vf; P.value_class = vc;
+    P.n_values = (uint32_t)vs.size(); P.value_json = vp.data(); P.value_falsy = vf; P.value_class = vc; P.value_kind = vk;
     int rc = mt_set_props(c, &P);
     return rc ? throw_rc(env, c, rc, "mt_set_props") : undefined(env);
 }
@@ -227,6 +230,26 @@ napi_value SetDocClientNames(napi_env env, napi_callback_info info) {
     for (size_t i = 0; i < s.size(); i++) p[i] = s[i].c_str();
     int rc = mt_set_doc_client_names(c, doc, (uint32_t)s.size(), p.data());
     return rc ? throw_rc(env, c, rc, "mt_set_doc_client_names") : undefined(env);
+}
+
+// setDocSnapshotChunk(ctx, docIds: Uint32Array, sizes: Float64Array): options.mergeTreeSnapshotChunkSize
+// per document (0: default; Infinity: one chunk; sizes are rounded up, snapshotV1.ts:55, :78).
+napi_value SetDocSnapshotChunk(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return nullptr;
+    mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
+    const uint32_t* docs; size_t nd;
+    if (!typed(env, argv[1], napi_uint32_array, &docs, &nd)) return nullptr;
+    const double* sz; size_t ns;
+    if (!typed(env, argv[2], napi_float64_array, &sz, &ns) || ns < nd) return nullptr;
+    std::vector<uint64_t> v(nd);
+    for (size_t i = 0; i < nd; i++) {
+        const double x = sz[i];
+        if (!(x >= 0)) { napi_throw_range_error(env, nullptr, "mergeTreeSnapshotChunkSize must be a positive number"); return nullptr; }
+        v[i] = x == 0 ? 0 : (x >= 1.8e19 ? UINT64_MAX : (uint64_t)std::ceil(x));
+    }
+    int rc = mt_set_doc_snapshot_chunk(c, (uint32_t)nd, docs, v.data());
+    return rc ? throw_rc(env, c, rc, "mt_set_doc_snapshot_chunk") : undefined(env);
 }
 
 // applyBatch(ctx, batch): copies the batch to HBM and enqueues the replay
@@ -551,6 +574,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"setProps", nullptr, SetProps, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"setClientNames", nullptr, SetClientNames, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"setDocClientNames", nullptr, SetDocClientNames, nullptr, nullptr, nullptr, kAttr, nullptr},
+        {"setDocSnapshotChunk", nullptr, SetDocSnapshotChunk, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"applyBatch", nullptr, ApplyBatch, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"loadSnapshot", nullptr, LoadSnapshot, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"sync", nullptr, Sync, nullptr, nullptr, nullptr, kAttr, nullptr},

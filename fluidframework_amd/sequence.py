@@ -50,7 +50,8 @@ _MISSING = object()
 
 def _member(v, k):
     if isinstance(v, dict):
-        return v.get(k, _MISSING)
+        x = v.get(k, _MISSING)
+        return _MISSING if x is jsjson.UNDEFINED else x          # `b[key] === undefined`
     if isinstance(v, (list, str)) and k.isdigit() and int(k) < len(v) and str(int(k)) == k:
         return v[int(k)]
     return _MISSING
@@ -110,7 +111,8 @@ def annotate_delta_keys(op: dict, before: dict | None) -> list:
     segment's key order) first, then every key of the op's props."""
     new = op.get("props") or {}
     keys: list = []
-    if (op.get("combiningOp") or {}).get("name") == "rewrite" and before:
+    cop = op.get("combiningOp")
+    if isinstance(cop, dict) and cop.get("name") == "rewrite" and before:
         keys += [k for k in jsjson.js_key_order(list(before)) if not _truthy(new.get(k))]
     keys += [k for k in jsjson.js_key_order(list(new)) if k not in keys]
     return jsjson.js_key_order(keys)
@@ -125,7 +127,9 @@ def ops_from_delta(member: dict, ranges: list) -> list:
     for r in ranges:
         if r["kind"] == ANNOTATE:
             after = r["after"] or {}
-            props = {k: after.get(k) for k in annotate_delta_keys(member, r["before"])}
+            # `r.segment.properties[key] === undefined ? null : r.segment.properties[key]`
+            props = {k: (None if after.get(k, jsjson.UNDEFINED) is jsjson.UNDEFINED else after[k])
+                     for k in annotate_delta_keys(member, r["before"])}
             last = ops[-1] if ops else None
             if last and last["type"] == ANNOTATE and last["pos2"] == r["pos"] and match_properties(last["props"], props):
                 last["pos2"] += r["len"]

@@ -61,7 +61,9 @@ extern "C" {
 #define MT_DS_ASSERT_SEQ     0x01u /* currentSeq >= seq   (MT/client.ts:482, :846) */
 #define MT_DS_ASSERT_MSN     0x02u /* msn went backwards  (MT/client.ts:484, mergeTree.ts:1716) */
 #define MT_DS_INSERT_FAILED  0x04u /* insert fell off the tree (mergeTree.ts:2228-2233) */
-#define MT_DS_UNSUPPORTED    0x08u /* combiningOp other than none/"rewrite", >64 clients, ... */
+#define MT_DS_UNSUPPORTED    0x08u /* an input off the batch path: a combining op whose result
+                                      is a string or would alias (MT_VAL_UNSUP), a reused
+                                      marker id, a second paste of a register, ... */
 #define MT_DS_OOM_ROWS       0x10u
 #define MT_DS_OOM_BLOCKS     0x20u
 #define MT_DS_OOM_TEXT       0x40u
@@ -106,7 +108,13 @@ extern "C" {
 #define MT_OPF_MARKER     0x02u /* insert of a Marker; pos2 holds refType          */
 #define MT_OPF_REWRITE    0x04u /* annotate with combiningOp {name:"rewrite"}      */
 #define MT_OPF_SEG_PROPS  0x08u /* insert seg has props (prop_id)                  */
-#define MT_OPF_COMBINE    0x10u /* annotate with another combiningOp: unsupported  */
+#define MT_OPF_COMBINE    0x10u /* annotate with another combiningOp (Properties.combine,
+                                   MT/properties.ts:24-62, through
+                                   MT/segmentPropertiesManager.ts:98-103):
+                                   COMBINE alone = {name:"incr"}; COMBINE|REWRITE =
+                                   {name:"consensus"} or any other name (a key that
+                                   holds a value keeps it).  prop_id then names a
+                                   combine set (below), not the op's props.        */
 #define MT_OPF_REL1       0x20u /* pos1 is an index into rel[]: op.relativePos1
                                    (posFromRelativePos, mergeTree.ts:1949-1972)    */
 #define MT_OPF_REL2       0x40u /* pos2 is an index into rel[]: op.relativePos2    */
@@ -166,7 +174,42 @@ typedef struct mt_op_rec {
  * Host-interned property sets (the `props` of an annotate op or of an inserted
  * segment spec), already in JS Object.keys() order.  Values are interned JS
  * values: value -1 means `null` (delete the key, segmentPropertiesManager.ts:104).
+ *
+ * Remote combining ops.  SegmentPropertiesManager.addProperties calls
+ * combine(op, previousValue, undefined, seq) for every key of the op's props
+ * (segmentPropertiesManager.ts:98-103: its `newValue` is never assigned), so the op's
+ * values are unused and the result depends on the key's previous value, the op's
+ * name and defaultValue, and the message's seq.  The host packs such an annotate as a
+ * *combine set*: the op's keys, each valued with what combine yields for a key the
+ * segment does not hold (previousValue undefined):
+ *   incr       defaultValue undefined / number / boolean / null -> MT_VAL_NAN (x + undefined);
+ *              a string / object / array default -> MT_VAL_UNSUP (string concatenation)
+ *   consensus  no defaultValue -> MT_VAL_CFRESH ({value: undefined, seq}); null -> MT_VAL_UNSUP
+ *              (the reference throws reading null.seq); an object whose seq is -1 -> that
+ *              object with seq = the message's seq (properties.ts:52-54); else the default
+ *   other      no defaultValue -> MT_VAL_UNDEF; null -> MT_VAL_NULL (the key is deleted);
+ *              else the default (combine's switch has no case: the default is returned)
+ * A key the segment holds: incr yields NaN from a number, boolean, NaN or undefined value
+ * (MT_VK_NUM) and MT_VAL_UNSUP from anything else; consensus and other names keep the
+ * value, except that an object whose seq is -1 (MT_VK_SEQM1) is MT_VAL_UNSUP (consensus
+ * would write the seq into an object every segment split from it shares).  MT_VAL_UNSUP
+ * sets MT_DS_UNSUPPORTED on the document.
+ *
+ * Stored values other than interned ids (never in an op's set): MT_VAL_NAN (JSON null,
+ * never matchProperties-equal: NaN !== NaN), MT_VAL_UNDEF (the key is present with
+ * value undefined: skipped by JSON.stringify, never equal) and MT_VAL_CONS(seq) (a fresh
+ * consensus object: JSON {"seq":seq}, never equal since its `value` is undefined,
+ * properties.ts:72-73).
  */
+#define MT_VAL_NULL   (-1)
+#define MT_VAL_NAN    (-2)
+#define MT_VAL_UNSUP  (-3)
+#define MT_VAL_CFRESH (-4)
+#define MT_VAL_UNDEF  (-5)
+#define MT_VAL_CONS_BASE (-16)                    /* MT_VAL_CONS(seq) = -16 - seq, seq >= 0 */
+#define MT_VAL_CONS(seq) (MT_VAL_CONS_BASE - (seq))
+#define MT_VK_NUM   0x01u   /* number or boolean: incr gives NaN                            */
+#define MT_VK_SEQM1 0x02u   /* a (non-array) object whose "seq" member is the number -1     */
 typedef struct mt_prop_table {
     uint32_t        n_sets;
     const uint32_t* set_off;      /* [n_sets+1] into key/value                  */
@@ -179,6 +222,8 @@ typedef struct mt_prop_table {
     const char* const* value_json;/* [n_values] JSON text of the value          */
     const uint8_t*  value_falsy;  /* [n_values] JS falsiness (rewrite rule)     */
     const uint32_t* value_class;  /* [n_values] matchProperties() equivalence   */
+    const uint8_t*  value_kind;   /* [n_values] MT_VK_* (null: every combine set
+                                     is MT_DS_UNSUPPORTED)                      */
 } mt_prop_table;
 
 /* Engine limits per document (pool capacities, sized from the op counts). */
@@ -335,8 +380,11 @@ int  mt_set_partition(mt_ctx* ctx, uint32_t min_ops, uint32_t cus);
  * batches in the kernel without that second engine (no scratch), an outgrown document
  * finishing in a second, all-HBM launch.  0: always the continuing kernel. */
 int  mt_set_continuation(mt_ctx* ctx, uint32_t min_ops);
-/* Per run of the last LDS-resident replay: the op index where it handed over to
- * the HBM kernel (== the run's end when it finished in LDS).  Diagnostic. */
+/* Per run of the last LDS-resident replay: the op index where it left LDS (== the run's
+ * end when it finished in LDS).  Bit 31 (MT_CURSOR_DONE) set: the run continued from that
+ * op in HBM in the same wave and finished there (no second launch); mask it off to read
+ * the op index.  Diagnostic. */
+#define MT_CURSOR_DONE 0x80000000u
 int  mt_last_cursors(mt_ctx* ctx, uint32_t n_runs, uint32_t* out);
 /* Milliseconds of the last replay kernel(s), timed with HIP events on the
  * context stream. */
@@ -437,6 +485,16 @@ int  mt_snapshot_legacy(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
                         uint64_t* out_digest,
                         const char** arena, const uint64_t** blob_off,
                         const uint32_t** blob_first);
+/* options.mergeTreeSnapshotChunkSize of each document's Client (MergeTree options,
+ * MT/client.ts:82-84; SnapshotV1 reads `mergeTree.options?.mergeTreeSnapshotChunkSize ??
+ * SnapshotV1.chunkSize`, MT/snapshotV1.ts:55): mt_snapshot_v1 / mt_snapshot_digests close a
+ * chunk once its length reaches chunk_size[i] (getSeqLengthSegs, snapshotV1.ts:70-92).
+ * 0 = the default 10,000; UINT64_MAX = Infinity (one chunk).  Lengths are integers, so a
+ * positive non-integer size c acts as ceil(c); hosts reject c <= 0 and NaN, for which the
+ * reference's chunk loop never ends on a non-empty document.  SnapshotLegacy's first chunk
+ * stays sizeOfFirstChunk (10,000, snapshotlegacy.ts:57).  mt_docs_open resets the
+ * documents it opens to the default. */
+int  mt_set_doc_snapshot_chunk(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, const uint64_t* chunk_size);
 /* Digests only (same values as mt_snapshot_v1's), for many documents: one staged
  * download, serialization spread over `threads` host threads. */
 int  mt_snapshot_digests(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, const int32_t* msn,

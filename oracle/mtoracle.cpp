@@ -284,6 +284,121 @@ static bool match_properties(const JVal* a, const JVal* b) {
     return true;
 }
 
+struct PropTable {                       // host-interned op property sets
+    std::vector<std::vector<std::pair<u16s, int>>> sets;   // (key, value id or -1 = null)
+    std::vector<JVal> values;
+};
+
+// ---- MT/properties.ts:24-62 combine(), as SegmentPropertiesManager.addProperties calls it ----
+// (segmentPropertiesManager.ts:98-103: `newValue` is declared and never assigned, so combine
+// always gets undefined as the new value; the op's prop values are unused).
+enum { PM_SET = 0, PM_REWRITE = 1, PM_INCR = 2, PM_KEEP = 3 };
+struct Combining {                    // ICombiningOp (MT/ops.ts:32-37)
+    enum { Incr, Consensus, Other } kind = Other;
+    bool hasDef = false; JVal def;    // defaultValue (JSON null is a defined null)
+    bool hasMin = false; JVal minValue;
+};
+// String(v) for a JSON value (ToString / Array.prototype.join / Object.prototype.toString).
+static u16s js_to_string(const JVal& v) {
+    switch (v.t) {
+    case JVal::Undef: return u"undefined";
+    case JVal::Null: return u"null";
+    case JVal::Bool: return v.b ? u"true" : u"false";
+    case JVal::Num: { std::string o; num_to_js(o, v.n); return u16s(o.begin(), o.end()); }
+    case JVal::Str: return v.s;
+    case JVal::Arr: {
+        u16s o;
+        for (size_t i = 0; i < v.arr.size(); i++) {
+            if (i) o.push_back(u',');
+            if (v.arr[i].t != JVal::Undef && v.arr[i].t != JVal::Null) o += js_to_string(v.arr[i]);
+        }
+        return o;
+    }
+    case JVal::Obj: return u"[object Object]";
+    }
+    return u"";
+}
+static bool is_seq_minus1(const JVal& v) {            // `cv.seq === -1` on an object
+    if (v.t != JVal::Obj) return false;
+    const int i = obj_find(v, u"seq");
+    return i >= 0 && v.ovals[i].t == JVal::Num && v.ovals[i].n == -1;
+}
+static JVal nan_value() { JVal v; v.t = JVal::Num; v.n = std::nan(""); return v; }
+// combine(op, previousValue, undefined, seq) -> *out; *del when the result is null (the key is
+// deleted, segmentPropertiesManager.ts:104-106).  Returns false where the result is off the
+// engine's batch path (MT_DS_UNSUPPORTED there, include/mtgpu.h): an incr that yields a string,
+// consensus on null (the reference throws reading null.seq), and a consensus write into an
+// object a segment already holds (its seq is -1: every segment sharing the object changes).
+static bool js_combine(Combining& cb, const JVal* prev, int seq, JVal& out, bool& del) {
+    del = false;
+    JVal cur;
+    if (prev && prev->t != JVal::Undef) cur = *prev;
+    else if (cb.hasDef) cur = cb.def;                   // `_currentValue = combiningInfo.defaultValue`
+    switch (cb.kind) {
+    case Combining::Incr: {                             // `_currentValue += newValue` (undefined)
+        if (cur.t == JVal::Str || cur.t == JVal::Arr || cur.t == JVal::Obj) {
+            out.t = JVal::Str; out.s = js_to_string(cur) + u"undefined";      // string concatenation
+            if (cb.hasMin && truthy(&cb.minValue)) {
+                const bool strMin = cb.minValue.t == JVal::Str || cb.minValue.t == JVal::Arr || cb.minValue.t == JVal::Obj;
+                if (strMin && out.s < js_to_string(cb.minValue)) out = cb.minValue;   // both strings: code-unit order
+            }
+            return false;
+        }
+        out = nan_value();                              // ToNumber(...) + NaN; NaN < minValue is false
+        return true;
+    }
+    case Combining::Consensus:
+        if (cur.t == JVal::Undef) {                     // {value: newValue, seq}
+            out = make_obj(); JVal u; obj_set(out, u"value", u);
+            JVal sq; sq.t = JVal::Num; sq.n = seq; obj_set(out, u"seq", sq);
+            return true;
+        }
+        if (cur.t == JVal::Null) return false;          // TypeError: null.seq
+        if (is_seq_minus1(cur)) {
+            if (prev && prev->t != JVal::Undef) return false;        // a held (shared) object mutated
+            JVal sq; sq.t = JVal::Num; sq.n = seq;
+            obj_set(cb.def, u"seq", sq);                 // the op's defaultValue object itself
+            out = cb.def;
+            return true;
+        }
+        out = cur;
+        return true;
+    case Combining::Other:
+        if (prev && prev->t != JVal::Undef && is_seq_minus1(*prev)) return false;   // engine: held seq -1 objects
+        if (cur.t == JVal::Null) { del = true; return true; }
+        out = cur;                                      // no case: the value (or undefined) is returned
+        return true;
+    }
+    return true;
+}
+// The same step from a combine set (the hosts' packed form, include/mtgpu.h MT_VAL_*): code =
+// what combine yields for a key the segment does not hold.
+static bool packed_combine(const PropTable& pt, int code, int mode, const JVal* prev, int seq, JVal& out, bool& del) {
+    del = false;
+    if (prev && prev->t != JVal::Undef) {
+        if (mode == PM_INCR) {
+            if (prev->t != JVal::Num && prev->t != JVal::Bool) return false;
+            out = nan_value();
+            return true;
+        }
+        if (is_seq_minus1(*prev)) return false;
+        out = *prev;
+        return true;
+    }
+    if (code >= 0) { out = pt.values[code]; return true; }
+    switch (code) {
+    case MT_VAL_NULL: del = true; return true;
+    case MT_VAL_NAN: out = nan_value(); return true;
+    case MT_VAL_UNDEF: out = JVal(); return true;
+    case MT_VAL_CFRESH: {
+        out = make_obj(); JVal u; obj_set(out, u"value", u);
+        JVal sq; sq.t = JVal::Num; sq.n = seq; obj_set(out, u"seq", sq);
+        return true;
+    }
+    default: return false;                              // MT_VAL_UNSUP
+    }
+}
+
 /* ======================================================================== */
 /* Merge tree                                                                */
 /* ======================================================================== */
@@ -340,10 +455,6 @@ static int latestLEQ(const V& a, int key) {     // MT/partialLengths.ts:32-48
     return best;
 }
 
-struct PropTable {                       // host-interned op property sets
-    std::vector<std::vector<std::pair<u16s, int>>> sets;   // (key, value id or -1 = null)
-    std::vector<JVal> values;
-};
 
 struct Seg;
 static std::string seg_json(const Seg* s, const u16s* textOverride = nullptr);
@@ -929,9 +1040,9 @@ struct Tree {
         for (Seg* x : removed) { drec(1, x, x->cachedLength, 0); xrec(1, x); }                      // REMOVE callback :2725-2733
         if (collaborating && seq != UnassignedSeq) zamboni();
     }
-    void addProperties(Seg* s, const PropTable& pt, int set, bool rewrite, int seq, bool collab) {
+    void addProperties(Seg* s, const PropTable& pt, int set, int mode, int seq, bool collab, Combining* cb = nullptr) {
         // SegmentPropertiesManager.addProperties, MT/segmentPropertiesManager.ts:38-113 (observer: no pending keys)
-        (void)seq; (void)collab;
+        (void)collab;
         if (!s->hasProps) { s->hasProps = true; s->props = make_obj(); }
         const auto& np = pt.sets[set];
         JVal* dl = nullptr;                                   // the returned deltas' keys (:66-109)
@@ -940,24 +1051,35 @@ struct Tree {
             for (auto& kv : np) if (kv.first == k) return kv.second < 0 ? &nullv : &pt.values[kv.second];
             return nullptr;
         };
-        if (rewrite) {
+        if (mode == PM_REWRITE) {
             std::vector<u16s> keys; for (int i : obj_order(s->props)) keys.push_back(s->props.okeys[i]);
             for (auto& k : keys) if (!truthy(newVal(k))) { if (dl) obj_set(*dl, k, nullv); obj_del(s->props, k); }
         }
         for (auto& kv : np) {
             if (dl) obj_set(*dl, kv.first, nullv);
+            if (mode >= PM_INCR) {                            // combine(op, previousValue, undefined, seq) :98-103
+                const int i = obj_find(s->props, kv.first);
+                const JVal* prev = i >= 0 ? &s->props.ovals[i] : nullptr;
+                JVal nv; bool del = false;
+                const bool ok = cb ? js_combine(*cb, prev, seq, nv, del) : packed_combine(pt, kv.second, mode, prev, seq, nv, del);
+                if (!ok) { status |= MT_DS_UNSUPPORTED; return; }
+                if (del) obj_del(s->props, kv.first);
+                else obj_set(s->props, kv.first, nv);
+                continue;
+            }
             if (kv.second < 0) obj_del(s->props, kv.first);
             else obj_set(s->props, kv.first, pt.values[kv.second]);
         }
     }
     JVal nullv = [] { JVal v; v.t = JVal::Null; return v; }();
-    void annotateRange(int start, int end, const PropTable& pt, int set, bool rewrite, int refSeq, int clientId, int seq) { // :2584
+    void annotateRange(int start, int end, const PropTable& pt, int set, int mode, int refSeq, int clientId, int seq,
+                       Combining* cb = nullptr) { // :2584
         ensureIntervalBoundary(start, refSeq, clientId);
         ensureIntervalBoundary(end, refSeq, clientId);
         std::vector<std::pair<Seg*, std::string>> ann;
         auto leaf = [&](Seg* s, int, int, int) {
             std::string before = capture ? propsJson(s) : std::string();
-            addProperties(s, pt, set, rewrite, seq, collaborating);
+            addProperties(s, pt, set, mode, seq, collaborating, cb);
             if (capture || xform) ann.push_back({s, before});
             if (collaborating && seq != UnassignedSeq) addToLRUSet(s, seq);
         };
@@ -1080,6 +1202,7 @@ struct Doc {
     std::vector<int> shortToStream;          // short id -> stream client index (-1 observer)
     std::vector<int> streamToShort;
     int opCounter = 0;                       // op members applied (mt_op_batch indexing of the message stream)
+    double chunkSize = 10000;                // options.mergeTreeSnapshotChunkSize ?? SnapshotV1.chunkSize (snapshotV1.ts:55)
     std::vector<JVal> messagesSinceMSNChange;   // SharedSegmentSequence's legacy stash (sequence.ts:604-658)
     // RegisterCollection (MT/mergeTree.ts:864-896), keyed by (short client id, name): the
     // short id stands for the long id the reference keys by (one-to-one per document).
@@ -1207,12 +1330,12 @@ static std::vector<std::string> snapshot_v1(Doc& d, int msn, int seq) {
     };
     t.walkAll(t.root, extract);
     pushPrev();
-    // emit: chunks of approx 10000 chars (snapshotV1.ts:70-92, :98-163)
+    // emit: chunks of approx chunkSize chars (snapshotV1.ts:70-92, :98-163)
     struct Chunk { int start, count, length; };
     std::vector<Chunk> chunks; int totalCount = 0, totalLen = 0;
     do {
         Chunk c{totalCount, 0, 0};
-        while (c.length < 10000 && c.start + c.count < (int)segJson.size()) { c.length += segLen[c.start + c.count]; c.count++; }
+        while (c.length < d.chunkSize && c.start + c.count < (int)segJson.size()) { c.length += segLen[c.start + c.count]; c.count++; }
         chunks.push_back(c); totalCount += c.count; totalLen += c.length;
     } while (totalCount < (int)segJson.size());
     auto chunkStr = [&](const Chunk& c, bool header) {
@@ -1331,8 +1454,8 @@ static uint32_t apply_run(Doc& d, const mt_op_batch* b, uint32_t run) {
             } else if (ty == MT_OP_REMOVE) {
                 t.markRangeRemoved(b->pos1[i], b->pos2[i], ref, cl, seq);
             } else if (ty == MT_OP_ANNOTATE) {
-                if (fl & MT_OPF_COMBINE) t.status |= MT_DS_UNSUPPORTED;
-                t.annotateRange(b->pos1[i], b->pos2[i], d.props, b->prop_id[i], fl & MT_OPF_REWRITE, ref, cl, seq);
+                const int mode = (fl & MT_OPF_COMBINE) ? ((fl & MT_OPF_REWRITE) ? PM_KEEP : PM_INCR) : ((fl & MT_OPF_REWRITE) ? PM_REWRITE : PM_SET);
+                t.annotateRange(b->pos1[i], b->pos2[i], d.props, b->prop_id[i], mode, ref, cl, seq);
             } else if (ty == MT_OP_CUT || ty == MT_OP_COPY || ty == MT_OP_PASTE) {              // register name by index
                 std::string k = std::to_string(b->payload_off[i]);
                 const u16s name(k.begin(), k.end());
@@ -1482,6 +1605,7 @@ void ora_free(ora_doc* d) { delete d; }
 void ora_set_verify(int on) { g_verify = on; g_verify_bad = 0; g_verify_checks = 0; }
 long long ora_verify_result(long long* checks) { if (checks) *checks = g_verify_checks; return g_verify_bad; }
 void ora_free_buf(void* p) { free(p); }
+void ora_set_snapshot_chunk(ora_doc* d, double chunk_size) { d->d.chunkSize = chunk_size; }
 
 static void load_props(PropTable& pt, const mt_prop_table* p) {
     pt.sets.clear(); pt.values.clear();
@@ -1579,14 +1703,26 @@ static void apply_remote_member(Doc& d, const JVal& op, int cl, int ref, int seq
         } else {
             const JVal* props = jget(op, u"props");
             const JVal* cop = jget(op, u"combiningOp");
-            bool rewrite = false;
-            if (cop && cop->t == JVal::Obj) {
-                const JVal* nm = jget(*cop, u"name");
-                if (nm && nm->t == JVal::Str && nm->s == u"rewrite") rewrite = true;
-                else { t.status |= MT_DS_UNSUPPORTED; return; }
+            // segmentPropertiesManager.ts:55-56: rewrite = op && op.name === "rewrite";
+            // combiningOp = !rewrite ? (op ? op : undefined) : undefined
+            int mode = PM_SET;
+            Combining cb;
+            if (truthy(cop)) {
+                const JVal* nm = cop->t == JVal::Obj ? jget(*cop, u"name") : nullptr;
+                const bool isStr = nm && nm->t == JVal::Str;
+                if (isStr && nm->s == u"rewrite") mode = PM_REWRITE;
+                else {
+                    cb.kind = isStr && nm->s == u"incr" ? Combining::Incr
+                            : (isStr && nm->s == u"consensus" ? Combining::Consensus : Combining::Other);
+                    mode = cb.kind == Combining::Incr ? PM_INCR : PM_KEEP;
+                    const JVal* dv = cop->t == JVal::Obj ? jget(*cop, u"defaultValue") : nullptr;
+                    if (dv && dv->t != JVal::Undef) { cb.hasDef = true; cb.def = *dv; }
+                    const JVal* mv = cop->t == JVal::Obj ? jget(*cop, u"minValue") : nullptr;
+                    if (mv && mv->t != JVal::Undef) { cb.hasMin = true; cb.minValue = *mv; }
+                }
             }
             if (!props || props->t != JVal::Obj) { t.status |= MT_DS_UNSUPPORTED; return; }
-            t.annotateRange(p1, p2, d.props, intern_props_json(d, *props), rewrite, ref, cl, seq);
+            t.annotateRange(p1, p2, d.props, intern_props_json(d, *props), mode, ref, cl, seq, mode >= PM_INCR ? &cb : nullptr);
         }
         complete_op(t, seq, msn);
     } else if (type == 3) {                                                                       // GROUP :804-812
@@ -1773,7 +1909,7 @@ int ora_local_remove(ora_doc* o, int32_t start, int32_t end) {
     Tree& t = o->d.t; t.markRangeRemoved(start, end, t.currentSeq, t.cwClientId, t.collaborating ? UnassignedSeq : UniversalSeq); return (int)t.status;
 }
 int ora_local_annotate(ora_doc* o, int32_t start, int32_t end, int32_t ps, int32_t rewrite) {
-    Tree& t = o->d.t; t.annotateRange(start, end, o->d.props, ps, rewrite != 0, t.currentSeq, t.cwClientId, t.collaborating ? UnassignedSeq : UniversalSeq); return (int)t.status;
+    Tree& t = o->d.t; t.annotateRange(start, end, o->d.props, ps, rewrite != 0 ? PM_REWRITE : PM_SET, t.currentSeq, t.cwClientId, t.collaborating ? UnassignedSeq : UniversalSeq); return (int)t.status;
 }
 int ora_load_snapshot(ora_doc* o, uint32_t n_blobs, const char* const* blobs) {
     Doc& d = o->d; Tree& t = d.t;

@@ -73,6 +73,8 @@ int32_t  ora_get_length_exact(ora_doc* d, int32_t ref_seq, int32_t client);
 const char* ora_client_name(ora_doc* d, int32_t short_id);
 /* Snapshot: returns a malloc'd buffer: u32 n_blobs, then per blob u64 len + bytes. */
 uint8_t* ora_snapshot_v1(ora_doc* d, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total_bytes);
+/* options.mergeTreeSnapshotChunkSize of the document's MergeTree (snapshotV1.ts:55; default 10000). */
+void     ora_set_snapshot_chunk(ora_doc* d, double chunk_size);
 /* SnapshotLegacy (MT/snapshotlegacy.ts:104-240) blobs "header"[, "body"], same packing. */
 uint8_t* ora_snapshot_legacy(ora_doc* d, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total_bytes);
 uint16_t* ora_get_text(ora_doc* d, uint64_t* n_units);

@@ -55,13 +55,15 @@ def run_driver(name, spec, addon=None, timeout=240):
         return json.load(open(op))
 
 
-def run_node(doc_msgs, addon=None, limits=None, timeout=240, loads=None, legacy=None, queries=None):
+def run_node(doc_msgs, addon=None, limits=None, timeout=240, loads=None, legacy=None, queries=None, options=None):
     env = dict(os.environ)
     if addon:
         env["MTGPU_NAPI"] = addon
     with tempfile.TemporaryDirectory() as td:
         ip, op = os.path.join(td, "in.json"), os.path.join(td, "out.json")
-        json.dump({"docs": doc_msgs, "limits": limits or {}, "loads": loads, "legacy": legacy, "queries": queries},
-                  open(ip, "w"))
+        spec = {"docs": doc_msgs, "limits": limits or {}, "loads": loads, "legacy": legacy, "queries": queries}
+        if options is not None:
+            spec["options"] = options            # the Clients' options (newClient(options))
+        json.dump(spec, open(ip, "w"))
         subprocess.run([NODE, DRIVER, ip, op], check=True, env=env, timeout=timeout)
         return json.load(open(op))

@@ -40,6 +40,16 @@ KEYS = ["0", "1", "2", "10", "k", "bold", "a b", "ключ", "x\"y", "4294967295
 WIDE_KEYS = KEYS + [f"w{i}" for i in range(36)] + ["3", "7", "11", "12", "40", "99", "100", "1000", "255"]
 VALUES = ["s", "ü", "", 0, 1, -3, 1.5, 1e21, 0.25, True, False, {"a": 1}, [1, 2], {"0": "x", "b": [True]},
           {"n": None}, "😀"]
+# remote combining ops (the "combine" surface, MT/properties.ts:24-62 via
+# segmentPropertiesManager.ts:98-103): "incr" works on keys whose values are numbers or booleans
+# (NaN results); "consensus" and ops of other names on keys holding anything but objects whose
+# seq is -1 (fresh {value: undefined, seq} objects, defaults, undefined values)
+INCR_KEYS = ["n0", "n1", "3"]
+CONS_KEYS = ["v0", "v1", "7"]
+NUM_VALUES = [0, 1, -2, 2.5, True, False, 1e21]
+INCR_DEFAULTS = [None, 0, 5, True, 2.5, "__absent__", "__absent__"]
+CONS_DEFAULTS = ["__absent__", "__absent__", 7, "x", {"a": 1}, {"value": 3, "seq": -1}, [1, 2], {"seq": 4}, False]
+OTHER_DEFAULTS = ["__absent__", None, 1, "z", {"k": [1]}]
 
 
 class StreamGen:
@@ -48,7 +58,7 @@ class StreamGen:
                  p_special: float = 0.25, long_every: int = 40, max_ins: int = 9, id_prefix: str = "cli",
                  max_total_clients: int | None = None, p_marker_id: float = 0.0, p_relative: float = 0.0,
                  capture: bool = False, p_register: float = 0.0, p_wide: float = 0.0, reg_names: int = 0,
-                 reg_span: int = 10):
+                 reg_span: int = 10, p_combine: float = 0.0):
         self.rng = random.Random(seed)
         self.lag, self.churn, self.p_nonop, self.p_group = lag, churn, p_nonop, p_group
         self.p_marker, self.p_annotate, self.p_remove, self.p_special = p_marker, p_annotate, p_remove, p_special
@@ -62,6 +72,7 @@ class StreamGen:
         # register names per client (0: REGS) and the longest copy / cut range
         self.reg_names = [f"r{i}" for i in range(reg_names)] if reg_names else self.REGS
         self.reg_span = reg_span
+        self.p_combine = p_combine
         self.total = 0
         self.active: dict[str, int] = {}          # long id -> latest refSeq
         for _ in range(clients):
@@ -96,7 +107,31 @@ class StreamGen:
         for _ in range(r.randint(18, 45) if wide else r.randint(1, 3)):
             k = r.choice(WIDE_KEYS if wide else KEYS)
             d[k] = None if (allow_null and r.random() < 0.2) else r.choice(VALUES)
+        if self.p_combine and r.random() < 0.5:          # plain values on the combining ops' keys
+            if r.random() < 0.5:
+                d[r.choice(INCR_KEYS)] = None if (allow_null and r.random() < 0.2) else r.choice(NUM_VALUES)
+            else:
+                d[r.choice(CONS_KEYS)] = None if (allow_null and r.random() < 0.2) else r.choice(VALUES)
         return d
+
+    def _combining(self) -> tuple[dict, dict]:
+        """(props, combiningOp) of a remote annotate with a combining op other than rewrite."""
+        r = self.rng
+        x = r.random()
+        if x < 0.45:
+            cop, keys, defs = {"name": "incr"}, INCR_KEYS, INCR_DEFAULTS
+            if r.random() < 0.3:
+                cop["minValue"] = r.choice([3, "a", -1])         # NaN < minValue is false
+        elif x < 0.85:
+            cop, keys, defs = {"name": "consensus"}, CONS_KEYS, CONS_DEFAULTS
+        else:
+            cop, keys, defs = r.choice([{"name": "max"}, {"name": 5}, {}]), CONS_KEYS, OTHER_DEFAULTS
+        dv = r.choice(defs)
+        if dv != "__absent__":
+            cop["defaultValue"] = dv
+        # the op's values are unused (combine gets undefined); keys only, any values
+        props = {k: r.choice(VALUES + [None]) for k in r.sample(keys, r.randint(1, 2))}
+        return props, cop
 
     def _insert(self, L: int, k: int) -> tuple[dict, int]:
         r = self.rng
@@ -132,6 +167,9 @@ class StreamGen:
         if ty == 1:
             return {"type": 1, "pos1": s, "pos2": e}, -(e - s)
         op = {"type": 2, "pos1": s, "pos2": e}
+        if self.p_combine and r.random() < self.p_combine:
+            op["props"], op["combiningOp"] = self._combining()
+            return op, 0
         x = r.random()
         if x < 0.1:
             op["props"] = {}

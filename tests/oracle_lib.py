@@ -88,6 +88,7 @@ def lib():
         L.ora_client_name.restype = ctypes.c_char_p
         L.ora_client_name.argtypes = [P, I32]
         L.ora_containing_segment.argtypes = [P, I32, I32, I32, ctypes.c_char_p, P, ctypes.POINTER(P)]
+        L.ora_set_snapshot_chunk.argtypes = [P, ctypes.c_double]
         _lib = L
     return _lib
 
@@ -131,6 +132,10 @@ class OracleDoc:
         arr = (ctypes.c_char_p * max(1, len(json_literals)))(*[s.encode() for s in json_literals])
         self._names = arr
         self.L.ora_set_client_names(self.h, len(json_literals), ctypes.cast(arr, ctypes.c_void_p))
+
+    def set_snapshot_chunk(self, chunk_size: float):
+        """options.mergeTreeSnapshotChunkSize of the document's MergeTree (snapshotV1.ts:55)."""
+        self.L.ora_set_snapshot_chunk(self.h, float(chunk_size))
 
     def apply_msg(self, msg: dict) -> int:
         """Client.applyMsg on the message itself (JSON; the oracle parses and dispatches it)."""

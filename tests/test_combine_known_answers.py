@@ -1,0 +1,332 @@
+"""Remote combining ops and options.mergeTreeSnapshotChunkSize: known answers.
+
+Combining ops (ICombiningOp other than "rewrite", MT/ops.ts:32-37).  A remote annotate calls
+SegmentPropertiesManager.addProperties (MT/segmentPropertiesManager.ts:38-113), which for a
+combining op computes `Properties.combine(combiningOp, previousValue, newValue, seq)` with a
+`newValue` it never assigned (:98-103), so MT/properties.ts:24-62 always combines with
+undefined:
+  * incr: `x += undefined` is NaN for numbers, booleans, null and undefined; NaN is not null, so
+    it is stored; JSON.stringify writes it as null; and `NaN !== NaN`, so matchProperties
+    (:64-95) fails on it, which stops zamboni merges (mergeTree.ts:1306-1334) and snapshot
+    coalescing (snapshotV1.ts:195-213);
+  * consensus: a key without a value becomes {value: undefined, seq} (JSON {"seq":seq}, never
+    equal: its `value` is undefined); a defaultValue whose seq is -1 gets the op's seq; any
+    other held value is kept;
+  * any other name: the held value or the defaultValue (undefined included: the key is
+    present with value undefined, skipped by JSON.stringify, never equal).
+The expected texts below are those rules worked by hand; the oracle (oracle/mtoracle.cpp
+js_combine) must produce them, and the engine must equal the oracle byte for byte.
+
+mergeTreeSnapshotChunkSize (snapshotV1.ts:55, :70-114): SnapshotV1 closes a chunk once its
+length reaches the size; sizes 100 / 1,000 / 25,000 against the oracle and the chunk rule.
+"""
+import json
+
+import numpy as np
+import pytest
+
+from emu_lib import emu_engine
+from fluidframework_amd.engine import ClientGroup, Engine, MergeTreeError, snapshot_chunk_option
+from oracle_lib import OracleDoc
+
+UNSUPPORTED = 0x08
+LIMITS = dict(rows_per_doc=8192, window_per_doc=4096, propsets_per_doc=8192, text_per_doc=1 << 16)
+
+
+def msg(seq, ref, msn, contents, client="a"):
+    return dict(clientId=client, sequenceNumber=seq, referenceSequenceNumber=ref, minimumSequenceNumber=msn,
+                type="op", contents=contents)
+
+
+def ins(pos, seg):
+    return {"type": 0, "pos1": pos, "seg": seg}
+
+
+def ann(p1, p2, props, cop=None):
+    o = {"type": 2, "pos1": p1, "pos2": p2, "props": props}
+    if cop is not None:
+        o["combiningOp"] = cop
+    return o
+
+
+def rem(p1, p2):
+    return {"type": 1, "pos1": p1, "pos2": p2}
+
+
+def stream_of(ops, msn_lag=10 ** 9):
+    """Messages seq 1.. of one client, refSeq = seq - 1, MSN trailing by msn_lag."""
+    return [msg(i + 1, i, max(0, i - msn_lag), op) for i, op in enumerate(ops)]
+
+
+def body_props(blobs):
+    """The props JSON texts of every segment of a SnapshotV1, in order (None: no props)."""
+    out = []
+    for b in blobs:
+        for s in json.loads(b)["segments"]:
+            j = s["json"] if isinstance(s, dict) and "json" in s else s
+            out.append(json.dumps(j.get("props"), separators=(",", ":")) if isinstance(j, dict) else None)
+    return out
+
+
+def props_texts(blobs):
+    """The raw `"props":{...}` texts of a snapshot (as the bytes hold them: NaN is null)."""
+    import re
+    return re.findall(r'"props":(\{[^{}]*(?:\{[^{}]*\}[^{}]*)*\})', b"".join(blobs).decode())
+
+
+# Known answers: (name, ops, expected props texts in snapshot order or expected status)
+CASES = [
+    # incr without a default on an absent key: NaN (JSON null)
+    ("incr_absent", [ins(0, "abc"), ann(0, 3, {"k": 7}, {"name": "incr"})], ['{"k":null}']),
+    # incr on held numbers and booleans, a default of 5 and a minValue: all NaN (NaN < 3 is false)
+    ("incr_held", [ins(0, {"text": "ab", "props": {"x": 2, "y": True}}),
+                   ann(0, 2, {"x": None, "y": 1, "z": 0}, {"name": "incr", "defaultValue": 5, "minValue": 3})],
+     ['{"x":null,"y":null,"z":null}']),
+    # consensus on an absent key: {value: undefined, seq: 2} -> {"seq":2}; a held value is kept
+    ("consensus_fresh", [ins(0, {"text": "ab", "props": {"h": "keep"}}),
+                         ann(0, 2, {"c": 1, "h": 2}, {"name": "consensus"})], ['{"h":"keep","c":{"seq":2}}']),
+    # a consensus default whose seq is -1 takes the op's seq, key order kept
+    ("consensus_default_seq", [ins(0, "ab"), ann(0, 2, {"c": 0}, {"name": "consensus",
+                                                                  "defaultValue": {"value": 3, "seq": -1, "w": 1}})],
+     ['{"c":{"value":3,"seq":2,"w":1}}']),
+    ("consensus_default_plain", [ins(0, "ab"), ann(0, 2, {"c": 0}, {"name": "consensus", "defaultValue": [1, "x"]})],
+     ['{"c":[1,"x"]}']),
+    # another name: no case in combine's switch; no default -> the key holds undefined (omitted
+    # by JSON.stringify), a null default deletes it, another default is stored
+    ("other_undefined", [ins(0, {"text": "ab", "props": {"h": 1}}), ann(0, 2, {"u": 9}, {"name": "max"})],
+     ['{"h":1}']),
+    ("other_null_default", [ins(0, {"text": "ab", "props": {"h": 1, "d": 2}}),
+                            ann(0, 2, {"d": 0, "e": 0}, {"name": "max", "defaultValue": None})], ['{"h":1,"d":2}']),
+    ("other_default", [ins(0, "ab"), ann(0, 2, {"d": 0}, {"name": 5, "defaultValue": {"z": [True]}})],
+     ['{"d":{"z":[true]}}']),
+    # NaN maps never match: two segments annotated by one incr do not coalesce in the snapshot
+    # even at the MSN, where equal plain maps do (the control case)
+    ("nan_blocks_coalesce", [ins(0, "ab"), ins(2, "cd"), ann(0, 4, {"k": 1}, {"name": "incr"}),
+                             ins(4, "e")], ['{"k":null}', '{"k":null}']),
+    ("plain_coalesces", [ins(0, "ab"), ins(2, "cd"), ann(0, 4, {"k": 1}), ins(4, "e")], ['{"k":1}']),
+    # a segment split after its incr keeps one NaN map in both halves (the engine shares the
+    # map; the reference copies it): zamboni must not merge the halves back
+    ("nan_split_halves", [ins(0, "abcd"), ann(0, 4, {"k": 1}, {"name": "incr"}), ins(2, "X"), rem(2, 3),
+                          ins(4, "z")], ['{"k":null}', '{"k":null}']),
+    ("undefined_split_halves", [ins(0, "abcd"), ann(0, 4, {"u": 1}, {"name": "other"}), ins(2, "X"), rem(2, 3),
+                                ins(4, "z")], ['{}', '{}']),
+    # off the batch path (MT_DS_UNSUPPORTED): incr of a string (string concatenation), consensus
+    # on null (the reference throws), consensus writing into a held object whose seq is -1
+    ("incr_string", [ins(0, {"text": "ab", "props": {"s": "v"}}), ann(0, 2, {"s": 1}, {"name": "incr"})], UNSUPPORTED),
+    ("incr_string_default", [ins(0, "ab"), ann(0, 2, {"s": 1}, {"name": "incr", "defaultValue": "v"})], UNSUPPORTED),
+    ("consensus_null_default", [ins(0, "ab"), ann(0, 2, {"c": 1}, {"name": "consensus", "defaultValue": None})],
+     UNSUPPORTED),
+    ("consensus_held_seq_minus1", [ins(0, {"text": "ab", "props": {"c": {"seq": -1}}}),
+                                   ann(0, 2, {"c": 1}, {"name": "consensus"})], UNSUPPORTED),
+]
+
+
+def run_engine(factory, msgs, options=None):
+    g = ClientGroup(factory(1, **LIMITS))
+    c = g.new_client(options or {"newMergeTreeSnapshotFormat": True})
+    for m in msgs:
+        c.applyMsg(m)
+    g.flush()
+    return g, c
+
+
+@pytest.mark.parametrize("name,ops,want", CASES, ids=[c[0] for c in CASES])
+def test_combine_known_answers_oracle(name, ops, want):
+    """The oracle's restatement gives the hand-worked answers (MSN at the last message)."""
+    msgs = stream_of(ops, msn_lag=0)
+    o = OracleDoc(True)
+    st = 0
+    for m in msgs:
+        st |= o.apply_msg(m)
+    if isinstance(want, int):
+        assert st & want
+        return
+    assert st == 0
+    blobs, _ = o.snapshot(msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"])
+    assert props_texts(blobs) == want
+
+
+def check_engine_case(factory, ops, want):
+    msgs = stream_of(ops, msn_lag=0)
+    g, _ = run_engine(factory, msgs)
+    st = int(g.engine.status([0])[0])
+    if isinstance(want, int):
+        assert st & want, st
+        return
+    assert st == 0, st
+    o = OracleDoc(True)
+    for m in msgs:
+        assert o.apply_msg(m) == 0
+    ed, od = g.engine.dump(0), o.dump()
+    assert ed.shape == od.shape and (ed[:, [0, 1, 3, 7, 8, 9, 10, 11]] == od[:, [0, 1, 3, 7, 8, 9, 10, 11]]).all()
+    msn, seq = msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"]
+    for legacy in (True, False):
+        (eb, edig), = g.engine.snapshot([0], [msn], [seq], legacy=legacy)
+        ob, odig = o.snapshot(msn, seq, legacy=legacy)
+        assert eb == ob and edig == odig
+    assert props_texts(eb) == want                     # SnapshotV1
+
+
+@pytest.mark.parametrize("name,ops,want", CASES, ids=[c[0] for c in CASES])
+def test_combine_known_answers_on_emulation(name, ops, want):
+    check_engine_case(emu_engine, ops, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,ops,want", CASES, ids=[c[0] for c in CASES])
+def test_combine_known_answers_on_gpu(name, ops, want):
+    check_engine_case(lambda n, **kw: Engine(n, device=0, **kw), ops, want)
+
+
+def test_zamboni_keeps_nan_segments_apart_on_emulation():
+    """The split halves of one NaN segment stay two rows after zamboni (rows, not just the
+    snapshot): the reference's copies never matchProperties-match."""
+    ops = CASES[[c[0] for c in CASES].index("nan_split_halves")][1]
+    g, _ = run_engine(emu_engine, stream_of(ops, msn_lag=0))
+    o = OracleDoc(True)
+    for m in stream_of(ops, msn_lag=0):
+        o.apply_msg(m)
+    ed, od = g.engine.dump(0), o.dump()
+    assert len(ed) == len(od)
+    assert (ed[:, 0] == 2).sum() == (od[:, 0] == 2).sum() == 2     # "ab" and "cd" stay two segments
+
+
+def test_packers_emit_no_unsupported_for_combining_ops():
+    """incr / consensus / other names pack as combine sets (MT_OPF_COMBINE), not as
+    MT_OP_UNSUPPORTED records."""
+    from fluidframework_amd.batch import (MT_OP_ANNOTATE, MT_OPF_COMBINE, MT_OPF_REWRITE, MT_VAL_CFRESH, MT_VAL_NAN,
+                                          MT_VAL_UNDEF, BatchBuilder, ClientNames, PropTable)
+    pt = PropTable()
+    bb = BatchBuilder(pt, ClientNames())
+    bb.begin_doc(0)
+    for i, cop in enumerate([{"name": "incr"}, {"name": "consensus"}, {"name": "max"}, True]):
+        bb.add_message(msg(i + 1, i, 0, ann(0, 1, {"k": 1}, cop)))
+    b = bb.build()
+    assert (b.arrays["type"] == MT_OP_ANNOTATE).all()
+    fl = b.arrays["flags"]
+    assert fl[0] & MT_OPF_COMBINE and not fl[0] & MT_OPF_REWRITE
+    assert all(f & MT_OPF_COMBINE and f & MT_OPF_REWRITE for f in fl[1:])
+    codes = [pt.sets[int(p)][0][1] for p in b.arrays["prop_id"]]
+    assert codes == [MT_VAL_NAN, MT_VAL_CFRESH, MT_VAL_UNDEF, MT_VAL_UNDEF]
+
+
+# ---- options.mergeTreeSnapshotChunkSize -------------------------------------------------------
+def chunk_doc(n_segs=600, seed=3):
+    """One client's stream of n_segs appended segments of 1..60 units that never coalesce
+    (alternating property maps)."""
+    rng = np.random.default_rng(seed)
+    ops, L = [], 0
+    for i in range(n_segs):
+        n = int(rng.integers(1, 61))
+        ops.append(ins(L, {"text": "x" * n, "props": {"p": i % 2}}))
+        L += n
+    return stream_of(ops, msn_lag=0), L
+
+
+@pytest.mark.parametrize("size", [100, 1000, 25000, 0.5, 99.5, "300"])
+def test_snapshot_chunk_size_oracle_rule(size):
+    """The oracle's chunks follow getSeqLengthSegs (snapshotV1.ts:70-92): each chunk takes
+    segments until its length reaches the size; the header lists every body chunk."""
+    msgs, total = chunk_doc()
+    o = OracleDoc(True)
+    o.set_snapshot_chunk(float(size))
+    for m in msgs:
+        o.apply_msg(m)
+    blobs, _ = o.snapshot(msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"])
+    chunks = [json.loads(b) for b in blobs]
+    sz = float(size)
+    assert sum(c["length"] for c in chunks) == total
+    for c in chunks[:-1]:
+        lens = [len((s["json"] if "json" in s else s)["text"]) for s in c["segments"]]
+        assert sum(lens) >= sz and sum(lens[:-1]) < sz
+    assert len(chunks[0]["headerMetadata"]["orderedChunkMetadata"]) == len(chunks)
+
+
+def check_chunk_sizes(factory):
+    msgs, _ = chunk_doc()
+    msn, seq = msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"]
+    for size in (100, 1000, 25000, 99.5, "300", float("inf")):
+        g, c = run_engine(factory, msgs, {"newMergeTreeSnapshotFormat": True, "mergeTreeSnapshotChunkSize": size})
+        o = OracleDoc(True)
+        o.set_snapshot_chunk(float(size))
+        for m in msgs:
+            o.apply_msg(m)
+        ob, odig = o.snapshot(msn, seq)
+        (eb, edig), = g.engine.snapshot([0], [msn], [seq])
+        assert eb == ob and edig == odig, size
+        assert g.engine.snapshot_digests([0], [msn], [seq])[0] == odig
+        tree = c.snapshot()
+        assert [e["value"]["contents"].encode() for e in tree["entries"]] == ob
+        if size == 100:
+            assert len(ob) > 100
+        if size == float("inf"):
+            assert len(ob) == 1
+
+
+def test_snapshot_chunk_sizes_on_emulation():
+    check_chunk_sizes(emu_engine)
+
+
+@pytest.mark.gpu
+def test_snapshot_chunk_sizes_on_gpu():
+    check_chunk_sizes(lambda n, **kw: Engine(n, device=0, **kw))
+
+
+def test_snapshot_chunk_option_values():
+    assert snapshot_chunk_option(None) == 0 and snapshot_chunk_option({}) == 0
+    assert snapshot_chunk_option({"mergeTreeSnapshotChunkSize": None}) == 0      # `?? SnapshotV1.chunkSize`
+    assert snapshot_chunk_option({"mergeTreeSnapshotChunkSize": 100}) == 100
+    assert snapshot_chunk_option({"mergeTreeSnapshotChunkSize": 99.2}) == 100
+    assert snapshot_chunk_option({"mergeTreeSnapshotChunkSize": "7"}) == 7
+    assert snapshot_chunk_option({"mergeTreeSnapshotChunkSize": float("inf")}) == (1 << 64) - 1
+    for bad in (0, -5, float("nan"), "abc", True, [3]):
+        with pytest.raises(MergeTreeError):
+            snapshot_chunk_option({"mergeTreeSnapshotChunkSize": bad})
+
+
+def test_reopened_document_resets_chunk_size_on_emulation():
+    """mt_docs_open gives the document a new Client's default chunk size."""
+    msgs, _ = chunk_doc(200)
+    eng = emu_engine(1, **LIMITS)
+    eng.set_snapshot_chunk([0], [100])
+    g = ClientGroup(eng)
+    c = g.new_client({"newMergeTreeSnapshotFormat": True})      # opens document 0 again
+    for m in msgs:
+        c.applyMsg(m)
+    g.flush()
+    o = OracleDoc(True)
+    for m in msgs:
+        o.apply_msg(m)
+    msn, seq = msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"]
+    assert eng.snapshot([0], [msn], [seq])[0][0] == o.snapshot(msn, seq)[0]
+
+
+def check_node_chunk_and_combine(addon):
+    from js_lib import run_node
+    from msg_gen import stream
+    msgs, _ = chunk_doc(300)
+    got = run_node([msgs], addon=addon, options={"newMergeTreeSnapshotFormat": True, "mergeTreeSnapshotChunkSize": 250})
+    o = OracleDoc(True)
+    o.set_snapshot_chunk(250)
+    for m in msgs:
+        o.apply_msg(m)
+    blobs, _ = o.snapshot(msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"])
+    assert [b for _, b in got["blobs"][0]] == [b.decode() for b in blobs]
+    assert len(blobs) > 20
+
+
+def test_node_host_chunk_size_on_emulation():
+    from js_lib import NODE
+    from emu_lib import build_emu_napi
+    if NODE is None:
+        pytest.skip("node is not installed")
+    check_node_chunk_and_combine(build_emu_napi())
+
+
+@pytest.mark.gpu
+def test_node_host_chunk_size_on_gpu():
+    import os
+    from js_lib import NODE, ROOT
+    if NODE is None:
+        pytest.skip("node is not installed")
+    check_node_chunk_and_combine(os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"))
