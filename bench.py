@@ -223,6 +223,47 @@ def digest_parity(gpu_digests, oracle_digests, oracle_status):
     return f"DIGEST MISMATCH: {k - same} of {k} sample docs differ from the oracle"
 
 
+def manifest_parity(name, digs, **shape):
+    """Every document's SnapshotV1 digest against the oracle-made manifest of this workload
+    (tests/golden/digests, tools/make_digest_manifest.py) when one exists for this seed and
+    shape: {"checked", "of", "mismatches", "manifest"} or None.  Roll-up manifests (the
+    1,048,576-document run) compare xxh64 roll-ups of each 1,024 consecutive documents."""
+    d = os.path.join(ROOT, "tests", "golden", "digests")
+    try:
+        ent = json.load(open(os.path.join(d, "index.json")))[name]
+    except (OSError, ValueError, KeyError):
+        return None
+    if any(ent.get(k) != v for k, v in shape.items()):
+        return None
+    want = np.fromfile(os.path.join(d, ent["file"]), dtype="<u8")
+    got = np.asarray(digs, np.uint64)
+    if ent["file"].endswith(".roll.u64"):
+        import xxhash
+        k = int(ent["kind"].split()[3]) if "roll-ups" in ent["kind"] else 1024
+        if len(got) != ent["docs"]:
+            return None
+        roll = np.array([xxhash.xxh64(got[i:i + k].astype("<u8").tobytes(), seed=0).intdigest()
+                         for i in range(0, len(got), k)], np.uint64)
+        bad_groups = np.nonzero(roll != want)[0]
+        bad = int(sum(min(k, len(got) - g * k) for g in bad_groups))
+        return {"checked": len(got), "of": ent["docs"], "mismatches": bad,
+                "mismatch_groups": [int(g) for g in bad_groups[:16]], "manifest": f"tests/golden/digests/{ent['file']}"}
+    if len(got) != len(want):
+        return None
+    bad = int((got != want).sum())
+    return {"checked": len(got), "of": len(want), "mismatches": bad,
+            "first_mismatch": int(np.nonzero(got != want)[0][0]) if bad else None,
+            "manifest": f"tests/golden/digests/{ent['file']}"}
+
+
+def manifest_text(m):
+    if m is None:
+        return ""
+    if m["mismatches"] == 0:
+        return f"; every document's SnapshotV1 digest == the oracle's manifest: {m['checked']} of {m['of']}"
+    return f"; MANIFEST MISMATCH: {m['mismatches']} of {m['of']} documents differ from the oracle's manifest"
+
+
 def run_config4(args, c, world, rank, local):
     """Config 4: long documents.  Untimed: pre-build every document by
     c['prebuild'] appends (5 chars, segment props alternating between two sets,
@@ -337,6 +378,10 @@ def run_config4(args, c, world, rank, local):
             out["parity"] = digest_parity(digs, odg, ost)
     elif world > 1 and ok:
         out["parity"] = parity_text(par_bad, par_checked, world)
+    man = manifest_parity("config4", digs, seed=args.seed, docs=n, msgs_per_doc=ops, prebuild=pre) if ok else None
+    if man is not None:
+        out["parity_manifest"] = man
+        out["parity"] += manifest_text(man)
     print(json.dumps(out), flush=True)
 
 
@@ -490,6 +535,12 @@ def run_config5(args, c, world, rank, local):
             out["parity"] = config5_parity(args, c, sh, digs)
     elif world > 1 and int(bad[0].item()) == 0 and not args.no_cpu_baseline:
         out["parity"] = parity_text(int(par[0].item()), int(par[1].item()), world) + ", all ranks clean"
+    if int(bad[0].item()) == 0:
+        name = "config5_1m" if total_docs == 1048576 else "config5"
+        man = manifest_parity(name, digs, seed=args.seed, docs=total_docs, msgs_total=total_msgs)
+        if man is not None:
+            out["parity_manifest"] = man
+            out["parity"] += manifest_text(man)
     if int(bad[1].item()):
         out["parity"] = f"EXCHANGE CHECKSUM MISMATCH on {int(bad[1].item())} docs; " + out["parity"]
     print(json.dumps(out), flush=True)
@@ -874,6 +925,12 @@ def _main(argv=None):
                                                if counters_match(cnt2, len(odg)) else "COUNTER MISMATCH vs oracle")
     elif world > 1 and ok:
         out["parity"] = parity_text(par_bad, par_checked, world)
+    # rank 0's documents are the default seed's at any N (seed ^ rank * ...): all of them against
+    # the oracle-made manifest
+    man = manifest_parity(args.config, digs, seed=args.seed, docs=c["docs"], msgs_per_doc=c["ops"]) if ok else None
+    if man is not None:
+        out["parity_manifest"] = man
+        out["parity"] += manifest_text(man)
     if world == 1 and not args.no_ingest:
         out["ingest"] = ingest_leg(local, c, seed)
     print(json.dumps(out), flush=True)

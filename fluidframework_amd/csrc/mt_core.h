@@ -2798,7 +2798,8 @@ template <int RES, bool FULL = true> struct MtEngT {
         psetTop += nch;
         // never-equal values (NaN, undefined, fresh consensus objects; made by a combining op
         // or kept from the old map) mark the map
-        const int never = wave_ballot(wave_map(nn, [&](int i) MT_LAM { return own(vv, i) < 0; })) ? 1 : 0;
+        const int never = (pm >= MT_PM_INCR || mt_cold_v.pNever) &&
+                          wave_ballot(wave_map(nn, [&](int i) MT_LAM { return own(vv, i) < 0; })) ? 1 : 0;
         if (never) mt_cold_v.pNever = 1;
         wave_for(nch * MT_PSK, [&](int i) MT_LAM {
             pset[id + (i >> 4)].key[i & 15] = (uint16_t)(i < nn ? own(kk, i) : 0);

@@ -69,6 +69,44 @@ def generation_caps(ops: np.ndarray, ins_len: int) -> dict:
                 propsets_per_doc=np.full(len(o), 64))
 
 
+# Pool bytes per element / per document, as mt_create_impl lays them out (csrc/mt_api_impl.h):
+# rows 48 B (MtRow); blocks 64 B; heap 8 B (cap + 1 entries); window + U ids + U deltas 12 B;
+# ancestor chains 4 B x MT_MAXH (16) per window entry; text 2 x 2 B (two halves); property
+# sets 112 B (MtPSet); marker ids 4 B; register rows 2 x 4 B; per document: header, recycled
+# rows (4 x MT_RFL 128), layout, overlap side list (16 x 512), registers (32 x 64).
+_DOC_FIXED = 208 + 4 * 128 + 112 + 16 * 512 + 32 * 64
+
+
+def pool_bytes_estimate(caps: dict) -> int:
+    """HBM bytes an engine with these per-document caps allocates (mt_pool_bytes; markers 1,024
+    and register rows 256 per document unless given)."""
+    c = {k: np.asarray(v, np.int64) for k, v in caps.items()}
+    n = len(c["rows_per_doc"])
+    mark = c.get("markers_per_doc", np.full(n, 1024))
+    regr = c.get("register_rows_per_doc", np.full(n, 256))
+    per = (48 * c["rows_per_doc"] + 64 * c["blocks_per_doc"] + 8 * (c["heap_per_doc"] + 1) +
+           12 * c["window_per_doc"] + 4 * 16 * c["window_per_doc"] + 4 * c["text_per_doc"] +
+           112 * c["propsets_per_doc"] + 4 * mark + 8 * regr + _DOC_FIXED)
+    return int(per.sum())
+
+
+def rank0_peak_bytes(ops: np.ndarray, world: int, ins_len: int = 8, chunk_docs: int = 131072) -> dict:
+    """Rank 0's device memory peak in build_sharded + replay: the send buffer of every
+    document's rows (held while generation chunks come and go), the largest generating
+    engine, then the rows it receives and its own engine (generation caps: an upper bound of
+    the exact replay caps)."""
+    ops = np.asarray(ops, np.int64)
+    send = int(ops.sum()) * (REC_BYTES + 2 * ins_len)
+    gen = max(pool_bytes_estimate(generation_caps(ops[a:a + chunk_docs], ins_len))
+              for a in range(0, len(ops), chunk_docs))
+    owner = lpt_assign(ops, world)
+    mine = ops[owner == 0]
+    recv = int(mine.sum()) * (REC_BYTES + 2 * ins_len)
+    own = pool_bytes_estimate(generation_caps(mine, ins_len))
+    return {"send": send, "generate": gen, "recv": recv, "own_engine": own,
+            "total": send + max(gen, recv + own)}
+
+
 def replay_caps(pools: np.ndarray, gen_caps: dict, idx) -> np.ndarray:
     """[n, 6] caps (rows, blocks, heap, window, text, psets) from the generation's
     high-water marks (mt_doc_pools columns 0, 1, 8, 9, 5); text keeps the generation cap."""

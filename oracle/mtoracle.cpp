@@ -20,6 +20,7 @@
 #include "mtoracle.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -2068,19 +2069,20 @@ void ora_stats(ora_doc* o, int32_t* out) {
     out[0] = h; out[1] = (int)o->d.t.ovlHigh; out[2] = nseg; out[3] = (int)o->d.t.blocks.size();
 }
 
-uint32_t ora_generate_doc(const mt_gen_params* p, uint32_t doc, const mt_prop_table* props,
-                          uint8_t* type, uint8_t* flags, uint16_t* client, int32_t* seq,
-                          int32_t* ref_seq, int32_t* msn, int32_t* pos1, int32_t* pos2,
-                          uint32_t* payload_off, uint32_t* payload_len, int32_t* prop_id,
-                          uint16_t* payload, uint32_t payload_base, ora_doc** keep) {
-    ora_doc* o = ora_new(1);
-    load_props(o->d.props, props);
+// One document's stream generated with the oracle as sequencer + observer, by the device
+// generator's rules (csrc/mt_replay.h mt_gen_op / mt_replay_run): o continues from its current
+// window (seqs from currentSeq + 1, every client's last refSeq at the MSN: a fresh document
+// starts at 0), the stream seeded by the global document id.
+static uint32_t gen_stream(ora_doc* o, const mt_gen_params* p, uint32_t doc, uint32_t n_ops, uint32_t clients,
+                           uint8_t* type, uint8_t* flags, uint16_t* client, int32_t* seq, int32_t* ref_seq, int32_t* msn,
+                           int32_t* pos1, int32_t* pos2, uint32_t* payload_off, uint32_t* payload_len, int32_t* prop_id,
+                           uint16_t* payload, uint32_t payload_base) {
     SplitMix rng{p->seed ^ (0x9E3779B97F4A7C15ULL * (uint64_t)(doc + 1))};
-    std::vector<int> lastRef(p->clients, 0);
-    int cur = 0, curMsn = 0; uint32_t pw = 0;
+    std::vector<int> lastRef(clients, o->d.t.minSeq);
+    int cur = o->d.t.currentSeq, curMsn = o->d.t.minSeq; uint32_t pw = 0;
     uint32_t offs[2] = {0, 1};
-    for (uint32_t k = 0; k < p->ops_per_doc; k++) {
-        uint32_t a = rng.u(p->clients);
+    for (uint32_t k = 0; k < n_ops; k++) {
+        uint32_t a = rng.u(clients);
         uint32_t lag = rng.u(p->lag_max + 1);
         int r = cur - (int)lag; if (r < lastRef[a]) r = lastRef[a]; if (r < curMsn) r = curMsn;
         lastRef[a] = r;
@@ -2104,7 +2106,7 @@ uint32_t ora_generate_doc(const mt_gen_params* p, uint32_t doc, const mt_prop_ta
             s1 = (int)rng.u((uint32_t)L); uint32_t n = 1 + rng.u(p->rem_len_max); s2 = std::min(L, s1 + (int)n);
             if (ty == MT_OP_ANNOTATE) { pid = (int)rng.u(p->n_ann_sets); if (rng.u(100) < p->pct_rewrite) fl |= MT_OPF_REWRITE; }
         }
-        int mn = lastRef[0]; for (uint32_t c = 1; c < p->clients; c++) mn = std::min(mn, lastRef[c]);
+        int mn = lastRef[0]; for (uint32_t c = 1; c < clients; c++) mn = std::min(mn, lastRef[c]);
         type[k] = (uint8_t)ty; flags[k] = fl; client[k] = (uint16_t)a; seq[k] = cur + 1; ref_seq[k] = r; msn[k] = mn;
         pos1[k] = s1; pos2[k] = s2; payload_off[k] = payload_base + pw; payload_len[k] = plen; prop_id[k] = pid;
         // apply through the observer (a one-op batch over the caller's arrays)
@@ -2116,9 +2118,64 @@ uint32_t ora_generate_doc(const mt_gen_params* p, uint32_t doc, const mt_prop_ta
         pw += plen; cur = cur + 1; curMsn = mn;
         if (o->d.t.status) break;
     }
-    uint32_t st = o->d.t.status;
+    return o->d.t.status;
+}
+
+uint32_t ora_generate_doc(const mt_gen_params* p, uint32_t doc, const mt_prop_table* props,
+                          uint8_t* type, uint8_t* flags, uint16_t* client, int32_t* seq,
+                          int32_t* ref_seq, int32_t* msn, int32_t* pos1, int32_t* pos2,
+                          uint32_t* payload_off, uint32_t* payload_len, int32_t* prop_id,
+                          uint16_t* payload, uint32_t payload_base, ora_doc** keep) {
+    ora_doc* o = ora_new(1);
+    load_props(o->d.props, props);
+    uint32_t st = gen_stream(o, p, doc, p->ops_per_doc, p->clients, type, flags, client, seq, ref_seq, msn, pos1, pos2,
+                             payload_off, payload_len, prop_id, payload, payload_base);
     if (keep) *keep = o; else ora_free(o);
     return st;
+}
+
+// Test support (digest manifests, tools/make_digest_manifest.py): documents first..first+n-1
+// (global ids; p->seed as the device generation seeds them) generated and replayed by the
+// oracle on `threads` threads, and their SnapshotV1 digests at the final window.  pre
+// (optional): a stream generated first on the fresh document (config 4's pre-build), p's
+// stream then continues it (continue_docs).  ops / clients (optional): per-document counts
+// indexed by position (config 5), else p->ops_per_doc / p->clients.
+int ora_generate_digests(const mt_gen_params* p, const mt_gen_params* pre, const mt_prop_table* props, uint32_t first,
+                         uint32_t n, const uint32_t* ops, const uint32_t* clients, int threads, uint64_t* digests,
+                         uint32_t* status) {
+    PropTable pt; load_props(pt, props);
+    if (threads < 1) threads = 1;
+    std::atomic<uint32_t> next{0};
+    auto work = [&]() {
+        struct Cols {
+            std::vector<uint8_t> type, flags; std::vector<uint16_t> client, payload; std::vector<int32_t> seq, ref, msn, p1, p2, pid;
+            std::vector<uint32_t> poff, plen;
+            void size(uint32_t k, uint32_t L) {
+                type.resize(k); flags.resize(k); client.resize(k); seq.resize(k); ref.resize(k); msn.resize(k); p1.resize(k);
+                p2.resize(k); pid.resize(k); poff.resize(k); plen.resize(k); payload.resize((size_t)k * L + 1);
+            }
+        } c;
+        for (uint32_t j; (j = next.fetch_add(1)) < n;) {
+            ora_doc* o = ora_new(1); o->d.props = pt;
+            uint32_t st = 0;
+            auto run = [&](const mt_gen_params* g, uint32_t k, uint32_t cl) {
+                c.size(k, g->ins_len_max);
+                st |= gen_stream(o, g, first + j, k, cl, c.type.data(), c.flags.data(), c.client.data(), c.seq.data(),
+                                 c.ref.data(), c.msn.data(), c.p1.data(), c.p2.data(), c.poff.data(), c.plen.data(),
+                                 c.pid.data(), c.payload.data(), 0);
+            };
+            if (pre) run(pre, pre->ops_per_doc, pre->clients);
+            if (!st) run(p, ops ? ops[j] : p->ops_per_doc, clients ? clients[j] : p->clients);
+            if (status) status[j] = st;
+            digests[j] = st ? 0 : blobs_digest(snapshot_v1(o->d, o->d.t.minSeq, o->d.t.currentSeq));
+            ora_free(o);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; t++) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+    return 0;
 }
 
 double ora_replay_batch(const mt_op_batch* b, const mt_prop_table* props, int threads, uint64_t* digests, uint32_t* status,

@@ -91,6 +91,13 @@ uint32_t ora_generate_doc(const mt_gen_params* p, uint32_t doc, const mt_prop_ta
                           int32_t* ref_seq, int32_t* msn, int32_t* pos1, int32_t* pos2,
                           uint32_t* payload_off, uint32_t* payload_len, int32_t* prop_id,
                           uint16_t* payload, uint32_t payload_base, ora_doc** keep_doc);
+/* Test support (digest manifests): the SnapshotV1 digests of documents first..first+n-1
+ * generated and replayed by the oracle (ora_generate_doc's rules, global document ids), on
+ * `threads` threads; pre (optional) is generated first and p continues it; ops / clients
+ * (optional) are per-document counts. */
+int      ora_generate_digests(const mt_gen_params* p, const mt_gen_params* pre, const mt_prop_table* props,
+                              uint32_t first, uint32_t n, const uint32_t* ops, const uint32_t* clients, int threads,
+                              uint64_t* digests, uint32_t* status);
 
 /* Debug: verify partial lengths == exact leaf sums at every generated op. */
 void ora_set_verify(int on);

@@ -96,6 +96,50 @@ def test_sharded_replay_gloo_world2_matches_oracle(tmp_path):
     assert [int(x) for x in d2] == want
 
 
+@pytest.mark.parametrize("world", [4, 8])
+def test_sharded_replay_gloo_wide_matches_oracle(world, tmp_path):
+    """The 4- and 8-rank path on ~2,000 Zipf documents (sizes capped at 1,024 messages so the
+    emulation finishes in seconds): the LPT split gives every rank a share, rank 0 is the only
+    sender of the all_to_all_single (the other senders are empty), and the gathered digests
+    come back in global document order, equal to a single rank's and to the oracle's."""
+    from oracle_lib import gen_params, generate
+    from fluidframework_amd.batch import PropTable
+    docs = 2000
+    counts = zipf_op_counts(docs, 11, hi=1024)
+    clients = clients_per_doc(docs, 11)
+    owner = lpt_assign(counts, world)
+    assert (np.bincount(owner, minlength=world) > 0).all()
+    dw = _run(world, docs, counts, clients, tmp_path)
+    d1 = _run(1, docs, counts, clients, tmp_path)
+    assert np.array_equal(dw, d1)
+    p = gen_params(seed=77, n_docs=docs, clients=2, lag=32, ins=60, rem=40, ins_len=8, rem_len=8, ops=8)
+    batch, st, kept = generate(p, PropTable(), ops_per_doc=counts, clients_per_doc=clients, keep=True,
+                               threads=min(8, os.cpu_count() or 1))
+    assert not any(st)
+    last = batch.op_offsets[1:] - 1
+    want = np.array([kept[d].snapshot(int(batch.arrays["msn"][last[d]]), int(batch.arrays["seq"][last[d]]))[1]
+                     for d in range(docs)], np.uint64)
+    assert np.array_equal(dw, want)
+
+
+def test_north_star_rank0_memory_fits_at_8_ranks():
+    """Host-only sizing of rank 0 at N = 8 for the north_star's 1,048,576 Zipf documents:
+    the send buffer of every document's exchange rows, the largest generating engine (a chunk
+    of 131,072 documents with generation caps), the rows it receives and the engine for its
+    own share must fit in one MI355X's 288 GB.  The pool estimate is the library's own
+    (mt_pool_bytes), checked here against the emulation library on a small population."""
+    from emu_lib import emu_engine
+    from fluidframework_amd.shard import generation_caps, pool_bytes_estimate, rank0_peak_bytes
+    small = zipf_op_counts(40, 3, hi=2048)
+    caps = generation_caps(small, 8)
+    eng = emu_engine(len(small), per_doc=caps)
+    assert eng.pool_bytes() == pool_bytes_estimate(caps)
+    ops = zipf_op_counts(1048576, 20241015)
+    peak = rank0_peak_bytes(ops, world=8, ins_len=8)
+    assert peak["total"] < 288e9, peak
+    assert peak["send"] == int(ops.sum()) * (32 + 2 * 8)
+
+
 class HostRows:
     """Exchange-row buffers in host memory (the emulation's "device" pointers)."""
 
