@@ -66,6 +66,16 @@
 #ifndef MT_B_HEAP
 #define MT_B_HEAP 94
 #endif
+// Wide block residency (mt_replay_blkw_kernel, MT_RES_BLKW): the same engine with room for
+// the trees and heaps of long documents (~21 KB of LDS per workgroup), run for the size class
+// of long runs (mt_set_size_class) beside the block-residency kernel for the rest.
+#ifndef MT_BW_BLKS
+#define MT_BW_BLKS 248
+#endif
+#ifndef MT_BW_HEAP
+#define MT_BW_HEAP 254
+#endif
+#define MT_BW_BT 256
 // Long-document residency (mt_replay_big_kernel): a document whose blocks cannot fit
 // LDS (config 4: ~50k blocks) keeps its zamboni heap, collab window and the first
 // MT_G_U U-set entries with their ancestor chains in LDS (~68 KB: two documents per CU),
@@ -134,7 +144,7 @@ enum { MT_BIGF_NO_BCACHE = 1, MT_BIGF_NO_PREFETCH = 2, MT_BIGF_NO_TABLE = 4, MT_
 #define MT_G_BP (1 << MT_G_BPL)
 #define MT_BP_EMPTY 0xFFFFFFFFu
 #define MT_G_HTN (MT_G_HT * 3 / 4)
-enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2, MT_RES_BIG = 3 };
+enum { MT_RES_HBM = 0, MT_RES_LDS = 1, MT_RES_BLK = 2, MT_RES_BIG = 3, MT_RES_BLKW = 4 };
 // Diagnostic builds keep per-document phase/event counters (prof[]) across binds;
 // product builds never load or store them (8 SGPR pairs fewer live in the replay loop).
 #if defined(MT_PROFILE) || defined(MT_PROFILE2) || defined(MT_PROFILE3) || defined(MT_PROFILE4) || defined(MT_BPC_STATS) || defined(MT_EVCOUNT3) || defined(MT_EVCOUNT) || defined(MT_EVCOUNT2)
@@ -386,17 +396,20 @@ struct __attribute__((aligned(16))) MtLdsPools {
     uint8_t uanc[MT_L_ROWS * MT_L_H];
 };
 
-// LDS home of a document's blocks and heap while mt_replay_blk_kernel runs it.
-struct __attribute__((aligned(16))) MtLdsBlk {
-    MtBlk blk[MT_B_BLKS];
-    MtHeapE heap[MT_B_HEAP + 2];
+// LDS home of a document's blocks and heap while mt_replay_blk_kernel (NB = MT_B_BLKS) or
+// mt_replay_blkw_kernel (NB = MT_BW_BLKS) runs it.
+template <int NB, int NH, int NT> struct __attribute__((aligned(16))) MtLdsBlkT {
+    static_assert(NB <= NT, "block ids index the corrections table");
+    MtBlk blk[NB];
+    MtHeapE heap[NH + 2];
     int uid[MT_B_U], udelta[MT_B_U];
     // Per-block perspective corrections of the current U set (Σ delta of the U rows beneath
     // each block, indexed by block id): a descent level reads its children's lengths as
     // observer length + correction instead of scanning U (no ancestor chains kept).
-    int bcorr[MT_B_BT];
+    int bcorr[NT];
 };
-static_assert(MT_B_BLKS <= MT_B_BT, "block ids index the corrections table");
+using MtLdsBlk = MtLdsBlkT<MT_B_BLKS, MT_B_HEAP, MT_B_BT>;
+using MtLdsBlkW = MtLdsBlkT<MT_BW_BLKS, MT_BW_HEAP, MT_BW_BT>;
 
 // LDS home of a long document's heap, window and U set while mt_replay_big_kernel runs it.
 struct __attribute__((aligned(16))) MtLdsBig {
@@ -522,6 +535,12 @@ static MtLdsBlk mt_ldsb_v;
 #endif
 MT_INLINE MtLdsBlk& mt_ldsb() { return mt_ldsb_v; }
 #if defined(__HIP_DEVICE_COMPILE__)
+__shared__ MtLdsBlkW mt_ldsbw_v;
+#else
+static MtLdsBlkW mt_ldsbw_v;
+#endif
+MT_INLINE MtLdsBlkW& mt_ldsbw() { return mt_ldsbw_v; }
+#if defined(__HIP_DEVICE_COMPILE__)
 __shared__ MtLdsBig mt_ldsg_v;
 #else
 static MtLdsBig mt_ldsg_v;
@@ -570,14 +589,18 @@ template <int RES, bool FULL = true> struct MtEngT {
     static constexpr bool kFull = FULL;
     static constexpr bool LDS = RES == MT_RES_LDS;      // all hot pools in LDS
     static constexpr bool BIG = RES == MT_RES_BIG;      // heap, window, U set in LDS; blocks in HBM
-    static constexpr bool BLKL = RES == MT_RES_LDS || RES == MT_RES_BLK;   // blocks + heap in LDS
+    static constexpr bool BW = RES == MT_RES_BLKW;       // wide block residency (long runs)
+    static constexpr bool BLKR = RES == MT_RES_BLK || BW;   // block residency, either width
+    static constexpr bool BLKL = RES == MT_RES_LDS || BLKR;  // blocks + heap in LDS
+    // the block-residency LDS home of this instantiation
+    MT_HD auto& LB() const { if constexpr (BW) return mt_ldsbw(); else return mt_ldsb(); }
     MtEngParams& S = mt_cold_v.S;      // cold state (MtCold, LDS)
     MtDocHdr*& hdrp = mt_cold_v.hdr;
     // doc-local views
     MtRow* R;
     // Block residency keeps blocks, heap and the first U entries in LDS: their HBM homes (and
     // the property-set pool) are cold there and live in MtCold; other modes keep them in SGPRs.
-    template <class T> using Home = std::conditional_t<RES == MT_RES_BLK, T&, T>;
+    template <class T> using Home = std::conditional_t<BLKR, T&, T>;
     int* win;
     Home<int*> uid = mt_cold_v.uid; Home<int*> udelta = mt_cold_v.udelta; Home<int*> uanc = mt_cold_v.uanc;
     Home<MtBlk*> blk = mt_cold_v.blk; Home<MtHeapE*> heap = mt_cold_v.heap;
@@ -595,7 +618,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     // pool accessors: LDS (MT_RES_LDS, MT_RES_BLK for blocks + heap) or HBM homes
     MT_HD MtRow& row(int s) const { if constexpr (LDS) return mt_lds().rows[s]; else return R[s]; }
     MT_HD MtBlk& bk(int b) const {
-        if constexpr (LDS) return mt_lds().blk[b]; else if constexpr (BLKL) return mt_ldsb().blk[b];
+        if constexpr (LDS) return mt_lds().blk[b]; else if constexpr (BLKL) return LB().blk[b];
         else if constexpr (BIG && MT_G_BCACHE) {        // block cache hit: the LDS copy is the current one
             const int s = b & (MT_G_BC - 1);
             return mt_ldsg().btag[s] == b ? mt_ldsg().bc[s] : blk[b];
@@ -623,7 +646,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         else { (void)B; return 0; }
     }
     MT_HD MtHeapE& hp(int k) const {
-        if constexpr (LDS) return mt_lds().heap[k]; else if constexpr (BLKL) return mt_ldsb().heap[k];
+        if constexpr (LDS) return mt_lds().heap[k]; else if constexpr (BLKL) return LB().heap[k];
         else if constexpr (BIG) return mt_ldsg().heap[k]; else return heap[k];
     }
     MT_HD int& wn(int k) const {
@@ -636,21 +659,21 @@ template <int RES, bool FULL = true> struct MtEngT {
     // MT_RES_BLK keeps the first MT_B_U U-set entries in LDS, MT_RES_BIG the first
     // MT_G_U.  U loops run per 64-entry chunk (chunks never straddle the cap), so each
     // chunk picks its home at compile time: forU calls f(std::bool_constant<inLds>, base, m).
-    static constexpr bool UL = RES == MT_RES_BLK || RES == MT_RES_BIG;
-    static constexpr bool BT = RES == MT_RES_BLK;   // per-block corrections table (MtLdsBlk::bcorr)
-    static constexpr int UCAP = RES == MT_RES_BLK ? MT_B_U : (RES == MT_RES_BIG ? MT_G_U : 0);
+    static constexpr bool UL = BLKR || RES == MT_RES_BIG;
+    static constexpr bool BT = BLKR;   // per-block corrections table (MtLdsBlkT::bcorr)
+    static constexpr int UCAP = BLKR ? MT_B_U : (RES == MT_RES_BIG ? MT_G_U : 0);
     template <bool L> MT_HD int uiAt(int k) const {
-        if constexpr (UL && L) { if constexpr (BIG) return mt_ldsg().uid[k]; else return mt_ldsb().uid[k]; }
+        if constexpr (UL && L) { if constexpr (BIG) return mt_ldsg().uid[k]; else return LB().uid[k]; }
         else return ui(k);
     }
     template <bool L> MT_HD int udAt(int k) const {
-        if constexpr (UL && L) { if constexpr (BIG) return mt_ldsg().udelta[k]; else return mt_ldsb().udelta[k]; }
+        if constexpr (UL && L) { if constexpr (BIG) return mt_ldsg().udelta[k]; else return LB().udelta[k]; }
         else return ud(k);
     }
     template <bool L> MT_HD void uPutAt(int k, int id, int delta) {
         if constexpr (UL && L) {
             if constexpr (BIG) { mt_ldsg().uid[k] = id; mt_ldsg().udelta[k] = delta; }
-            else { mt_ldsb().uid[k] = id; mt_ldsb().udelta[k] = delta; }
+            else { LB().uid[k] = id; LB().udelta[k] = delta; }
         } else { ui(k) = id; ud(k) = delta; }
     }
     template <bool L> MT_HD void ancPutAt(int u, int h, int a) {
@@ -910,11 +933,12 @@ template <int RES, bool FULL = true> struct MtEngT {
             nU = 0; uValid = false;
             return true;
         }
-        if constexpr (!LDS) {                                   // MT_RES_BLK: blocks + heap only
-            if (lb > MT_B_BLKS) lb = MT_B_BLKS;
-            if (lh > MT_B_HEAP) lh = MT_B_HEAP;
+        if constexpr (!LDS) {                                   // MT_RES_BLK / BLKW: blocks + heap only
+            constexpr int kB = BW ? MT_BW_BLKS : MT_B_BLKS, kH = BW ? MT_BW_HEAP : MT_B_HEAP;
+            if (lb <= 0 || lb > kB) lb = kB;
+            if (lh <= 0 || lh > kH) lh = kH;
             if (blkTop > lb || heapN > lh || height + 3 > MT_L_H) return false;
-            MtLdsBlk& B = mt_ldsb();
+            auto& B = LB();
             copyQ((MtQ16*)B.blk, (const MtQ16*)blk, blkTop * (int)(sizeof(MtBlk) / 16));
             copyI((int*)B.heap, (const int*)heap, 2 * (heapN + 1));
             wave_sync();
@@ -966,7 +990,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             return;
         }
         if constexpr (!LDS) {
-            MtLdsBlk& B = mt_ldsb();
+            auto& B = LB();
             copyQ((MtQ16*)blk, (const MtQ16*)B.blk, blkTop * (int)(sizeof(MtBlk) / 16));
             copyI((int*)heap, (const int*)B.heap, 2 * (heapN + 1));
             wave_sync();
@@ -1459,7 +1483,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         if constexpr (BT) {                               // corrections table: cleared per U set
             for (int base = 0; base < blkTop; base += MT_WAVE) {
                 const int m = (blkTop - base) < MT_WAVE ? (blkTop - base) : MT_WAVE;
-                wave_for(m, [&](int k) MT_LAM { mt_ldsb().bcorr[base + k] = 0; });
+                wave_for(m, [&](int k) MT_LAM { LB().bcorr[base + k] = 0; });
             }
             wave_sync();
         }
@@ -1535,7 +1559,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                 int a = w.parent;
                 if constexpr (BT) {                       // the row's delta into every block above it
                     if (pos < UCAP) uPutAt<true>(pos, w.id, w.delta); else uPutAt<false>(pos, w.id, w.delta);
-                    for (int h = 0; h <= HH && a >= 0; h++) { lds_add(&mt_ldsb().bcorr[a], w.delta); a = bk(a).parent; }
+                    for (int h = 0; h <= HH && a >= 0; h++) { lds_add(&LB().bcorr[a], w.delta); a = bk(a).parent; }
                 } else if constexpr (UL) {
                     if (pos < UCAP) {
                         uPutAt<true>(pos, w.id, w.delta);
@@ -1795,7 +1819,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         if constexpr (BT) {                              // the children's corrections from the table
             return wave_map(h.n, [&](int j) MT_LAM {
                 const int b = own(ch, j);
-                ChildL o; o.len = bk(b).len + mt_ldsb().bcorr[b]; o.tie = true; return o;
+                ChildL o; o.len = bk(b).len + LB().bcorr[b]; o.tie = true; return o;
             });
         } else return childLensU(B, h, ch, r, c, haveLen, kl, lsN);
     }
@@ -2060,7 +2084,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                        "parent=%d vis=%d\n", lane, ch, cl.len, (int)cl.tie, ln, sq, rs, mt, rc, ov, par, (int)vis);
             } else {
                 int corr = 0;
-                if constexpr (BT) corr = mt_ldsb().bcorr[ch];
+                if constexpr (BT) corr = LB().bcorr[ch];
                 const volatile MtBlk* v = (const volatile MtBlk*)&bk(ch);
                 printf("  WALKFAIL child %d blk=%d used_len=%d | bk.len=%d bcorr=%d n=%d parent=%d height=%d\n", lane, ch, cl.len,
                        v->len, corr, v->n, v->parent, v->height);

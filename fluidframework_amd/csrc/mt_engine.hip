@@ -220,12 +220,15 @@ static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) 
         return;
     }
     if (c->use_lds == 2 && c->big_min_ops && c->n_long) {
-        // size classes: long runs on stream2 in the long-document kernel, the rest here, joined
+        // size classes: long runs on stream2 in the wide block-residency kernel (launched first,
+        // so the long runs take their slots before the short ones fill the CUs), the rest here,
+        // joined; capture batches (FULL) take the long-document kernel
         const uint32_t* runs = (const uint32_t*)c->b_runs.p;
         hipStream_t s2 = (hipStream_t)c->stream2;
         (void)hipEventRecord((hipEvent_t)c->ev_fork, s);
         (void)hipStreamWaitEvent(s2, (hipEvent_t)c->ev_fork, 0);
-        mtk_big(full, s2, c->n_long, c->S, c->ops, runs, cur, MT_G_WIN, 0, MT_G_HEAP);
+        if (full) mtk_big(full, s2, c->n_long, c->S, c->ops, runs, cur, MT_G_WIN, 0, MT_G_HEAP);
+        else mtk_blkw(s2, c->n_long, c->S, c->ops, runs, cur);
         if (c->n_short) {
             if (full) mtk_blk_full(s, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);
             else mtk_blk_fast(s, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);

@@ -7,6 +7,7 @@
 //   MT_KSET 1: mt_replay_blk_kernel<true, true>   5: mt_replay_blk_kernel<false, true> (long runs)
 //   MT_KSET 2: mt_replay_big_kernel<false / true>  3: mt_replay_lds_kernel<false / true>
 //   MT_KSET 4: the all-HBM kernels and the generator
+//   MT_KSET 6: mt_replay_blkw_kernel<false, true> (the size class of long runs)
 #include <hip/hip_runtime.h>
 #include "mt_ctx.h"
 #include "mt_kernels.h"
@@ -40,6 +41,17 @@ __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_blk_kernel(Mt
     __shared__ MtScratch sc;
     const uint32_t run = runs ? runs[blockIdx.x] : blockIdx.x;          // size classes: a run list
     const uint32_t cur = mt_replay_doc<MT_RES_BLK, FULL, CONT>(S, ops, run, &sc, 0, lb, lh);
+    if (__lane_id() == 0) cursor[run] = cur;
+}
+// Wide block residency (MT_RES_BLKW): the block-residency engine with room for long documents'
+// trees and heaps (MT_BW_BLKS blocks, ~21 KB per workgroup), for the size class of long runs;
+// continues in HBM in-wave if even that is outgrown.
+template <bool FULL, bool CONT>
+__global__ __launch_bounds__(64, 2) void mt_replay_blkw_kernel(MtState S, MtOps ops, const uint32_t* runs,
+                                                               uint32_t* cursor) {
+    __shared__ MtScratch sc;
+    const uint32_t run = runs ? runs[blockIdx.x] : blockIdx.x;
+    const uint32_t cur = mt_replay_doc<MT_RES_BLKW, FULL, CONT>(S, ops, run, &sc, 0, MT_BW_BLKS, MT_BW_HEAP);
     if (__lane_id() == 0) cursor[run] = cur;
 }
 // Long documents (MT_RES_BIG): heap, window, U set and a block cache of the tree's upper
@@ -109,6 +121,10 @@ void mtk_blk_fast(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, c
 void mtk_blk_fast_cont(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,
                        int lb, int lh, uint32_t pad) {
     hipLaunchKernelGGL((mt_replay_blk_kernel<false, true>), dim3(n), dim3(64), pad, s, S, o, runs, cur, lb, lh);
+}
+#elif MT_KSET == 6
+void mtk_blkw(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur) {
+    hipLaunchKernelGGL((mt_replay_blkw_kernel<false, true>), dim3(n), dim3(64), 0, s, S, o, runs, cur);
 }
 #elif MT_KSET == 1
 void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,

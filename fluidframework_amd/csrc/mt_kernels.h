@@ -12,6 +12,8 @@ void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, c
 // the block-residency kernel with the in-wave HBM continuation (long runs)
 void mtk_blk_fast_cont(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,
                        int lb, int lh, uint32_t pad = 0);
+// wide block residency (MT_BW_BLKS blocks in LDS) with the in-wave continuation: long runs
+void mtk_blkw(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur);
 void mtk_big(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur,
              int lw, int lb, int lh);
 void mtk_lds(bool full, hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, uint32_t* cur, int lr, int lb, int lh);

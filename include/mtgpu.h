@@ -364,9 +364,10 @@ int  mt_replay_resident(mt_ctx* ctx);
  * small caps to force the hand-over. */
 int  mt_set_residency(mt_ctx* ctx, int use_lds, int rows, int blocks, int heap);
 /* Size classes under block residency (mt_set_residency 2): runs of at least big_min_ops op
- * records replay in the long-document kernel (heap, window and U set in LDS, blocks and rows
- * in HBM, one wave per SIMD) on a second stream, concurrently with the block-residency kernel
- * for the other runs; 0 (the default) turns it off.  Results are identical either way. */
+ * records replay in the wide block-residency kernel (the same engine with room for 248 blocks
+ * and a 254-entry zamboni heap in LDS, ~21 KB per workgroup; capture batches: the long-document
+ * kernel) on a second stream launched first, concurrently with the block-residency kernel for
+ * the other runs; 0 (the default) turns it off.  Results are identical either way. */
 int  mt_set_size_class(mt_ctx* ctx, uint32_t big_min_ops);
 /* Partitioned size classes under block residency (mt_set_residency 2): runs of at least
  * min_ops op records replay in the block-residency kernel on `cus` CUs reserved for them, one

@@ -20,13 +20,21 @@ def _atomic_build(cmd, out):
     os.replace(tmp, out)
 
 
+# MT_EMU_SANITIZE=1: the suite runs on an UndefinedBehaviorSanitizer build of the emulation
+# (every UB check aborts the process; tests/emu/sanitize_driver.cpp covers AddressSanitizer)
+SANITIZE = os.environ.get("MT_EMU_SANITIZE") == "1"
+if SANITIZE:
+    LIB = os.path.join(ROOT, "tests", "emu", "libmtemu_ubsan.so")
+
+
 def build_emu(force=False):
     if force or not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(d) for d in DEPS):
         # long-document residency: windows above 64 entries take the multi-wave scan (the device
         # scans up to 512 in wave 0 alone), so the CPU tests' small windows run both paths; every
         # parent-cache hit is checked against the block's parent field (abort on a stale entry)
+        san = ["-fsanitize=undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"] if SANITIZE else []
         _atomic_build(["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wno-unknown-pragmas",
-                       "-DMT_G_MWMIN=64", "-DMT_BPC_CHECK=1", "-o", None, SRC], LIB)
+                       "-DMT_G_MWMIN=64", "-DMT_BPC_CHECK=1"] + san + ["-o", None, SRC], LIB)
     return LIB
 
 
@@ -34,7 +42,7 @@ def emu_engine(max_docs, **kw):
     return Engine(max_docs, lib_path=build_emu(), prefix="emu_", **kw)
 
 
-NAPI_EMU = os.path.join(ROOT, "tests", "emu", "mtgpu_emu.node")
+NAPI_EMU = os.path.join(ROOT, "tests", "emu", "mtgpu_emu_ubsan.node" if SANITIZE else "mtgpu_emu.node")
 
 
 def build_emu_napi():
