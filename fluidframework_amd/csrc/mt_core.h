@@ -2308,8 +2308,8 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int key = pkey(a, k);
             const uint32_t ca = pclass(pval(a, k));
             bool f = false;
-            for (int i = 0; i < nb; i++) f |= (pkey(b, i) == key) & (pclass(pval(b, i)) == ca);
-            return (f & (ca != 0xFFFFFFFFu)) != 0;
+            for (int i = 0; i < nb; i++) f |= (int)(pkey(b, i) == key) & (int)(pclass(pval(b, i)) == ca);
+            return (f & (int)(ca != 0xFFFFFFFFu)) != 0;
         });
         return wave_count(ok) == na;
     }

@@ -196,18 +196,18 @@ static int mtb_partition_streams(mt_ctx* c) {
 static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) {
     uint32_t* cur = (uint32_t*)c->b_cursor.p;
     if (c->use_lds == 2 && c->big_min_ops && c->n_long && c->part_cus && !mtb_partition_streams(c)) {
-        // partitioned size classes: long runs on stream A's CUs, one workgroup per SIMD (each
-        // padded to a quarter of the CU's 160 KB of LDS), the rest on stream B's CUs; joined
+        // partitioned size classes: long runs on stream A's CUs in the wide block-residency
+        // kernel (~21 KB of LDS, up to 7 per CU), the rest on stream B's CUs; joined.  Capture
+        // batches (FULL): the block-residency kernel, one workgroup per SIMD (each padded to a
+        // quarter of the CU's 160 KB of LDS: any total in (160 KB / 5, 160 KB / 4] leaves four)
         const uint32_t* runs = (const uint32_t*)c->b_runs.p;
         hipStream_t sa = (hipStream_t)c->streamA, sb = (hipStream_t)c->streamB;
-        // any workgroup total in (160 KB / 5, 160 KB / 4] leaves four per CU; the kernels'
-        // static LDS is ~10-13 KB
         const uint32_t pad = 27u << 10;
         (void)hipEventRecord((hipEvent_t)c->ev_fork, s);
         (void)hipStreamWaitEvent(sa, (hipEvent_t)c->ev_fork, 0);
         (void)hipStreamWaitEvent(sb, (hipEvent_t)c->ev_fork, 0);
         if (full) mtk_blk_full(sa, c->n_long, c->S, c->ops, runs, cur, c->lds_blks, c->lds_heap, pad);
-        else mtk_blk_fast_cont(sa, c->n_long, c->S, c->ops, runs, cur, c->lds_blks, c->lds_heap, pad);
+        else mtk_blkw(sa, c->n_long, c->S, c->ops, runs, cur);
         if (c->n_short) {
             if (full) mtk_blk_full(sb, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);
             else mtk_blk_fast(sb, c->n_short, c->S, c->ops, runs + c->n_long, cur, c->lds_blks, c->lds_heap);

@@ -38,7 +38,7 @@ static void replay_runs(mt_ctx* c, uint32_t n_runs) {
     for (uint32_t run = 0; run < n_runs; run++) {
         MtScratch sc;
         if (c->use_lds == 3) cursor[run] = mt_replay_doc<MT_RES_BIG, FULL>(c->S, c->ops, run, &sc, c->lds_rows, c->lds_blks, c->lds_heap);
-        else if (c->use_lds == 2 && c->big_min_ops && !c->part_cus && c->run_off.size() == n_runs + 1 &&
+        else if (c->use_lds == 2 && c->big_min_ops && c->run_off.size() == n_runs + 1 &&
                  c->run_off[run + 1] - c->run_off[run] >= c->big_min_ops)      // size classes (mt_set_size_class)
             cursor[run] = FULL ? mt_replay_doc<MT_RES_BIG, FULL>(c->S, c->ops, run, &sc, MT_G_WIN, 0, MT_G_HEAP)
                                : mt_replay_doc<MT_RES_BLKW, FULL, true>(c->S, c->ops, run, &sc, 0, MT_BW_BLKS, MT_BW_HEAP);
