@@ -1052,8 +1052,10 @@ template <int RES, bool FULL = true> struct MtEngT {
     // winAdd for the rows of lanes [0, n) where sel: one meta load for all, the rows not yet
     // in the window appended in lane order (one round trip instead of one per row).
     MT_HD void winAddLanes(const LaneArr<int>& ids, const LaneArr<bool>& sel, int n) {
+        if (!wave_ballot(wave_map(n, [&](int j) MT_LAM { return (bool)own(sel, j); }))) return;   // uniform skip
         auto add = wave_map(n, [&](int j) MT_LAM {
-            return own(sel, j) && !(row(own(ids, j)).meta & MT_M_INWIN);
+            const bool q = own(sel, j);                           // branch-free
+            return (bool)(q & !(row(q ? own(ids, j) : 0).meta & MT_M_INWIN));
         });
         const int cnt = wave_count(add);
         if (!cnt) return;
@@ -1302,7 +1304,9 @@ template <int RES, bool FULL = true> struct MtEngT {
                     const uint32_t mt = row(ch).meta;
                     int v = row(ch).seq ^ row(ch).rseq ^ row(ch).props ^ row(ch).tcap ^ (int)mt;
                     const int ix = tf + ln - 1;
-                    if (!(mt & MT_M_MARKER) && ix >= 0 && (unsigned)ix < tc) v ^= (int)text[ix];
+                    const bool q = !(mt & MT_M_MARKER) & (ix >= 0) & ((unsigned)ix < tc);
+                    const int tv = (int)text[q ? ix : 0];
+                    v ^= q ? tv : 0;
                     mt_keep(v);
                 });
             }
@@ -1454,7 +1458,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                 const auto a = wave_map(m, [&](int k) MT_LAM {
                     const int p = own(par, k);
                     bool w = false; int x = 0;
-                    if (p >= 0 && p != rt) x = htAdd(p, own(val, k), w);
+                    if ((p >= 0) & (p != rt)) x = htAdd(p, own(val, k), w);
                     return w ? x : ~x;
                 });
                 htList(wave_map(m, [&](int k) MT_LAM { return own(a, k) >= 0 ? own(a, k) : ~own(a, k); }),
@@ -1559,7 +1563,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                 int a = w.parent;
                 if constexpr (BT) {                       // the row's delta into every block above it
                     if (pos < UCAP) uPutAt<true>(pos, w.id, w.delta); else uPutAt<false>(pos, w.id, w.delta);
-                    for (int h = 0; h <= HH && a >= 0; h++) { lds_add(&LB().bcorr[a], w.delta); a = bk(a).parent; }
+                    for (int h = 0; (h <= HH) & (a >= 0); h++) { lds_add(&LB().bcorr[a], w.delta); a = bk(a).parent; }
                 } else if constexpr (UL) {
                     if (pos < UCAP) {
                         uPutAt<true>(pos, w.id, w.delta);
@@ -1624,10 +1628,10 @@ template <int RES, bool FULL = true> struct MtEngT {
                 const uint32_t mt = row(id).meta;
                 const bool removed = (mt & MT_M_REMOVED) != 0;
                 const int sq = row(id).seq, rs = row(id).rseq;
-                const bool live = row(id).parent >= 0 && (sq > minSeq || (removed && rs > minSeq));
-                if (!live) return 0;
+                const int ln = row(id).len;
+                const bool live = (row(id).parent >= 0) & ((sq > minSeq) | (removed & (rs > minSeq)));
                 const bool vr = vis_rc(sq, mt, rs, row(id).rcl, row(id).ovl, r, c, ovx, ovxN, id);
-                return (vr ? row(id).len : 0) - (removed ? 0 : row(id).len);
+                return live ? (vr ? ln : 0) - (removed ? 0 : ln) : 0;     // branch-free
             }));
         }
         return uni(bk(root).len) + s;
@@ -1906,7 +1910,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int m = (ovxN - base) < MT_WAVE ? (ovxN - base) : MT_WAVE;
             auto keep = wave_map(m, [&](int k) MT_LAM {
                 const MtOvx e = ovx[base + k];
-                return row(e.row).parent >= 0 && row(e.row).rseq == e.rseq && e.rseq > minSeq;
+                return (bool)((row(e.row).parent >= 0) & (row(e.row).rseq == e.rseq) & (e.rseq > minSeq));
             });
             auto ent = wave_map(m, [&](int k) MT_LAM { return ovx[base + k]; });
             auto rk = wave_rank(keep);
@@ -2326,7 +2330,9 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int m = (rowTop - base) < MT_WAVE ? (rowTop - base) : MT_WAVE;
             auto ln = wave_map(m, [&](int k) MT_LAM {
                 const int s = base + k;
-                return ((row(s).parent >= 0 || (row(s).meta & MT_M_REG)) && !(row(s).meta & MT_M_MARKER)) ? row(s).len : 0;
+                const uint32_t mt = row(s).meta;
+                const int ln = row(s).len;
+                return (((row(s).parent >= 0) | ((mt & MT_M_REG) != 0)) & !(mt & MT_M_MARKER)) ? ln : 0;
             });
             auto pre = wave_excl_scan(ln);
             const int tot = wave_sum(ln);
@@ -2334,7 +2340,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                 const int s = base + k, l = own(ln, k);
                 if (l <= 0) return;
                 const int o = w + own(pre, k), t0 = row(s).toff;
-                for (int q = 0; q < l; q++) dst[o + q] = text[t0 + q];
+                lane_copy16(dst + o, text + t0, l);
                 row(s).toff = o; row(s).tcap = l;
             });
             w += tot;
@@ -2508,10 +2514,16 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (pm) {
             // prev's last unit (canAppend: no trailing "\n") for lanes followed by a pair
             const uint64_t needLast = pm >> 1;
-            auto lastNL = wave_map(span, [&](int t) MT_LAM {
-                const bool need = ((needLast >> t) & 1ull) && !((uint32_t)own(fm, t) & MT_M_NONL);
-                return need ? (text[own(ft, t) + own(fl, t) - 1] == (uint16_t)'\n' ? 1 : 0) : 0;
+            const auto need = wave_map(span, [&](int t) MT_LAM {
+                return (((needLast >> t) & 1ull) != 0) & !((uint32_t)own(fm, t) & MT_M_NONL);
             });
+            auto lastNL = wave_map(span, [&](int) MT_LAM { return 0; });
+            if (wave_ballot(wave_map(span, [&](int t) MT_LAM { return (bool)own(need, t); })))   // uniform skip
+                lastNL = wave_map(span, [&](int t) MT_LAM {              // per lane branch-free
+                    const bool q = own(need, t);
+                    const int last = (int)text[q ? own(ft, t) + own(fl, t) - 1 : 0];
+                    return (q & (last == '\n')) ? 1 : 0;
+                });
             const auto lastNL1 = wave_from8<-1>(lastNL);
             // matchProperties: equal ids match; a missing map never matches a present one;
             // two different maps compare key by key (propsMatch)
@@ -2526,7 +2538,8 @@ template <int RES, bool FULL = true> struct MtEngT {
             if (mt_cold_v.pNever)                        // a shared map holding NaN / undefined
                 propOk &= ~wave_ballot(wave_map(span, [&](int t) MT_LAM {
                     const int a = own(fp1, t), b = own(fp, t);
-                    return ((pm >> t) & 1ull) && a == b && a >= 0 && pset[a].pad[2] != 0;
+                    const bool q = (((pm >> t) & 1ull) != 0) & (a == b) & (a >= 0);
+                    return (bool)(q & (pset[q ? a : 0].pad[2] != 0));
                 }));
             for (uint64_t sb = slow; sb; sb &= sb - 1) {
                 const int k = __builtin_ctzll(sb);
@@ -2894,7 +2907,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                         const auto rk = wave_rank(cond);
                         const int k0 = regTop + nCol;               // into the register arena's free tail
                         wave_for(h.n, [&](int j) MT_LAM {
-                            if (own(cond, j) && k0 + own(rk, j) < regCap) regRow(k0 + own(rk, j)) = own(ch, j);
+                            if (own(cond, j) & (k0 + own(rk, j) < regCap)) regRow(k0 + own(rk, j)) = own(ch, j);
                         });
                         nCol += nact;
                     } else if (mode == MT_MAP_REMOVE) {
@@ -2915,7 +2928,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                         wave_sync();
                         if (c >= 63) {                                 // removedClientOverlap beyond the mask
                             const uint64_t ob = wave_ballot(wave_map(h.n, [&](int j) MT_LAM {
-                                return own(cond, j) && (row(own(ch, j)).rseq != sq);
+                                return (bool)(own(cond, j) & (row(own(ch, j)).rseq != sq));
                             }));
                             for (uint64_t b = ob; b; b &= b - 1) {
                                 const int j = __builtin_ctzll(b), s = wave_at(ch, j);
@@ -3060,7 +3073,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int m = (nh - base) < MT_WAVE ? (nh - base) : MT_WAVE;
             auto inw = wave_map(m, [&](int k) MT_LAM {
                 const int s = base + k;
-                return row(s).seq > minSeq || (row(s).meta & MT_M_REMOVED) != 0;
+                return (bool)((row(s).seq > minSeq) | ((row(s).meta & MT_M_REMOVED) != 0));
             });
             const int cnt = wave_count(inw);
             if (winN + cnt > (int)S.winCap) { status |= MT_DS_OOM_WINDOW; return; }

@@ -314,3 +314,18 @@ def check_bench_docs(factory):
 
 def test_emu_bench_docs_match_oracle():
     check_bench_docs(emu_engine)
+
+
+# Text arena pressure: small arenas make zamboni's merge runs compact the arena while they
+# are planned (then re-planned with exactly sized regions) and reuse the spaces of split
+# halves and unlinked removals (MtEngT::mergeRuns); long runs grow segments past the
+# 256-unit granularity.  Results must not change.
+@pytest.mark.parametrize("cfg,text,ops", [("cfg2", 4200, 3000), ("cfg3", 600, 3000), ("grow", 8000, 2500),
+                                          ("cfg2", 1 << 18, 6000)])
+def test_emu_text_arena_pressure_matches_oracle(cfg, text, ops):
+    props = ann_props()
+    c = dict(CONFIGS[cfg]); c["ops"] = ops
+    p = gen_params(seed=31, n_docs=3, **c)
+    batch, st, _ = generate(p, props)
+    assert st == [0] * 3
+    compare(batch, props, 3, text=text, residency=(2, 0, 104, 94))

@@ -2,7 +2,7 @@
 
 Reads the gfx950 code objects out of fluidframework_amd/libmtgpu.so (clang offload bundles in
 its .hip_fatbin data) and prints each kernel's AMDGPU metadata from `llvm-readelf --notes`.
-usage: python tools/kernel_resources.py [lib.so] [name-substring]
+usage: python tools/kernel_resources.py [lib.so] [name-substring]   (code = the kernel symbol's bytes)
 """
 import os
 import re
@@ -34,6 +34,9 @@ def code_objects(data: bytes):
         at = i + len(MAGIC)
 
 
+sizes = {}                    # kernel symbol -> code bytes
+
+
 def kernels(path: str):
     out = []
     data = open(path, "rb").read()
@@ -42,6 +45,11 @@ def kernels(path: str):
             f = os.path.join(td, f"co{k}.o")
             open(f, "wb").write(co)
             txt = subprocess.run([READELF, "--notes", f], capture_output=True, text=True).stdout
+            syms = subprocess.run([READELF, "-sW", f], capture_output=True, text=True).stdout
+            for line in syms.splitlines():
+                p = line.split()
+                if len(p) >= 8 and p[3] == "FUNC":
+                    sizes[p[7]] = int(p[2], 0) if p[2].startswith("0x") else int(p[2])
             cur = None
             for line in txt.splitlines():
                 m = re.match(r"\s*-?\s*(\.[a-z_]+):\s*(.*)$", line)
@@ -77,7 +85,7 @@ def main():
         print(f"{name[:90]:90s} vgpr {k.get('.vgpr_count', '?'):>3} agpr {k.get('.agpr_count', '0'):>3} "
               f"sgpr {k.get('.sgpr_count', '?'):>3} vspill {k.get('.vgpr_spill_count', '?'):>3} "
               f"sspill {k.get('.sgpr_spill_count', '?'):>4} scratch {k.get('.private_segment_fixed_size', '?'):>4} "
-              f"lds {k.get('.group_segment_fixed_size', '?'):>6}")
+              f"lds {k.get('.group_segment_fixed_size', '?'):>6} code {sizes.get(name, 0):>7}")
 
 
 if __name__ == "__main__":

@@ -13,7 +13,7 @@ from fluidframework_amd.batch import MtGenParams
 import bench
 
 flag = os.environ.get("MT_PROF_FLAG", "MT_PROFILE")
-lib = os.path.join(ROOT, "fluidframework_amd", f"libmtgpu_{flag.lower()}.so")
+lib = os.environ.get("MTGPU_PROF_LIB") or os.path.join(ROOT, "fluidframework_amd", f"libmtgpu_{flag.lower()}.so")
 if not os.path.exists(lib):                       # build here (CPU) before shipping it to a GPU run
     sys.path.insert(0, ROOT)
     import __graft_entry__
