@@ -909,6 +909,24 @@ static int mt_staged_groups(mt_ctx* c, uint32_t n, const uint32_t* docs, const M
     // double-buffered: group g+1 is staged (device pack + download into the other pinned
     // buffer) while group g is emitted on the host threads
     std::vector<MtSnapView> cur, nxt;
+    {   // both pinned buffers sized once for the call's largest group (estimates bound the packed
+        // bytes): no buffer is re-pinned between groups
+        uint64_t big = 0;
+        for (uint32_t g = 0; g < n;) {
+            const uint32_t e = groupEnd(g);
+            uint64_t bytes = 0;
+            for (uint32_t i = g; i < e; i++) {
+                const MtDocHdr& d = h[i];
+                bytes += 48ull * (uint64_t)(d.rowTop > 0 ? d.rowTop : 0) + 64ull * (uint64_t)(d.blkTop > 0 ? d.blkTop : 0) +
+                         2ull * (uint64_t)(d.textTop > 0 ? d.textTop : 0) +
+                         (uint64_t)sizeof(MtPSet) * (uint64_t)(d.psetTop > 0 ? d.psetTop : 0) + 1024;
+            }
+            if (bytes > big) big = bytes;
+            g = e;
+        }
+        for (int buf = 0; buf < 2 && n; buf++)
+            if (!mtb_host_stage(c, big + 16, buf)) { c->err = "pinned staging allocation failed"; return MT_E_OOM; }
+    }
     uint32_t a = 0, b = n ? groupEnd(0) : 0;
     if (n && ((rc = mt_stage_docs(c, b - a, docs + a, cur, 0)) || (rc = mt_check_staged_status(c, b - a, docs + a, cur))))
         return rc;
@@ -930,6 +948,13 @@ static int mt_staged_groups(mt_ctx* c, uint32_t n, const uint32_t* docs, const M
         std::swap(cur, nxt);
         a = b; b = b2;
     }
+    return MT_OK;
+}
+int MT_FN(reserve_staging)(mt_ctx* c, uint64_t bytes) {
+    if (!c) return MT_E_INVALID;
+    if (!bytes) bytes = MT_STAGE_BUDGET + 16;
+    for (int buf = 0; buf < 2; buf++)
+        if (!mtb_host_stage(c, bytes, buf)) { c->err = "pinned staging allocation failed"; return MT_E_OOM; }
     return MT_OK;
 }
 // Client.snapshot (client.ts:923-956): SnapshotV1 or, with legacy set, SnapshotLegacy.

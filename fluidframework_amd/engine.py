@@ -117,6 +117,7 @@ def _bind(lib, prefix: str):
                                  [P, U32, P, P, P, P, P, ctypes.POINTER(P), ctypes.POINTER(P)]),
         resolve_remote_position=f("resolve_remote_position", ctypes.c_int, [P, U32, P, P, P, P, P]),
         set_doc_snapshot_chunk=f("set_doc_snapshot_chunk", ctypes.c_int, [P, U32, P, P]),
+        reserve_staging=f("reserve_staging", ctypes.c_int, [P, ctypes.c_uint64]),
     )
 
 
@@ -424,6 +425,11 @@ class Engine:
         c = np.ascontiguousarray(chunk_size, np.uint64)
         self._check(self.fn["set_doc_snapshot_chunk"](self.h, len(d), d.ctypes.data, c.ctypes.data),
                     "mt_set_doc_snapshot_chunk")
+
+    def reserve_staging(self, nbytes: int = 0):
+        """mt_reserve_staging: pin the two host staging buffers snapshots and text reads download
+        through (0: the default group budget), once, ahead of the calls that use them."""
+        self._check(self.fn["reserve_staging"](self.h, int(nbytes)), "mt_reserve_staging")
 
     def update_seq(self, docs, msn, seq):
         d, m, s = _u32(docs), _i32(msn), _i32(seq)

@@ -263,6 +263,8 @@ class Engine {
     }
     /** options.mergeTreeSnapshotChunkSize of documents (snapshotV1.ts:55; 0: the default). */
     setSnapshotChunk(docs, sizes) { addon.setDocSnapshotChunk(this.h, Uint32Array.from(docs), Float64Array.from(sizes)); }
+    /** mt_reserve_staging: pin the snapshot / text staging buffers once (0: default budget). */
+    reserveStaging(bytes = 0) { addon.reserveStaging(this.h, bytes); }
 }
 
 /**

@@ -252,6 +252,21 @@ napi_value SetDocSnapshotChunk(napi_env env, napi_callback_info info) {
     return rc ? throw_rc(env, c, rc, "mt_set_doc_snapshot_chunk") : undefined(env);
 }
 
+// reserveStaging(ctx, bytes?: number): mt_reserve_staging (pin the snapshot / text staging
+// buffers once; 0 or absent: the default group budget).
+napi_value ReserveStaging(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+    if (argc < 1) { napi_throw_type_error(env, nullptr, "reserveStaging(ctx, bytes?)"); return nullptr; }
+    mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
+    double b = 0;
+    if (argc > 1) napi_get_value_double(env, argv[1], &b);
+    if (!(b >= 0)) { napi_throw_range_error(env, nullptr, "bytes must be >= 0"); return nullptr; }
+    int rc = mt_reserve_staging(c, (uint64_t)b);
+    return rc ? throw_rc(env, c, rc, "mt_reserve_staging") : undefined(env);
+}
+
 // applyBatch(ctx, batch): copies the batch to HBM and enqueues the replay
 // (Client.applyMsg for every message of every document run).
 napi_value ApplyBatch(napi_env env, napi_callback_info info) {
@@ -575,6 +590,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"setClientNames", nullptr, SetClientNames, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"setDocClientNames", nullptr, SetDocClientNames, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"setDocSnapshotChunk", nullptr, SetDocSnapshotChunk, nullptr, nullptr, nullptr, kAttr, nullptr},
+        {"reserveStaging", nullptr, ReserveStaging, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"applyBatch", nullptr, ApplyBatch, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"loadSnapshot", nullptr, LoadSnapshot, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"sync", nullptr, Sync, nullptr, nullptr, nullptr, kAttr, nullptr},

@@ -500,6 +500,12 @@ int  mt_set_doc_snapshot_chunk(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
  * download, serialization spread over `threads` host threads. */
 int  mt_snapshot_digests(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, const int32_t* msn,
                          const int32_t* seq, uint64_t* out_digest, int threads);
+/* Pin the two host staging buffers that mt_snapshot_* and mt_get_text download documents
+ * through (double-buffered groups of documents), each at least `bytes` (0: the default group
+ * budget, 384 MiB), so later calls do not pay for pinning host memory: a serving process
+ * reserves once at startup.  Calls without a reservation pin on first use and grow the buffers
+ * to the largest group of the call. */
+int  mt_reserve_staging(mt_ctx* ctx, uint64_t bytes);
 /* Observer text (UTF-16) of each document into a library-owned arena. */
 int  mt_get_text(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
                  const uint16_t** arena, const uint64_t** off);

@@ -38,6 +38,8 @@ def compare(batch, props, n_docs, factory=None, **cap):
         eng.set_residency(*cap["residency"])
     if "cont" in cap:
         eng.set_continuation(cap["cont"])
+    if "reserve" in cap:
+        eng.reserve_staging(cap["reserve"])
     eng.upload_props(props)
     eng.upload_names(NAMES)
     eng.open_docs(0, n_docs)
@@ -96,6 +98,18 @@ def test_emu_snapshots_in_staging_groups_match_oracle(monkeypatch):
     batch, st, _ = generate(p, props)
     assert st == [0] * 5
     compare(batch, props, 5)
+
+
+@pytest.mark.parametrize("reserve", [0, 1 << 12])
+def test_emu_snapshots_after_reserved_staging_match_oracle(reserve, monkeypatch):
+    """mt_reserve_staging (the default budget, or buffers smaller than a group: grown on use)
+    changes nothing in the snapshots."""
+    monkeypatch.setenv("MT_STAGE_BUDGET", str(1 << 16))
+    props = ann_props()
+    p = gen_params(seed=13, n_docs=4, **CONFIGS["cfg2"])
+    batch, st, _ = generate(p, props)
+    assert st == [0] * 4
+    compare(batch, props, 4, reserve=reserve)
 
 
 # LDS residency hand-over: tiny LDS caps make documents leave LDS mid-run (at

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 
 EXPORTS = ["applyBatch", "create", "deltaCapture", "deltaRecords", "deltaText", "destroy", "docPset", "docStatus", "docsOpen",
            "getContainingSegment", "getLength", "getText", "lastError",
-           "loadSnapshot", "setClientNames", "setDocClientNames", "setDocSnapshotChunk", "setProps", "setResidency", "snapshotLegacy", "snapshotV1", "sync",
+           "loadSnapshot", "reserveStaging", "setClientNames", "setDocClientNames", "setDocSnapshotChunk", "setProps", "setResidency", "snapshotLegacy", "snapshotV1", "sync",
            "syncAsync",
            "updateSeq"]
 
