@@ -717,6 +717,67 @@ def ingest_leg(local, c, seed, sample_docs=64):
                     "SnapshotV1 digests of every document; the timed replay starts from resident streams"}
 
 
+def write_doc_bins(batch, td):
+    """Each document's op columns as doc<i>.bin (js/pack_worker.js binToJson's layout), the
+    input of js/ingest_scale.js."""
+    a = batch.arrays
+    off = batch.op_offsets
+    pay = batch.payload
+    for d in range(len(off) - 1):
+        o0, o1 = int(off[d]), int(off[d + 1])
+        po = a["payload_off"][o0:o1].astype(np.int64)
+        pl = a["payload_len"][o0:o1].astype(np.int64)
+        ins = (a["type"][o0:o1] == 0) & (pl > 0)
+        p0 = int(po[ins].min()) if ins.any() else 0
+        p1 = int((po + pl)[ins].max()) if ins.any() else 0
+        rel = np.where(ins, po - p0, 0)
+        cols = [a["type"][o0:o1], a["client"][o0:o1], a["seq"][o0:o1], a["ref_seq"][o0:o1], a["msn"][o0:o1],
+                a["pos1"][o0:o1], a["pos2"][o0:o1], rel, pl]
+        head = np.array([o1 - o0, p1 - p0], np.int32)
+        with open(os.path.join(td, f"doc{d}.bin"), "wb") as f:
+            f.write(head.tobytes())
+            for col in cols:
+                f.write(np.ascontiguousarray(col, np.int32).tobytes())
+            f.write(np.ascontiguousarray(pay[p0:p1], np.uint16).tobytes())
+
+
+def ingest_scale_leg(eng, params, c, dig_xor, windows=8):
+    """Node host ingest at the workload's full size (every document of the config): message JSON
+    parsed and packed on a worker pool, then end to end through the addon with packing of message
+    window k+1 (of every document) overlapped with the upload and replay of window k
+    (js/ingest_scale.js).  Its SnapshotV1 digests must equal the bench's own (same messages,
+    replayed from JSON).  The workload is generated again first (the CPU baseline's sample
+    generation replaced it on the engine)."""
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("node")
+    if not exe or Host.factory is not None:
+        return None
+    eng.generate(params)
+    eng.sync()
+    batch = eng.generated_download()
+    workers = max(1, min(16, os.cpu_count() or 1))
+    with tempfile.TemporaryDirectory() as td:
+        t0 = time.perf_counter()
+        write_doc_bins(batch, td)
+        write_s = time.perf_counter() - t0
+        del batch
+        cmd = [exe, "--max-old-space-size=8192", os.path.join(ROOT, "fluidframework_amd", "js", "ingest_scale.js"), td,
+               str(workers), str(windows), "--gpu"]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        return {"error": r.stderr[-800:]}
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    res["digests_equal_bench"] = res.get("digest_xor") == f"{dig_xor:016x}"
+    res["input_write_s"] = write_s
+    res["note"] = (f"all {c['docs']} documents: per-document message JSON in {windows} message windows made "
+                   "inside the workers (untimed); pack_ms = parse + pack of every window on the pool (the host "
+                   "bound); e2e_ms = parse/pack of window k+1 of every document overlapped with mt_apply_batch "
+                   "upload + replay of window k, one sync, SnapshotV1 of every document")
+    return res
+
+
 def finish_dist():
     """Every rank leaves together and tears its process group down (a rank that exits with
     its group still up can abort in the communication library's exit handlers)."""
@@ -950,6 +1011,8 @@ def _main(argv=None):
         out["parity"] += manifest_text(man)
     if world == 1 and not args.no_ingest:
         out["ingest"] = ingest_leg(local, c, seed)
+        if args.config == "config2" and ok:
+            out["ingest"]["node_full_scale"] = ingest_scale_leg(eng, params, c, dig_xor)
     print(json.dumps(out), flush=True)
 
 

@@ -30,6 +30,48 @@ class ParallelPacker {
      * PropTable of the engine the batch goes to.  Resolves to { batch, names } with
      * names[i] the long client ids of docs[i] in short-id order.
      */
+    /**
+     * Hand each worker its share of documents (contiguous, equal counts) to hold as JSON text
+     * in `windows` consecutive message windows: docs [{ id, bin }] (binary op columns,
+     * pack_worker.js binToJson).  packHeld(ids, props, k) then packs window k of held documents
+     * on the workers that hold them; each document's client-name table carries over from window
+     * to window (resetNames() starts them again).
+     */
+    async prepare(docs, windows = 1) {
+        const W = this.workers.length;
+        this.owner = new Map();
+        const per = Math.ceil(docs.length / W);
+        const jobs = [];
+        for (let w = 0; w < W; w++) {
+            const sl = docs.slice(w * per, (w + 1) * per);
+            if (!sl.length) continue;
+            for (const d of sl) this.owner.set(d.id, w);
+            jobs.push(this.post(w, { prepare: sl, windows }));
+        }
+        const r = await Promise.all(jobs);
+        for (const m of r) if (m.error) throw new Error(m.error);
+        return r.reduce((a, m) => a + m.bytes, 0);
+    }
+    async resetNames() { await Promise.all(this.workers.map((_, w) => this.post(w, { resetNames: true }))); }
+    async packHeld(ids, props, win = 0) {
+        const by = this.workers.map(() => []);
+        for (const id of ids) by[this.owner.get(id)].push({ id, held: true, win });
+        const parts = await Promise.all(by.map((l, w) => l.length ? this.post(w, { docs: l }) : null).filter((x) => x));
+        const t0 = process.hrtime.bigint();
+        const out = merge(parts, props);
+        this.lastMergeMs = Number(process.hrtime.bigint() - t0) / 1e6;
+        return out;
+    }
+    post(w, msg) {
+        const wk = this.workers[w];
+        return new Promise((resolve, reject) => {
+            const onMsg = (m) => { wk.off("error", onErr); resolve(m); };
+            const onErr = (e) => { wk.off("message", onMsg); reject(e); };
+            wk.once("message", onMsg);
+            wk.once("error", onErr);
+            wk.postMessage(msg);
+        });
+    }
     async pack(docs, props) {
         const W = this.workers.length;
         // contiguous slices balanced by text size (a proxy for messages)

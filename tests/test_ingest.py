@@ -2,6 +2,8 @@
 are validated and packed into 32-byte records on several host threads.  The result must be
 the single-threaded one: the same replay (digests equal to the oracle's) and, for a bad
 batch, the error of the lowest offending op."""
+import os
+
 import numpy as np
 import pytest
 
@@ -10,6 +12,8 @@ from fluidframework_amd.batch import OpBatch
 from fluidframework_amd.engine import Engine, MergeTreeError
 from oracle_lib import gen_params, generate, replay
 from test_emu_parity import CONFIGS, ann_props
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 NAMES = ['"c%d"' % i for i in range(64)]
 
@@ -65,3 +69,45 @@ def test_large_batch_validation_reports_lowest_bad_op(bad, msg):
     eng.upload_names(NAMES)
     with pytest.raises(MergeTreeError, match=msg):
         eng.upload(_bad_batch(100000, bad))
+
+
+def test_node_full_scale_ingest_packs_every_message(tmp_path):
+    """js/ingest_scale.js (bench.py's full-scale Node ingest leg) on the CPU: every document's
+    binary op columns become message JSON inside the workers, and the pool packs every message."""
+    import json
+    import shutil
+    import subprocess
+    import bench
+    from fluidframework_amd.batch import MtGenParams
+    if shutil.which("node") is None:
+        pytest.skip("node is not installed")
+    c = dict(bench.CONFIGS["config2"]); c["docs"] = 6; c["ops"] = 600
+    eng = emu_engine(6, **bench.caps_for(c))
+    eng.upload_props(bench.ann_props()); eng.upload_names(['"c%d"' % i for i in range(64)])
+    eng.generate(MtGenParams(7, 6, c["ops"], c["clients"], c["lag"], c["ins"], c["rem"], c["ins_len"], c["rem_len"],
+                             c["ann_sets"], c["rewrite"]))
+    eng.sync()
+    bench.write_doc_bins(eng.generated_download(), str(tmp_path))
+    r = subprocess.run(["node", os.path.join(ROOT, "fluidframework_amd", "js", "ingest_scale.js"), str(tmp_path), "3", "4"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["docs"] == 6 and out["msgs"] == 6 * 600
+    # end to end through the Node addon (built on the host emulation): the windowed pipeline's
+    # SnapshotV1 digests equal a replay of the same generated streams
+    from emu_lib import build_emu_napi
+    addon = build_emu_napi()
+    if addon is None:
+        return
+    env = dict(os.environ, MTGPU_NAPI=addon)
+    r = subprocess.run(["node", os.path.join(ROOT, "fluidframework_amd", "js", "ingest_scale.js"), str(tmp_path), "3", "4",
+                        "--gpu"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr
+    node = json.loads(r.stdout.strip().splitlines()[-1])
+    eng.generated_to_resident()
+    eng.open_docs(0, 6)
+    eng.replay_resident()
+    eng.sync()
+    neg = np.full(6, -1, np.int32)
+    digs = eng.snapshot_digests(range(6), neg, neg, threads=2)
+    assert node["digest_xor"] == f"{int(np.bitwise_xor.reduce(digs)):016x}"
