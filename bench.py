@@ -51,7 +51,7 @@ CONFIGS = {
                     desc="256 long docs (pre-built to 200k segments / 1M chars) x 50k msgs, 8 clients, lag U[0,1024]"),
     # docs = per GPU (weak scaling; 8 GPUs = 1,048,576 docs); ops ~ Zipf(1.5) on [8, 65536], clients U[2,16]
     "config5": dict(docs=131072, ops=0, clients=0, lag=32, ins=60, rem=40, ins_len=8, rem_len=8, ann_sets=1, rewrite=0,
-                    partition="8192:128",   # profiles/r05/c5sc: runs >= 8192 msgs on 128 reserved CUs (wide kernel)
+                    partition="2048:224",   # profiles/r05/c5part: runs >= 2048 msgs on 224 reserved CUs (wide kernel)
                     desc="Zipf(1.5)-sized docs (8..65536 msgs, clients U[2,16]), 131072 docs per GPU, rank-0 ingest, "
                          "LPT rebalance + digest gather over RCCL"),
 }

@@ -886,7 +886,8 @@ static int mt_check_staged_status(mt_ctx* c, uint32_t n, const uint32_t* docs, c
 // staged; a group holds a multiple of `mult` documents (whole rounds of the emitting threads).
 #define MT_STAGE_BUDGET (384ull << 20)
 typedef std::function<int(uint32_t, uint32_t, const std::vector<MtSnapView>&)> MtGroupFn;
-static int mt_staged_groups(mt_ctx* c, uint32_t n, const uint32_t* docs, const MtGroupFn& fn, uint32_t mult = 1) {
+static int mt_staged_groups(mt_ctx* c, uint32_t n, const uint32_t* docs, const MtGroupFn& fn, uint32_t mult = 1,
+                            bool check_status = true) {
     std::vector<MtDocHdr> h;
     int rc = mt_read_hdrs(c, n, docs, h);
     if (rc) return rc;
@@ -928,7 +929,8 @@ static int mt_staged_groups(mt_ctx* c, uint32_t n, const uint32_t* docs, const M
             if (!mtb_host_stage(c, big + 16, buf)) { c->err = "pinned staging allocation failed"; return MT_E_OOM; }
     }
     uint32_t a = 0, b = n ? groupEnd(0) : 0;
-    if (n && ((rc = mt_stage_docs(c, b - a, docs + a, cur, 0)) || (rc = mt_check_staged_status(c, b - a, docs + a, cur))))
+    if (n && ((rc = mt_stage_docs(c, b - a, docs + a, cur, 0)) ||
+              (check_status && (rc = mt_check_staged_status(c, b - a, docs + a, cur)))))
         return rc;
     for (int buf = 0; a < n; buf ^= 1) {
         const auto t0 = std::chrono::steady_clock::now();
@@ -936,7 +938,8 @@ static int mt_staged_groups(mt_ctx* c, uint32_t n, const uint32_t* docs, const M
         std::thread emit([&] { erc = fn(a, b - a, cur); });
         const uint32_t b2 = b < n ? groupEnd(b) : b;
         int src = MT_OK;
-        if (b < n && !(src = mt_stage_docs(c, b2 - b, docs + b, nxt, buf ^ 1))) src = mt_check_staged_status(c, b2 - b, docs + b, nxt);
+        if (b < n && !(src = mt_stage_docs(c, b2 - b, docs + b, nxt, buf ^ 1)) && check_status)
+            src = mt_check_staged_status(c, b2 - b, docs + b, nxt);
         const auto t1 = std::chrono::steady_clock::now();
         emit.join();
         if (timing)
@@ -1027,13 +1030,18 @@ int MT_FN(get_text)(mt_ctx* c, uint32_t n, const uint32_t* docs, const uint16_t*
     if (!c) return MT_E_INVALID;
     int rc = mtb_sync(c);
     if (rc) return rc;
-    std::vector<MtSnapView> views;
-    if ((rc = mt_stage_docs(c, n, docs, views))) return rc;
+    for (uint32_t i = 0; i < n; i++) if (docs[i] >= c->S.maxDocs) { c->err = "doc id out of range"; return MT_E_INVALID; }
     c->text_arena.clear(); c->text_off.assign(1, 0);
-    for (uint32_t i = 0; i < n; i++) {
-        mtsnap::observer_text(views[i], c->text_arena);
-        c->text_off.push_back(c->text_arena.size());
-    }
+    // bounded groups through the two reused pinned buffers (mt_staged_groups), documents in order;
+    // a document with a status word still has its text (no status check)
+    rc = mt_staged_groups(c, n, docs, [&](uint32_t, uint32_t m, const std::vector<MtSnapView>& views) {
+        for (uint32_t j = 0; j < m; j++) {
+            mtsnap::observer_text(views[j], c->text_arena);
+            c->text_off.push_back(c->text_arena.size());
+        }
+        return (int)MT_OK;
+    }, 1, false);
+    if (rc) return rc;
     if (arena) *arena = c->text_arena.data();
     if (off) *off = c->text_off.data();
     return MT_OK;

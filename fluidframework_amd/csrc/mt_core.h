@@ -59,7 +59,7 @@
 #define MT_B_BLKS 104
 #endif
 #ifndef MT_B_SLACK
-#define MT_B_SLACK 10                 // block residency: free blocks kept beyond 2 * height before each message
+#define MT_B_SLACK 13                 // block residency: free blocks kept beyond 2 * height before each message
 #endif
 #define MT_B_BT 128                   // corrections-table slots (block ids < MT_B_BLKS)
 #define MT_B_U 64                     // U-set entries kept in LDS (the rest, if any, in HBM)
@@ -1009,21 +1009,25 @@ template <int RES, bool FULL = true> struct MtEngT {
     }
     // Can the next op run without outgrowing the LDS pools?  Per op at most 2
     // row splits + 1 new row, 2 split cascades of height+2 blocks and packParent
-    // regrowth; one heap entry per op plus one per message.
-    MT_HD bool ldsHeadroom() const {
-        if constexpr (BIG) return (lHeap - heapN) >= 4 && height + 3 <= MT_G_H;
+    // regrowth; one heap entry per op plus one per message.  k: the further segments the op
+    // inserts (a paste's clones): k rows and heap entries, and at most ceil(k / 3) + 1 more
+    // blocks (a leaf split per 4 inserted rows, an interior one per 4 new blocks).
+    MT_HD bool ldsHeadroom(int k = 0) const {
+        const int kb = k > 0 ? (k + 2) / 3 + 1 : 0;
+        if constexpr (BIG) return (lHeap - heapN) >= 4 + k && height + 3 <= MT_G_H;
         if constexpr (!BLKL) return true;
-        // Block budget per message: the split + insert cascades allocate at most
-        // 2*height + 5 blocks; packParent regrowth (+2 per level at most, and rare) gets
-        // MT_B_SLACK - 5 more.  The largest growth of a message (op and both zamboni calls)
-        // measured in the host emulation is 2*height + 2, on every one of 704 documents of
-        // configs 2 and 3 and lag-256/1,024 variants (tools/micro/block_growth.py,
-        // MT_EVCOUNT3).  Exceeding the budget would set MT_DS_OOM_BLOCKS (never silently
-        // wrong); mt_set_residency(ctx, 0, ...) avoids LDS entirely.
-        if constexpr (!LDS) return (lBlks - blkTop + blkFreeN) >= 2 * height + MT_B_SLACK && (lHeap - heapN) >= 4 &&
+        // Block budget per message, an upper bound: the op's two cascades (two
+        // split walks, or a split and an insert) allocate at most (h + 2) + (h + 3) blocks; a
+        // zamboni pop's packParent chain grows the tree by at most 2 blocks in all (a level
+        // re-deals its n child blocks' <= 8(n - 1) + 3 children into min(7, floor(nh / 4))
+        // blocks: at most n + 2, and the chain climbs only past a level left with fewer than
+        // 4 blocks, which cannot have grown), with MT_ZMAX pops in each of a message's two
+        // zamboni calls: 2h + 5 + 2 * 2 * MT_ZMAX = 2h + 13.  The largest growth measured in
+        // the host emulation is 2h + 2 (tools/micro/block_growth.py, MT_EVCOUNT3).
+        if constexpr (!LDS) return (lBlks - blkTop + blkFreeN) >= 2 * height + MT_B_SLACK + kb && (lHeap - heapN) >= 4 + k &&
                                    height + 3 <= MT_L_H;
-        return (lRows - rowTop + rfN) >= 4 && (lBlks - blkTop + blkFreeN) >= 6 * (height + 2) + 8 &&
-               (lHeap - heapN) >= 4 && height + 3 <= MT_L_H;
+        return (lRows - rowTop + rfN) >= 4 + k && (lBlks - blkTop + blkFreeN) >= 6 * (height + 2) + 8 + kb &&
+               (lHeap - heapN) >= 4 + k && height + 3 <= MT_L_H;
     }
     MT_HD void ancPut(int u, int h, int a) {
         if constexpr (LDS) mt_lds().uanc[u * MT_L_H + h] = (uint8_t)(a < 0 ? 255 : a);

@@ -89,7 +89,16 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
 #endif
     for (uint32_t i = o0; i < o1; i++) {
         e.curOp = i;
-        if (Eng::kLds && !e.ldsHeadroom()) return i;
+        if constexpr (Eng::kLds) {
+            int k = 0;                                   // a paste inserts every clone of its register
+            if constexpr (Eng::kFull) {
+                if (!g) {
+                    const uint32_t r0 = (uint32_t)uni(((const int*)&ops.rec[i])[0]);
+                    if ((int)(r0 & 0xFF) == MT_OP_PASTE) k = e.regCount((int)(r0 >> 16), uni(((const int*)&ops.rec[i])[6]));
+                }
+            }
+            if (!e.ldsHeadroom(k)) return i;
+        }
 #if defined(MT_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
         const unsigned long long tg = __builtin_amdgcn_s_memtime();
         if (g) mt_gen_op(e, ops, i, i - o0, nc, *g, rng, lastRef);

@@ -112,6 +112,23 @@ def test_emu_snapshots_after_reserved_staging_match_oracle(reserve, monkeypatch)
     compare(batch, props, 4, reserve=reserve)
 
 
+# Block-residency budget under adversarial streams: one-unit inserts build many segments and
+# deep trees, 48-unit removals then unlink them in bursts (scours that leave blocks under half
+# full, packParent re-dealing whole levels); with lag 0 the zamboni runs every message.  Every
+# message must fit the per-message block budget (MtEngT::ldsHeadroom, 2h + 13) or hand the
+# document over to HBM first: never MT_DS_OOM_BLOCKS.
+ADVERSARIAL = dict(clients=2, lag=0, ins=70, rem=30, ins_len=1, rem_len=48, ops=5000)
+
+
+@pytest.mark.parametrize("res", [(2, 0, 40, 12), (2, 0, 104, 94), (1, 90, 48, 24)])
+def test_emu_block_budget_adversarial_matches_oracle(res):
+    props = ann_props()
+    p = gen_params(seed=41, n_docs=3, **ADVERSARIAL)
+    batch, st, _ = generate(p, props)
+    assert st == [0] * 3
+    compare(batch, props, 3, residency=res)
+
+
 # LDS residency hand-over: tiny LDS caps make documents leave LDS mid-run (at
 # different ops, with different pools the binding one) and finish from HBM;
 # (0, ...) runs the HBM-pool kernel alone.  Results must not change.
