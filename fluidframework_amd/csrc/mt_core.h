@@ -1914,7 +1914,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int m = (ovxN - base) < MT_WAVE ? (ovxN - base) : MT_WAVE;
             auto keep = wave_map(m, [&](int k) MT_LAM {
                 const MtOvx e = ovx[base + k];
-                return (bool)((row(e.row).parent >= 0) & (row(e.row).rseq == e.rseq) & (e.rseq > minSeq));
+                return (bool)((int)(row(e.row).parent >= 0) & (int)(row(e.row).rseq == e.rseq) & (int)(e.rseq > minSeq));
             });
             auto ent = wave_map(m, [&](int k) MT_LAM { return ovx[base + k]; });
             auto rk = wave_rank(keep);
@@ -2911,7 +2911,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                         const auto rk = wave_rank(cond);
                         const int k0 = regTop + nCol;               // into the register arena's free tail
                         wave_for(h.n, [&](int j) MT_LAM {
-                            if (own(cond, j) & (k0 + own(rk, j) < regCap)) regRow(k0 + own(rk, j)) = own(ch, j);
+                            if ((int)own(cond, j) & (int)(k0 + own(rk, j) < regCap)) regRow(k0 + own(rk, j)) = own(ch, j);
                         });
                         nCol += nact;
                     } else if (mode == MT_MAP_REMOVE) {
@@ -2932,7 +2932,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                         wave_sync();
                         if (c >= 63) {                                 // removedClientOverlap beyond the mask
                             const uint64_t ob = wave_ballot(wave_map(h.n, [&](int j) MT_LAM {
-                                return (bool)(own(cond, j) & (row(own(ch, j)).rseq != sq));
+                                return (bool)((int)own(cond, j) & (int)(row(own(ch, j)).rseq != sq));
                             }));
                             for (uint64_t b = ob; b; b &= b - 1) {
                                 const int j = __builtin_ctzll(b), s = wave_at(ch, j);

@@ -26,7 +26,10 @@ pa = MtGenParams(1, n, pre, 1, 0, 100, 0, 5, 1, 1, 0); pa.ins_len_min, pa.seg_pr
 eng.generate(pa); eng.sync(); eng.checkpoint()
 pb = MtGenParams(2, n, ops, 8, 1024, 60, 40, 8, 8, 2, 0); pb.continue_docs = 1
 eng.generate(pb); eng.sync(); eng.generated_to_resident(); eng.restore()
-eng.set_residency(bench.RESIDENCY[res])
+if res == "big" and os.environ.get("MT_BIG_FLAGS"):
+    eng.set_residency(bench.RESIDENCY[res], 0, int(os.environ["MT_BIG_FLAGS"]), 0)   # MT_BIGF_* switches (A/B)
+else:
+    eng.set_residency(bench.RESIDENCY[res])
 fn = eng.lib.mt_prof_get; fn.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
 base = np.zeros((n, 8), np.uint64); fn(eng.h, n, base.ctypes.data)
 t = time.time(); eng.replay_resident(); eng.sync(); dt = time.time() - t
