@@ -51,7 +51,7 @@ CONFIGS = {
                     desc="256 long docs (pre-built to 200k segments / 1M chars) x 50k msgs, 8 clients, lag U[0,1024]"),
     # docs = per GPU (weak scaling; 8 GPUs = 1,048,576 docs); ops ~ Zipf(1.5) on [8, 65536], clients U[2,16]
     "config5": dict(docs=131072, ops=0, clients=0, lag=32, ins=60, rem=40, ins_len=8, rem_len=8, ann_sets=1, rewrite=0,
-                    partition="2048:224",   # profiles/r05/c5part: runs >= 2048 msgs on 224 reserved CUs (wide kernel)
+                    partition="256:224",    # profiles/r05/c5part: runs >= 256 msgs on 224 reserved CUs (wide kernel)
                     desc="Zipf(1.5)-sized docs (8..65536 msgs, clients U[2,16]), 131072 docs per GPU, rank-0 ingest, "
                          "LPT rebalance + digest gather over RCCL"),
 }
@@ -513,7 +513,9 @@ def run_config5(args, c, world, rank, local):
     kern_s = float(np.mean(kms)) / 1e3
     achieved = bytes_per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
     # the PMC passes run at N = 1 (rank 0 replays every document): per launch of that workload
-    traffic = measured_traffic("config5", {"docs": c["docs"], "ops": 0}, REPLAY_KERNEL[args.residency]) if world == 1 else None
+    # the replay launch's kernels: partitioned size classes run the wide kernel beside the block one
+    kname = "mt_replay_blkw_kernel+mt_replay_blk_kernel" if args.residency == "blk" and part else REPLAY_KERNEL[args.residency]
+    traffic = measured_traffic("config5", {"docs": c["docs"], "ops": 0}, kname) if world == 1 else None
     out = {
         "metric": "sequenced merge-tree ops applied/sec (whole node) + achieved HBM GB/s",
         "value": total_msgs * args.steps / dt, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
@@ -528,7 +530,7 @@ def run_config5(args, c, world, rank, local):
                    "partition": {"min_msgs": part[0], "cus": part[1]} if args.residency == "blk" and part else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic[0] if traffic else None,
-                     "traffic_source": traffic[1] if traffic else None, "kernel": REPLAY_KERNEL[args.residency] + " (rank 0)",
+                     "traffic_source": traffic[1] if traffic else None, "kernel": kname + " (rank 0)",
                      "kernel_ms": kern_s * 1e3, "bytes_per_launch": bytes_per_launch},
         "parity": "status words clean on every rank" if int(bad[0].item()) == 0 else "STATUS ERROR",
         "exchange": {"docs_checked": int(bad[2].item()), "checksum_mismatch_docs": int(bad[1].item()),
