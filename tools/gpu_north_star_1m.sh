@@ -5,6 +5,6 @@
 set -o pipefail
 OUT=gpurun_out/${1:-north_star_1m}; mkdir -p $OUT
 export PYTHONUNBUFFERED=1
-timeout -k 10 1100 python -u bench.py --config config5 --docs 1048576 --steps 2 --warmup 1 > $OUT/config5_1m.json 2> $OUT/config5_1m.err
+timeout -k 10 1100 python -u bench.py --config config5 --docs 1048576 --steps 2 --warmup 1 --partition ${PARTITION:-8192:128} > $OUT/config5_1m.json 2> $OUT/config5_1m.err
 rc=$?; echo "bench rc=$rc"; tail -c 1500 $OUT/config5_1m.json; tail -5 $OUT/config5_1m.err
 exit $rc
