@@ -91,8 +91,13 @@ __global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_kernel(MtStat
     __shared__ MtScratch sc;
     (void)mt_replay_doc<MT_RES_HBM, FULL>(S, ops, blockIdx.x, &sc, 0, 0, 0);
 }
+// The rest of runs that outgrew LDS: usually none or a few documents, so two waves per SIMD
+// (a 256-VGPR budget: no spills, no scratch) rather than the hot kernels' four.
+#ifndef MT_REST_WAVES_PER_SIMD
+#define MT_REST_WAVES_PER_SIMD 2
+#endif
 template <bool FULL>
-__global__ __launch_bounds__(64, MT_WAVES_PER_SIMD) void mt_replay_rest_kernel(MtState S, MtOps ops, const uint32_t* cursor) {
+__global__ __launch_bounds__(64, MT_REST_WAVES_PER_SIMD) void mt_replay_rest_kernel(MtState S, MtOps ops, const uint32_t* cursor) {
     __shared__ MtScratch sc;
     mt_replay_doc_rest<FULL>(S, ops, blockIdx.x, &sc, cursor[blockIdx.x]);
 }
@@ -123,8 +128,11 @@ void mtk_blk_fast_cont(hipStream_t s, uint32_t n, const MtState& S, const MtOps&
     hipLaunchKernelGGL((mt_replay_blk_kernel<false, true>), dim3(n), dim3(64), pad, s, S, o, runs, cur, lb, lh);
 }
 #elif MT_KSET == 6
+#ifndef MT_BLKW_PAD_BYTES
+#define MT_BLKW_PAD_BYTES 0           // diagnostic builds only: dynamic LDS per workgroup (fewer per CU)
+#endif
 void mtk_blkw(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur) {
-    hipLaunchKernelGGL((mt_replay_blkw_kernel<false, true>), dim3(n), dim3(64), 0, s, S, o, runs, cur);
+    hipLaunchKernelGGL((mt_replay_blkw_kernel<false, true>), dim3(n), dim3(64), MT_BLKW_PAD_BYTES, s, S, o, runs, cur);
 }
 #elif MT_KSET == 1
 void mtk_blk_full(hipStream_t s, uint32_t n, const MtState& S, const MtOps& o, const uint32_t* runs, uint32_t* cur, int lb,
