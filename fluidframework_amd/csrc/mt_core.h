@@ -438,6 +438,7 @@ struct MtScratch {
     int pathOff[MT_MAXH + 2], pathLen[MT_MAXH + 2];   // a walk's path blocks: perspective start, length
     int hold[64];
     int holdLen[64];                  // observer length of each held child (scourLeaves)
+    uint8_t holdBlk[64];              // index (in its parent) of the block each held child was in (packParent)
     int rfree[MT_RFL];                // recycled rows (unlinked, out of the window, no heap entry)
     int corr[MT_MAXN];                // per-child perspective corrections (childLens)
 };
@@ -2639,6 +2640,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int c = own(cls, t);
             sc->hold[h0 + own(rkK, t)] = own(f, t);
             sc->holdLen[h0 + own(rkK, t)] = c == 2 ? 0 : (c == 4 ? own(runLen, t) : own(fl, t));
+            sc->holdBlk[h0 + own(rkK, t)] = (uint8_t)(t >> 3);
         });
         wave_sync();
         return nh + nK;
@@ -2665,19 +2667,22 @@ template <int RES, bool FULL = true> struct MtEngT {
                 for (int i = 0; i < ph.n; i++) {
                     const int cb = wave_at(pch, i);
                     const int n = uni(bk(cb).n), base = nh;
-                    wave_for(n, [&](int k) MT_LAM { const int g = bk(cb).c[k]; sc->hold[base + k] = g; sc->holdLen[base + k] = bk(g).len; });
+                    wave_for(n, [&](int k) MT_LAM {
+                        const int g = bk(cb).c[k];
+                        sc->hold[base + k] = g; sc->holdLen[base + k] = bk(g).len; sc->holdBlk[base + k] = (uint8_t)i;
+                    });
                     nh += n;
                 }
             }
             int cc = nh / (MT_MAXN / 2); if (cc > MT_MAXN - 1) cc = MT_MAXN - 1; if (cc < 1) cc = 1;
-            // The old children go on the free list and the new blocks come off it, LIFO: the first
-            // min(cc, n) new blocks are the last old children, in reverse order, so those are taken
-            // directly and only the rest are freed (the same blocks and free list as freeing all,
-            // then allocating, without a dependent LDS load per allocation).
+            // New block ni < min(cc, n) is old child ni (block ids are internal: any assignment
+            // gives the same tree), so a child dealt to the group of its own old block keeps its
+            // parent field and is not written (about half of them); the other old children are
+            // freed, and blocks beyond n come off the free list (rare).
             const int reuse = cc < ph.n ? cc : ph.n;
-            for (int i = 0; i < ph.n - reuse; i++) freeBlock(wave_at(pch, i));
             const int pn = ph.n;
-            auto nbid = wave_shfl(pch, [=](int ni) MT_LAM { return ni < reuse ? pn - 1 - ni : 0; });
+            for (int i = reuse; i < pn; i++) freeBlock(wave_at(pch, i));
+            auto nbid = wave_shfl(pch, [=](int ni) MT_LAM { return ni < reuse ? ni : 0; });
             for (int ni = reuse; ni < cc; ni++) {            // more blocks than P had (rare)
                 const int NB = allocBlock();
                 if (NB < 0) return;
@@ -2689,13 +2694,20 @@ template <int RES, bool FULL = true> struct MtEngT {
             // its child's parent), then lane ni block ni's header.
             const int base = nh / cc, extra = nh % cc;
             const auto nb8 = wave_gather8(nbid);
+            // the old block of each dealt child (lane t: slot t & 7 of new block t >> 3)
+            const auto oi = wave_map(8 * cc, [&](int t) MT_LAM {
+                const int ni = t >> 3, slot = t & 7;
+                const int cnt = base + (ni < extra ? 1 : 0), st = ni * base + (ni < extra ? ni : extra);
+                return slot < cnt ? (int)sc->holdBlk[st + slot] : 0;
+            });
+            const auto ob = wave_shfl(pch, [&](int t) MT_LAM { return own(oi, t) & 7; });
             wave_for(8 * cc, [&](int t) MT_LAM {
                 const int ni = t >> 3, slot = t & 7;
                 const int cnt = base + (ni < extra ? 1 : 0), st = ni * base + (ni < extra ? ni : extra);
                 const int ch = slot < cnt ? sc->hold[st + slot] : -1;
                 const int NB = own(nb8, t);
                 bk(NB).c[slot] = ch;
-                if (ch >= 0) setChildParent(chh, ch, NB);
+                if ((int)(ch >= 0) & (int)(own(ob, t) != NB)) setChildParent(chh, ch, NB);
             });
             wave_for(cc, [&](int ni) MT_LAM {
                 const int cnt = base + (ni < extra ? 1 : 0), st = ni * base + (ni < extra ? ni : extra);
