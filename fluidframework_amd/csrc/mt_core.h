@@ -2200,23 +2200,31 @@ template <int RES, bool FULL = true> struct MtEngT {
     }
 
     /* --------------------------------------------------------- zamboni -- */
-    // Heap.add + fixup (collections.ts:238-251).  A heap of <= 63 entries is
-    // sifted in registers (lane k = entry k): one load, readlanes, one store.
+    // Heap.add + fixup (collections.ts:238-251).  A heap of <= 63 entries is sifted
+    // wave-parallel (lane k = slot k): one load round, a ballot, stores to the moved slots only.
     MT_HD void heapAdd(int s, int ms) {
         if (heapN + 1 > (int)S.heapCap) { status |= MT_DS_OOM_HEAP; return; }
         int k = ++heapN;
         if (heapN > heapHW) heapHW = heapN;
         if (heapN < MT_WAVE) {
-            const int n = heapN;
-            auto hs = wave_map(n, [&](int i) MT_LAM { return hp(i).seg; });
-            auto hm = wave_map(n, [&](int i) MT_LAM { return hp(i).maxSeq; });
-            while (k > 1) {
-                const int pm = wave_at(hm, k >> 1);
-                if (pm > ms) { hs = wave_set(hs, k, wave_at(hs, k >> 1)); hm = wave_set(hm, k, pm); k >>= 1; } else break;
-            }
-            hs = wave_set(hs, k, s); hm = wave_set(hm, k, ms);
-            const int n1 = n + 1;
-            wave_for(n1, [&](int i) MT_LAM { if (i >= k) { hp(i).seg = own(hs, i); hp(i).maxSeq = own(hm, i); } });
+            // Sift-up in one step: the parents on the path from the root to slot n hold
+            // non-decreasing keys, so the entries that move down one slot (parent key > ms) are
+            // the path's lowest ones; each path lane loads its parent once (no readlane chain).
+            const int n = heapN, dn = 31 - __builtin_clz((unsigned)n);
+            auto mv = wave_map(n + 1, [&](int c) MT_LAM {
+                c = mt_opaque(c);
+                const int dc = 31 - __builtin_clz((unsigned)(c | 1));
+                return (bool)((int)(c >= 2) & (int)((n >> (dn - dc)) == c));
+            });
+            auto pms = wave_map(n + 1, [&](int c) MT_LAM { return own(mv, c) ? (int)hp(mt_opaque(c) >> 1).maxSeq : 0; });
+            auto psg = wave_map(n + 1, [&](int c) MT_LAM { return own(mv, c) ? (int)hp(mt_opaque(c) >> 1).seg : 0; });
+            mv = wave_map(n + 1, [&](int c) MT_LAM { return own(mv, c) && own(pms, c) > ms; });
+            const int top = wave_first(mv);
+            k = top < 0 ? n : top >> 1;
+            wave_for(n + 1, [&](int c) MT_LAM {
+                if (own(mv, c)) { hp(c).seg = own(psg, c); hp(c).maxSeq = own(pms, c); }
+                if (c == k) { hp(c).seg = s; hp(c).maxSeq = ms; }
+            });
             if (k == 1) heapTop = ms;
             return;
         }
@@ -2230,32 +2238,37 @@ template <int RES, bool FULL = true> struct MtEngT {
     MT_HD MtHeapE heapGet() {                                 // Heap.get + fixdown, collections.ts:230-268
         MT_EV(3, 1); MT_EV(7, heapN - 1);
         if (heapN < MT_WAVE) {
-            const int n0 = heapN + 1;
-            auto hs = wave_map(n0, [&](int i) MT_LAM { return hp(i).seg; });
-            auto hm = wave_map(n0, [&](int i) MT_LAM { return hp(i).maxSeq; });
-            MtHeapE x; x.seg = wave_at(hs, 1); x.maxSeq = wave_at(hm, 1);
-            const int lseg = wave_at(hs, heapN), lms = wave_at(hm, heapN);
-            heapN--;
+            // Fix-down as a pointer chase: every slot i computes in parallel the child j(i) the
+            // reference's loop would take (the left one on ties) and whether the moving last
+            // entry would pass it (key > the child's); the wave then follows j from the root,
+            // one readlane per level, and the slots on the path take their child's entry.
+            const int N = heapN, n = N - 1;
+            MtHeapE x; x.seg = uni(hp(1).seg); x.maxSeq = uni(hp(1).maxSeq);
+            const int lseg = uni(hp(N).seg), lms = uni(hp(N).maxSeq);
+            heapN = n;
             heapTop = 0x7FFFFFFF;
-            if (heapN >= 1) {
-                const int n = heapN;
+            if (n >= 1) {
+                auto lm = wave_map(n + 1, [&](int i) MT_LAM { return (int)(i >= 1) & (int)(2 * i <= n) ? (int)hp(2 * mt_opaque(i)).maxSeq : 0; });
+                auto rm = wave_map(n + 1, [&](int i) MT_LAM { return (int)(i >= 1) & (int)(2 * i < n) ? (int)hp(2 * mt_opaque(i) + 1).maxSeq : 0; });
+                auto ls = wave_map(n + 1, [&](int i) MT_LAM { return (int)(i >= 1) & (int)(2 * i <= n) ? (int)hp(2 * mt_opaque(i)).seg : 0; });
+                auto rs = wave_map(n + 1, [&](int i) MT_LAM { return (int)(i >= 1) & (int)(2 * i < n) ? (int)hp(2 * mt_opaque(i) + 1).seg : 0; });
+                auto right = wave_map(n + 1, [&](int i) MT_LAM { return (bool)((int)(2 * i < n) & (int)(own(lm, i) > own(rm, i))); });
+                auto cm = wave_map(n + 1, [&](int i) MT_LAM { return own(right, i) ? own(rm, i) : own(lm, i); });
+                auto cs = wave_map(n + 1, [&](int i) MT_LAM { return own(right, i) ? own(rs, i) : own(ls, i); });
+                auto nx = wave_map(n + 1, [&](int i) MT_LAM {
+                    return (int)(i >= 1) & (int)(2 * i <= n) & (int)(own(cm, i) < lms) ? 2 * i + (int)own(right, i) : 0;
+                });
                 int k = 1;
-                heapTop = lms;
-                while ((k << 1) <= n) {
-                    int j = k << 1;
-                    int cs = wave_at(hs, j), cm = wave_at(hm, j);
-                    if (j < n) {
-                        const int cm1 = wave_at(hm, j + 1);
-                        if (cm > cm1) { j++; cs = wave_at(hs, j); cm = cm1; }
-                    }
-                    if (lms <= cm) break;
-                    MT_EV(4, 1);
-                    if (k == 1) heapTop = cm;
-                    hs = wave_set(hs, k, cs); hm = wave_set(hm, k, cm); k = j;
-                }
-                hs = wave_set(hs, k, lseg); hm = wave_set(hm, k, lms);
-                const int n1 = n + 1;
-                wave_for(n1, [&](int i) MT_LAM { if (i >= 1) { hp(i).seg = own(hs, i); hp(i).maxSeq = own(hm, i); } });
+                for (int t = wave_at(nx, 1); t != 0; t = wave_at(nx, t)) { MT_EV(4, 1); k = t; }
+                const int dk = 31 - __builtin_clz((unsigned)k);
+                wave_for(n + 1, [&](int i) MT_LAM {
+                    if (i < 1 || i > k) return;
+                    const int di = 31 - __builtin_clz((unsigned)i);
+                    if ((k >> (dk - di)) != i) return;
+                    if (i == k) { hp(i).seg = lseg; hp(i).maxSeq = lms; }
+                    else { hp(i).seg = own(cs, i); hp(i).maxSeq = own(cm, i); }
+                });
+                heapTop = k == 1 ? lms : wave_at(cm, 1);
             }
             return x;
         }

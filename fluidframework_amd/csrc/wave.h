@@ -127,6 +127,9 @@ __device__ __forceinline__ int wave_set(int a, int k, int v) { return __lane_id(
 __device__ __forceinline__ void lds_add(int* p, int v) { __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
 // keeps a loaded value alive (a prefetch whose result is otherwise unused)
 __device__ __forceinline__ void mt_keep(int v) { __asm__ volatile("" ::"v"(v)); }
+// the same value, opaque to the compiler: lane-index arithmetic behind it is not hoisted to the
+// kernel's entry (where it would hold a VGPR, or a spill slot, across the whole replay loop)
+__device__ __forceinline__ int mt_opaque(int v) { __asm__ volatile("" : "+v"(v)); return v; }
 // per-lane compare-and-swap on LDS; returns the old value
 __device__ __forceinline__ int lds_cas(int* p, int cmp, int v) {
     __hip_atomic_compare_exchange_strong(p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -231,6 +234,7 @@ inline LaneArr<int> wave_set(LaneArr<int> a, int k, int v) { if (k >= 0 && k < M
 inline void lds_add(int* p, int v) { *p += v; }
 inline int lds_cas(int* p, int cmp, int v) { const int o = *p; if (o == cmp) *p = v; return o; }
 inline void mt_keep(int) {}
+inline int mt_opaque(int v) { return v; }
 inline unsigned long long wave_atomic_add(unsigned long long* p, unsigned long long d) { return __atomic_fetch_add(p, d, __ATOMIC_RELAXED); }
 inline unsigned long long wave_atomic_next(unsigned long long* p) { return wave_atomic_add(p, 1ull); }
 inline unsigned long long wave_sum64(const LaneArr<unsigned long long>& a) {
