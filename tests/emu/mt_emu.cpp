@@ -130,3 +130,22 @@ static int mtb_launch_rows(mt_ctx* c, bool pack, uint32_t first, uint32_t n, uin
 }
 #define MT_FN(name) emu_##name
 #include "../../fluidframework_amd/csrc/mt_api_impl.h"
+
+// Test hook: Heap.add / Heap.get (mt_core.h heapAdd / heapGet) driven directly on document
+// `doc`'s heap: ops[i] >= 0 adds {seg i, maxSeq ops[i]}, ops[i] < 0 pops; each pop writes its
+// {seg, maxSeq} to out (two ints).  Returns the number of pops, or -1 on an engine status.
+extern "C" int emu_test_heap(mt_ctx* c, uint32_t doc, const int32_t* ops, int n, int32_t* out) {
+    MtScratch sc;
+    MtEng e;
+    e.bind(c->S, doc, &sc);
+    int np = 0;
+    for (int i = 0; i < n; i++) {
+        if (ops[i] >= 0) e.heapAdd(i, ops[i]);
+        else {
+            const MtHeapE x = e.heapGet();
+            out[2 * np] = x.seg; out[2 * np + 1] = x.maxSeq; np++;
+        }
+        if (e.status) return -1;
+    }
+    return np;
+}
