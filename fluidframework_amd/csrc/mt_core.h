@@ -2753,11 +2753,16 @@ template <int RES, bool FULL = true> struct MtEngT {
             MT_EV2(6, 1);
             MT_QB(q0); MT_QC(6);
             MT_ZB(z5); MT_ZC(7);
+            // the popped row's parent and meta are loaded before the sift (which touches only
+            // the heap), so their round trip overlaps it
+            const int s0 = uni(hp(1).seg);
+            const int pv = row(s0).parent;
+            const uint32_t mv = row(s0).meta;
             const MtHeapE e = heapGet();
             MT_ZE(5, z5);
             MT_QE(5, q0);
-            const int p = uni(row(e.seg).parent);
-            uint32_t em = uni(row(e.seg).meta);
+            const int p = uni(pv);
+            uint32_t em = uni(mv);
             if ((em & MT_M_HREF) != MT_M_HREF) { em -= MT_M_HREF1; row(e.seg).meta = em; }
             if (p < 0 && !(em & (MT_M_HREF | MT_M_INWIN))) freeRow(e.seg);
             if (p >= 0 && uni(bk(p).scour) != 0) {
