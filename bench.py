@@ -51,7 +51,6 @@ CONFIGS = {
                     desc="256 long docs (pre-built to 200k segments / 1M chars) x 50k msgs, 8 clients, lag U[0,1024]"),
     # docs = per GPU (weak scaling; 8 GPUs = 1,048,576 docs); ops ~ Zipf(1.5) on [8, 65536], clients U[2,16]
     "config5": dict(docs=131072, ops=0, clients=0, lag=32, ins=60, rem=40, ins_len=8, rem_len=8, ann_sets=1, rewrite=0,
-                    partition="256:224",    # profiles/r05/c5part: runs >= 256 msgs on 224 reserved CUs (wide kernel)
                     desc="Zipf(1.5)-sized docs (8..65536 msgs, clients U[2,16]), 131072 docs per GPU, rank-0 ingest, "
                          "LPT rebalance + digest gather over RCCL"),
 }
@@ -134,12 +133,34 @@ def reserve_staging(eng):
 
 
 def partition_of(args, c):
-    """(min_ops, cus) of --partition MIN:CUS (or the config's default), None when off."""
-    spec = args.partition if args.partition else c.get("partition", "")
+    """(min_ops, cus) of --partition MIN:CUS, "auto" (the default: mt_plan_partition's rule
+    applied by the library to each resident batch), None when off."""
+    spec = args.partition if args.partition else c.get("partition", "auto")
     if not spec or spec == "off":
         return None
+    if spec == "auto":
+        return "auto"
     a, b = spec.split(":")
     return int(a), int(b)
+
+
+def apply_partition(eng, args, c):
+    part = partition_of(args, c)
+    if args.residency == "blk" and part:
+        eng.set_partition(*((part,) if part == "auto" else part))
+    return part
+
+
+def partition_report(eng, args, part):
+    """The partition a run used: {"min_msgs", "cus", "rule"} (rule "auto" when the library
+    chose it), None for none."""
+    if args.residency != "blk" or not part:
+        return None
+    got = eng.partition_info() if eng.fn.get("last_partition") else None
+    if got is None:
+        return {"min_msgs": 0, "cus": 0, "rule": "auto: none"} if part == "auto" else None
+    got["rule"] = "auto" if part == "auto" else "fixed"
+    return got
 
 
 def caps_for(c):
@@ -471,9 +492,7 @@ def run_config5(args, c, world, rank, local):
     big = c.get("big_min_ops", 0) if args.big_min_ops < 0 else args.big_min_ops
     if args.residency == "blk" and big:
         eng.set_size_class(big)
-    part = partition_of(args, c)
-    if args.residency == "blk" and part:
-        eng.set_partition(*part)
+    part = apply_partition(eng, args, c)
     if args.cont_min >= 0:
         eng.set_continuation(args.cont_min)
     my_msgs = int(sh.ops.sum())
@@ -514,7 +533,9 @@ def run_config5(args, c, world, rank, local):
     achieved = bytes_per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
     # the PMC passes run at N = 1 (rank 0 replays every document): per launch of that workload
     # the replay launch's kernels: partitioned size classes run the wide kernel beside the block one
-    kname = "mt_replay_blkw_kernel+mt_replay_blk_kernel" if args.residency == "blk" and part else REPLAY_KERNEL[args.residency]
+    part_used = partition_report(eng, args, part)
+    kname = ("mt_replay_blkw_kernel+mt_replay_blk_kernel" if part_used and part_used["cus"]
+             else REPLAY_KERNEL[args.residency])
     traffic = measured_traffic("config5", {"docs": c["docs"], "ops": 0}, kname) if world == 1 else None
     out = {
         "metric": "sequenced merge-tree ops applied/sec (whole node) + achieved HBM GB/s",
@@ -527,7 +548,7 @@ def run_config5(args, c, world, rank, local):
                    "msgs_total": total_msgs, "msgs_mean": total_msgs / total_docs,
                    "msgs_max": int(sh.all_ops.max()), "parallelism": f"doc-sharded x{world} (LPT)",
                    "residency": args.residency, "big_min_ops": big if args.residency == "blk" else None,
-                   "partition": {"min_msgs": part[0], "cus": part[1]} if args.residency == "blk" and part else None},
+                   "partition": part_used},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic[0] if traffic else None,
                      "traffic_source": traffic[1] if traffic else None, "kernel": kname + " (rank 0)",
@@ -560,6 +581,83 @@ def run_config5(args, c, world, rank, local):
             out["parity"] += manifest_text(man)
     if int(bad[1].item()):
         out["parity"] = f"EXCHANGE CHECKSUM MISMATCH on {int(bad[1].item())} docs; " + out["parity"]
+    print(json.dumps(out), flush=True)
+
+
+def run_config5_shares(args, c, local):
+    """Config 5's N-rank LPT plan for c['docs'] x N documents, every rank's share replayed in turn
+    on this one GPU (review item: the eight shares of north_star's 1,048,576-document plan on
+    hardware without an 8-GPU node).  Each share is timed as bench's config-5 step is (warmup, then
+    `steps` replays bracketed by syncs); the node step is the slowest share's.  The SnapshotV1
+    digests of every share land in global document order and are checked against the manifest."""
+    import torch
+    from fluidframework_amd.batch import MtGenParams
+    from fluidframework_amd.shard import rank_shares
+    device = torch.device(Host.device_type, local) if Host.device_type == "cuda" else torch.device("cpu")
+    world = args.shares
+    total_docs = c["docs"] * world
+    gen_kw = dict(lag_max=c["lag"], pct_insert=c["ins"], pct_remove=c["rem"], ins_len_max=c["ins_len"],
+                  rem_len_max=c["rem_len"], n_ann_sets=c["ann_sets"], pct_rewrite=c["rewrite"])
+    names = ['"c%d"' % i for i in range(64)]
+    fac = lambda n, caps: Host.engine(n, local, per_doc=caps)
+    digs = np.zeros(total_docs, np.uint64)
+    shares, msgs_all, bad = [], 0, 0
+    t_setup = time.time()
+    for r, sh in rank_shares(device, fac, total_docs, world, args.seed, MtGenParams, gen_kw, names=names):
+        eng = sh.engine
+        if r == 0:
+            gen_s = time.time() - t_setup
+        if int(sh.timings.get("exchange_bad_docs", 0)):
+            raise SystemExit(f"share {r}: {sh.timings['exchange_bad_docs']} documents failed the exchange checksum")
+        set_residency(eng, args)
+        part = apply_partition(eng, args, c)
+        my_msgs = int(sh.ops.sum())
+        msgs_all += my_msgs
+        for _ in range(args.warmup):
+            sh.replay()
+        eng.sync()
+        t0 = time.perf_counter()
+        kms = []
+        for _ in range(args.steps):
+            sh.replay()
+            eng.sync()
+            kms.append(eng.last_replay_ms())
+        eng.sync()
+        dt = (time.perf_counter() - t0) / args.steps
+        st = eng.status(range(sh.n_docs))
+        cnt = eng.counters(range(sh.n_docs))
+        ok = (not st.any()) and int(cnt["msgs"].sum()) == my_msgs
+        bad += int(not ok)
+        neg = np.full(sh.n_docs, -1, np.int32)
+        digs[sh.owned] = eng.snapshot_digests(range(sh.n_docs), neg, neg, threads=min(16, os.cpu_count() or 1))
+        shares.append({"rank": r, "docs": sh.n_docs, "msgs": my_msgs, "msgs_max": int(sh.ops.max()),
+                       "ms_per_step": dt * 1e3, "kernel_ms": float(np.mean(kms)),
+                       "exchange_bytes": sh.timings.get("rebalance_bytes"),
+                       "partition": partition_report(eng, args, part),
+                       "status_clean": ok})
+        print(f"share {r}: {sh.n_docs} docs, {my_msgs} msgs, {dt * 1e3:.1f} ms/step", file=sys.stderr, flush=True)
+    step_max = max(s_["ms_per_step"] for s_ in shares)
+    out = {
+        "metric": "sequenced merge-tree ops applied/sec (whole node) + achieved HBM GB/s",
+        "value": msgs_all / (step_max / 1e3), "unit": "ops/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": step_max, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic (device-generated sequenced op streams, SURVEY.md §8(d) config-5 rules)",
+        "kind": f"projection: the {world} ranks' LPT shares replayed one after another on one GPU; value = all "
+                f"shares' messages / the slowest share's step (what an {world}-GPU node's step would be with no "
+                f"exchange inside the timed region)",
+        "config": {"workload": f"config5 at {total_docs} documents, N = {world} LPT plan", "docs_total": total_docs,
+                   "msgs_total": msgs_all, "residency": args.residency},
+        "shares": shares,
+        "parity": "status words clean on every share" if bad == 0 else f"STATUS ERROR on {bad} shares",
+        "setup_s": gen_s, "digest_xor": f"{int(np.bitwise_xor.reduce(digs)):016x}",
+    }
+    if bad == 0:
+        name = "config5_1m" if total_docs == 1048576 else "config5"
+        man = manifest_parity(name, digs, seed=args.seed, docs=total_docs, msgs_total=msgs_all)
+        if man is not None:
+            out["parity_manifest"] = man
+            out["parity"] += manifest_text(man)
     print(json.dumps(out), flush=True)
 
 
@@ -833,11 +931,15 @@ def _main(argv=None):
                     help="block residency: runs of at least this many messages keep the in-wave HBM "
                          "continuation (mt_set_continuation; -1: the library default)")
     ap.add_argument("--partition", default="",
-                    help="partitioned size classes under blk residency, MIN_MSGS:CUS (runs of at least MIN_MSGS "
-                         "messages on CUS reserved CUs, one per SIMD; 'off' to disable the config's default)")
+                    help="partitioned size classes under blk residency: 'auto' (default: the library's rule, "
+                         "mt_plan_partition, per resident batch), 'off', or MIN_MSGS:CUS (runs of at least MIN_MSGS "
+                         "messages in the wide kernel on CUS reserved CUs)")
     ap.add_argument("--big-min-ops", type=int, default=-1,
                     help="size classes under blk residency: runs of at least this many messages replay in the "
                          "long-document kernel on a second stream (0: off; default: the config's)")
+    ap.add_argument("--shares", type=int, default=0,
+                    help="config5: replay each rank's share of the N-rank LPT plan (docs per GPU x N documents) in "
+                         "turn on this one GPU and report the slowest share's step (an N-GPU projection)")
     args = ap.parse_args(argv)
     if args.residency == "auto":
         args.residency = "big" if args.config == "config4" else "blk"
@@ -863,6 +965,8 @@ def _main(argv=None):
         c = dict(CONFIGS["config5"])
         if args.docs:
             c["docs"] = args.docs
+        if args.shares:
+            return run_config5_shares(args, c, local)
         return run_config5(args, c, world, rank, local)
     dist = None
     if world > 1:
@@ -888,6 +992,7 @@ def _main(argv=None):
     big = c.get("big_min_ops", 0) if args.big_min_ops < 0 else args.big_min_ops
     if args.residency == "blk" and big:
         eng.set_size_class(big)
+    part = apply_partition(eng, args, c) if not big else None
     if args.cont_min >= 0:
         eng.set_continuation(args.cont_min)
     eng.upload_props(ann_props())
@@ -982,7 +1087,8 @@ def _main(argv=None):
                    "clients": c["clients"], "lag_max": c["lag"], "mix_ins_rem_ann": [c["ins"], c["rem"],
                                                                                    100 - c["ins"] - c["rem"]],
                    "parallelism": f"doc-sharded x{world}", "residency": args.residency,
-                   "big_min_ops": big if args.residency == "blk" else None, "lds_handover_docs": handover},
+                   "big_min_ops": big if args.residency == "blk" else None, "lds_handover_docs": handover,
+                   "partition": partition_report(eng, args, part)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic[0] if traffic else None,

@@ -56,6 +56,75 @@ static int mt_size_class_lists(mt_ctx* c) {
     return MT_OK;
 }
 
+// The partition rule (mt_plan_partition): a model of the measured kernels.
+// Per-message times of one document's wave, in microseconds: MT_PLAN_T_BLK in the block-
+// residency kernel with 16 documents per CU (config 2: 153.5 ms / 10,000 messages; MT_PLAN_T_LONE
+// alone), the same kernel's long document whose tree outgrows LDS and continues in HBM
+// (MT_PLAN_T_CONT past about MT_PLAN_LDS_FIT messages: config 5's 1,302 ms / 65,521 messages
+// unpartitioned), MT_PLAN_T_WIDE in the wide kernel with MT_PLAN_WIDE_PER_CU documents per CU
+// (LDS-bound: 21.2 KB each; 1,048,576-document config 5 at 256:224, 5,338 ms for 699 M messages
+// on 224 CUs) and MT_PLAN_T_WLONE its lone longest document (config 5: 887.9 ms / 65,521).
+#define MT_PLAN_T_BLK   15.3
+#define MT_PLAN_T_LONE  13.4
+#define MT_PLAN_T_CONT  19.9
+#define MT_PLAN_T_WIDE  12.0
+#define MT_PLAN_WIDE_PER_CU 7
+#define MT_PLAN_T_WLONE 13.5
+#define MT_PLAN_LDS_FIT 10000u
+struct MtPlanSide { double msgs = 0, extra = 0; uint32_t longest = 0; };
+// Step estimate (microseconds) of one kernel on `cus` CUs holding `per_cu` documents each.
+static double mt_plan_side(const MtPlanSide& s, double cus, double per_cu, double t_thr, double t_lone, bool cont) {
+    if (s.msgs == 0) return 0;
+    const double thr = (s.msgs * t_thr + (cont ? s.extra * (MT_PLAN_T_CONT - MT_PLAN_T_BLK) : 0)) / (cus * per_cu);
+    const double lat = cont && s.longest > MT_PLAN_LDS_FIT
+                           ? MT_PLAN_LDS_FIT * t_lone + (double)(s.longest - MT_PLAN_LDS_FIT) * MT_PLAN_T_CONT
+                           : (double)s.longest * t_lone;
+    return thr > lat ? thr : lat;
+}
+static void mt_plan_partition_impl(const uint32_t* len, uint32_t n, uint32_t ncu, uint32_t* min_ops, uint32_t* cus,
+                                   double* est_us) {
+    *min_ops = 0; *cus = 0;
+    std::vector<uint32_t> L(len, len + n);
+    std::sort(L.begin(), L.end(), std::greater<uint32_t>());
+    // suffix sums over the sorted lengths: messages and continuation messages of the runs < m
+    MtPlanSide all;
+    for (uint32_t x : L) { all.msgs += x; all.extra += x > MT_PLAN_LDS_FIT ? x - MT_PLAN_LDS_FIT : 0; }
+    all.longest = n ? L[0] : 0;
+    const double off = mt_plan_side(all, ncu, 16, MT_PLAN_T_BLK, MT_PLAN_T_LONE, true);
+    double best = off, bestSum = 0; uint32_t bm = 0, bk = 0;
+    const uint32_t step = ncu >= 8 ? ncu / 8 : 1;                      // whole XCD shares
+    for (uint32_t m = 256; m <= 32768 && ncu >= 2; m *= 2) {
+        MtPlanSide A, B;
+        for (uint32_t x : L) {
+            MtPlanSide& s = x >= m ? A : B;
+            s.msgs += x; s.extra += x > MT_PLAN_LDS_FIT ? x - MT_PLAN_LDS_FIT : 0;
+            if (x > s.longest) s.longest = x;
+        }
+        if (A.msgs == 0) break;
+        for (uint32_t k = step; k < ncu; k += step) {
+            const double ta = mt_plan_side(A, k, MT_PLAN_WIDE_PER_CU, MT_PLAN_T_WIDE, MT_PLAN_T_WLONE, false);
+            const double tb = mt_plan_side(B, ncu - k, 16, MT_PLAN_T_BLK, MT_PLAN_T_LONE, true);
+            const double t = ta > tb ? ta : tb, sum = ta + tb;
+            // the lowest step; within 1 % of it, the lowest total busy time
+            if (t < best * 0.99 || (t <= best * 1.01 && bm && sum < bestSum)) { best = t < best ? t : best; bestSum = sum; bm = m; bk = k; }
+        }
+    }
+    if (bm && best < off * 0.95) { *min_ops = bm; *cus = bk; if (est_us) *est_us = best; }
+    else if (est_us) *est_us = off;
+}
+// MT_PARTITION_AUTO: the resident batch's partition from its run lengths (once per batch).
+static void mt_auto_partition(mt_ctx* c) {
+    if (!c->part_auto || c->use_lds != 2 || c->auto_gen == c->batch_gen) return;
+    c->auto_gen = c->batch_gen;
+    const uint32_t R = c->n_runs;
+    if (c->run_off.size() != R + 1) { c->big_min_ops = 0; c->part_cus = 0; return; }
+    std::vector<uint32_t> len(R);
+    for (uint32_t r = 0; r < R; r++) len[r] = c->run_off[r + 1] - c->run_off[r];
+    uint32_t m = 0, k = 0;
+    mt_plan_partition_impl(len.data(), R, mtb_cu_count(c), &m, &k, nullptr);
+    c->big_min_ops = m; c->part_cus = m ? k : 0;
+}
+
 // The continuation class of block residency for the resident batch: whether any run has at
 // least cont_min_ops op records (n_cont > 0 launches the kernel with the in-wave continuation).
 static int mt_cont_lists(mt_ctx* c) {
@@ -589,7 +658,7 @@ int MT_FN(doc_pset)(mt_ctx* c, uint32_t doc, int32_t id, uint16_t* keys, int32_t
 int MT_FN(set_size_class)(mt_ctx* c, uint32_t big_min_ops) {
     if (!c) return MT_E_INVALID;
     c->big_min_ops = big_min_ops;
-    c->part_cus = 0;
+    c->part_cus = 0; c->part_auto = false;
     return MT_OK;
 }
 int MT_FN(set_continuation)(mt_ctx* c, uint32_t min_ops) {
@@ -599,8 +668,23 @@ int MT_FN(set_continuation)(mt_ctx* c, uint32_t min_ops) {
 }
 int MT_FN(set_partition)(mt_ctx* c, uint32_t min_ops, uint32_t cus) {
     if (!c) return MT_E_INVALID;
-    c->big_min_ops = min_ops;
-    c->part_cus = min_ops ? cus : 0;
+    c->part_auto = min_ops == MT_PARTITION_AUTO;
+    c->auto_gen = ~0ull;
+    c->big_min_ops = c->part_auto ? 0 : min_ops;
+    c->part_cus = (min_ops && !c->part_auto) ? cus : 0;
+    return MT_OK;
+}
+int MT_FN(plan_partition)(const uint32_t* run_ops, uint32_t n, uint32_t n_cus, uint32_t* min_ops, uint32_t* cus,
+                          double* est_ms) {
+    if ((n && !run_ops) || !min_ops || !cus || n_cus == 0) return MT_E_INVALID;
+    double us = 0;
+    mt_plan_partition_impl(run_ops, n, n_cus, min_ops, cus, &us);
+    if (est_ms) *est_ms = us / 1e3;
+    return MT_OK;
+}
+int MT_FN(last_partition)(mt_ctx* c, uint32_t* min_ops, uint32_t* cus) {
+    if (!c || !min_ops || !cus) return MT_E_INVALID;
+    *min_ops = c->part_cus ? c->big_min_ops : 0; *cus = c->part_cus;
     return MT_OK;
 }
 int MT_FN(set_residency)(mt_ctx* c, int use_lds, int rows, int blocks, int heap) {
@@ -960,6 +1044,12 @@ int MT_FN(reserve_staging)(mt_ctx* c, uint64_t bytes) {
         if (!mtb_host_stage(c, bytes, buf)) { c->err = "pinned staging allocation failed"; return MT_E_OOM; }
     return MT_OK;
 }
+// SnapshotV1 of a non-empty document whose chunk size no length is below (MT_CHUNK_NONE):
+// the reference's chunk loop (snapshotV1.ts:98-114) never ends; reported instead.
+static std::string mt_chunk_hang_msg(uint32_t doc) {
+    return "document " + std::to_string(doc) + ": mergeTreeSnapshotChunkSize is not a positive number, and "
+           "SnapshotV1's chunk loop (snapshotV1.ts:98-114) never ends on a non-empty document";
+}
 // Client.snapshot (client.ts:923-956): SnapshotV1 or, with legacy set, SnapshotLegacy.
 static int mt_snapshot_blobs(mt_ctx* c, uint32_t n, const uint32_t* docs, const int32_t* msn, const int32_t* seq,
                              uint64_t* digest, const char** arena, const uint64_t** blob_off,
@@ -972,10 +1062,11 @@ static int mt_snapshot_blobs(mt_ctx* c, uint32_t n, const uint32_t* docs, const 
         for (uint32_t j = 0; j < m; j++) {
             const uint32_t i = a + j;
             auto dn = c->doc_clients.find(docs[i]);
-            std::vector<std::string> blobs = legacy ? mtsnap::snapshot_legacy_blobs(views[j], c->names)
+            std::vector<std::string> blobs = legacy ? mtsnap::snapshot_legacy_blobs(views[j], c->names, c->chunk_of(docs[i]))
                                                     : mtsnap::snapshot_blobs(views[j], c->names,
                                                                              dn == c->doc_clients.end() ? nullptr : &dn->second,
                                                                              c->chunk_of(docs[i]));
+            if (blobs.empty()) { c->err = mt_chunk_hang_msg(docs[i]); return (int)MT_E_INVALID; }
             if (digest) digest[i] = mtsnap::blobs_digest(blobs);
             for (auto& b : blobs) { c->snap_arena += b; c->blob_off.push_back(c->snap_arena.size()); }
             c->blob_first.push_back((uint32_t)(c->blob_off.size() - 1));
@@ -1010,18 +1101,23 @@ int MT_FN(snapshot_digests)(mt_ctx* c, uint32_t n, const uint32_t* docs, const i
     // documents (a million Zipf documents stage ~20 GB)
     return mt_staged_groups(c, n, docs, [&](uint32_t a, uint32_t m, const std::vector<MtSnapView>& views) {
         const int th = (uint32_t)threads > m ? (int)m : threads;
+        std::vector<uint32_t> hang(th, UINT32_MAX);
         auto work = [&](int t) {
             for (uint32_t i = (uint32_t)t; i < m; i += (uint32_t)th) {
                 auto dn = c->doc_clients.find(docs[a + i]);
-                digest[a + i] = mtsnap::blobs_digest(mtsnap::snapshot_blobs(views[i], c->names,
-                                                                            dn == c->doc_clients.end() ? nullptr : &dn->second,
-                                                                            c->chunk_of(docs[a + i])));
+                std::vector<std::string> blobs = mtsnap::snapshot_blobs(views[i], c->names,
+                                                                        dn == c->doc_clients.end() ? nullptr : &dn->second,
+                                                                        c->chunk_of(docs[a + i]));
+                if (blobs.empty()) { hang[t] = std::min(hang[t], a + i); continue; }
+                digest[a + i] = mtsnap::blobs_digest(blobs);
             }
         };
         std::vector<std::thread> pool;
         for (int t = 1; t < th; t++) pool.emplace_back(work, t);
         work(0);
         for (auto& t : pool) t.join();
+        const uint32_t h = *std::min_element(hang.begin(), hang.end());
+        if (h != UINT32_MAX) { c->err = mt_chunk_hang_msg(docs[h]); return (int)MT_E_INVALID; }
         return (int)MT_OK;
     }, (uint32_t)threads);
 }

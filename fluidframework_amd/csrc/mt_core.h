@@ -2843,7 +2843,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                     if (pm == MT_PM_INCR) nv = (kd & MT_VK_NUM) ? MT_VAL_NAN : MT_VAL_UNSUP;
                     else nv = (kd & MT_VK_SEQM1) ? MT_VAL_UNSUP : pv;
                 }
-                if (nv == MT_VAL_CFRESH) nv = sq >= 0 ? MT_VAL_CONS(sq) : MT_VAL_UNSUP;
+                if (nv == MT_VAL_CFRESH) nv = (sq >= 0 && sq <= 0x7FFFFFEF) ? MT_VAL_CONS(sq) : MT_VAL_UNSUP;   // -16 - seq fits int32
                 if (nv == MT_VAL_UNSUP) { status |= MT_DS_UNSUPPORTED; return old; }
             }
             if (nv == MT_VAL_NULL) {

@@ -52,6 +52,8 @@ struct mt_ctx {
     // block-residency kernel on a stream masked to part_cus CUs, one document per SIMD (the
     // launch pads each workgroup's LDS to a quarter of the CU's), and the rest to the other CUs.
     uint32_t part_cus = 0, part_made = 0;
+    // MT_PARTITION_AUTO: big_min_ops / part_cus chosen per resident batch (mt_plan_partition)
+    bool part_auto = false; uint64_t auto_gen = ~0ull;
     // Block residency: a batch with a run of at least cont_min_ops op records replays in the
     // kernel with the in-wave HBM continuation (a long document that outgrows LDS keeps its head
     // start); other batches in the one without it (no scratch; an outgrown document finishes

@@ -258,8 +258,14 @@ static void launch_replay(mt_ctx* c, hipStream_t s, uint32_t n_runs, bool full) 
 }
 static int mt_size_class_lists(mt_ctx* c);
 static int mt_cont_lists(mt_ctx* c);
+static void mt_auto_partition(mt_ctx* c);
+static uint32_t mtb_cu_count(mt_ctx* c) {
+    int ncu = 0;
+    return hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && ncu > 0 ? (uint32_t)ncu : 256u;
+}
 static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     if (n_runs == 0) return MT_OK;
+    if (!g.enabled) mt_auto_partition(c);
     if (!g.enabled && c->use_lds == 2 && !c->big_min_ops) {
         int rc = mt_cont_lists(c);
         if (rc) return rc;

@@ -10,6 +10,7 @@
 // options.mergeTreeSnapshotChunkSize (default 10,000) characters, and serialize exactly as
 // JSON.stringify does.
 #pragma once
+#include <limits.h>
 #include <stdint.h>
 #include <string.h>
 #include <algorithm>
@@ -185,11 +186,13 @@ struct PropsMatch {
         return val[h];
     }
 };
-// chunk: options.mergeTreeSnapshotChunkSize (snapshotV1.ts:55; 0: SnapshotV1.chunkSize).
+// chunk: options.mergeTreeSnapshotChunkSize (snapshotV1.ts:55; 0: SnapshotV1.chunkSize;
+// MT_CHUNK_NONE: no length is below it).  Returns no blobs where the reference's chunk loop
+// (snapshotV1.ts:98-114) never ends: a chunk that takes no segment while segments remain.
 inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtNames& nm,
                                                const std::vector<std::string>* doc_clients = nullptr,
                                                uint64_t chunk = 0) {
-    const unsigned long long chunkLen = chunk ? (unsigned long long)chunk : 10000ull;
+    const unsigned long long chunkLen = chunk == MT_CHUNK_NONE ? 0ull : (chunk ? (unsigned long long)chunk : 10000ull);
     const std::vector<std::string>& cj = doc_clients ? *doc_clients : nm.client_json;
     const int minSeq = v.hdr.minSeq, curSeq = v.hdr.curSeq;
     PropsJson pj(v, nm);
@@ -243,6 +246,7 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
     do {
         Chunk c{total, 0, 0};
         while ((unsigned long long)c.length < chunkLen && c.start + c.count < segs.size()) { c.length += lens[c.start + c.count]; c.count++; }
+        if (c.count == 0 && total < segs.size()) return {};       // the reference loops forever here
         chunks.push_back(c); total += c.count; totalLen += c.length;
     } while (total < segs.size());
     std::vector<std::string> blobs;
@@ -273,8 +277,9 @@ inline std::vector<std::string> snapshot_blobs(const MtSnapView& v, const MtName
 // below the MSN and not removed at or below it (removes above the MSN keep their
 // text); all of them coalesce greedily (canAppend + matchProperties on clones).
 // Rows above the MSN are left to the catch-up ops blob, which the host appends.
-// Blob 0 is "header"; blob 1, if any, is "body".
-inline std::vector<std::string> snapshot_legacy_blobs(const MtSnapView& v, const MtNames& nm) {
+// Blob 0 is "header"; blob 1, if any, is "body".  chunk: options.mergeTreeSnapshotChunkSize as
+// in snapshot_blobs, the header chunk's approximate length (snapshotlegacy.ts:71, :109).
+inline std::vector<std::string> snapshot_legacy_blobs(const MtSnapView& v, const MtNames& nm, uint64_t chunk = 0) {
     const int minSeq = v.hdr.minSeq;
     PropsJson pj(v, nm);
     PropsMatch pm_(v, nm);
@@ -343,7 +348,8 @@ inline std::vector<std::string> snapshot_legacy_blobs(const MtSnapView& v, const
         return o;
     };
     std::vector<std::string> blobs;
-    const Chunk c1 = take(10000, 0);                                   // SnapshotLegacy.sizeOfFirstChunk
+    const long long first = chunk == MT_CHUNK_NONE ? 0 : (chunk == 0 ? 10000 : (chunk >= (uint64_t)LLONG_MAX ? LLONG_MAX : (long long)chunk));
+    const Chunk c1 = take(first, 0);                                   // chunkSize ?? SnapshotLegacy.sizeOfFirstChunk
     blobs.push_back(chunkStr(c1, true));
     if (c1.count < segs.size()) blobs.push_back(chunkStr(take(total, c1.count), false));
     return blobs;

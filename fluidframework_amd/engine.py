@@ -76,6 +76,9 @@ def _bind(lib, prefix: str):
         set_residency=f("set_residency", ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
         set_size_class=f("set_size_class", ctypes.c_int, [P, U32]),
         set_partition=f("set_partition", ctypes.c_int, [P, U32, U32]),
+        last_partition=f("last_partition", ctypes.c_int, [P, ctypes.POINTER(U32), ctypes.POINTER(U32)]),
+        plan_partition=f("plan_partition", ctypes.c_int, [P, U32, U32, ctypes.POINTER(U32), ctypes.POINTER(U32),
+                                                          ctypes.POINTER(ctypes.c_double)]),
         set_continuation=f("set_continuation", ctypes.c_int, [P, U32]),
         set_props=f("set_props", ctypes.c_int, [P, ctypes.POINTER(MtPropTable)]),
         set_client_names=f("set_client_names", ctypes.c_int, [P, U32, P]),
@@ -125,6 +128,20 @@ SEG_INFO_FIELDS = ("found", "offset", "obs_pos", "len", "seq", "client", "remove
                    "marker_ref_type", "depth", "path_lo", "path_hi", "row", "resolved", "pad")
 SEG_INFO_DTYPE = np.dtype([(f, np.uint32 if f.startswith("path") else np.int32) for f in SEG_INFO_FIELDS])
 POS_UNDEFINED = -(1 << 31)              # MT_POS_UNDEFINED
+MT_CHUNK_INFINITY = (1 << 64) - 1      # mt_set_doc_snapshot_chunk: Infinity (one chunk)
+MT_CHUNK_NONE = (1 << 64) - 2          # a size no length is below (0, negative, NaN)
+MT_PARTITION_AUTO = 0xFFFFFFFF         # mt_set_partition: chosen per batch (mt_plan_partition)
+
+
+def plan_partition(fn: dict, run_ops, n_cus: int = 256):
+    """mt_plan_partition through a bound function table (no context, no GPU call)."""
+    r = _u32(run_ops)
+    m, k, est = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_double()
+    rc = fn["plan_partition"](r.ctypes.data if len(r) else None, len(r), int(n_cus), ctypes.byref(m), ctypes.byref(k),
+                              ctypes.byref(est))
+    if rc:
+        raise MergeTreeError(f"mt_plan_partition failed ({rc})")
+    return int(m.value), int(k.value), float(est.value)
 
 DELTA_DTYPE = np.dtype([("op", np.uint32), ("kind", np.int32), ("pos", np.int32), ("len", np.int32),
                         ("seg", np.int32), ("a", np.int32), ("b", np.int32), ("pad", np.int32)])
@@ -350,10 +367,23 @@ class Engine:
         second launch."""
         self._check(self.fn["set_continuation"](self.h, int(min_ops)), "mt_set_continuation")
 
-    def set_partition(self, min_ops: int, cus: int):
-        """mt_set_partition: under block residency, runs of at least min_ops op records replay on
-        `cus` CUs reserved for them, one document per SIMD; the rest on the other CUs (0: off)."""
-        self._check(self.fn["set_partition"](self.h, int(min_ops), int(cus)), "mt_set_partition")
+    def set_partition(self, min_ops, cus: int = 0):
+        """mt_set_partition: under block residency, runs of at least min_ops op records replay in
+        the wide kernel on `cus` reserved CUs beside the rest (0: off; "auto": MT_PARTITION_AUTO,
+        chosen per resident batch by mt_plan_partition)."""
+        m = MT_PARTITION_AUTO if min_ops == "auto" else int(min_ops)
+        self._check(self.fn["set_partition"](self.h, m, int(cus)), "mt_set_partition")
+
+    def partition_info(self) -> dict:
+        """mt_last_partition: the partition the last replay launch used."""
+        m, k = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self.fn["last_partition"](self.h, ctypes.byref(m), ctypes.byref(k)), "mt_last_partition")
+        return {"min_msgs": int(m.value), "cus": int(k.value)} if k.value else None
+
+    def plan_partition(self, run_ops, n_cus: int = 256):
+        """mt_plan_partition: (min_ops, cus, estimated ms) the partition rule picks for these run
+        lengths ((0, 0, est) for no partition)."""
+        return plan_partition(self.fn, run_ops, n_cus)
 
     def checkpoint(self):
         """mt_checkpoint: device copy of every document's state."""
@@ -547,24 +577,23 @@ NON_COLLAB_CLIENT = -2                  # NonCollabClient, MT/constants.ts
 
 
 def snapshot_chunk_option(options: dict | None) -> int:
-    """options.mergeTreeSnapshotChunkSize as mt_set_doc_snapshot_chunk takes it (snapshotV1.ts:55:
-    `?? SnapshotV1.chunkSize`): 0 for the default, the size rounded up (lengths are integers,
-    `length < chunkSize`), 2**64-1 for Infinity.  The reference's chunk loop never ends for a
-    size that is not a positive number (NaN, 0, negative, a non-numeric value), so those raise."""
+    """options.mergeTreeSnapshotChunkSize as mt_set_doc_snapshot_chunk takes it: 0 for the default
+    (`?? 10000`, snapshotV1.ts:55, snapshotlegacy.ts:71), else the value the reference's
+    `length < chunkSize` compares against, i.e. JS ToNumber of it (jsjson.js_to_number): rounded
+    up (lengths are integers), MT_CHUNK_INFINITY for Infinity, MT_CHUNK_NONE when no length is
+    below it (0, negative, NaN: the legacy header chunk is empty; SnapshotV1 of a non-empty
+    document fails at snapshot time, where the reference's chunk loop never ends)."""
     import math
+    from .jsjson import _Undefined, js_to_number
     v = (options or {}).get("mergeTreeSnapshotChunkSize")
-    if v is None:
+    if v is None or isinstance(v, _Undefined):
         return 0
-    if isinstance(v, str):               # `length < "100"` compares numerically
-        try:
-            v = float(v.strip()) if v.strip() else 0.0
-        except ValueError:
-            v = float("nan")
-    if isinstance(v, bool) or not isinstance(v, (int, float)) or not (v > 0):
-        raise MergeTreeError(f"mergeTreeSnapshotChunkSize {v!r}: the reference's chunk loop would not end")
-    if math.isinf(v):
-        return (1 << 64) - 1
-    return min(int(math.ceil(v)), (1 << 64) - 2)
+    x = js_to_number(v)
+    if not (x > 0):
+        return MT_CHUNK_NONE
+    if math.isinf(x):
+        return MT_CHUNK_INFINITY
+    return min(int(math.ceil(x)), MT_CHUNK_NONE - 1)
 
 
 class Segment:

@@ -181,18 +181,17 @@ function decodeValue(v, valueJson) {
 }
 
 /**
- * options.mergeTreeSnapshotChunkSize as mt_set_doc_snapshot_chunk takes it
- * (`options?.mergeTreeSnapshotChunkSize ?? SnapshotV1.chunkSize`, snapshotV1.ts:55): 0 for the
- * default; the reference's chunk loop (`length < chunkSize`) never ends for NaN or a size <= 0.
+ * options.mergeTreeSnapshotChunkSize as setDocSnapshotChunk takes it: null for the default
+ * (`?? 10000`, snapshotV1.ts:55, snapshotlegacy.ts:71), else the number the reference's
+ * `length < chunkSize` compares against (ToNumber: "300" is 300, [100] is 100, true is 1).
+ * A value no length is below (0, negative, NaN) is passed on: the legacy header chunk is then
+ * empty, and SnapshotV1 of a non-empty document fails at snapshot time, where the reference's
+ * chunk loop never ends.
  */
 function snapshotChunkOption(options) {
     const v = options ? options.mergeTreeSnapshotChunkSize : undefined;
-    if (v === undefined || v === null) return 0;
-    const x = Number(v);
-    if (typeof v === "object" || typeof v === "boolean" || !(x > 0)) {
-        throw new Error(`mergeTreeSnapshotChunkSize ${String(v)}: the reference's chunk loop would not end`);
-    }
-    return x;
+    if (v === undefined || v === null) return null;
+    return Number(v);
 }
 
 /** One engine context (one GPU) and the documents it holds. */
@@ -446,7 +445,7 @@ class ClientGroup {
         if (d >= this.engine.maxDocs) throw new Error("engine document capacity exhausted");
         const cs = snapshotChunkOption(options);
         this.engine.openDocs(d, 1);
-        if (cs) this.engine.setSnapshotChunk([d], [cs]);
+        if (cs !== null) this.engine.setSnapshotChunk([d], [cs]);
         const c = new MergeTreeClient(this, d, options);
         this.clients.push(c);
         return c;

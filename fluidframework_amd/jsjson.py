@@ -17,6 +17,7 @@ Rules restated here:
 from __future__ import annotations
 
 import math
+import re
 from typing import Any
 
 class _Undefined:
@@ -170,3 +171,57 @@ def match_class_key(v: Any):
     if isinstance(v, str):
         return ("s", v)
     return ("z", None)
+
+
+# StrWhiteSpaceChar (ECMA-262 7.1.4.1.1): WhiteSpace and LineTerminator
+_JS_WS = "\t\n\v\f\r \u00a0\u1680\u2000\u2001\u2002\u2003\u2004\u2005\u2006\u2007\u2008\u2009\u200a" \
+         "\u2028\u2029\u202f\u205f\u3000\ufeff"
+_JS_DEC = re.compile(r"[+-]?(?:(?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][+-]?[0-9]+)?|Infinity)\Z")
+_JS_RADIX = {"0x": (16, re.compile(r"[0-9a-fA-F]+\Z")), "0o": (8, re.compile(r"[0-7]+\Z")),
+             "0b": (2, re.compile(r"[01]+\Z"))}
+
+
+def js_to_string(v: Any) -> str:
+    """ToString of a JSON-like value (ECMA-262 7.1.17) as the relational operators' ToPrimitive
+    reaches it: arrays join their elements' strings with "," (null / undefined as ""), plain
+    objects are "[object Object]"."""
+    if v is None or isinstance(v, _Undefined):
+        return ""
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (int, float)):
+        return number_to_js(float(v)) if not (isinstance(v, float) and (math.isnan(v) or math.isinf(v))) else \
+            ("NaN" if math.isnan(v) else ("Infinity" if v > 0 else "-Infinity"))
+    if isinstance(v, str):
+        return v
+    if isinstance(v, (list, tuple)):
+        return ",".join(js_to_string(e) for e in v)
+    return "[object Object]"
+
+
+def js_to_number(v: Any) -> float:
+    """ECMAScript ToNumber (7.1.4) of a JSON-like value, as `length < v` applies it: undefined and
+    objects give NaN, null and false 0, true 1, strings by StringToNumber (whitespace trimmed, ""
+    is 0, 0x / 0o / 0b literals, "Infinity"; anything else NaN), arrays through their joined
+    string ([] is 0, [100] is 100, [1, 2] is NaN)."""
+    if isinstance(v, _Undefined):
+        return float("nan")
+    if v is None:
+        return 0.0
+    if isinstance(v, bool):
+        return 1.0 if v else 0.0
+    if isinstance(v, (int, float)):
+        return float(v)
+    if isinstance(v, (list, tuple)):
+        return js_to_number(js_to_string(v))
+    if not isinstance(v, str):
+        return float("nan")
+    t = v.strip(_JS_WS)
+    if not t:
+        return 0.0
+    r = _JS_RADIX.get(t[:2].lower())
+    if r is not None:
+        return float(int(t[2:], r[0])) if r[1].match(t[2:]) else float("nan")
+    if not _JS_DEC.match(t):
+        return float("nan")
+    return float(t.replace("Infinity", "inf"))

@@ -233,7 +233,8 @@ napi_value SetDocClientNames(napi_env env, napi_callback_info info) {
 }
 
 // setDocSnapshotChunk(ctx, docIds: Uint32Array, sizes: Float64Array): options.mergeTreeSnapshotChunkSize
-// per document (0: default; Infinity: one chunk; sizes are rounded up, snapshotV1.ts:55, :78).
+// per document after ToNumber (Infinity: one chunk; sizes are rounded up, snapshotV1.ts:55, :78;
+// 0, negative and NaN: no length is below it, MT_CHUNK_NONE).  New documents have the default.
 napi_value SetDocSnapshotChunk(napi_env env, napi_callback_info info) {
     napi_value argv[3];
     if (!get_args(env, info, 3, argv)) return nullptr;
@@ -245,8 +246,7 @@ napi_value SetDocSnapshotChunk(napi_env env, napi_callback_info info) {
     std::vector<uint64_t> v(nd);
     for (size_t i = 0; i < nd; i++) {
         const double x = sz[i];
-        if (!(x >= 0)) { napi_throw_range_error(env, nullptr, "mergeTreeSnapshotChunkSize must be a positive number"); return nullptr; }
-        v[i] = x == 0 ? 0 : (x >= 1.8e19 ? UINT64_MAX : (uint64_t)std::ceil(x));
+        v[i] = !(x > 0) ? MT_CHUNK_NONE : (x >= 1.8e19 ? MT_CHUNK_INFINITY : (uint64_t)std::ceil(x));
     }
     int rc = mt_set_doc_snapshot_chunk(c, (uint32_t)nd, docs, v.data());
     return rc ? throw_rc(env, c, rc, "mt_set_doc_snapshot_chunk") : undefined(env);

@@ -206,6 +206,91 @@ class ShardedReplay:
         return res
 
 
+class SharePlan:
+    """The LPT plan every rank computes from the broadcast op counts: owner of every document,
+    the send order (documents grouped by owning rank, largest first), each document's first row
+    in rank 0's send buffer and each rank's op count."""
+
+    def __init__(self, ops: np.ndarray, world: int):
+        self.ops, self.world = ops, world
+        self.owner = lpt_assign(ops, world)
+        self.order = rank_order(self.owner, ops)
+        self.row_of = np.empty(len(ops), np.int64)
+        self.row_of[self.order] = np.concatenate(([0], np.cumsum(ops[self.order].astype(np.int64))[:-1]))
+        self.per_rank_ops = np.array([int(ops[self.owner == r].sum()) for r in range(world)], np.int64)
+        self.rank_row0 = np.concatenate(([0], np.cumsum(self.per_rank_ops)))      # rank r's rows in the send buffer
+
+    def owned(self, rank: int) -> np.ndarray:
+        """Rank `rank`'s documents in its engine's slot order (the send order)."""
+        return self.order[self.owner[self.order] == rank]
+
+
+def generate_send_rows(device, engine_factory, plan: SharePlan, cli: np.ndarray, seed: int, gen_params_cls,
+                       gen_kw: dict, props, names, chunk_docs: int, W: int):
+    """Rank 0's ingest: every document's stream generated in chunks (untimed) and packed by the
+    engine straight into its plan position of the send buffer (mt_generated_pack_rows, a HIP
+    kernel) with a 64-bit checksum per document.  Returns (send rows, replay caps [n, 6],
+    checksums) as device tensors."""
+    import torch
+    ops = plan.ops
+    docs_total = len(ops)
+    L = int(gen_kw["ins_len_max"])
+    caps_t = torch.zeros((docs_total, 6), dtype=torch.int32, device=device)
+    cs_t = torch.zeros(docs_total, dtype=torch.int64, device=device)
+    send = torch.empty((int(ops.sum(dtype=np.int64)), W), dtype=torch.int64, device=device)
+    gcaps = generation_caps(ops, L)
+    for a in range(0, docs_total, chunk_docs):
+        b = min(docs_total, a + chunk_docs)
+        idx = np.arange(a, b)
+        eng = engine_factory(b - a, {k: np.asarray(v)[idx] for k, v in gcaps.items()})
+        if props is not None:
+            eng.upload_props(props)
+        if names is not None:
+            eng.upload_names(names)
+        p = gen_params_cls(**{**gen_kw, "seed": seed, "n_docs": b - a, "ops_per_doc": 0, "clients": 2,
+                              "doc_id_base": a})
+        eng.generate(p, ops_per_doc=ops[idx], clients_per_doc=cli[idx])
+        eng.sync()
+        st = eng.status(range(b - a))
+        if st.any():
+            raise RuntimeError(f"generation failed for docs {a}..{b}: status {np.unique(st)}")
+        caps_t[a:b] = torch.from_numpy(replay_caps(eng.pools(range(b - a)), gcaps, idx)).to(device)
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        cs = eng.generated_pack_rows(0, b - a, plan.row_of[a:b].astype(np.uint64), send.data_ptr())
+        cs_t[a:b] = torch.from_numpy(cs.view(np.int64)).to(device)
+        eng.close()
+    return send, caps_t, cs_t
+
+
+def rank_engine(engine_factory, owned: np.ndarray, ops: np.ndarray, caps: np.ndarray, sums: np.ndarray, recv_ptr: int,
+                L: int, props, names, tm: dict):
+    """A rank's engine, sized exactly from the generation's high-water marks; the received rows
+    (at device address recv_ptr) become its resident batch (mt_upload_rows_dev: unpacked by a
+    HIP kernel, every document's checksum compared with rank 0's)."""
+    mine = caps[owned]
+    eng = engine_factory(len(owned), {k: mine[:, i] for i, k in enumerate(CAP_KEYS)})
+    if props is not None:
+        eng.upload_props(props)
+    if names is not None:
+        eng.upload_names(names)
+    loc_off = np.zeros(len(owned) + 1, np.int64)
+    loc_off[1:] = np.cumsum(ops[owned], dtype=np.int64)
+    if loc_off[-1] >= 2 ** 32:
+        raise RuntimeError("more than 2^32 ops on one rank")
+    from .engine import ExchangeError
+    t0 = time.perf_counter()
+    try:
+        eng.upload_rows_dev(np.arange(len(owned)), loc_off.astype(np.uint32), recv_ptr if loc_off[-1] else 0, L,
+                            sums[owned])
+        tm["exchange_bad_docs"] = 0
+    except ExchangeError as e:          # reported by the caller after every rank checked its share
+        tm["exchange_bad_docs"] = int(e.bad_runs.sum())
+    tm["unpack_ms"] = (time.perf_counter() - t0) * 1e3
+    tm["exchange_checked_docs"] = len(owned)
+    return eng
+
+
 def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_params_cls, gen_kw: dict,
                   props=None, names=None, chunk_docs: int = 131072, counts=None, clients=None) -> ShardedReplay:
     """Rank 0 generates every document's stream (the ingest point), every rank
@@ -233,52 +318,23 @@ def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_
     dist.broadcast(cli_t, 0)
     ops = cnt_t.cpu().numpy().astype(np.uint32)
     cli = cli_t.cpu().numpy().astype(np.uint32)
-    owner = lpt_assign(ops, world)
-    op_off = np.zeros(docs_total + 1, np.int64)
-    op_off[1:] = np.cumsum(ops, dtype=np.int64)
-    n_total = int(op_off[-1])
+    # -- the plan's send order: documents grouped by owning rank, largest first
+    plan = SharePlan(ops, world)
+    owner = plan.owner
+    W = REC_BYTES // 8 + 2 * L // 8                  # 8-byte words per exchange row (mt_shard.h)
+    per_rank_ops = plan.per_rank_ops
+    my_ops = int(per_rank_ops[rank])
     tm["plan_ms"] = (time.perf_counter() - t0) * 1e3
 
-    # -- the plan's send order: documents grouped by owning rank, largest first; each
-    #    document's rows start at row_of[doc] of rank 0's send buffer
-    order = rank_order(owner, ops)
-    row_of = np.empty(docs_total, np.int64)
-    row_of[order] = np.concatenate(([0], np.cumsum(ops[order].astype(np.int64))[:-1]))
-    W = REC_BYTES // 8 + 2 * L // 8                  # 8-byte words per exchange row (mt_shard.h)
-    per_rank_ops = np.array([int(ops[owner == r].sum()) for r in range(world)], np.int64)
-    my_ops = int(per_rank_ops[rank])
-
-    # -- rank 0: generate every stream in chunks (untimed ingest); the engine packs each
-    #    chunk's runs straight into their plan positions of the send buffer (a HIP kernel,
-    #    mt_generated_pack_rows) with a 64-bit checksum per document
-    caps_t = torch.zeros((docs_total, 6), dtype=torch.int32, device=device)
-    cs_t = torch.zeros(docs_total, dtype=torch.int64, device=device)
+    # -- rank 0: generate every stream (untimed ingest) into the send buffer
     if rank == 0:
         t0 = time.perf_counter()
-        send = torch.empty((n_total, W), dtype=torch.int64, device=device)
-        gcaps = generation_caps(ops, L)
-        for a in range(0, docs_total, chunk_docs):
-            b = min(docs_total, a + chunk_docs)
-            idx = np.arange(a, b)
-            eng = engine_factory(b - a, {k: np.asarray(v)[idx] for k, v in gcaps.items()})
-            if props is not None:
-                eng.upload_props(props)
-            if names is not None:
-                eng.upload_names(names)
-            p = gen_params_cls(**{**gen_kw, "seed": seed, "n_docs": b - a, "ops_per_doc": 0, "clients": 2,
-                                  "doc_id_base": a})
-            eng.generate(p, ops_per_doc=ops[idx], clients_per_doc=cli[idx])
-            eng.sync()
-            st = eng.status(range(b - a))
-            if st.any():
-                raise RuntimeError(f"generation failed for docs {a}..{b}: status {np.unique(st)}")
-            caps_t[a:b] = torch.from_numpy(replay_caps(eng.pools(range(b - a)), gcaps, idx)).to(device)
-            if device.type == "cuda":
-                torch.cuda.synchronize(device)
-            cs = eng.generated_pack_rows(0, b - a, row_of[a:b].astype(np.uint64), send.data_ptr())
-            cs_t[a:b] = torch.from_numpy(cs.view(np.int64)).to(device)
-            eng.close()
+        send, caps_t, cs_t = generate_send_rows(device, engine_factory, plan, cli, seed, gen_params_cls, gen_kw,
+                                                props, names, chunk_docs, W)
         tm["generate_s"] = time.perf_counter() - t0
+    else:
+        caps_t = torch.zeros((docs_total, 6), dtype=torch.int32, device=device)
+        cs_t = torch.zeros(docs_total, dtype=torch.int64, device=device)
     dist.broadcast(caps_t, 0)
     dist.broadcast(cs_t, 0)
     caps = caps_t.cpu().numpy()
@@ -289,7 +345,7 @@ def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_
         torch.cuda.synchronize(device)
     dist.barrier()
     t0 = time.perf_counter()
-    owned = order[owner[order] == rank]
+    owned = plan.owned(rank)
     if rank == 0:
         in_split = per_rank_ops.tolist()
     else:
@@ -305,27 +361,38 @@ def build_sharded(dist, device, engine_factory, docs_total: int, seed: int, gen_
     tm["rebalance_bytes"] = int(per_rank_ops.sum()) * (REC_BYTES + 2 * L)
 
     # -- this rank's engine, sized exactly; the received rows become its resident batch
-    #    (mt_upload_rows_dev: unpacked by a HIP kernel, every document's checksum compared
-    #    with rank 0's)
-    mine = caps[owned]
-    eng = engine_factory(len(owned), {k: mine[:, i] for i, k in enumerate(CAP_KEYS)})
-    if props is not None:
-        eng.upload_props(props)
-    if names is not None:
-        eng.upload_names(names)
-    loc_off = np.zeros(len(owned) + 1, np.int64)
-    loc_off[1:] = np.cumsum(ops[owned], dtype=np.int64)
-    if my_ops >= 2 ** 32:
-        raise RuntimeError("more than 2^32 ops on one rank")
-    from .engine import ExchangeError
-    t0 = time.perf_counter()
-    try:
-        eng.upload_rows_dev(np.arange(len(owned)), loc_off.astype(np.uint32), recv.data_ptr() if my_ops else 0, L,
-                            sums[owned])
-        tm["exchange_bad_docs"] = 0
-    except ExchangeError as e:          # reported by the caller after every rank checked its share
-        tm["exchange_bad_docs"] = int(e.bad_runs.sum())
-    tm["unpack_ms"] = (time.perf_counter() - t0) * 1e3
-    tm["exchange_checked_docs"] = len(owned)
+    eng = rank_engine(engine_factory, owned, ops, caps, sums, recv.data_ptr() if my_ops else 0, L, props, names, tm)
     del recv
     return ShardedReplay(eng, owned, ops, owner, tm, cli)
+
+
+def rank_shares(device, engine_factory, docs_total: int, world: int, seed: int, gen_params_cls, gen_kw: dict,
+                props=None, names=None, chunk_docs: int = 131072):
+    """Every rank's share of the N = `world` LPT plan, one after another on this one device
+    (review item: all eight shares of north_star's 1,048,576-document plan on hardware without an
+    8-GPU node).  This process plays rank 0 (generation into the send buffer) and then each rank in
+    turn: rank r's rows are the send buffer's slice for r, exactly what all_to_all_single
+    delivers to r.  Yields (r, ShardedReplay) with one engine alive at a time."""
+    import torch
+    L = int(gen_kw["ins_len_max"])
+    ops = zipf_op_counts(docs_total, seed)
+    cli = clients_per_doc(docs_total, seed)
+    plan = SharePlan(ops, world)
+    W = REC_BYTES // 8 + 2 * L // 8
+    t0 = time.perf_counter()
+    send, caps_t, cs_t = generate_send_rows(device, engine_factory, plan, cli, seed, gen_params_cls, gen_kw,
+                                            props, names, chunk_docs, W)
+    gen_s = time.perf_counter() - t0
+    caps = caps_t.cpu().numpy()
+    sums = cs_t.cpu().numpy().view(np.uint64)
+    for r in range(world):
+        tm = {"generate_s": gen_s, "rebalance_bytes": int(plan.per_rank_ops[r]) * (REC_BYTES + 2 * L)}
+        owned = plan.owned(r)
+        a, b = int(plan.rank_row0[r]), int(plan.rank_row0[r + 1])
+        recv = send[a:b]
+        eng = rank_engine(engine_factory, owned, ops, caps, sums, recv.data_ptr() if b > a else 0, L, props, names, tm)
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        sh = ShardedReplay(eng, owned, ops, plan.owner, tm, cli)
+        yield r, sh
+        eng.close()

@@ -206,7 +206,7 @@ typedef struct mt_op_rec {
 #define MT_VAL_UNSUP  (-3)
 #define MT_VAL_CFRESH (-4)
 #define MT_VAL_UNDEF  (-5)
-#define MT_VAL_CONS_BASE (-16)                    /* MT_VAL_CONS(seq) = -16 - seq, seq >= 0 */
+#define MT_VAL_CONS_BASE (-16)                    /* MT_VAL_CONS(seq) = -16 - seq, 0 <= seq <= INT32_MAX - 16 (a larger seq: MT_DS_UNSUPPORTED) */
 #define MT_VAL_CONS(seq) (MT_VAL_CONS_BASE - (seq))
 #define MT_VK_NUM   0x01u   /* number or boolean: incr gives NaN                            */
 #define MT_VK_SEQM1 0x02u   /* a (non-array) object whose "seq" member is the number -1     */
@@ -370,12 +370,29 @@ int  mt_set_residency(mt_ctx* ctx, int use_lds, int rows, int blocks, int heap);
  * the other runs; 0 (the default) turns it off.  Results are identical either way. */
 int  mt_set_size_class(mt_ctx* ctx, uint32_t big_min_ops);
 /* Partitioned size classes under block residency (mt_set_residency 2): runs of at least
- * min_ops op records replay in the block-residency kernel on `cus` CUs reserved for them, one
- * document per SIMD (their workgroups' LDS is padded so four fit a CU), concurrently with the
- * other runs on the remaining CUs (CU-masked streams, joined before the call returns its
- * event).  A long run then shares its SIMD with no other document: the step of a batch whose
- * longest documents set it shortens.  cus = 0 or min_ops = 0: off. */
+ * min_ops op records replay in the wide block-residency kernel (mt_set_size_class) on `cus` CUs
+ * reserved for them (a CU-masked stream, the CUs spread evenly over the XCDs; capture batches:
+ * the block-residency kernel, one document per SIMD), concurrently with the other runs in the
+ * block-residency kernel on the remaining CUs; joined before the call returns its event.  The
+ * longest documents then stay in LDS and no short run delays their start, which shortens the
+ * step of a batch whose longest documents set it.  cus = 0 or min_ops = 0: off.
+ * min_ops = MT_PARTITION_AUTO: chosen per resident batch by mt_plan_partition from the batch's
+ * run lengths and the device's CU count (the bench default).  Results are identical whatever
+ * the partition. */
+#define MT_PARTITION_AUTO 0xFFFFFFFFu
 int  mt_set_partition(mt_ctx* ctx, uint32_t min_ops, uint32_t cus);
+/* The partition rule (host only, no context): for runs of run_ops[i] op records on a device of
+ * n_cus CUs, the (min_ops, cus) whose estimated step is lowest, or (0, 0) for no partition,
+ * with that estimate in *est_ms (null: not wanted).  The estimate is a model of the measured
+ * kernels (DESIGN.md §3 "partition rule"): a batch's step is the larger of its throughput bound
+ * (messages x per-message time / concurrent documents, 16 per CU in the block-residency
+ * kernel, 7 in the wide one) and its latency bound (the longest run x one document's
+ * per-message time, higher for a run that outgrows the block kernel's LDS); a partition must
+ * beat no partition by 5 %. */
+int  mt_plan_partition(const uint32_t* run_ops, uint32_t n_runs, uint32_t n_cus, uint32_t* min_ops, uint32_t* cus,
+                       double* est_ms);
+/* The partition the last replay launch used (after MT_PARTITION_AUTO: the one chosen). */
+int  mt_last_partition(mt_ctx* ctx, uint32_t* min_ops, uint32_t* cus);
 /* Block residency: a batch holding a run of at least min_ops op records (default 16,384)
  * replays in the kernel that continues an outgrown document in HBM in the same wave; other
  * batches in the kernel without that second engine (no scratch), an outgrown document
@@ -489,12 +506,18 @@ int  mt_snapshot_legacy(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids,
 /* options.mergeTreeSnapshotChunkSize of each document's Client (MergeTree options,
  * MT/client.ts:82-84; SnapshotV1 reads `mergeTree.options?.mergeTreeSnapshotChunkSize ??
  * SnapshotV1.chunkSize`, MT/snapshotV1.ts:55): mt_snapshot_v1 / mt_snapshot_digests close a
- * chunk once its length reaches chunk_size[i] (getSeqLengthSegs, snapshotV1.ts:70-92).
- * 0 = the default 10,000; UINT64_MAX = Infinity (one chunk).  Lengths are integers, so a
- * positive non-integer size c acts as ceil(c); hosts reject c <= 0 and NaN, for which the
- * reference's chunk loop never ends on a non-empty document.  SnapshotLegacy's first chunk
- * stays sizeOfFirstChunk (10,000, snapshotlegacy.ts:57).  mt_docs_open resets the
- * documents it opens to the default. */
+ * chunk once its length reaches chunk_size[i] (getSeqLengthSegs, snapshotV1.ts:70-92), and
+ * mt_snapshot_legacy cuts its first ("header") chunk at it (`options?.mergeTreeSnapshotChunkSize
+ * ?? sizeOfFirstChunk`, snapshotlegacy.ts:71, :109).  The value is the option after JS
+ * ToNumber (the comparison `length < chunkSize`): 0 = the default 10,000;
+ * MT_CHUNK_INFINITY = Infinity (one chunk); MT_CHUNK_NONE = a size no length is below (0, a
+ * negative number, NaN, -Infinity: the legacy header chunk is empty and the body holds every
+ * segment; SnapshotV1's chunk loop never ends on a non-empty document, so mt_snapshot_v1 /
+ * mt_snapshot_digests fail with MT_E_INVALID there instead of hanging).  Lengths are integers,
+ * so a positive non-integer size c acts as ceil(c).  mt_docs_open resets the documents it
+ * opens to the default. */
+#define MT_CHUNK_INFINITY   0xFFFFFFFFFFFFFFFFull
+#define MT_CHUNK_NONE       0xFFFFFFFFFFFFFFFEull
 int  mt_set_doc_snapshot_chunk(mt_ctx* ctx, uint32_t n, const uint32_t* doc_ids, const uint64_t* chunk_size);
 /* Digests only (same values as mt_snapshot_v1's), for many documents: one staged
  * download, serialization spread over `threads` host threads. */

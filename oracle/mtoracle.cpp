@@ -1203,7 +1203,7 @@ struct Doc {
     std::vector<int> shortToStream;          // short id -> stream client index (-1 observer)
     std::vector<int> streamToShort;
     int opCounter = 0;                       // op members applied (mt_op_batch indexing of the message stream)
-    double chunkSize = 10000;                // options.mergeTreeSnapshotChunkSize ?? SnapshotV1.chunkSize (snapshotV1.ts:55)
+    double chunkSize = 10000;                // options.mergeTreeSnapshotChunkSize ?? 10,000 (snapshotV1.ts:55, snapshotlegacy.ts:71)
     std::vector<JVal> messagesSinceMSNChange;   // SharedSegmentSequence's legacy stash (sequence.ts:604-658)
     // RegisterCollection (MT/mergeTree.ts:864-896), keyed by (short client id, name): the
     // short id stands for the long id the reference keys by (one-to-one per document).
@@ -1337,6 +1337,9 @@ static std::vector<std::string> snapshot_v1(Doc& d, int msn, int seq) {
     do {
         Chunk c{totalCount, 0, 0};
         while (c.length < d.chunkSize && c.start + c.count < (int)segJson.size()) { c.length += segLen[c.start + c.count]; c.count++; }
+        // a size no length is below (NaN, <= 0): the reference's do/while never ends on a
+        // non-empty document; the restatement reports it (no blobs) instead of hanging
+        if (c.count == 0 && totalCount < (int)segJson.size()) return {};
         chunks.push_back(c); totalCount += c.count; totalLen += c.length;
     } while (totalCount < (int)segJson.size());
     auto chunkStr = [&](const Chunk& c, bool header) {
@@ -1397,7 +1400,7 @@ static std::vector<std::string> snapshot_legacy(Doc& d, int msn, int seq) {
     pushPrev();
     int total = 0; for (auto& o : segs) total += o.len;                                           // :216-237 (mismatch -> totalLength)
     struct Chunk { int start, count, length; };
-    auto take = [&](int approx, int start) {                                                      // getSeqLengthSegs (:74-98)
+    auto take = [&](double approx, int start) {                                                   // getSeqLengthSegs (:74-98)
         Chunk c{start, 0, 0};
         while (c.length < approx && c.start + c.count < (int)segs.size()) { c.length += segs[c.start + c.count].len; c.count++; }
         return c;
@@ -1423,7 +1426,7 @@ static std::vector<std::string> snapshot_legacy(Doc& d, int msn, int seq) {
         return o;
     };
     std::vector<std::string> blobs;
-    Chunk c1 = take(10000, 0);                                                                    // SnapshotLegacy.sizeOfFirstChunk (:57)
+    Chunk c1 = take(d.chunkSize, 0);                                    // options?.mergeTreeSnapshotChunkSize ?? sizeOfFirstChunk (:71, :109)
     blobs.push_back(chunkStr(c1, true));
     if (c1.count < (int)segs.size()) blobs.push_back(chunkStr(take(total, c1.count), false));    // :132-152
     return blobs;
@@ -2018,7 +2021,9 @@ const char* ora_client_name(ora_doc* o, int32_t short_id) {
 }
 static uint8_t* pack_blobs(const std::vector<std::string>& blobs, uint64_t* digest, uint64_t* total);
 uint8_t* ora_snapshot_v1(ora_doc* o, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total) {
-    return pack_blobs(snapshot_v1(o->d, msn, seq), digest, total);
+    std::vector<std::string> blobs = snapshot_v1(o->d, msn, seq);
+    if (blobs.empty()) return nullptr;                                  // the reference's chunk loop never ends
+    return pack_blobs(blobs, digest, total);
 }
 uint8_t* ora_snapshot_legacy(ora_doc* o, int32_t msn, int32_t seq, uint64_t* digest, uint64_t* total) {
     return pack_blobs(snapshot_legacy(o->d, msn, seq), digest, total);

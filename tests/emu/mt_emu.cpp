@@ -59,7 +59,10 @@ static void replay_runs(mt_ctx* c, uint32_t n_runs) {
 }
 // Same two launches as the device (mt_engine.hip): LDS-resident pass, then the
 // HBM pass resuming at each run's cursor.
+static void mt_auto_partition(mt_ctx* c);
+static uint32_t mtb_cu_count(mt_ctx*) { return 256; }                // an MI355X's CUs
 static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
+    if (!g.enabled) mt_auto_partition(c);
     if (g.enabled) {
         for (uint32_t run = 0; run < n_runs; run++) {
             MtScratch sc; int lastRef[64];

@@ -55,7 +55,10 @@ if (spec.queries) {
         return r;
     });
 }
-const snaps = eng.snapshot(clients.map((c) => c.docId), clients.map((c) => c.minSeq), clients.map((c) => c.getCurrentSeq()));
+// digests of the Clients' own format (SnapshotLegacy without newMergeTreeSnapshotFormat)
+const legacyFormat = (spec.options || { newMergeTreeSnapshotFormat: true }).newMergeTreeSnapshotFormat !== true;
+const snaps = eng.snapshot(clients.map((c) => c.docId), clients.map((c) => c.minSeq), clients.map((c) => c.getCurrentSeq()),
+    legacyFormat);
 out.digests = snaps.map((s) => s.digest.toString(16));
 fs.writeFileSync(outPath, JSON.stringify(out));
 eng.close();

@@ -231,6 +231,8 @@ class OracleDoc:
         dig, tot = ctypes.c_uint64(), ctypes.c_uint64()
         fn = self.L.ora_snapshot_legacy if legacy else self.L.ora_snapshot_v1
         buf = fn(self.h, msn, seq, ctypes.byref(dig), ctypes.byref(tot))
+        if not buf:
+            raise RuntimeError("oracle: SnapshotV1's chunk loop never ends (chunk size no length is below)")
         blobs = parse_blobs(buf, tot.value)
         self.L.ora_free_buf(buf)
         return blobs, dig.value

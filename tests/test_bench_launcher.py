@@ -56,3 +56,16 @@ def test_single_rank_digest_parity_against_oracle():
     assert out["parity"].startswith("SnapshotV1 digests == oracle on"), out["parity"]
     assert out["cpu_baseline"]["kind"] == "port"
     assert out["roofline"]["bytes_pinned"].startswith("mt_doc_counters == oracle"), out["roofline"]
+
+
+def test_config5_rank_shares_equal_one_rank_replay():
+    """--shares 4: the four ranks' LPT shares of 20 documents replayed in turn give every
+    document the SnapshotV1 digest a one-rank replay of all 20 gives (each share's rows are the
+    send buffer's slice all_to_all_single would deliver)."""
+    sh = run("--config", "config5", "--docs", "5", "--shares", "4", "--steps", "1", "--warmup", "0", "--no-cpu-baseline")
+    one = run("--config", "config5", "--docs", "20", "--steps", "1", "--warmup", "0", "--no-cpu-baseline")
+    assert len(sh["shares"]) == 4 and sum(x["docs"] for x in sh["shares"]) == 20
+    assert all(x["status_clean"] for x in sh["shares"])
+    assert sh["config"]["msgs_total"] == one["config"]["msgs_total"]
+    assert sh["digest_xor"] == one["sharding"]["digest_xor"]
+    assert sh["ms_per_step"] == max(x["ms_per_step"] for x in sh["shares"])
