@@ -841,7 +841,7 @@ def write_doc_bins(batch, td):
             f.write(np.ascontiguousarray(pay[p0:p1], np.uint16).tobytes())
 
 
-def ingest_scale_leg(eng, params, c, dig_xor, windows=8):
+def ingest_scale_leg(eng, params, c, dig_xor, windows=8, objects=False):
     """Node host ingest at the workload's full size (every document of the config): message JSON
     parsed and packed on a worker pool, then end to end through the addon with packing of message
     window k+1 (of every document) overlapped with the upload and replay of window k
@@ -864,17 +864,25 @@ def ingest_scale_leg(eng, params, c, dig_xor, windows=8):
         write_s = time.perf_counter() - t0
         del batch
         cmd = [exe, "--max-old-space-size=8192", os.path.join(ROOT, "fluidframework_amd", "js", "ingest_scale.js"), td,
-               str(workers), str(windows), "--gpu"]
+               str(workers), str(windows), "--gpu"] + (["--objects"] if objects else [])
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
     if r.returncode != 0:
         return {"error": r.stderr[-800:]}
     res = json.loads(r.stdout.strip().splitlines()[-1])
     res["digests_equal_bench"] = res.get("digest_xor") == f"{dig_xor:016x}"
     res["input_write_s"] = write_s
-    res["note"] = (f"all {c['docs']} documents: per-document message JSON in {windows} message windows made "
-                   "inside the workers (untimed); pack_ms = parse + pack of every window on the pool (the host "
-                   "bound); e2e_ms = parse/pack of window k+1 of every document overlapped with mt_apply_batch "
-                   "upload + replay of window k, one sync, SnapshotV1 of every document")
+    if objects:
+        res["note"] = (f"all {c['docs']} documents: per-document ISequencedDocumentMessage objects (already parsed, "
+                       f"as SharedSegmentSequence.processCore receives them) in {windows} message windows made inside "
+                       "the workers (untimed); pack_ms = BatchBuilder.addMessages of every window on the pool, parts "
+                       "left unmerged; e2e_ms = pack of window k+1 of every document overlapped with "
+                       "mt_apply_batch_parts (the parts concatenated and re-based on the library's host threads) "
+                       "upload + replay of window k, one sync, SnapshotV1 of every document")
+    else:
+        res["note"] = (f"all {c['docs']} documents: per-document message JSON in {windows} message windows made "
+                       "inside the workers (untimed); pack_ms = parse + pack of every window on the pool (the host "
+                       "bound); e2e_ms = parse/pack of window k+1 of every document overlapped with mt_apply_batch "
+                       "upload + replay of window k, one sync, SnapshotV1 of every document")
     return res
 
 
@@ -1121,6 +1129,7 @@ def _main(argv=None):
         out["ingest"] = ingest_leg(local, c, seed)
         if args.config == "config2" and ok:
             out["ingest"]["node_full_scale"] = ingest_scale_leg(eng, params, c, dig_xor)
+            out["ingest"]["node_objects_full_scale"] = ingest_scale_leg(eng, params, c, dig_xor, objects=True)
     print(json.dumps(out), flush=True)
 
 

@@ -427,6 +427,115 @@ int MT_FN(upload_batch)(mt_ctx* c, const mt_op_batch* B) {
     if (rc) return rc;
     return mt_upload_ops(c, B);                           // stream-ordered: no synchronization
 }
+// Parts concatenated into the staging layout of mt_upload_ops, re-based while packed (one pass
+// over every op on the library's host threads; validation as mt_check_batch, on the re-based
+// values).
+static int mt_upload_parts(mt_ctx* c, uint32_t P, const mt_op_batch* parts, const int32_t* const* pmap,
+                           const uint32_t* pmapLen) {
+    std::vector<uint64_t> opB(P + 1, 0), payB(P + 1, 0), relB(P + 1, 0), runB(P + 1, 0);
+    for (uint32_t p = 0; p < P; p++) {
+        const mt_op_batch* B = &parts[p];
+        if (!B->op_offsets || (B->n_runs && !B->doc_ids) || B->op_offsets[B->n_runs] != B->n_ops ||
+            (B->n_rel && !B->rel) || (B->payload_units && !B->payload)) { c->err = "bad batch part"; return MT_E_INVALID; }
+        for (uint32_t r = 0; r < B->n_runs; r++) {
+            if (B->doc_ids[r] >= c->S.maxDocs) { c->err = "doc id out of range"; return MT_E_INVALID; }
+            if (B->op_offsets[r] > B->op_offsets[r + 1]) { c->err = "op_offsets not monotone"; return MT_E_INVALID; }
+        }
+        opB[p + 1] = opB[p] + B->n_ops; payB[p + 1] = payB[p] + B->payload_units;
+        relB[p + 1] = relB[p] + (B->rel ? B->n_rel : 0); runB[p + 1] = runB[p] + B->n_runs;
+    }
+    const size_t N = opB[P], R = runB[P], PU = payB[P], NR = relB[P];
+    if (N >= (1ull << 32) || R >= (1ull << 32) || PU >= (1ull << 32)) { c->err = "batch parts exceed 32-bit indices"; return MT_E_INVALID; }
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_doc = 0, o_off = al(o_doc + 4 * R), o_rec = al(o_off + 4 * (R + 1)),
+                 o_pay = al(o_rec + sizeof(MtOpRec) * N), o_rel = al(o_pay + 2 * PU),
+                 total = al(o_rel + sizeof(MtRelPos) * NR) + 256;
+    int rc;
+    if ((rc = mtb_ensure(c, c->b_batch, total))) return rc;
+    uint8_t* h = (uint8_t*)mtb_stage_get(c, total);
+    if (!h) { c->err = "pinned staging allocation failed"; return MT_E_OOM; }
+    uint32_t* docs = (uint32_t*)(h + o_doc);
+    uint32_t* off = (uint32_t*)(h + o_off);
+    std::vector<uint32_t> runOff(R + 1);
+    off[0] = 0; runOff[0] = 0;
+    for (uint32_t p = 0; p < P; p++) {
+        const mt_op_batch* B = &parts[p];
+        for (uint32_t r = 0; r < B->n_runs; r++) {
+            docs[runB[p] + r] = B->doc_ids[r];
+            off[runB[p] + r + 1] = runOff[runB[p] + r + 1] = (uint32_t)(opB[p] + B->op_offsets[r + 1]);
+        }
+        if (B->rel && B->n_rel) memcpy(h + o_rel + sizeof(MtRelPos) * relB[p], B->rel, sizeof(MtRelPos) * B->n_rel);
+    }
+    MtOpRec* rec = (MtOpRec*)(h + o_rec);
+    const uint32_t nsets = c->S.p_nsets;
+    const char* errT[16] = {nullptr};
+    size_t errI[16];
+    uint8_t regT[16] = {0};
+    mt_par_for(N, [&](size_t i0, size_t i1, unsigned t) {
+        bool reg = false;
+        uint32_t p = (uint32_t)(std::upper_bound(opB.begin(), opB.end(), (uint64_t)i0) - opB.begin()) - 1;
+        for (size_t i = i0; i < i1; i++) {
+            while (i >= opB[p + 1]) p++;
+            const mt_op_batch* B = &parts[p];
+            const size_t j = i - opB[p];
+            MtOpRec& o = rec[i];
+            const uint8_t ty = B->type[j], fl = B->flags[j];
+            int32_t pid = B->prop_id[j];
+            const char* e = nullptr;
+            if (pid >= 0 && pmap && pmap[p]) {
+                if ((uint32_t)pid >= pmapLen[p]) e = "prop_id out of its part's map";
+                else pid = pmap[p][pid];
+            }
+            const bool text = ty == MT_OP_INSERT && !(fl & MT_OPF_MARKER);
+            if (ty > MT_OP_PASTE) e = "unknown op type";
+            else if (text && (uint64_t)B->payload_off[j] + B->payload_len[j] > B->payload_units) e = "payload out of range";
+            else if (pid >= 0 && (uint32_t)pid >= nsets) e = "prop_id out of range (mt_set_props first)";
+            else if (pid > 32767) e = "more than 32767 property sets";
+            else if (B->payload_len[j] > 65535) e = "insert longer than 65535 UTF-16 units";
+            else if (((fl & MT_OPF_REL1) && (uint32_t)B->pos1[j] >= B->n_rel) ||
+                     ((fl & MT_OPF_REL2) && (uint32_t)B->pos2[j] >= B->n_rel)) e = "relative position index out of range";
+            if (e && !errT[t]) { errT[t] = e; errI[t] = i; }
+            o.type = ty; o.flags = fl; o.client = B->client[j]; o.seq = B->seq[j]; o.ref_seq = B->ref_seq[j]; o.msn = B->msn[j];
+            o.pos1 = B->pos1[j] + ((fl & MT_OPF_REL1) ? (int32_t)relB[p] : 0);
+            o.pos2 = B->pos2[j] + ((fl & MT_OPF_REL2) ? (int32_t)relB[p] : 0);
+            o.payload_off = B->payload_off[j] + (text ? (uint32_t)payB[p] : 0u);
+            o.payload_len = (uint16_t)B->payload_len[j]; o.prop_id = (int16_t)pid;
+            reg |= ty >= MT_OP_CUT && ty <= MT_OP_PASTE;
+        }
+        regT[t] = reg;
+    });
+    const char* e = nullptr; size_t ei = 0;
+    for (int t = 0; t < 16; t++) if (errT[t] && (!e || errI[t] < ei)) { e = errT[t]; ei = errI[t]; }
+    if (e) { c->err = e; return MT_E_INVALID; }
+    mt_par_for(P, [&](size_t p0, size_t p1, unsigned) {           // payloads, part by part
+        for (size_t p = p0; p < p1; p++)
+            if (parts[p].payload_units) memcpy(h + o_pay + 2 * payB[p], parts[p].payload, 2 * parts[p].payload_units);
+    });
+    bool reg = false;
+    for (int t = 0; t < 16; t++) reg |= regT[t] != 0;
+    mtb_stage_send(c, c->b_batch.p, total);
+    uint8_t* d = (uint8_t*)c->b_batch.p;
+    MtOps& o = c->ops;
+    o.doc_ids = (const uint32_t*)(d + o_doc); o.op_off = (const uint32_t*)(d + o_off); o.rec = (MtOpRec*)(d + o_rec);
+    o.payload = (uint16_t*)(d + o_pay); o.n_runs = (uint32_t)R; o.payload_units = PU; o.pay_base = nullptr;
+    o.rel = (const MtRelPos*)(d + o_rel); o.n_rel = (uint32_t)NR;
+    c->n_runs = (uint32_t)R;
+    c->run_off.swap(runOff); c->batch_gen++;
+    c->batch_reg = reg;
+    return MT_OK;
+}
+int MT_FN(upload_batch_parts)(mt_ctx* c, uint32_t n_parts, const mt_op_batch* parts, const int32_t* const* prop_map,
+                              const uint32_t* prop_map_len) {
+    if (!c || (n_parts && !parts) || (prop_map && !prop_map_len)) return MT_E_INVALID;
+    return mt_upload_parts(c, n_parts, parts, prop_map, prop_map_len);
+}
+int MT_FN(replay_resident)(mt_ctx* c);
+int MT_FN(apply_batch_parts)(mt_ctx* c, uint32_t n_parts, const mt_op_batch* parts, const int32_t* const* prop_map,
+                             const uint32_t* prop_map_len) {
+    int rc = MT_FN(upload_batch_parts)(c, n_parts, parts, prop_map, prop_map_len);
+    if (rc) return rc;
+    return MT_FN(replay_resident)(c);
+}
 // A capture batch (mt_delta_capture armed): each launch appends records until a document
 // has no headroom left for its next message (MtEngT::dReserve); that run stops there, the
 // records and pasted text so far move to the host, and the next launch resumes the stopped

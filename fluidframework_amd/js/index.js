@@ -212,6 +212,11 @@ class Engine {
         }
         addon.applyBatch(this.h, batch);
     }
+    /** Several packed parts applied as one batch (mt_apply_batch_parts; ParallelPacker.packHeldParts). */
+    applyParts(parts, propMaps) {
+        this.uploadProps();
+        addon.applyBatchParts(this.h, parts, propMaps);
+    }
     uploadProps() {
         if (this.uploadedSets !== this.props.sets.length) {
             addon.setProps(this.h, this.props.toNative());

@@ -10,7 +10,11 @@
 //             every document is parsed and packed on the workers while the GPU uploads
 //             (mt_apply_batch: pinned staging, async H2D) and replays window k of every document;
 //             then one sync and SnapshotV1 of every document
-// Prints one JSON line.  usage: node ingest_scale.js DIR WORKERS WINDOWS [--gpu]
+// With --objects every worker holds its documents' messages as parsed objects (what DeltaManager
+// hands SharedSegmentSequence.processCore; made untimed), packs them with BatchBuilder.addMessages
+// and the parts go to the addon as they are (mt_apply_batch_parts concatenates them on the
+// library's host threads): pack_ms is objects -> packed parts, e2e_ms objects -> digests.
+// Prints one JSON line.  usage: node ingest_scale.js DIR WORKERS WINDOWS [--gpu] [--objects]
 const fs = require("fs");
 const path = require("path");
 const { PropTable } = require(path.join(__dirname, "builder.js"));
@@ -19,7 +23,7 @@ const { ParallelPacker } = require(path.join(__dirname, "parallel.js"));
 async function main() {
     const dir = process.argv[2];
     const W = Number(process.argv[3] || 16), K = Number(process.argv[4] || 8);
-    const gpu = process.argv.includes("--gpu");
+    const gpu = process.argv.includes("--gpu"), objects = process.argv.includes("--objects");
     const n = fs.readdirSync(dir).filter((f) => /^doc[0-9]+\.bin$/.test(f)).length;
     const docs = [];
     for (let id = 0; id < n; id++) docs.push({ id, bin: path.join(dir, `doc${id}.bin`) });
@@ -27,17 +31,25 @@ async function main() {
     const now = () => Number(process.hrtime.bigint()) / 1e6;
     const pool = new ParallelPacker(W);
     let t0 = now();
-    const jsonBytes = await pool.prepare(docs, K);
-    const out = { docs: n, workers: W, windows: K, json_bytes: jsonBytes, prepare_ms: now() - t0 };
-    await pool.packHeld(ids.slice(0, Math.min(n, 4 * W)), new PropTable(), 0);       // JIT warm-up, untimed
+    const jsonBytes = await pool.prepare(docs, K, objects);
+    const out = { docs: n, workers: W, windows: K, input: objects ? "objects" : "json", json_bytes: objects ? null : jsonBytes,
+        prepare_ms: now() - t0 };
+    // one window's parts of a pack (objects: unmerged parts; JSON: one merged batch)
+    const packWin = async (props, k) => {
+        if (!objects) { const r = await pool.packHeld(ids, props, k); return { parts: [r.batch], propMaps: [null], names: r.names }; }
+        return pool.packHeldParts(ids, props, k);
+    };
+    await packWin(new PropTable(), 0);                                               // JIT warm-up, untimed
     await pool.resetNames();
     let msgs = 0, maxOps = 0;
     const opsOf = new Uint32Array(n);
     t0 = now();
     for (let k = 0; k < K; k++) {
-        const { batch } = await pool.packHeld(ids, new PropTable(), k);
-        msgs += batch.type.length;
-        for (let r = 0; r < batch.docIds.length; r++) opsOf[batch.docIds[r]] += batch.opOffsets[r + 1] - batch.opOffsets[r];
+        const { parts } = await packWin(new PropTable(), k);
+        for (const batch of parts) {
+            msgs += batch.type.length;
+            for (let r = 0; r < batch.docIds.length; r++) opsOf[batch.docIds[r]] += batch.opOffsets[r + 1] - batch.opOffsets[r];
+        }
     }
     out.pack_ms = now() - t0;
     out.msgs = msgs;
@@ -55,18 +67,22 @@ async function main() {
             let applyMs = 0, packMs = 0;
             for (let k = 0; k < K; k++) {
                 const tp = now();
-                const { batch, names } = await pool.packHeld(ids, eng.props, k);   // overlaps the replay of window k-1
+                const { parts, propMaps, names } = await packWin(eng.props, k);   // overlaps the replay of window k-1
                 packMs += now() - tp;
-                for (let r = 0; r < batch.docIds.length; r++) {
-                    const d = batch.docIds[r];
-                    mt.addon.setDocClientNames(eng.h, d, names[r].map((x) => JSON.stringify(x)));
-                    if (batch.opOffsets[r + 1] > batch.opOffsets[r]) {
-                        const last = batch.opOffsets[r + 1] - 1;
-                        msn[d] = batch.msn[last]; seq[d] = batch.seq[last];
+                let q = 0;
+                for (const batch of parts) {
+                    for (let r = 0; r < batch.docIds.length; r++, q++) {
+                        const d = batch.docIds[r];
+                        mt.addon.setDocClientNames(eng.h, d, names[q].map((x) => JSON.stringify(x)));
+                        if (batch.opOffsets[r + 1] > batch.opOffsets[r]) {
+                            const last = batch.opOffsets[r + 1] - 1;
+                            msn[d] = batch.msn[last]; seq[d] = batch.seq[last];
+                        }
                     }
                 }
                 const ta = now();
-                eng.apply(batch);                 // staged + enqueued: the replay runs while the next window packs
+                // staged + enqueued: the replay runs while the next window packs
+                if (objects) eng.applyParts(parts, propMaps); else eng.apply(parts[0]);
                 applyMs += now() - ta;
             }
             const ts = now();

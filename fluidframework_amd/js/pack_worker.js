@@ -10,7 +10,7 @@ const { BatchBuilder, ClientNames, PropTable } = require("./builder.js");
 // text a summarizer would receive, made inside the worker that will parse it; untimed).
 // File layout (little-endian int32): nOps, nPayload, then type, client, seq, refSeq, msn, pos1,
 // pos2, payloadOff, payloadLen columns of nOps each, then nPayload UTF-16 units.
-function binToJson(file, windows) {
+function binToJson(file, windows, objects = false) {
     const buf = fs.readFileSync(file);
     const i32 = new Int32Array(buf.buffer, buf.byteOffset, buf.length >> 2);
     const n = i32[0], np = i32[1];
@@ -29,24 +29,27 @@ function binToJson(file, windows) {
         out[i] = m;
     }
     // `windows` consecutive message windows of equal counts, one JSON text each (a stream
-    // arriving over time)
+    // arriving over time), or (objects) the message objects themselves, as DeltaManager hands
+    // them to SharedSegmentSequence.processCore already parsed
     const texts = [];
-    for (let k = 0; k < windows; k++)
-        texts.push(JSON.stringify(out.slice(Math.floor((k * n) / windows), Math.floor(((k + 1) * n) / windows))));
+    for (let k = 0; k < windows; k++) {
+        const w = out.slice(Math.floor((k * n) / windows), Math.floor(((k + 1) * n) / windows));
+        texts.push(objects ? w : JSON.stringify(w));
+    }
     return texts;
 }
 const held = new Map();            // doc id -> its stream's window JSON texts (ParallelPacker.prepare)
 const heldNames = new Map();       // doc id -> its ClientNames, kept across windows
 
-parentPort.on("message", ({ docs, prepare, windows, resetNames }) => {
+parentPort.on("message", ({ docs, prepare, windows, objects, resetNames }) => {
     if (resetNames) { heldNames.clear(); parentPort.postMessage({ reset: true }); return; }
     if (prepare) {
         try {
             let bytes = 0;
             for (const d of prepare) {
-                const t = binToJson(d.bin, windows || 1);
+                const t = binToJson(d.bin, windows || 1, !!objects);
                 held.set(d.id, t);
-                for (const x of t) bytes += x.length;
+                for (const x of t) bytes += objects ? 0 : x.length;
             }
             parentPort.postMessage({ prepared: prepare.length, bytes });
         } catch (e) {
@@ -66,7 +69,7 @@ parentPort.on("message", ({ docs, prepare, windows, resetNames }) => {
             // a document's stream: its JSON text, or a file the worker reads itself (a worker
             // that owns its documents' streams: nothing is cloned through the main thread)
             const text = d.held ? held.get(d.id)[d.win || 0] : d.json !== undefined ? d.json : fs.readFileSync(d.file, "utf8");
-            for (const m of JSON.parse(text)) bb.addMessage(m);
+            bb.addMessages(typeof text === "string" ? JSON.parse(text) : text);
             names.push(nm.names.slice());
         }
         const nPayload = bb.payload.n;

@@ -37,7 +37,7 @@ class ParallelPacker {
      * on the workers that hold them; each document's client-name table carries over from window
      * to window (resetNames() starts them again).
      */
-    async prepare(docs, windows = 1) {
+    async prepare(docs, windows = 1, objects = false) {
         const W = this.workers.length;
         this.owner = new Map();
         const per = Math.ceil(docs.length / W);
@@ -46,7 +46,7 @@ class ParallelPacker {
             const sl = docs.slice(w * per, (w + 1) * per);
             if (!sl.length) continue;
             for (const d of sl) this.owner.set(d.id, w);
-            jobs.push(this.post(w, { prepare: sl, windows }));
+            jobs.push(this.post(w, { prepare: sl, windows, objects }));
         }
         const r = await Promise.all(jobs);
         for (const m of r) if (m.error) throw new Error(m.error);
@@ -61,6 +61,24 @@ class ParallelPacker {
         const out = merge(parts, props);
         this.lastMergeMs = Number(process.hrtime.bigint() - t0) / 1e6;
         return out;
+    }
+    /**
+     * packHeld without the merge: { parts, propMaps, names } for Engine.applyParts
+     * (mt_apply_batch_parts re-bases and concatenates the parts on the library's host threads).
+     * Each worker's property sets join `props`; propMaps[p] maps part p's set ids to the table's
+     * (null when the part interned none).
+     */
+    async packHeldParts(ids, props, win = 0) {
+        const by = this.workers.map(() => []);
+        for (const id of ids) by[this.owner.get(id)].push({ id, held: true, win });
+        const parts = await Promise.all(by.map((l, w) => l.length ? this.post(w, { docs: l }) : null).filter((x) => x));
+        const names = [], propMaps = [];
+        for (const p of parts) {
+            if (p.error) throw new Error(p.error);
+            propMaps.push(p.props.sets.length ? absorb(p.props, props) : null);
+            for (const nm of p.names) names.push(nm);
+        }
+        return { parts: parts.map((p) => p.batch), propMaps, names };
     }
     post(w, msg) {
         const wk = this.workers[w];
@@ -99,6 +117,13 @@ class ParallelPacker {
     }
 }
 
+// A worker's interned property sets as set ids of the engine's table: keys and values re-interned,
+// the non-value codes of combine sets (MT_VAL_*, negative) kept as they are.
+function absorb(wp, props) {
+    return Int32Array.from(wp.sets.map((pairs) => props.internPairs(pairs.map(([k, v]) =>
+        [props.keyId(wp.keys[k]), v < 0 ? v : props.valueId(JSON.parse(wp.valueJson[v]))]))));
+}
+
 function merge(parts, props) {
     let nOps = 0, nPay = 0, nRel = 0, nRuns = 0;
     for (const p of parts) {
@@ -121,8 +146,7 @@ function merge(parts, props) {
         out.docIds.set(b.docIds, run);
         for (let r = 0; r < b.docIds.length; r++) out.opOffsets[run + r + 1] = o + b.opOffsets[r + 1];
         // the worker's property sets join the engine's table; its indices are re-based
-        const map = p.props.sets.map((pairs) => props.intern(Object.fromEntries(pairs.map(([k, v]) =>
-            [p.props.keys[k], v < 0 ? null : JSON.parse(p.props.valueJson[v])]))));
+        const map = absorb(p.props, props);
         const ty = out.type, fl = out.flags, pid = out.propId, poff = out.payloadOff, p1 = out.pos1, p2 = out.pos2;
         for (let i = o; i < o + n; i++) {
             if (pid[i] >= 0) pid[i] = map[pid[i]];
@@ -136,4 +160,4 @@ function merge(parts, props) {
     return { batch: out, names };
 }
 
-module.exports = { ParallelPacker, merge };
+module.exports = { ParallelPacker, merge, absorb };

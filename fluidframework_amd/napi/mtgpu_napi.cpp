@@ -267,46 +267,85 @@ napi_value ReserveStaging(napi_env env, napi_callback_info info) {
     return rc ? throw_rc(env, c, rc, "mt_reserve_staging") : undefined(env);
 }
 
+// A JS batch object (BatchBuilder.build / ParallelPacker parts) as an mt_op_batch over its
+// typed arrays' memory; false with a pending JS exception on a malformed batch.
+bool read_batch(napi_env env, napi_value obj, mt_op_batch& B) {
+    B = mt_op_batch{};
+    size_t nd, no, n[11], np;
+    if (!field(env, obj, "docIds", napi_uint32_array, &B.doc_ids, &nd) ||
+        !field(env, obj, "opOffsets", napi_uint32_array, &B.op_offsets, &no) ||
+        !field(env, obj, "type", napi_uint8_array, &B.type, &n[0]) ||
+        !field(env, obj, "flags", napi_uint8_array, &B.flags, &n[1]) ||
+        !field(env, obj, "client", napi_uint16_array, &B.client, &n[2]) ||
+        !field(env, obj, "seq", napi_int32_array, &B.seq, &n[3]) ||
+        !field(env, obj, "refSeq", napi_int32_array, &B.ref_seq, &n[4]) ||
+        !field(env, obj, "msn", napi_int32_array, &B.msn, &n[5]) ||
+        !field(env, obj, "pos1", napi_int32_array, &B.pos1, &n[6]) ||
+        !field(env, obj, "pos2", napi_int32_array, &B.pos2, &n[7]) ||
+        !field(env, obj, "payloadOff", napi_uint32_array, &B.payload_off, &n[8]) ||
+        !field(env, obj, "payloadLen", napi_uint32_array, &B.payload_len, &n[9]) ||
+        !field(env, obj, "propId", napi_int32_array, &B.prop_id, &n[10]) ||
+        !field(env, obj, "payload", napi_uint16_array, &B.payload, &np))
+        return false;
+    if (no != nd + 1) { napi_throw_range_error(env, nullptr, "opOffsets must have docIds.length + 1 entries"); return false; }
+    B.n_runs = (uint32_t)nd;
+    B.n_ops = B.op_offsets[nd];
+    for (int i = 0; i < 11; i++)
+        if (n[i] < B.n_ops) { napi_throw_range_error(env, nullptr, "an op array is shorter than opOffsets[n]"); return false; }
+    B.payload_units = np;
+    {   // optional rel: Int32Array of (marker, before, offset, pad) quads (mt_rel_pos)
+        bool has = false;
+        napi_has_named_property(env, obj, "rel", &has);
+        if (has) {
+            const int32_t* rel = nullptr; size_t nr = 0;
+            if (!field(env, obj, "rel", napi_int32_array, &rel, &nr)) return false;
+            B.n_rel = (uint32_t)(nr / 4); B.rel = (const mt_rel_pos*)rel;
+        }
+    }
+    return true;
+}
+
 // applyBatch(ctx, batch): copies the batch to HBM and enqueues the replay
 // (Client.applyMsg for every message of every document run).
 napi_value ApplyBatch(napi_env env, napi_callback_info info) {
     napi_value argv[2];
     if (!get_args(env, info, 2, argv)) return nullptr;
     mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
-    mt_op_batch B{};
-    size_t nd, no, n[11], np;
-    if (!field(env, argv[1], "docIds", napi_uint32_array, &B.doc_ids, &nd) ||
-        !field(env, argv[1], "opOffsets", napi_uint32_array, &B.op_offsets, &no) ||
-        !field(env, argv[1], "type", napi_uint8_array, &B.type, &n[0]) ||
-        !field(env, argv[1], "flags", napi_uint8_array, &B.flags, &n[1]) ||
-        !field(env, argv[1], "client", napi_uint16_array, &B.client, &n[2]) ||
-        !field(env, argv[1], "seq", napi_int32_array, &B.seq, &n[3]) ||
-        !field(env, argv[1], "refSeq", napi_int32_array, &B.ref_seq, &n[4]) ||
-        !field(env, argv[1], "msn", napi_int32_array, &B.msn, &n[5]) ||
-        !field(env, argv[1], "pos1", napi_int32_array, &B.pos1, &n[6]) ||
-        !field(env, argv[1], "pos2", napi_int32_array, &B.pos2, &n[7]) ||
-        !field(env, argv[1], "payloadOff", napi_uint32_array, &B.payload_off, &n[8]) ||
-        !field(env, argv[1], "payloadLen", napi_uint32_array, &B.payload_len, &n[9]) ||
-        !field(env, argv[1], "propId", napi_int32_array, &B.prop_id, &n[10]) ||
-        !field(env, argv[1], "payload", napi_uint16_array, &B.payload, &np))
-        return nullptr;
-    if (no != nd + 1) { napi_throw_range_error(env, nullptr, "opOffsets must have docIds.length + 1 entries"); return nullptr; }
-    B.n_runs = (uint32_t)nd;
-    B.n_ops = B.op_offsets[nd];
-    for (int i = 0; i < 11; i++)
-        if (n[i] < B.n_ops) { napi_throw_range_error(env, nullptr, "an op array is shorter than opOffsets[n]"); return nullptr; }
-    B.payload_units = np;
-    {   // optional rel: Int32Array of (marker, before, offset, pad) quads (mt_rel_pos)
-        bool has = false;
-        napi_has_named_property(env, argv[1], "rel", &has);
-        if (has) {
-            const int32_t* rel = nullptr; size_t nr = 0;
-            if (!field(env, argv[1], "rel", napi_int32_array, &rel, &nr)) return nullptr;
-            B.n_rel = (uint32_t)(nr / 4); B.rel = (const mt_rel_pos*)rel;
-        }
-    }
+    mt_op_batch B;
+    if (!read_batch(env, argv[1], B)) return nullptr;
     int rc = mt_apply_batch(c, &B);     // copies host arrays before returning
     return rc ? throw_rc(env, c, rc, "mt_apply_batch") : undefined(env);
+}
+
+// applyBatchParts(ctx, parts: batch[], propMaps: (Int32Array | null)[]): mt_apply_batch_parts,
+// the parts of several packing threads applied as one batch without a JS-side merge
+// (propMaps[p]: part p's property-set ids -> the engine table's).
+napi_value ApplyBatchParts(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return nullptr;
+    mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
+    bool isArr = false, isArr2 = false;
+    napi_is_array(env, argv[1], &isArr); napi_is_array(env, argv[2], &isArr2);
+    if (!isArr || !isArr2) { napi_throw_type_error(env, nullptr, "applyBatchParts(ctx, parts[], propMaps[])"); return nullptr; }
+    uint32_t P = 0, PM = 0;
+    napi_get_array_length(env, argv[1], &P); napi_get_array_length(env, argv[2], &PM);
+    if (PM != P) { napi_throw_range_error(env, nullptr, "one property map per part"); return nullptr; }
+    std::vector<mt_op_batch> parts(P);
+    std::vector<const int32_t*> maps(P, nullptr);
+    std::vector<uint32_t> mlen(P, 0);
+    for (uint32_t p = 0; p < P; p++) {
+        napi_value e, m;
+        napi_get_element(env, argv[1], p, &e);
+        if (!read_batch(env, e, parts[p])) return nullptr;
+        napi_get_element(env, argv[2], p, &m);
+        napi_valuetype t; napi_typeof(env, m, &t);
+        if (t == napi_null || t == napi_undefined) continue;
+        size_t n = 0;
+        if (!typed(env, m, napi_int32_array, &maps[p], &n)) return nullptr;
+        mlen[p] = (uint32_t)n;
+    }
+    int rc = mt_apply_batch_parts(c, P, parts.data(), maps.data(), mlen.data());   // copies before returning
+    return rc ? throw_rc(env, c, rc, "mt_apply_batch_parts") : undefined(env);
 }
 
 // loadSnapshot(ctx, batch): SnapshotLoader for every document of the batch
@@ -592,6 +631,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"setDocSnapshotChunk", nullptr, SetDocSnapshotChunk, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"reserveStaging", nullptr, ReserveStaging, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"applyBatch", nullptr, ApplyBatch, nullptr, nullptr, nullptr, kAttr, nullptr},
+        {"applyBatchParts", nullptr, ApplyBatchParts, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"loadSnapshot", nullptr, LoadSnapshot, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"sync", nullptr, Sync, nullptr, nullptr, nullptr, kAttr, nullptr},
         {"syncAsync", nullptr, SyncAsync, nullptr, nullptr, nullptr, kAttr, nullptr},

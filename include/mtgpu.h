@@ -350,6 +350,18 @@ int  mt_apply_batch(mt_ctx* ctx, const mt_op_batch* batch);
  * documents it names without any host->device traffic (the bench's timed path). */
 int  mt_upload_batch(mt_ctx* ctx, const mt_op_batch* batch);
 int  mt_replay_resident(mt_ctx* ctx);
+/* Several batches applied as one (runs in part order): a host that packs on several threads
+ * (the Node host's worker_threads, each packing a slice of the documents into its own columns)
+ * hands its parts over as they are and the library concatenates them while it packs the op
+ * records into the pinned staging buffer, on its own host threads.  Part p's indices are local
+ * to it and are re-based here: payload_off of text inserts by the payload units of parts < p,
+ * REL1/REL2 position indices by their relative positions, and property-set ids through
+ * prop_map[p] (prop_map_len[p] entries; prop_map or prop_map[p] null: ids already global).
+ * The result is the same as mt_upload_batch / mt_apply_batch of the concatenated batch. */
+int  mt_upload_batch_parts(mt_ctx* ctx, uint32_t n_parts, const mt_op_batch* parts,
+                           const int32_t* const* prop_map, const uint32_t* prop_map_len);
+int  mt_apply_batch_parts(mt_ctx* ctx, uint32_t n_parts, const mt_op_batch* parts,
+                          const int32_t* const* prop_map, const uint32_t* prop_map_len);
 /* Residency of the replay.  use_lds = 2 (default): blocks and zamboni heap move
  * to LDS (9.6 KB per document, 4 waves per SIMD), rows/window/text stay in HBM,
  * and a document that outgrows the LDS blocks continues from HBM in the same

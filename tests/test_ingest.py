@@ -111,3 +111,11 @@ def test_node_full_scale_ingest_packs_every_message(tmp_path):
     neg = np.full(6, -1, np.int32)
     digs = eng.snapshot_digests(range(6), neg, neg, threads=2)
     assert node["digest_xor"] == f"{int(np.bitwise_xor.reduce(digs)):016x}"
+    # --objects: the workers hold parsed message objects, pack them with addMessages and hand the
+    # parts to mt_apply_batch_parts unmerged; the same digests
+    r = subprocess.run(["node", os.path.join(ROOT, "fluidframework_amd", "js", "ingest_scale.js"), str(tmp_path), "3", "4",
+                        "--gpu", "--objects"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr
+    obj = json.loads(r.stdout.strip().splitlines()[-1])
+    assert obj["input"] == "objects" and obj["msgs"] == 6 * 600
+    assert obj["digest_xor"] == node["digest_xor"]

@@ -286,3 +286,40 @@ def test_register_known_answers_on_emulation(twice):
 @pytest.mark.parametrize("twice", [False, True])
 def test_register_known_answers_on_gpu(twice):
     check_register_known_answers(lambda n, **kw: Engine(n, device=0, **kw), twice)
+
+
+# ---- the Node host's parallel packing: parts applied as one batch (mt_apply_batch_parts) ----
+def check_parts(addon, surface, seed=5, n_docs=7, n_msgs=600, parts=3):
+    """Documents packed by several BatchBuilders (each its own PropTable, addMessages: what the
+    ParallelPacker workers do) and applied as parts give every document the text and SnapshotV1
+    digest of one BatchBuilder's batch (addMessage per message, mt_apply_batch)."""
+    from js_lib import run_driver
+    streams = [stream(seed * 101 + d, n_msgs, **SURFACES[surface]) for d in range(n_docs)]
+    got = run_driver("parts_check.js", {"docs": [m for m, _ in streams], "parts": parts}, addon=addon)
+    assert got["a"]["texts"] == got["b"]["texts"]
+    assert got["a"]["digests"] == got["b"]["digests"]
+    for d, (msgs, obs) in enumerate(streams):                  # and both equal the oracle's
+        _, dig = obs.snapshot(msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"])
+        assert int(got["b"]["digests"][d], 16) == dig, f"doc {d}"
+        assert got["b"]["texts"][d] == obs.get_text()
+
+
+PART_SURFACES = ["groups", "markers_props", "unicode", "relative", "combine"]
+
+
+@pytest.mark.parametrize("surface", PART_SURFACES)
+def test_batch_parts_node_host_on_emulation(surface):
+    from js_lib import NODE
+    from emu_lib import build_emu_napi
+    if NODE is None:
+        pytest.skip("node is not installed")
+    check_parts(build_emu_napi(), surface)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("surface", PART_SURFACES)
+def test_batch_parts_node_host_on_gpu(surface):
+    from js_lib import NODE, ROOT
+    if NODE is None:
+        pytest.skip("node is not installed")
+    check_parts(os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"), surface)
