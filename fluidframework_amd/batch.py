@@ -21,11 +21,13 @@ from . import jsjson
 
 MT_OP_INSERT, MT_OP_REMOVE, MT_OP_ANNOTATE, MT_OP_NOOP, MT_OP_UNSUPPORTED = 0, 1, 2, 3, 4
 MT_OPF_END_OF_MSG, MT_OPF_MARKER, MT_OPF_REWRITE, MT_OPF_SEG_PROPS, MT_OPF_COMBINE = 1, 2, 4, 8, 16
+MT_OPF_CONSENSUS, MT_OPF_INCR_STRMIN = 2, 8          # on combining annotates (include/mtgpu.h)
 MT_OP_CUT, MT_OP_COPY, MT_OP_PASTE = 5, 6, 7      # register ops (include/mtgpu.h)
 MT_OPF_REL1, MT_OPF_REL2, MT_OPF_MARKER_ID = 0x20, 0x40, 0x80
 MARKER_ID_KEY = "markerId"            # reservedMarkerIdKey, MT/mergeTree.ts:591
 # property values other than interned ids (include/mtgpu.h MT_VAL_*, MT_VK_*)
-MT_VAL_NULL, MT_VAL_NAN, MT_VAL_UNSUP, MT_VAL_CFRESH, MT_VAL_UNDEF, MT_VAL_CONS_BASE = -1, -2, -3, -4, -5, -16
+MT_VAL_NULL, MT_VAL_NAN, MT_VAL_UNSUP, MT_VAL_CFRESH, MT_VAL_UNDEF, MT_VAL_THROW, MT_VAL_CONS_BASE = -1, -2, -3, -4, -5, -6, -16
+INCR_CHAIN_MAX = 64        # incr results of a held string precomputed per value (PropTable.to_c)
 MT_VK_NUM, MT_VK_SEQM1 = 1, 2
 
 
@@ -61,7 +63,7 @@ MT_DS_NAMES = {
     0x01: "ASSERT_SEQ", 0x02: "ASSERT_MSN", 0x04: "INSERT_FAILED", 0x08: "UNSUPPORTED",
     0x10: "OOM_ROWS", 0x20: "OOM_BLOCKS", 0x40: "OOM_TEXT", 0x80: "OOM_PROPS",
     0x100: "OOM_HEAP", 0x200: "OOM_WINDOW", 0x400: "PROPS_TOO_MANY", 0x800: "BAD_OP",
-    0x1000: "REFSEQ_BELOW_MSN",
+    0x1000: "REFSEQ_BELOW_MSN", 0x2000: "OOM_OVERLAP", 0x4000: "THROWS",
 }
 
 
@@ -87,6 +89,7 @@ class MtPropTable(ctypes.Structure):
         ("value", ctypes.c_void_p), ("n_keys", ctypes.c_uint32), ("key_json", ctypes.c_void_p),
         ("key_index", ctypes.c_void_p), ("n_values", ctypes.c_uint32), ("value_json", ctypes.c_void_p),
         ("value_falsy", ctypes.c_void_p), ("value_class", ctypes.c_void_p), ("value_kind", ctypes.c_void_p),
+        ("value_incr", ctypes.c_void_p), ("incr_object", ctypes.c_int32),
     ]
 
 
@@ -123,6 +126,8 @@ class PropTable:
         self._class_ids: dict[Any, int] = {}
         self.set_ids: dict[tuple, int] = {}
         self.sets: list[tuple] = []
+        self._incr_keys: set[int] = set()      # keys some incr op names
+        self._n_incr = 0                       # incr ops interned
         self._c = None
 
     def key_id(self, k: str) -> int:
@@ -161,17 +166,28 @@ class PropTable:
         name = cop.get("name") if isinstance(cop, dict) else None
         has_def = isinstance(cop, dict) and "defaultValue" in cop
         d = cop.get("defaultValue") if has_def else None
-        if name == "incr":                  # x + undefined: NaN, or a string for strings / objects
-            code = MT_VAL_NAN if (not has_def or d is None or _is_number(d)) else MT_VAL_UNSUP
-            fl = MT_OPF_COMBINE
+        if name == "incr":                  # x + undefined: NaN, or String(x) + "undefined"
+            mv = cop.get("minValue")
+            str_min = jsjson.js_truthy(mv) and isinstance(mv, (str, list, dict))
+            if not has_def or d is None or _is_number(d):
+                code = MT_VAL_NAN           # NaN < minValue is false
+            else:
+                r = jsjson.js_to_string(d) + "undefined"
+                # `if (_currentValue < minValue)` compares two strings by UTF-16 code units
+                below = str_min and jsjson.utf16_units(r) < jsjson.utf16_units(jsjson.js_to_string(mv))
+                code = self.value_id(mv) if below else self.value_id(r)
+            fl = MT_OPF_COMBINE | (MT_OPF_INCR_STRMIN if str_min else 0)
+            self._n_incr += 1
+            for k in props.keys():
+                self._incr_keys.add(self.key_id(k))
         elif name == "consensus":           # {value: undefined, seq}; null.seq throws; seq -1 is set
             if not has_def:
                 code = MT_VAL_CFRESH
             elif d is None:
-                code = MT_VAL_UNSUP
+                code = MT_VAL_THROW
             else:
                 code = self.value_id({**d, "seq": seq} if _seq_minus1(d) else d)
-            fl = MT_OPF_COMBINE | MT_OPF_REWRITE
+            fl = MT_OPF_COMBINE | MT_OPF_REWRITE | MT_OPF_CONSENSUS
         else:                               # no case in combine's switch: the (default) value
             code = MT_VAL_UNDEF if not has_def else (MT_VAL_NULL if d is None else self.value_id(d))
             fl = MT_OPF_COMBINE | MT_OPF_REWRITE
@@ -186,9 +202,41 @@ class PropTable:
             self._c = None
         return i
 
+    def _incr_table(self):
+        """(value_incr, incr_object) for mt_prop_table: what incr yields from each value held
+        (properties.ts:33-34, `v += undefined`): the id of String(v) + "undefined" for a string,
+        array or object that can be held under a key some incr op names (a value some set
+        gives that key, and the strings incr makes from those, INCR_CHAIN_MAX deep at most),
+        MT_VAL_UNSUP for the rest; numbers and booleans give NaN on the device (MT_VK_NUM)."""
+        import json as _json
+        if not self._n_incr:
+            return [MT_VAL_UNSUP] * len(self.values_json), MT_VAL_UNSUP
+        depth_max = min(self._n_incr, INCR_CHAIN_MAX)
+        obj = self.value_id("[object Object]undefined")        # incr of a fresh consensus object
+        depth = {obj: 1}
+        for s_ in self.sets:
+            for k, v in s_:
+                if k in self._incr_keys and v >= 0:
+                    depth.setdefault(v, 0)
+        succ = {}
+        frontier = list(depth)
+        while frontier:
+            nxt = []
+            for v in frontier:
+                if v in succ or self.values_kind[v] & MT_VK_NUM or depth[v] >= depth_max:
+                    continue
+                w = self.value_id(jsjson.js_to_string(_json.loads(self.values_json[v])) + "undefined")
+                succ[v] = w
+                if w not in depth:
+                    depth[w] = depth[v] + 1
+                    nxt.append(w)
+            frontier = nxt
+        return [succ.get(v, MT_VAL_UNSUP) for v in range(len(self.values_json))], obj
+
     def to_c(self) -> MtPropTable:
         if self._c is not None:
             return self._c[0]
+        incr, incr_obj = self._incr_table()     # may intern strings: before the arrays are built
         off = np.zeros(len(self.sets) + 1, np.uint32)
         keys, vals = [], []
         for i, s in enumerate(self.sets):
@@ -205,10 +253,11 @@ class PropTable:
         vf = np.asarray(self.values_falsy or [0], np.uint8)
         vc = np.asarray(self.values_class or [0], np.uint32)
         vkd = np.asarray(self.values_kind or [0], np.uint8)
+        vin = np.asarray(incr or [MT_VAL_UNSUP], np.int32)
         t = MtPropTable(len(self.sets), _ptr(off), _ptr(keys), _ptr(vals), len(self.keys),
                         ctypes.cast(kj, ctypes.c_void_p).value, _ptr(kidx), len(self.values_json),
-                        ctypes.cast(vj, ctypes.c_void_p).value, _ptr(vf), _ptr(vc), _ptr(vkd))
-        self._c = (t, [off, keys, vals, kj, kk, kidx, vj, vk, vf, vc, vkd])
+                        ctypes.cast(vj, ctypes.c_void_p).value, _ptr(vf), _ptr(vc), _ptr(vkd), _ptr(vin), incr_obj)
+        self._c = (t, [off, keys, vals, kj, kk, kidx, vj, vk, vf, vc, vkd, vin])
         return t
 
 

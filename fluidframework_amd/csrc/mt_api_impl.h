@@ -310,16 +310,27 @@ int MT_FN(set_props)(mt_ctx* c, const mt_prop_table* P) {
     if ((rc = mtb_ensure(c, c->b_pval, 4ull * npairs + 4))) return rc;
     if ((rc = mtb_ensure(c, c->b_pfalsy, 1ull * P->n_values + 1))) return rc;
     if ((rc = mtb_ensure(c, c->b_pclass, 4ull * P->n_values + 4))) return rc;
-    if ((rc = mtb_ensure(c, c->b_pkind, 1ull * P->n_values + 1))) return rc;
+    if ((rc = mtb_ensure(c, c->b_pkind, 4ull * P->n_values + 8))) return rc;
     mtb_h2d(c, c->b_pset_off.p, P->set_off, 4ull * (P->n_sets + 1));
     if (npairs) { mtb_h2d(c, c->b_pkey.p, P->key, 2ull * npairs); mtb_h2d(c, c->b_pval.p, P->value, 4ull * npairs); }
     if (P->n_values) { mtb_h2d(c, c->b_pfalsy.p, P->value_falsy, P->n_values); mtb_h2d(c, c->b_pclass.p, P->value_class, 4ull * P->n_values); }
-    if (P->n_values && P->value_kind) mtb_h2d(c, c->b_pkind.p, P->value_kind, P->n_values);
+    // per value: what incr yields from it held, and the consensus seq -1 mark (MtState::p_vinfo);
+    // element 0: incr of a fresh consensus object
+    std::vector<int32_t> vinfo(P->n_values + 1);
+    vinfo[0] = P->value_incr && P->incr_object >= 0 && (uint32_t)P->incr_object < P->n_values ? P->incr_object : MT_VINFO_NONE;
+    for (uint32_t v = 0; P->value_kind && v < P->n_values; v++) {
+        const uint8_t k = P->value_kind[v];
+        const int32_t inc = P->value_incr ? P->value_incr[v] : MT_VAL_UNSUP;
+        vinfo[v + 1] = (k & MT_VK_NUM) ? MT_VAL_NAN
+                                       : (((inc >= 0 && (uint32_t)inc < P->n_values) ? inc : MT_VINFO_NONE) |
+                                          ((k & MT_VK_SEQM1) ? MT_VINFO_SEQM1 : 0));
+    }
+    mtb_h2d(c, c->b_pkind.p, vinfo.data(), 4ull * vinfo.size());
     mtb_sync(c);
     c->S.p_off = (const uint32_t*)c->b_pset_off.p; c->S.p_key = (const uint16_t*)c->b_pkey.p;
     c->S.p_val = (const int32_t*)c->b_pval.p; c->S.p_falsy = (const uint8_t*)c->b_pfalsy.p;
     c->S.p_class = (const uint32_t*)c->b_pclass.p; c->S.p_nsets = P->n_sets;
-    c->S.p_kind = (P->value_kind || !P->n_values) ? (const uint8_t*)c->b_pkind.p : nullptr;
+    c->S.p_vinfo = (P->value_kind || !P->n_values) ? (const int32_t*)c->b_pkind.p + 1 : nullptr;
     c->names.key_json.assign(P->key_json, P->key_json + P->n_keys);
     c->names.key_index.assign(P->key_index, P->key_index + P->n_keys);
     c->names.value_json.assign(P->value_json, P->value_json + P->n_values);

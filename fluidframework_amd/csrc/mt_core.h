@@ -309,8 +309,15 @@ struct MtState {                              // device pools, doc-major
     // interned op property sets (mt_prop_table)
     const uint32_t* p_off; const uint16_t* p_key; const int32_t* p_val;
     const uint8_t* p_falsy; const uint32_t* p_class; uint32_t p_nsets;
-    const uint8_t* p_kind;                    // MT_VK_* per value (null: combine sets unsupported)
+    // per value: incr's result from it held (MT_VAL_NAN for a number / boolean, else the
+    // interned String(v) + "undefined" in bits 0..29, MT_VINFO_NONE there when not interned)
+    // and MT_VINFO_SEQM1; element -1: incr of a fresh consensus object (null: combine sets
+    // unsupported); mt_set_props
+    const int32_t* p_vinfo;
 };
+#define MT_VINFO_ID    0x3FFFFFFF
+#define MT_VINFO_NONE  0x3FFFFFFF
+#define MT_VINFO_SEQM1 0x40000000
 
 struct __attribute__((aligned(16))) MtOpRec {  // one 32-byte op record (mt_op_batch member, packed)
     uint8_t type, flags; uint16_t client;
@@ -506,10 +513,13 @@ enum { MT_WALK_SPLIT = 0, MT_WALK_INSERT = 1 };
 enum { MT_W_OK = 0, MT_W_NOCHANGE = 1, MT_W_FAIL = 2 };
 enum { MT_MAP_REMOVE = 0, MT_MAP_ANNOTATE = 1, MT_MAP_COLLECT = 2 };
 // How an annotate's prop set applies (applyPropSet): plain, rewrite, or a combining op
-// (MT_OPF_COMBINE: incr; MT_OPF_COMBINE | MT_OPF_REWRITE: consensus and other names).
-enum { MT_PM_SET = 0, MT_PM_REWRITE = 1, MT_PM_INCR = 2, MT_PM_KEEP = 3 };
+// (MT_OPF_COMBINE: incr, MT_PM_INCR_SMIN with a string minValue; MT_OPF_COMBINE |
+// MT_OPF_REWRITE: other names, with MT_OPF_CONSENSUS consensus).
+enum { MT_PM_SET = 0, MT_PM_REWRITE = 1, MT_PM_INCR = 2, MT_PM_KEEP = 3, MT_PM_CONS = 4, MT_PM_INCR_SMIN = 5 };
 MT_INLINE int mt_prop_mode(uint32_t fl) {
-    return (fl & MT_OPF_COMBINE) ? ((fl & MT_OPF_REWRITE) ? MT_PM_KEEP : MT_PM_INCR) : ((fl & MT_OPF_REWRITE) ? MT_PM_REWRITE : MT_PM_SET);
+    if (!(fl & MT_OPF_COMBINE)) return (fl & MT_OPF_REWRITE) ? MT_PM_REWRITE : MT_PM_SET;
+    if (fl & MT_OPF_REWRITE) return (fl & MT_OPF_CONSENSUS) ? MT_PM_CONS : MT_PM_KEEP;
+    return (fl & MT_OPF_INCR_STRMIN) ? MT_PM_INCR_SMIN : MT_PM_INCR;
 }
 
 // The wave's view of one document: doc-local pool pointers and the few global
@@ -518,7 +528,7 @@ struct MtEngParams {
     uint32_t rowCap, heapCap, winCap, textCap, psetCap, p_nsets;
     uint16_t* textBase;
     const uint32_t* p_off; const uint16_t* p_key; const int32_t* p_val;
-    const uint8_t* p_falsy; const uint32_t* p_class; const uint8_t* p_kind;
+    const uint8_t* p_falsy; const uint32_t* p_class; const int32_t* p_vinfo;
 };
 // The LDS pools live in one file-scope __shared__ object, so every access of
 // the LDS-resident engine (MtEngT<MT_RES_LDS / MT_RES_BLK>) is a ds_* instruction; the host
@@ -740,7 +750,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         };
         S.rowCap = uni(Ly->rowCap); S.heapCap = uni(Ly->heapCap); S.winCap = uni(Ly->winCap); S.textCap = uni(Ly->textCap);
         S.psetCap = uni(Ly->psetCap); S.p_nsets = st.p_nsets; S.p_off = st.p_off; S.p_key = st.p_key; S.p_val = st.p_val;
-        S.p_falsy = st.p_falsy; S.p_class = st.p_class; S.p_kind = st.p_kind; S.textBase = st.text + off(&Ly->text);
+        S.p_falsy = st.p_falsy; S.p_class = st.p_class; S.p_vinfo = st.p_vinfo; S.textBase = st.text + off(&Ly->text);
         blkCap = uni(Ly->blkCap); hdrp = st.hdr + d;
         R = st.rows + off(&Ly->row);
         blk = st.blk + off(&Ly->blk); heap = st.heap + off(&Ly->heap);
@@ -2827,23 +2837,30 @@ template <int RES, bool FULL = true> struct MtEngT {
             vv = wave_map(n, [&](int i) MT_LAM { return sc->holdLen[i]; });
             wave_sync();
         }
-        if (pm >= MT_PM_INCR && !S.p_kind) { status |= MT_DS_UNSUPPORTED; return old; }
+        if (pm >= MT_PM_INCR && !S.p_vinfo) { status |= MT_DS_UNSUPPORTED; return old; }
+        const bool incr = pm == MT_PM_INCR || pm == MT_PM_INCR_SMIN;
         for (int q = o0; q < o1; q++) {
             const int key = uni((int)S.p_key[q]);
             int nv = uni((int)S.p_val[q]);
             const int at = wave_first(wave_map(n, [&](int i) MT_LAM { return own(kk, i) == key; }));
             if (pm >= MT_PM_INCR) {
                 // combine(op, previousValue, undefined, seq): a held value undefined counts as
-                // not held; incr of a number / boolean / NaN is NaN, of anything else a string
-                // (off the path); consensus keeps the value unless it is an object whose seq
-                // is -1 (shared by every segment split from the one it was set on)
+                // not held; incr of a number / boolean / NaN is NaN, of a string / array /
+                // object (a fresh consensus object included) the interned String(v) +
+                // "undefined"; consensus keeps the value unless it is an object whose seq is -1
+                // (shared by every segment split from the one it was set on); other names keep it
                 const int pv = at >= 0 ? wave_at(vv, at) : MT_VAL_UNDEF;
                 if (pv != MT_VAL_UNDEF) {
-                    const uint32_t kd = pv >= 0 ? (uint32_t)uni((int)S.p_kind[pv]) : (pv == MT_VAL_NAN ? MT_VK_NUM : 0u);
-                    if (pm == MT_PM_INCR) nv = (kd & MT_VK_NUM) ? MT_VAL_NAN : MT_VAL_UNSUP;
-                    else nv = (kd & MT_VK_SEQM1) ? MT_VAL_UNSUP : pv;
+                    const int vi = pv >= 0 ? uni(S.p_vinfo[pv]) : (pv == MT_VAL_NAN ? MT_VAL_NAN : uni(S.p_vinfo[-1]));
+                    if (incr) {
+                        const int sid = vi & MT_VINFO_ID;
+                        nv = vi == MT_VAL_NAN ? MT_VAL_NAN
+                                              : ((vi < 0 || sid == MT_VINFO_NONE || pm == MT_PM_INCR_SMIN) ? MT_VAL_UNSUP : sid);
+                    } else if (pm == MT_PM_CONS) nv = (pv >= 0 && vi >= 0 && (vi & MT_VINFO_SEQM1)) ? MT_VAL_UNSUP : pv;
+                    else nv = pv;
                 }
                 if (nv == MT_VAL_CFRESH) nv = (sq >= 0 && sq <= 0x7FFFFFEF) ? MT_VAL_CONS(sq) : MT_VAL_UNSUP;   // -16 - seq fits int32
+                if (nv == MT_VAL_THROW) { status |= MT_DS_THROWS; return old; }
                 if (nv == MT_VAL_UNSUP) { status |= MT_DS_UNSUPPORTED; return old; }
             }
             if (nv == MT_VAL_NULL) {

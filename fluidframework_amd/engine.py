@@ -34,6 +34,11 @@ class MergeTreeError(RuntimeError):
     pass
 
 
+class ReferenceTypeError(MergeTreeError, TypeError):
+    """Where the reference's Client throws a TypeError (MT_DS_THROWS): a consensus combine on a
+    segment without the key and a null defaultValue reads null.seq (properties.ts:51-52)."""
+
+
 class ExchangeError(MergeTreeError):
     """Exchanged document rows whose checksum differs from the sender's (MT_E_EXCHANGE)."""
 
@@ -663,6 +668,9 @@ class MergeTreeClient:
 
     def _raise_status(self):
         st = int(self.engine.status([self.doc_id])[0])
+        if st & 0x4000:            # MT_DS_THROWS: the reference's applyMsg throws a TypeError here
+            raise ReferenceTypeError(f"document {self.doc_id}: Cannot read property 'seq' of null "
+                                     "(a consensus combine on a null defaultValue, properties.ts:51-52)")
         if st:
             raise MergeTreeError(f"document {self.doc_id}: {', '.join(status_names(st))}")
 

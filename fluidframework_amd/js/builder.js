@@ -13,7 +13,9 @@ const F_END = 1, F_MARKER = 2, F_REWRITE = 4, F_SEG_PROPS = 8, F_COMBINE = 16, F
     F_MARKER_ID = 0x80;
 const MARKER_ID_KEY = "markerId";   // reservedMarkerIdKey, MT/mergeTree.ts:591
 // property values other than interned ids, and value kinds (include/mtgpu.h MT_VAL_*, MT_VK_*)
-const VAL_NULL = -1, VAL_NAN = -2, VAL_UNSUP = -3, VAL_CFRESH = -4, VAL_UNDEF = -5, VAL_CONS_BASE = -16;
+const VAL_NULL = -1, VAL_NAN = -2, VAL_UNSUP = -3, VAL_CFRESH = -4, VAL_UNDEF = -5, VAL_THROW = -6, VAL_CONS_BASE = -16;
+const F_CONSENSUS = 2, F_INCR_STRMIN = 8;   // on combining annotates (include/mtgpu.h)
+const INCR_CHAIN_MAX = 64;                  // incr results of a held string precomputed per value
 const VK_NUM = 1, VK_SEQM1 = 2;
 const isNumberLike = (v) => typeof v === "number" || typeof v === "boolean";      // x + undefined is NaN
 const seqMinus1 = (v) => v !== null && typeof v === "object" && !Array.isArray(v) && v.seq === -1;   // properties.ts:52
@@ -42,6 +44,7 @@ class PropTable {
         this.valueIds = new Map(); this.valueJson = []; this.valueFalsy = []; this.valueClass = []; this.valueKind = [];
         this.classIds = new Map();
         this.setIds = new Map(); this.sets = [];
+        this.incrKeys = new Set(); this.nIncr = 0;
     }
     keyId(k) {
         let i = this.keyIds.get(k);
@@ -76,12 +79,21 @@ class PropTable {
     internCombine(props, cop, seq) {
         const d = cop.defaultValue;
         let code, fl;
-        if (cop.name === "incr") {                          // x + undefined: NaN, or a string
-            code = (d === undefined || d === null || isNumberLike(d)) ? VAL_NAN : VAL_UNSUP;
-            fl = F_COMBINE;
+        if (cop.name === "incr") {                          // x + undefined: NaN, or String(x) + "undefined"
+            const mv = cop.minValue;
+            const strMin = !!mv && typeof mv === "object" || (typeof mv === "string" && mv.length > 0);
+            if (d === undefined || d === null || isNumberLike(d)) code = VAL_NAN;     // NaN < minValue is false
+            else {
+                let r = d + undefined;                          // `_currentValue += newValue`
+                if (strMin && r < mv) r = mv;                   // both strings: UTF-16 code-unit order
+                code = this.valueId(r);
+            }
+            fl = F_COMBINE | (strMin ? F_INCR_STRMIN : 0);
+            this.nIncr++;
+            for (const k of Object.keys(props)) this.incrKeys.add(this.keyId(k));
         } else if (cop.name === "consensus") {              // {value: undefined, seq}; null.seq throws
-            code = d === undefined ? VAL_CFRESH : (d === null ? VAL_UNSUP : this.valueId(seqMinus1(d) ? { ...d, seq } : d));
-            fl = F_COMBINE | F_REWRITE;
+            code = d === undefined ? VAL_CFRESH : (d === null ? VAL_THROW : this.valueId(seqMinus1(d) ? { ...d, seq } : d));
+            fl = F_COMBINE | F_REWRITE | F_CONSENSUS;
         } else {                                            // no case in combine's switch
             code = d === undefined ? VAL_UNDEF : (d === null ? VAL_NULL : this.valueId(d));
             fl = F_COMBINE | F_REWRITE;
@@ -94,7 +106,36 @@ class PropTable {
         if (i === undefined) { i = this.sets.length; this.setIds.set(sig, i); this.sets.push(pairs); }
         return i;
     }
+    /**
+     * [valueIncr, incrObject] for mt_prop_table: what incr yields from each value held
+     * (properties.ts:33-34, `v += undefined`): the id of that string for a string, array or
+     * object that can be held under a key some incr op names (the values sets give those keys,
+     * and the strings incr makes from them, INCR_CHAIN_MAX deep at most), VAL_UNSUP otherwise.
+     */
+    incrTable() {
+        if (!this.nIncr) return [new Int32Array(Math.max(1, this.valueJson.length)).fill(VAL_UNSUP), VAL_UNSUP];
+        const depthMax = Math.min(this.nIncr, INCR_CHAIN_MAX);
+        const obj = this.valueId("[object Object]undefined");         // incr of a fresh consensus object
+        const depth = new Map([[obj, 1]]);
+        for (const s of this.sets) for (const [k, v] of s) if (this.incrKeys.has(k) && v >= 0 && !depth.has(v)) depth.set(v, 0);
+        const succ = new Map();
+        let frontier = [...depth.keys()];
+        while (frontier.length) {
+            const nxt = [];
+            for (const v of frontier) {
+                if (succ.has(v) || (this.valueKind[v] & VK_NUM) || depth.get(v) >= depthMax) continue;
+                const w = this.valueId(JSON.parse(this.valueJson[v]) + undefined);
+                succ.set(v, w);
+                if (!depth.has(w)) { depth.set(w, depth.get(v) + 1); nxt.push(w); }
+            }
+            frontier = nxt;
+        }
+        const t = new Int32Array(Math.max(1, this.valueJson.length)).fill(VAL_UNSUP);
+        for (const [v, w] of succ) t[v] = w;
+        return [t, obj];
+    }
     toNative() {
+        const [valueIncr, incrObject] = this.incrTable();      // may intern strings: first
         const setOff = new Uint32Array(this.sets.length + 1);
         const key = [], value = [];
         this.sets.forEach((s, i) => { setOff[i + 1] = setOff[i] + s.length; for (const [k, v] of s) { key.push(k); value.push(v); } });
@@ -106,6 +147,7 @@ class PropTable {
             valueFalsy: Uint8Array.from(this.valueFalsy.length ? this.valueFalsy : [0]),
             valueClass: Uint32Array.from(this.valueClass.length ? this.valueClass : [0]),
             valueKind: Uint8Array.from(this.valueKind.length ? this.valueKind : [0]),
+            valueIncr, incrObject,
         };
     }
 }
@@ -349,7 +391,7 @@ class BatchBuilder {
 }
 
 
-module.exports = { VAL_NULL, VAL_NAN, VAL_UNSUP, VAL_CFRESH, VAL_UNDEF, VAL_CONS_BASE, VK_NUM, VK_SEQM1,
+module.exports = { VAL_NULL, VAL_NAN, VAL_UNSUP, VAL_CFRESH, VAL_UNDEF, VAL_THROW, VAL_CONS_BASE, VK_NUM, VK_SEQM1,
     OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_GROUP, OP_UNSUPPORTED, OP_CUT, OP_COPY, OP_PASTE,
     F_END, F_MARKER, F_REWRITE, F_SEG_PROPS, F_COMBINE, F_REL1, F_REL2, F_MARKER_ID, MARKER_ID_KEY, arrayIndex,
     matchClassKey, PropTable, ClientNames, mergeTreeMembers, COLS, Col, BatchBuilder };

@@ -33,6 +33,7 @@ const STATUS = {
     0x01: "ASSERT_SEQ", 0x02: "ASSERT_MSN", 0x04: "INSERT_FAILED", 0x08: "UNSUPPORTED",
     0x10: "OOM_ROWS", 0x20: "OOM_BLOCKS", 0x40: "OOM_TEXT", 0x80: "OOM_PROPS",
     0x100: "OOM_HEAP", 0x200: "OOM_WINDOW", 0x400: "PROPS_TOO_MANY", 0x800: "BAD_OP", 0x1000: "REFSEQ_BELOW_MSN",
+    0x2000: "OOM_OVERLAP", 0x4000: "THROWS",
 };
 function statusNames(st) {
     return Object.keys(STATUS).filter((b) => st & Number(b)).map((b) => STATUS[b]);
@@ -334,6 +335,9 @@ class MergeTreeClient {
     }
     checkStatus() {
         const st = this.group.engine.status([this.docId])[0];
+        // MT_DS_THROWS: where the reference's applyMsg throws (consensus on a null default reads
+        // null.seq, properties.ts:51-52), the same TypeError
+        if (st & 0x4000) throw new TypeError(`document ${this.docId}: Cannot read property 'seq' of null`);
         if (st) throw new Error(`document ${this.docId}: ${statusNames(st).join(", ")}`);
     }
     updateSeqNumbers(min, seq) {

@@ -81,7 +81,8 @@ parentPort.on("message", ({ docs, prepare, windows, objects, resetNames }) => {
             transfer.push(batch[k].buffer);
         }
         parentPort.postMessage({ batch, nPayload, names,
-            props: { keys: props.keys, valueJson: props.valueJson, sets: props.sets } }, transfer);
+            props: { keys: props.keys, valueJson: props.valueJson, sets: props.sets, incrKeys: [...props.incrKeys],
+                nIncr: props.nIncr } }, transfer);
     } catch (e) {
         parentPort.postMessage({ error: String(e && e.stack || e) });
     }

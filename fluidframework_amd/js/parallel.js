@@ -120,6 +120,9 @@ class ParallelPacker {
 // A worker's interned property sets as set ids of the engine's table: keys and values re-interned,
 // the non-value codes of combine sets (MT_VAL_*, negative) kept as they are.
 function absorb(wp, props) {
+    // the keys incr ops name, and their count (PropTable.incrTable's inputs)
+    for (const k of wp.incrKeys || []) props.incrKeys.add(props.keyId(wp.keys[k]));
+    props.nIncr += wp.nIncr || 0;
     return Int32Array.from(wp.sets.map((pairs) => props.internPairs(pairs.map(([k, v]) =>
         [props.keyId(wp.keys[k]), v < 0 ? v : props.valueId(JSON.parse(wp.valueJson[v]))]))));
 }

@@ -174,7 +174,8 @@ napi_value SetResidency(napi_env env, napi_callback_info info) {
     return rc ? throw_rc(env, c, rc, "mt_set_residency") : undefined(env);
 }
 
-// setProps(ctx, {setOff, key, value, keyJson[], keyIndex, valueJson[], valueFalsy, valueClass, valueKind})
+// setProps(ctx, {setOff, key, value, keyJson[], keyIndex, valueJson[], valueFalsy, valueClass, valueKind,
+//                valueIncr?, incrObject?})
 napi_value SetProps(napi_env env, napi_callback_info info) {
     napi_value argv[2];
     if (!get_args(env, info, 2, argv)) return nullptr;
@@ -203,6 +204,20 @@ napi_value SetProps(napi_env env, napi_callback_info info) {
     P.n_sets = (uint32_t)(noff - 1); P.set_off = off; P.key = key; P.value = val;
     P.n_keys = (uint32_t)ks.size(); P.key_json = kp.data(); P.key_index = kidx;
     P.n_values = (uint32_t)vs.size(); P.value_json = vp.data(); P.value_falsy = vf; P.value_class = vc; P.value_kind = vk;
+    P.incr_object = MT_VAL_UNSUP;
+    {   // optional: valueIncr (Int32Array, one per value) and incrObject (PropTable.incrTable)
+        bool has = false;
+        napi_has_named_property(env, argv[1], "valueIncr", &has);
+        if (has) {
+            const int32_t* vi; size_t nvi;
+            if (!field(env, argv[1], "valueIncr", napi_int32_array, &vi, &nvi)) return nullptr;
+            if (nvi < vs.size()) { napi_throw_range_error(env, nullptr, "valueIncr shorter than valueJson"); return nullptr; }
+            P.value_incr = vi;
+            napi_value io; int32_t x = MT_VAL_UNSUP;
+            if (napi_get_named_property(env, argv[1], "incrObject", &io) == napi_ok) napi_get_value_int32(env, io, &x);
+            P.incr_object = x;
+        }
+    }
     int rc = mt_set_props(c, &P);
     return rc ? throw_rc(env, c, rc, "mt_set_props") : undefined(env);
 }

@@ -74,6 +74,10 @@ extern "C" {
 #define MT_DS_BAD_OP         0x800u /* an op record out of its batch's bounds (payload /
                                        property table), checked on the device         */
 #define MT_DS_OOM_OVERLAP    0x2000u /* removedClientOverlap side list (clients >= 63) full */
+#define MT_DS_THROWS         0x4000u /* an op on which the reference's Client throws: a
+                                       consensus combine on a segment without the key whose
+                                       defaultValue is null reads null.seq (properties.ts:
+                                       41-52, TypeError); the document stops there        */
 #define MT_DS_REFSEQ_BELOW_MSN 0x1000u /* refSeq < minSeq: deli nacks such ops
                                        (deli/lambda.ts:302-318); the window aggregate
                                        is exact only for refSeq >= minSeq             */
@@ -111,10 +115,16 @@ extern "C" {
 #define MT_OPF_COMBINE    0x10u /* annotate with another combiningOp (Properties.combine,
                                    MT/properties.ts:24-62, through
                                    MT/segmentPropertiesManager.ts:98-103):
-                                   COMBINE alone = {name:"incr"}; COMBINE|REWRITE =
-                                   {name:"consensus"} or any other name (a key that
-                                   holds a value keeps it).  prop_id then names a
-                                   combine set (below), not the op's props.        */
+                                   COMBINE alone = {name:"incr"}; COMBINE|REWRITE|
+                                   CONSENSUS = {name:"consensus"}; COMBINE|REWRITE =
+                                   any other name (a key that holds a value keeps
+                                   it).  prop_id then names a combine set (below),
+                                   not the op's props.                             */
+#define MT_OPF_CONSENSUS  0x02u /* on a combining annotate: the name is "consensus" */
+#define MT_OPF_INCR_STRMIN 0x08u /* on an incr annotate: a truthy string / array /
+                                   object minValue, which a string result compares
+                                   against (properties.ts:35-38): such a result from
+                                   a held value sets MT_DS_UNSUPPORTED            */
 #define MT_OPF_REL1       0x20u /* pos1 is an index into rel[]: op.relativePos1
                                    (posFromRelativePos, mergeTree.ts:1949-1972)    */
 #define MT_OPF_REL2       0x40u /* pos2 is an index into rel[]: op.relativePos2    */
@@ -183,17 +193,22 @@ typedef struct mt_op_rec {
  * *combine set*: the op's keys, each valued with what combine yields for a key the
  * segment does not hold (previousValue undefined):
  *   incr       defaultValue undefined / number / boolean / null -> MT_VAL_NAN (x + undefined);
- *              a string / object / array default -> MT_VAL_UNSUP (string concatenation)
- *   consensus  no defaultValue -> MT_VAL_CFRESH ({value: undefined, seq}); null -> MT_VAL_UNSUP
- *              (the reference throws reading null.seq); an object whose seq is -1 -> that
- *              object with seq = the message's seq (properties.ts:52-54); else the default
+ *              a string / object / array default -> the interned string String(default) +
+ *              "undefined" (JS `+=`), or the minValue where a truthy string / array /
+ *              object minValue compares above it (properties.ts:33-40)
+ *   consensus  no defaultValue -> MT_VAL_CFRESH ({value: undefined, seq}); null ->
+ *              MT_VAL_THROW (the reference throws reading null.seq); an object whose seq is
+ *              -1 -> that object with seq = the message's seq (properties.ts:52-54); else the
+ *              default
  *   other      no defaultValue -> MT_VAL_UNDEF; null -> MT_VAL_NULL (the key is deleted);
  *              else the default (combine's switch has no case: the default is returned)
  * A key the segment holds: incr yields NaN from a number, boolean, NaN or undefined value
- * (MT_VK_NUM) and MT_VAL_UNSUP from anything else; consensus and other names keep the
- * value, except that an object whose seq is -1 (MT_VK_SEQM1) is MT_VAL_UNSUP (consensus
- * would write the seq into an object every segment split from it shares).  MT_VAL_UNSUP
- * sets MT_DS_UNSUPPORTED on the document.
+ * (MT_VK_NUM), and String(value) + "undefined" from a string, array or object (the table's
+ * value_incr; a fresh consensus object: incr_object), MT_VAL_UNSUP where the host left that
+ * string out of the table or the op has MT_OPF_INCR_STRMIN; consensus keeps the value,
+ * except that an object whose seq is -1 (MT_VK_SEQM1) is MT_VAL_UNSUP (consensus would write
+ * the seq into an object every segment split from it shares); other names keep the value.
+ * MT_VAL_UNSUP sets MT_DS_UNSUPPORTED on the document, MT_VAL_THROW MT_DS_THROWS.
  *
  * Stored values other than interned ids (never in an op's set): MT_VAL_NAN (JSON null,
  * never matchProperties-equal: NaN !== NaN), MT_VAL_UNDEF (the key is present with
@@ -206,6 +221,7 @@ typedef struct mt_op_rec {
 #define MT_VAL_UNSUP  (-3)
 #define MT_VAL_CFRESH (-4)
 #define MT_VAL_UNDEF  (-5)
+#define MT_VAL_THROW  (-6)
 #define MT_VAL_CONS_BASE (-16)                    /* MT_VAL_CONS(seq) = -16 - seq, 0 <= seq <= INT32_MAX - 16 (a larger seq: MT_DS_UNSUPPORTED) */
 #define MT_VAL_CONS(seq) (MT_VAL_CONS_BASE - (seq))
 #define MT_VK_NUM   0x01u   /* number or boolean: incr gives NaN                            */
@@ -224,6 +240,14 @@ typedef struct mt_prop_table {
     const uint32_t* value_class;  /* [n_values] matchProperties() equivalence   */
     const uint8_t*  value_kind;   /* [n_values] MT_VK_* (null: every combine set
                                      is MT_DS_UNSUPPORTED)                      */
+    const int32_t*  value_incr;   /* [n_values] incr of a held value (`v += undefined`,
+                                     properties.ts:33-34): for a string / array / object,
+                                     the id of the string String(v) + "undefined",
+                                     MT_VAL_UNSUP when not interned (null: all UNSUP);
+                                     ignored for MT_VK_NUM values (NaN)           */
+    int32_t         incr_object;  /* the id of "[object Object]undefined" (incr of a held
+                                     fresh consensus object), or MT_VAL_UNSUP; read only
+                                     with value_incr                               */
 } mt_prop_table;
 
 /* Engine limits per document (pool capacities, sized from the op counts). */

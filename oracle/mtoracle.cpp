@@ -293,7 +293,10 @@ struct PropTable {                       // host-interned op property sets
 // ---- MT/properties.ts:24-62 combine(), as SegmentPropertiesManager.addProperties calls it ----
 // (segmentPropertiesManager.ts:98-103: `newValue` is declared and never assigned, so combine
 // always gets undefined as the new value; the op's prop values are unused).
-enum { PM_SET = 0, PM_REWRITE = 1, PM_INCR = 2, PM_KEEP = 3 };
+enum { PM_SET = 0, PM_REWRITE = 1, PM_INCR = 2, PM_KEEP = 3, PM_CONS = 4, PM_INCR_SMIN = 5 };
+// combine's outcome for one key: a value (or a delete), off the engine's batch path, or the
+// reference throws (TypeError)
+enum CombineOutcome { CB_OK = 0, CB_UNSUP = 1, CB_THROW = 2 };
 struct Combining {                    // ICombiningOp (MT/ops.ts:32-37)
     enum { Incr, Consensus, Other } kind = Other;
     bool hasDef = false; JVal def;    // defaultValue (JSON null is a defined null)
@@ -326,77 +329,85 @@ static bool is_seq_minus1(const JVal& v) {            // `cv.seq === -1` on an o
 }
 static JVal nan_value() { JVal v; v.t = JVal::Num; v.n = std::nan(""); return v; }
 // combine(op, previousValue, undefined, seq) -> *out; *del when the result is null (the key is
-// deleted, segmentPropertiesManager.ts:104-106).  Returns false where the result is off the
-// engine's batch path (MT_DS_UNSUPPORTED there, include/mtgpu.h): an incr that yields a string,
-// consensus on null (the reference throws reading null.seq), and a consensus write into an
-// object a segment already holds (its seq is -1: every segment sharing the object changes).
-static bool js_combine(Combining& cb, const JVal* prev, int seq, JVal& out, bool& del) {
+// deleted, segmentPropertiesManager.ts:104-106).  CB_THROW where the reference throws (consensus
+// on a null current value reads null.seq, properties.ts:51-52), CB_UNSUP where the result is
+// off the engine's batch path (MT_DS_UNSUPPORTED there, include/mtgpu.h): a consensus write into
+// an object a segment already holds (its seq is -1: every segment sharing the object changes)
+// and an incr string result from a held value that a string minValue would be compared with.
+static u16s js_concat_undefined(const JVal& v) { return js_to_string(v) + u"undefined"; }
+static bool js_string_like(const JVal& v) { return v.t == JVal::Str || v.t == JVal::Arr || v.t == JVal::Obj; }
+static CombineOutcome js_combine(Combining& cb, const JVal* prev, int seq, JVal& out, bool& del) {
     del = false;
     JVal cur;
-    if (prev && prev->t != JVal::Undef) cur = *prev;
+    const bool held = prev && prev->t != JVal::Undef;
+    if (held) cur = *prev;
     else if (cb.hasDef) cur = cb.def;                   // `_currentValue = combiningInfo.defaultValue`
     switch (cb.kind) {
     case Combining::Incr: {                             // `_currentValue += newValue` (undefined)
-        if (cur.t == JVal::Str || cur.t == JVal::Arr || cur.t == JVal::Obj) {
-            out.t = JVal::Str; out.s = js_to_string(cur) + u"undefined";      // string concatenation
+        if (js_string_like(cur)) {
+            out.t = JVal::Str; out.s = js_concat_undefined(cur);             // string concatenation
             if (cb.hasMin && truthy(&cb.minValue)) {
-                const bool strMin = cb.minValue.t == JVal::Str || cb.minValue.t == JVal::Arr || cb.minValue.t == JVal::Obj;
+                const bool strMin = js_string_like(cb.minValue);
+                if (strMin && held) return CB_UNSUP;    // the engine's boundary (MT_OPF_INCR_STRMIN)
                 if (strMin && out.s < js_to_string(cb.minValue)) out = cb.minValue;   // both strings: code-unit order
             }
-            return false;
+            return CB_OK;
         }
         out = nan_value();                              // ToNumber(...) + NaN; NaN < minValue is false
-        return true;
+        return CB_OK;
     }
     case Combining::Consensus:
         if (cur.t == JVal::Undef) {                     // {value: newValue, seq}
             out = make_obj(); JVal u; obj_set(out, u"value", u);
             JVal sq; sq.t = JVal::Num; sq.n = seq; obj_set(out, u"seq", sq);
-            return true;
+            return CB_OK;
         }
-        if (cur.t == JVal::Null) return false;          // TypeError: null.seq
+        if (cur.t == JVal::Null) return CB_THROW;       // TypeError: null.seq
         if (is_seq_minus1(cur)) {
-            if (prev && prev->t != JVal::Undef) return false;        // a held (shared) object mutated
+            if (held) return CB_UNSUP;                  // a held (shared) object mutated
             JVal sq; sq.t = JVal::Num; sq.n = seq;
             obj_set(cb.def, u"seq", sq);                 // the op's defaultValue object itself
             out = cb.def;
-            return true;
+            return CB_OK;
         }
         out = cur;
-        return true;
+        return CB_OK;
     case Combining::Other:
-        if (prev && prev->t != JVal::Undef && is_seq_minus1(*prev)) return false;   // engine: held seq -1 objects
-        if (cur.t == JVal::Null) { del = true; return true; }
+        if (cur.t == JVal::Null) { del = true; return CB_OK; }
         out = cur;                                      // no case: the value (or undefined) is returned
-        return true;
+        return CB_OK;
     }
-    return true;
+    return CB_OK;
 }
 // The same step from a combine set (the hosts' packed form, include/mtgpu.h MT_VAL_*): code =
-// what combine yields for a key the segment does not hold.
-static bool packed_combine(const PropTable& pt, int code, int mode, const JVal* prev, int seq, JVal& out, bool& del) {
+// what combine yields for a key the segment does not hold; a held value's result follows from
+// the value itself (mode: PM_INCR / PM_INCR_SMIN, PM_CONS, PM_KEEP).
+static CombineOutcome packed_combine(const PropTable& pt, int code, int mode, const JVal* prev, int seq, JVal& out,
+                                     bool& del) {
     del = false;
     if (prev && prev->t != JVal::Undef) {
-        if (mode == PM_INCR) {
-            if (prev->t != JVal::Num && prev->t != JVal::Bool) return false;
-            out = nan_value();
-            return true;
+        if (mode == PM_INCR || mode == PM_INCR_SMIN) {
+            if (!js_string_like(*prev)) { out = nan_value(); return CB_OK; }
+            if (mode == PM_INCR_SMIN) return CB_UNSUP;
+            out = JVal(); out.t = JVal::Str; out.s = js_concat_undefined(*prev);
+            return CB_OK;
         }
-        if (is_seq_minus1(*prev)) return false;
+        if (mode == PM_CONS && is_seq_minus1(*prev)) return CB_UNSUP;
         out = *prev;
-        return true;
+        return CB_OK;
     }
-    if (code >= 0) { out = pt.values[code]; return true; }
+    if (code >= 0) { out = pt.values[code]; return CB_OK; }
     switch (code) {
-    case MT_VAL_NULL: del = true; return true;
-    case MT_VAL_NAN: out = nan_value(); return true;
-    case MT_VAL_UNDEF: out = JVal(); return true;
+    case MT_VAL_NULL: del = true; return CB_OK;
+    case MT_VAL_NAN: out = nan_value(); return CB_OK;
+    case MT_VAL_UNDEF: out = JVal(); return CB_OK;
     case MT_VAL_CFRESH: {
         out = make_obj(); JVal u; obj_set(out, u"value", u);
         JVal sq; sq.t = JVal::Num; sq.n = seq; obj_set(out, u"seq", sq);
-        return true;
+        return CB_OK;
     }
-    default: return false;                              // MT_VAL_UNSUP
+    case MT_VAL_THROW: return CB_THROW;
+    default: return CB_UNSUP;                           // MT_VAL_UNSUP
     }
 }
 
@@ -1062,8 +1073,9 @@ struct Tree {
                 const int i = obj_find(s->props, kv.first);
                 const JVal* prev = i >= 0 ? &s->props.ovals[i] : nullptr;
                 JVal nv; bool del = false;
-                const bool ok = cb ? js_combine(*cb, prev, seq, nv, del) : packed_combine(pt, kv.second, mode, prev, seq, nv, del);
-                if (!ok) { status |= MT_DS_UNSUPPORTED; return; }
+                const CombineOutcome r = cb ? js_combine(*cb, prev, seq, nv, del) : packed_combine(pt, kv.second, mode, prev, seq, nv, del);
+                if (r == CB_THROW) { status |= MT_DS_THROWS; return; }
+                if (r == CB_UNSUP) { status |= MT_DS_UNSUPPORTED; return; }
                 if (del) obj_del(s->props, kv.first);
                 else obj_set(s->props, kv.first, nv);
                 continue;
@@ -1458,7 +1470,9 @@ static uint32_t apply_run(Doc& d, const mt_op_batch* b, uint32_t run) {
             } else if (ty == MT_OP_REMOVE) {
                 t.markRangeRemoved(b->pos1[i], b->pos2[i], ref, cl, seq);
             } else if (ty == MT_OP_ANNOTATE) {
-                const int mode = (fl & MT_OPF_COMBINE) ? ((fl & MT_OPF_REWRITE) ? PM_KEEP : PM_INCR) : ((fl & MT_OPF_REWRITE) ? PM_REWRITE : PM_SET);
+                const int mode = !(fl & MT_OPF_COMBINE) ? ((fl & MT_OPF_REWRITE) ? PM_REWRITE : PM_SET)
+                               : ((fl & MT_OPF_REWRITE) ? ((fl & MT_OPF_CONSENSUS) ? PM_CONS : PM_KEEP)
+                                                        : ((fl & MT_OPF_INCR_STRMIN) ? PM_INCR_SMIN : PM_INCR));
                 t.annotateRange(b->pos1[i], b->pos2[i], d.props, b->prop_id[i], mode, ref, cl, seq);
             } else if (ty == MT_OP_CUT || ty == MT_OP_COPY || ty == MT_OP_PASTE) {              // register name by index
                 std::string k = std::to_string(b->payload_off[i]);
@@ -1718,7 +1732,7 @@ static void apply_remote_member(Doc& d, const JVal& op, int cl, int ref, int seq
                 else {
                     cb.kind = isStr && nm->s == u"incr" ? Combining::Incr
                             : (isStr && nm->s == u"consensus" ? Combining::Consensus : Combining::Other);
-                    mode = cb.kind == Combining::Incr ? PM_INCR : PM_KEEP;
+                    mode = cb.kind == Combining::Incr ? PM_INCR : (cb.kind == Combining::Consensus ? PM_CONS : PM_KEEP);
                     const JVal* dv = cop->t == JVal::Obj ? jget(*cop, u"defaultValue") : nullptr;
                     if (dv && dv->t != JVal::Undef) { cb.hasDef = true; cb.def = *dv; }
                     const JVal* mv = cop->t == JVal::Obj ? jget(*cop, u"minValue") : nullptr;

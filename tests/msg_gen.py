@@ -42,12 +42,14 @@ VALUES = ["s", "ü", "", 0, 1, -3, 1.5, 1e21, 0.25, True, False, {"a": 1}, [1, 2
           {"n": None}, "😀"]
 # remote combining ops (the "combine" surface, MT/properties.ts:24-62 via
 # segmentPropertiesManager.ts:98-103): "incr" works on keys whose values are numbers or booleans
-# (NaN results); "consensus" and ops of other names on keys holding anything but objects whose
-# seq is -1 (fresh {value: undefined, seq} objects, defaults, undefined values)
+# (NaN results) and strings, arrays and objects (string concatenation with "undefined");
+# "consensus" and ops of other names on keys holding anything but objects whose seq is -1 (fresh
+# {value: undefined, seq} objects, defaults, undefined values).  String minValues stay out of
+# the streams (a held string's incr result compared with one is off the batch path).
 INCR_KEYS = ["n0", "n1", "3"]
 CONS_KEYS = ["v0", "v1", "7"]
-NUM_VALUES = [0, 1, -2, 2.5, True, False, 1e21]
-INCR_DEFAULTS = [None, 0, 5, True, 2.5, "__absent__", "__absent__"]
+NUM_VALUES = [0, 1, -2, 2.5, True, False, 1e21, 3, 4, "s", "ü😀", {"a": 1}, [1, [2, "x"]]]
+INCR_DEFAULTS = [None, 0, 5, True, 2.5, "v", [1, 2], "__absent__", "__absent__"]
 CONS_DEFAULTS = ["__absent__", "__absent__", 7, "x", {"a": 1}, {"value": 3, "seq": -1}, [1, 2], {"seq": 4}, False]
 OTHER_DEFAULTS = ["__absent__", None, 1, "z", {"k": [1]}]
 
@@ -121,7 +123,7 @@ class StreamGen:
         if x < 0.45:
             cop, keys, defs = {"name": "incr"}, INCR_KEYS, INCR_DEFAULTS
             if r.random() < 0.3:
-                cop["minValue"] = r.choice([3, "a", -1])         # NaN < minValue is false
+                cop["minValue"] = r.choice([3, 0, -1])           # NaN < minValue is false
         elif x < 0.85:
             cop, keys, defs = {"name": "consensus"}, CONS_KEYS, CONS_DEFAULTS
         else:

@@ -8,10 +8,14 @@ undefined:
   * incr: `x += undefined` is NaN for numbers, booleans, null and undefined; NaN is not null, so
     it is stored; JSON.stringify writes it as null; and `NaN !== NaN`, so matchProperties
     (:64-95) fails on it, which stops zamboni merges (mergeTree.ts:1306-1334) and snapshot
-    coalescing (snapshotV1.ts:195-213);
+    coalescing (snapshotV1.ts:195-213).  For a string, array or object it is string
+    concatenation: String(x) + "undefined" ("v" -> "vundefined", [1, [2, "x"]] ->
+    "1,2,xundefined", {} -> "[object Object]undefined"), which a truthy string / array / object
+    minValue replaces when it compares above it (:35-38);
   * consensus: a key without a value becomes {value: undefined, seq} (JSON {"seq":seq}, never
     equal: its `value` is undefined); a defaultValue whose seq is -1 gets the op's seq; any
-    other held value is kept;
+    other held value is kept; a null defaultValue on a key without a value throws (null.seq:
+    the engine's MT_DS_THROWS, a TypeError from the hosts);
   * any other name: the held value or the defaultValue (undefined included: the key is
     present with value undefined, skipped by JSON.stringify, never equal).
 The expected texts below are those rules worked by hand; the oracle (oracle/mtoracle.cpp
@@ -30,6 +34,7 @@ from fluidframework_amd.engine import ClientGroup, Engine, MergeTreeError, snaps
 from oracle_lib import OracleDoc
 
 UNSUPPORTED = 0x08
+THROWS = 0x4000
 LIMITS = dict(rows_per_doc=8192, window_per_doc=4096, propsets_per_doc=8192, text_per_doc=1 << 16)
 
 
@@ -110,14 +115,41 @@ CASES = [
                           ins(4, "z")], ['{"k":null}', '{"k":null}']),
     ("undefined_split_halves", [ins(0, "abcd"), ann(0, 4, {"u": 1}, {"name": "other"}), ins(2, "X"), rem(2, 3),
                                 ins(4, "z")], ['{}', '{}']),
-    # off the batch path (MT_DS_UNSUPPORTED): incr of a string (string concatenation), consensus
-    # on null (the reference throws), consensus writing into a held object whose seq is -1
-    ("incr_string", [ins(0, {"text": "ab", "props": {"s": "v"}}), ann(0, 2, {"s": 1}, {"name": "incr"})], UNSUPPORTED),
-    ("incr_string_default", [ins(0, "ab"), ann(0, 2, {"s": 1}, {"name": "incr", "defaultValue": "v"})], UNSUPPORTED),
+    # incr of a string, array or object: string concatenation with "undefined"
+    ("incr_string", [ins(0, {"text": "ab", "props": {"s": "v"}}), ann(0, 2, {"s": 1}, {"name": "incr"})],
+     ['{"s":"vundefined"}']),
+    ("incr_string_twice", [ins(0, {"text": "ab", "props": {"s": "v"}}), ann(0, 2, {"s": 1}, {"name": "incr"}),
+                           ann(0, 1, {"s": 1}, {"name": "incr"})], ['{"s":"vundefinedundefined"}', '{"s":"vundefined"}']),
+    ("incr_string_default", [ins(0, "ab"), ann(0, 2, {"s": 1}, {"name": "incr", "defaultValue": "v"})],
+     ['{"s":"vundefined"}']),
+    ("incr_held_object_array", [ins(0, {"text": "ab", "props": {"o": {"a": 1}, "r": [1, [2, "x"], None]}}),
+                                ann(0, 2, {"o": 0, "r": 0}, {"name": "incr"})],
+     ['{"o":"[object Object]undefined","r":"1,2,x,undefined"}']),
+    ("incr_default_array", [ins(0, "ab"), ann(0, 2, {"a": 0}, {"name": "incr", "defaultValue": [1, 2]})],
+     ['{"a":"1,2undefined"}']),
+    ("incr_fresh_consensus", [ins(0, "ab"), ann(0, 2, {"c": 1}, {"name": "consensus"}),
+                              ann(0, 2, {"c": 1}, {"name": "incr"})], ['{"c":"[object Object]undefined"}']),
+    # a truthy string minValue above the default's result replaces it ("zzz" > "vundefined");
+    # one below it does not; a number minValue never does (NaN comparison)
+    ("incr_default_min_above", [ins(0, "ab"), ann(0, 2, {"s": 1}, {"name": "incr", "defaultValue": "v",
+                                                                  "minValue": "zzz"})], ['{"s":"zzz"}']),
+    ("incr_default_min_below", [ins(0, "ab"), ann(0, 2, {"s": 1}, {"name": "incr", "defaultValue": "v",
+                                                                  "minValue": "a"})], ['{"s":"vundefined"}']),
+    ("incr_default_min_number", [ins(0, "ab"), ann(0, 2, {"s": 1}, {"name": "incr", "defaultValue": "v",
+                                                                   "minValue": 9})], ['{"s":"vundefined"}']),
+    # another name keeps a held object whose seq is -1 (only consensus writes into it)
+    ("other_held_seq_minus1", [ins(0, {"text": "ab", "props": {"c": {"seq": -1}}}), ann(0, 2, {"c": 1}, {"name": "max"})],
+     ['{"c":{"seq":-1}}']),
+    # the reference throws (null.seq): MT_DS_THROWS
     ("consensus_null_default", [ins(0, "ab"), ann(0, 2, {"c": 1}, {"name": "consensus", "defaultValue": None})],
-     UNSUPPORTED),
+     THROWS),
+    # off the batch path (MT_DS_UNSUPPORTED): consensus writing into a held object whose seq is -1
+    # (every segment split from it shares it), and a held string's incr result that a string
+    # minValue would be compared with
     ("consensus_held_seq_minus1", [ins(0, {"text": "ab", "props": {"c": {"seq": -1}}}),
                                    ann(0, 2, {"c": 1}, {"name": "consensus"})], UNSUPPORTED),
+    ("incr_held_string_min", [ins(0, {"text": "ab", "props": {"s": "v"}}),
+                              ann(0, 2, {"s": 1}, {"name": "incr", "minValue": "zzz"})], UNSUPPORTED),
 ]
 
 
@@ -418,3 +450,42 @@ def test_node_host_chunk_size_on_gpu():
     if NODE is None:
         pytest.skip("node is not installed")
     check_node_chunk_and_combine(os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"))
+
+
+def consensus_null_case():
+    return stream_of(dict((c[0], c[1]) for c in CASES)["consensus_null_default"], msn_lag=0)
+
+
+def test_consensus_null_default_throws_a_type_error_on_emulation():
+    """Where the reference's applyMsg throws (null.seq, properties.ts:51-52) the Python host
+    raises a TypeError too (MT_DS_THROWS), not an "unsupported input"."""
+    from fluidframework_amd.engine import ReferenceTypeError
+    g, c = run_engine(emu_engine, consensus_null_case())
+    assert int(g.engine.status([0])[0]) == THROWS
+    with pytest.raises(TypeError, match="Cannot read property 'seq' of null"):
+        c.getText()
+    with pytest.raises(ReferenceTypeError):
+        c.snapshot()
+
+
+def test_consensus_null_default_throws_a_type_error_in_node_on_emulation(tmp_path):
+    """The Node host throws the reference's TypeError."""
+    import os
+    import subprocess
+    from js_lib import NODE, ROOT
+    from emu_lib import build_emu_napi
+    if NODE is None:
+        pytest.skip("node is not installed")
+    addon = build_emu_napi()
+    script = tmp_path / "t.js"
+    script.write_text(
+        "const mt = require(process.argv[2]);\n"
+        "const g = new mt.ClientGroup(new mt.Engine(1, {}));\n"
+        "const c = g.newClient({ newMergeTreeSnapshotFormat: true });\n"
+        f"for (const m of {json.dumps(consensus_null_case())}) c.applyMsg(m);\n"
+        "try { c.getText(); console.log('no throw'); }\n"
+        "catch (e) { console.log((e instanceof TypeError ? 'TypeError: ' : 'Error: ') + e.message); }\n")
+    r = subprocess.run([NODE, str(script), os.path.join(ROOT, "fluidframework_amd", "js")], capture_output=True,
+                       text=True, env=dict(os.environ, MTGPU_NAPI=addon), timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("TypeError: ") and "Cannot read property 'seq' of null" in r.stdout, r.stdout

@@ -5,7 +5,7 @@
 set -o pipefail
 OUT=gpurun_out/${1:-r06_part}; shift; mkdir -p $OUT
 export PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_combine_known_answers.py \
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_combine_known_answers.py tests/test_message_surface.py \
     > $OUT/pytest_combine.txt 2>&1 || { echo FAIL pytest; tail -30 $OUT/pytest_combine.txt; exit 1; }
 tail -2 $OUT/pytest_combine.txt
 summ() { python -c "import json;d=json.load(open('$1'));print('$2', round(d['value']/1e6,2), 'M ops/s', round(d['ms_per_step'],1), 'ms', d['config'].get('partition'), d['parity'][-48:])"; }
