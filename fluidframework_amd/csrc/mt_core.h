@@ -31,7 +31,8 @@
 
 #define MT_MAXH 16                    // max tree height (7^16 segments)
 #define MT_PSK 16                     // property keys per MtPSet chunk
-#define MT_PKEYS 64                   // keys of one property map, one per lane (more: PROPS_TOO_MANY)
+#define MT_PKEYS MT_MAX_PROP_KEYS      // keys of one property map (more: PROPS_TOO_MANY); up to a
+                                      // wave's 64 one per lane, past that in the pool (applyPropSetWide)
 #ifndef MT_PATH_RESUME
 #define MT_PATH_RESUME 1              // opRange: end walk and range walk start below the root
 #endif
@@ -2336,14 +2337,18 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (a < 0 || b < 0) return false;
         const int na = uni(pset[a].n), nb = uni(pset[b].n);
         if (na != nb) return false;
-        auto ok = wave_map(na, [&](int k) MT_LAM {
-            const int key = pkey(a, k);
-            const uint32_t ca = pclass(pval(a, k));
-            bool f = false;
-            for (int i = 0; i < nb; i++) f |= (int)(pkey(b, i) == key) & (int)(pclass(pval(b, i)) == ca);
-            return (f & (int)(ca != 0xFFFFFFFFu)) != 0;
-        });
-        return wave_count(ok) == na;
+        for (int base = 0; base < na; base += MT_WAVE) {              // a's keys one per lane
+            const int cnt = (na - base) < MT_WAVE ? (na - base) : MT_WAVE;
+            auto ok = wave_map(cnt, [&](int k) MT_LAM {
+                const int key = pkey(a, base + k);
+                const uint32_t ca = pclass(pval(a, base + k));
+                bool f = false;
+                for (int i = 0; i < nb; i++) f |= (int)(pkey(b, i) == key) & (int)(pclass(pval(b, i)) == ca);
+                return (f & (int)(ca != 0xFFFFFFFFu)) != 0;
+            });
+            if (wave_count(ok) != cnt) return false;
+        }
+        return true;
     }
     // Text-arena compaction: copy the text of every linked row into the other
     // half of the document's arena (rows are immutable slices, so garbage from
@@ -2814,19 +2819,121 @@ template <int RES, bool FULL = true> struct MtEngT {
     // and other names): opset is then a combine set whose values are what combine yields
     // for a key the segment does not hold (include/mtgpu.h), and a held key's new value
     // follows from its old one (segmentPropertiesManager.ts:98-109, properties.ts:24-62).
+    // combine(op, previousValue, undefined, seq) for one key: pv the held value (MT_VAL_UNDEF:
+    // not held, a held undefined counts as not held), code what combine yields without one.
+    // Incr of a number / boolean / NaN is NaN, of a string / array / object (a fresh consensus
+    // object included) the interned String(v) + "undefined"; consensus keeps the value unless it
+    // is an object whose seq is -1 (shared by every segment split from the one it was set on);
+    // other names keep it.  MT_VAL_UNSUP after setting the document's status (UNSUPPORTED or
+    // THROWS).
+    MT_HD int combineValue(int pv, int code, int pm, int sq) {
+        int nv = code;
+        if (pv != MT_VAL_UNDEF) {
+            const int vi = pv >= 0 ? uni(S.p_vinfo[pv]) : (pv == MT_VAL_NAN ? MT_VAL_NAN : uni(S.p_vinfo[-1]));
+            if (pm == MT_PM_INCR || pm == MT_PM_INCR_SMIN) {
+                const int sid = vi & MT_VINFO_ID;
+                nv = vi == MT_VAL_NAN ? MT_VAL_NAN
+                                      : ((vi < 0 || sid == MT_VINFO_NONE || pm == MT_PM_INCR_SMIN) ? MT_VAL_UNSUP : sid);
+            } else if (pm == MT_PM_CONS) nv = (pv >= 0 && vi >= 0 && (vi & MT_VINFO_SEQM1)) ? MT_VAL_UNSUP : pv;
+            else nv = pv;
+        }
+        if (nv == MT_VAL_CFRESH) nv = (sq >= 0 && sq <= 0x7FFFFFEF) ? MT_VAL_CONS(sq) : MT_VAL_UNSUP;   // -16 - seq fits int32
+        if (nv == MT_VAL_THROW) { status |= MT_DS_THROWS; return MT_VAL_UNSUP; }
+        if (nv == MT_VAL_UNSUP) status |= MT_DS_UNSUPPORTED;
+        return nv;
+    }
+    // Whether key `key` survives a rewrite by op set [o0, o1): the set gives it a truthy value.
+    MT_HD bool rewriteKeeps(int key, int o0, int o1) const {
+        bool kp = false;
+        for (int q = o0; q < o1; q++) if ((int)S.p_key[q] == key) { const int nv = S.p_val[q]; kp = nv >= 0 && !S.p_falsy[nv]; }
+        return kp;
+    }
+    // applyPropSet past one key per lane (the old map and the op set together above MT_WAVE
+    // keys): the new map is built in place in the pool at psetTop, chunk by chunk, and
+    // committed at the end (nothing is allocated on an early return).
+    MT_HD int applyPropSetWide(int old, int opset, int pm, int sq) {
+        const int n0 = old >= 0 ? uni(pset[old].n) : 0;
+        const int o0 = uni((int)S.p_off[opset]), o1 = uni((int)S.p_off[opset + 1]);
+        const int room = (n0 + (o1 - o0)) < MT_PKEYS ? n0 + (o1 - o0) : MT_PKEYS;
+        const int chCap = room > MT_PSK ? (room + MT_PSK - 1) / MT_PSK : 1;
+        if (psetTop + chCap > (int)S.psetCap) { status |= MT_DS_OOM_PROPS; return old; }
+        if (pm >= MT_PM_INCR && !S.p_vinfo) { status |= MT_DS_UNSUPPORTED; return old; }
+        const int id = psetTop;
+        int n = 0;
+        for (int base = 0; base < n0; base += MT_WAVE) {          // the old map (rewrite: the kept keys)
+            const int cnt = (n0 - base) < MT_WAVE ? (n0 - base) : MT_WAVE;
+            const auto k = wave_map(cnt, [&](int i) MT_LAM { return pkey(old, base + i); });
+            const auto v = wave_map(cnt, [&](int i) MT_LAM { return pval(old, base + i); });
+            const auto keep = wave_map(cnt, [&](int i) MT_LAM { return pm != MT_PM_REWRITE || rewriteKeeps(own(k, i), o0, o1); });
+            const auto rk = wave_rank(keep);
+            const int m = n;
+            wave_for(cnt, [&](int i) MT_LAM {
+                if (own(keep, i)) { const int j = m + own(rk, i); pset[id + (j >> 4)].key[j & 15] = (uint16_t)own(k, i); pset[id + (j >> 4)].val[j & 15] = own(v, i); }
+            });
+            n += wave_count(keep);
+        }
+        wave_sync();
+        for (int q = o0; q < o1; q++) {
+            const int key = uni((int)S.p_key[q]);
+            int nv = uni((int)S.p_val[q]);
+            int at = -1;
+            for (int base = 0; base < n && at < 0; base += MT_WAVE) {
+                const int cnt = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
+                const int f = wave_first(wave_map(cnt, [&](int i) MT_LAM { return pkey(id, base + i) == key; }));
+                if (f >= 0) at = base + f;
+            }
+            if (pm >= MT_PM_INCR) {
+                nv = combineValue(at >= 0 ? uni(pval(id, at)) : MT_VAL_UNDEF, nv, pm, sq);
+                if (nv == MT_VAL_UNSUP) return old;
+            }
+            if (nv == MT_VAL_NULL) {
+                if (at >= 0) {                                     // the keys after it move down one
+                    for (int base = at; base < n - 1; base += MT_WAVE) {
+                        const int cnt = (n - 1 - base) < MT_WAVE ? (n - 1 - base) : MT_WAVE;
+                        const auto k = wave_map(cnt, [&](int i) MT_LAM { return pkey(id, base + i + 1); });
+                        const auto v = wave_map(cnt, [&](int i) MT_LAM { return pval(id, base + i + 1); });
+                        wave_sync();
+                        wave_for(cnt, [&](int i) MT_LAM {
+                            const int j = base + i;
+                            pset[id + (j >> 4)].key[j & 15] = (uint16_t)own(k, i); pset[id + (j >> 4)].val[j & 15] = own(v, i);
+                        });
+                        wave_sync();
+                    }
+                    n--;
+                }
+            } else if (at >= 0) {
+                wave_for(1, [&](int) MT_LAM { pset[id + (at >> 4)].val[at & 15] = nv; });
+            } else {
+                if (n >= MT_PKEYS) { status |= MT_DS_PROPS_TOO_MANY; return old; }
+                const int j = n;
+                wave_for(1, [&](int) MT_LAM { pset[id + (j >> 4)].key[j & 15] = (uint16_t)key; pset[id + (j >> 4)].val[j & 15] = nv; });
+                n++;
+            }
+            wave_sync();
+        }
+        const int nch = n > MT_PSK ? (n + MT_PSK - 1) / MT_PSK : 1;
+        int never = 0;
+        if (pm >= MT_PM_INCR || mt_cold_v.pNever)
+            for (int base = 0; base < n; base += MT_WAVE) {
+                const int cnt = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
+                never |= wave_ballot(wave_map(cnt, [&](int i) MT_LAM { return pval(id, base + i) < 0; })) ? 1 : 0;
+            }
+        if (never) mt_cold_v.pNever = 1;
+        wave_for(nch * MT_PSK - n, [&](int i) MT_LAM { const int j = n + i; pset[id + (j >> 4)].key[j & 15] = 0; pset[id + (j >> 4)].val[j & 15] = 0; });
+        wave_for(nch, [&](int k) MT_LAM { pset[id + k].n = n; pset[id + k].pad[2] = never; });
+        wave_sync();
+        psetTop += nch;
+        return id;
+    }
     MT_HD int applyPropSet(int old, int opset, int pm, int sq = 0) {
         if (opset < 0 || opset >= (int)S.p_nsets) { status |= MT_DS_UNSUPPORTED; return old; }
         int n = old >= 0 ? uni(pset[old].n) : 0;
+        if (n + (uni((int)S.p_off[opset + 1]) - uni((int)S.p_off[opset])) > MT_WAVE) return applyPropSetWide(old, opset, pm, sq);
         auto kk = wave_map(n, [&](int i) MT_LAM { return pkey(old, i); });
         auto vv = wave_map(n, [&](int i) MT_LAM { return pval(old, i); });
         const int o0 = uni((int)S.p_off[opset]), o1 = uni((int)S.p_off[opset + 1]);
         if (pm == MT_PM_REWRITE && n > 0) {
-            auto keep = wave_map(n, [&](int i) MT_LAM {
-                const int key = own(kk, i);
-                bool kp = false;
-                for (int q = o0; q < o1; q++) if ((int)S.p_key[q] == key) { const int nv = S.p_val[q]; kp = nv >= 0 && !S.p_falsy[nv]; }
-                return kp;
-            });
+            auto keep = wave_map(n, [&](int i) MT_LAM { return rewriteKeeps(own(kk, i), o0, o1); });
             auto rk = wave_rank(keep);
             const int cntk = wave_count(keep);
             // compaction through the hold scratch (free here: no scour or collect is in flight)
@@ -2838,45 +2945,27 @@ template <int RES, bool FULL = true> struct MtEngT {
             wave_sync();
         }
         if (pm >= MT_PM_INCR && !S.p_vinfo) { status |= MT_DS_UNSUPPORTED; return old; }
-        const bool incr = pm == MT_PM_INCR || pm == MT_PM_INCR_SMIN;
         for (int q = o0; q < o1; q++) {
             const int key = uni((int)S.p_key[q]);
             int nv = uni((int)S.p_val[q]);
             const int at = wave_first(wave_map(n, [&](int i) MT_LAM { return own(kk, i) == key; }));
             if (pm >= MT_PM_INCR) {
-                // combine(op, previousValue, undefined, seq): a held value undefined counts as
-                // not held; incr of a number / boolean / NaN is NaN, of a string / array /
-                // object (a fresh consensus object included) the interned String(v) +
-                // "undefined"; consensus keeps the value unless it is an object whose seq is -1
-                // (shared by every segment split from the one it was set on); other names keep it
-                const int pv = at >= 0 ? wave_at(vv, at) : MT_VAL_UNDEF;
-                if (pv != MT_VAL_UNDEF) {
-                    const int vi = pv >= 0 ? uni(S.p_vinfo[pv]) : (pv == MT_VAL_NAN ? MT_VAL_NAN : uni(S.p_vinfo[-1]));
-                    if (incr) {
-                        const int sid = vi & MT_VINFO_ID;
-                        nv = vi == MT_VAL_NAN ? MT_VAL_NAN
-                                              : ((vi < 0 || sid == MT_VINFO_NONE || pm == MT_PM_INCR_SMIN) ? MT_VAL_UNSUP : sid);
-                    } else if (pm == MT_PM_CONS) nv = (pv >= 0 && vi >= 0 && (vi & MT_VINFO_SEQM1)) ? MT_VAL_UNSUP : pv;
-                    else nv = pv;
-                }
-                if (nv == MT_VAL_CFRESH) nv = (sq >= 0 && sq <= 0x7FFFFFEF) ? MT_VAL_CONS(sq) : MT_VAL_UNSUP;   // -16 - seq fits int32
-                if (nv == MT_VAL_THROW) { status |= MT_DS_THROWS; return old; }
-                if (nv == MT_VAL_UNSUP) { status |= MT_DS_UNSUPPORTED; return old; }
+                nv = combineValue(at >= 0 ? wave_at(vv, at) : MT_VAL_UNDEF, nv, pm, sq);
+                if (nv == MT_VAL_UNSUP) return old;
             }
             if (nv == MT_VAL_NULL) {
                 if (at >= 0) {
                     auto k1 = wave_from(kk, 1), v1 = wave_from(vv, 1);
-                    kk = wave_map(MT_PKEYS, [&](int i) MT_LAM { const int a = own(kk, i), b = own(k1, i); return i < at ? a : b; });
-                    vv = wave_map(MT_PKEYS, [&](int i) MT_LAM { const int a = own(vv, i), b = own(v1, i); return i < at ? a : b; });
+                    kk = wave_map(MT_WAVE, [&](int i) MT_LAM { const int a = own(kk, i), b = own(k1, i); return i < at ? a : b; });
+                    vv = wave_map(MT_WAVE, [&](int i) MT_LAM { const int a = own(vv, i), b = own(v1, i); return i < at ? a : b; });
                     n--;
                 }
             } else if (at >= 0) {
-                vv = wave_map(MT_PKEYS, [&](int i) MT_LAM { return i == at ? nv : own(vv, i); });
+                vv = wave_map(MT_WAVE, [&](int i) MT_LAM { return i == at ? nv : own(vv, i); });
             } else {
-                if (n >= MT_PKEYS) { status |= MT_DS_PROPS_TOO_MANY; return old; }
-                const int at2 = n;
-                kk = wave_map(MT_PKEYS, [&](int i) MT_LAM { return i == at2 ? key : own(kk, i); });
-                vv = wave_map(MT_PKEYS, [&](int i) MT_LAM { return i == at2 ? nv : own(vv, i); });
+                const int at2 = n;                   // n + (o1 - o0) <= MT_WAVE here
+                kk = wave_map(MT_WAVE, [&](int i) MT_LAM { return i == at2 ? key : own(kk, i); });
+                vv = wave_map(MT_WAVE, [&](int i) MT_LAM { return i == at2 ? nv : own(vv, i); });
                 n++;
             }
         }

@@ -439,7 +439,7 @@ class Engine:
 
     def doc_pset(self, doc: int, pset_id: int):
         """(key ids, value ids) of a document's device property set, insertion order."""
-        k, v, n = np.zeros(64, np.uint16), np.zeros(64, np.int32), ctypes.c_uint32()
+        k, v, n = np.zeros(256, np.uint16), np.zeros(256, np.int32), ctypes.c_uint32()   # MT_MAX_PROP_KEYS
         self._check(self.fn["doc_pset"](self.h, doc, pset_id, k.ctypes.data, v.ctypes.data, ctypes.byref(n)),
                     "mt_doc_pset")
         return k[:n.value].copy(), v[:n.value].copy()

@@ -611,10 +611,10 @@ napi_value DocPset(napi_env env, napi_callback_info info) {
     mt_ctx* c = get_ctx(env, argv[0]); if (!c) return nullptr;
     uint32_t doc = 0; int32_t id = -1;
     napi_get_value_uint32(env, argv[1], &doc); napi_get_value_int32(env, argv[2], &id);
-    uint16_t k[64]; int32_t v[64]; uint32_t n = 0;
+    uint16_t k[MT_MAX_PROP_KEYS]; int32_t v[MT_MAX_PROP_KEYS]; uint32_t n = 0;
     int rc = mt_doc_pset(c, doc, id, k, v, &n);
     if (rc) return throw_rc(env, c, rc, "mt_doc_pset");
-    uint32_t k32[64];
+    uint32_t k32[MT_MAX_PROP_KEYS];
     for (uint32_t i = 0; i < n; i++) k32[i] = k[i];
     napi_value o;
     napi_create_object(env, &o);

@@ -603,8 +603,9 @@ int  mt_delta_records(mt_ctx* ctx, const mt_delta_rec** out, uint64_t* n);
  * launches the batch took. */
 int  mt_delta_text(mt_ctx* ctx, const uint16_t** out, uint64_t* n, uint32_t* launches);
 /* The keys and values (host-interned ids, value -1 never occurs) of property set
- * pset_id of document doc, in insertion order; returns the count in *n (<= 64: keys and
- * values must have room for 64 entries). */
+ * pset_id of document doc, in insertion order; returns the count in *n (<= MT_MAX_PROP_KEYS:
+ * keys and values must have room for MT_MAX_PROP_KEYS entries). */
+#define MT_MAX_PROP_KEYS 256   /* keys of one segment's property map (more: MT_DS_PROPS_TOO_MANY) */
 int  mt_doc_pset(mt_ctx* ctx, uint32_t doc, int32_t pset_id, uint16_t* keys, int32_t* values, uint32_t* n);
 int  mt_dump_segments(mt_ctx* ctx, uint32_t doc_id, int32_t** rows, uint32_t* n_rows);
 void mt_free(void* p);

@@ -38,6 +38,9 @@ KEYS = ["0", "1", "2", "10", "k", "bold", "a b", "ключ", "x\"y", "4294967295
 # wide property maps (the "wide_props" surface): 45 more keys, index-like ones among them, so
 # one segment's map grows well past 16 keys (56 distinct keys at most: within MT_PKEYS = 64)
 WIDE_KEYS = KEYS + [f"w{i}" for i in range(36)] + ["3", "7", "11", "12", "40", "99", "100", "1000", "255"]
+# very wide maps (the "very_wide_props" surface): 220 distinct keys, so one segment's map grows
+# past a wave's 64 lanes (applyPropSetWide) toward MT_MAX_PROP_KEYS = 256
+VERY_WIDE_KEYS = WIDE_KEYS + [f"v{i}" for i in range(164)]
 VALUES = ["s", "ü", "", 0, 1, -3, 1.5, 1e21, 0.25, True, False, {"a": 1}, [1, 2], {"0": "x", "b": [True]},
           {"n": None}, "😀"]
 # remote combining ops (the "combine" surface, MT/properties.ts:24-62 via
@@ -60,7 +63,7 @@ class StreamGen:
                  p_special: float = 0.25, long_every: int = 40, max_ins: int = 9, id_prefix: str = "cli",
                  max_total_clients: int | None = None, p_marker_id: float = 0.0, p_relative: float = 0.0,
                  capture: bool = False, p_register: float = 0.0, p_wide: float = 0.0, reg_names: int = 0,
-                 reg_span: int = 10, p_combine: float = 0.0):
+                 reg_span: int = 10, p_combine: float = 0.0, p_vwide: float = 0.0):
         self.rng = random.Random(seed)
         self.lag, self.churn, self.p_nonop, self.p_group = lag, churn, p_nonop, p_group
         self.p_marker, self.p_annotate, self.p_remove, self.p_special = p_marker, p_annotate, p_remove, p_special
@@ -75,6 +78,7 @@ class StreamGen:
         self.reg_names = [f"r{i}" for i in range(reg_names)] if reg_names else self.REGS
         self.reg_span = reg_span
         self.p_combine = p_combine
+        self.p_vwide = p_vwide
         self.total = 0
         self.active: dict[str, int] = {}          # long id -> latest refSeq
         for _ in range(clients):
@@ -106,8 +110,9 @@ class StreamGen:
         r = self.rng
         d = {}
         wide = self.p_wide > 0 and r.random() < self.p_wide     # (no draw otherwise: other surfaces keep their streams)
-        for _ in range(r.randint(18, 45) if wide else r.randint(1, 3)):
-            k = r.choice(WIDE_KEYS if wide else KEYS)
+        vwide = self.p_vwide > 0 and r.random() < self.p_vwide
+        for _ in range(r.randint(60, 140) if vwide else (r.randint(18, 45) if wide else r.randint(1, 3))):
+            k = r.choice(VERY_WIDE_KEYS if vwide else (WIDE_KEYS if wide else KEYS))
             d[k] = None if (allow_null and r.random() < 0.2) else r.choice(VALUES)
         if self.p_combine and r.random() < 0.5:          # plain values on the combining ops' keys
             if r.random() < 0.5:

@@ -489,3 +489,32 @@ def test_consensus_null_default_throws_a_type_error_in_node_on_emulation(tmp_pat
                        text=True, env=dict(os.environ, MTGPU_NAPI=addon), timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("TypeError: ") and "Cannot read property 'seq' of null" in r.stdout, r.stdout
+
+
+def key_limit_case(factory):
+    """A map of MT_MAX_PROP_KEYS (256) keys replays equal to the oracle (segment props past a
+    wave's 64 lanes: applyPropSetWide); one key more sets MT_DS_PROPS_TOO_MANY."""
+    full = {f"k{i}": i for i in range(256)}
+    ops = [ins(0, {"text": "ab", "props": {f"k{i}": i for i in range(100)}}), ins(2, "cd"),
+           ann(0, 4, {f"k{i}": -i for i in range(60, 256)}), ann(1, 3, {"k5": None, "k200": None}),
+           ann(0, 4, {"k5": 1, "k200": 2}, {"name": "rewrite"}), ann(2, 4, full)]
+    check_engine_case(factory, ops, props_texts(_oracle_blobs(ops)))
+    g, _ = run_engine(factory, stream_of([ins(0, {"text": "x", "props": {**full, "one_more": 1}})], msn_lag=0))
+    assert int(g.engine.status([0])[0]) & 0x400
+
+
+def _oracle_blobs(ops):
+    msgs = stream_of(ops, msn_lag=0)
+    o = OracleDoc(True)
+    for m in msgs:
+        assert o.apply_msg(m) == 0
+    return o.snapshot(msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"])[0]
+
+
+def test_prop_key_limit_on_emulation():
+    key_limit_case(emu_engine)
+
+
+@pytest.mark.gpu
+def test_prop_key_limit_on_gpu():
+    key_limit_case(lambda n, **kw: Engine(n, device=0, **kw))

@@ -18,7 +18,7 @@ from test_emu_parity import CONFIGS, ann_props
 
 pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 
-EXPORTS = ["applyBatch", "create", "deltaCapture", "deltaRecords", "deltaText", "destroy", "docPset", "docStatus", "docsOpen",
+EXPORTS = ["applyBatch", "applyBatchParts", "create", "deltaCapture", "deltaRecords", "deltaText", "destroy", "docPset", "docStatus", "docsOpen",
            "getContainingSegment", "getLength", "getText", "lastError",
            "loadSnapshot", "reserveStaging", "setClientNames", "setDocClientNames", "setDocSnapshotChunk", "setProps", "setResidency", "snapshotLegacy", "snapshotV1", "sync",
            "syncAsync",

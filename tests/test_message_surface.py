@@ -40,6 +40,7 @@ SURFACES = {
                            p_annotate=0.35, long_every=0),
     # property maps of 18-56 keys (segment specs and annotates): several MtPSet chunks per map
     "wide_props": dict(clients=3, lag=10, p_annotate=0.45, p_marker=0.15, p_wide=0.5),
+    "very_wide_props": dict(clients=3, lag=10, p_annotate=0.45, p_marker=0.15, p_vwide=0.5),
     # remote combining ops "incr" / "consensus" / other names (MT/properties.ts:24-62): NaN,
     # {seq} objects and undefined values, which never matchProperties-match (zamboni and
     # snapshot coalescing stop at them)
@@ -121,6 +122,11 @@ def test_stream_generator_covers_the_surface():
     segs = [x["json"] if isinstance(x, dict) and "json" in x else x for b in blobs for x in json.loads(b).get("segments", [])]
     widths = [len(j["props"]) for j in segs if isinstance(j, dict) and "props" in j]
     assert max(widths) > 32 and sum(w > 16 for w in widths) > 20      # maps of several MtPSet chunks
+    msgs, obs = stream(11, 1200, **SURFACES["very_wide_props"])
+    blobs, _ = obs.snapshot(msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"])
+    segs = [x["json"] if isinstance(x, dict) and "json" in x else x for b in blobs for x in json.loads(b).get("segments", [])]
+    widths = [len(j["props"]) for j in segs if isinstance(j, dict) and "props" in j]
+    assert max(widths) > 150 and sum(w > 64 for w in widths) > 20     # past one key per lane
 
 
 @pytest.mark.gpu
