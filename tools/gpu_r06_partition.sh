@@ -5,9 +5,9 @@
 set -o pipefail
 OUT=gpurun_out/${1:-r06_part}; shift; mkdir -p $OUT
 export PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_combine_known_answers.py tests/test_message_surface.py \
-    > $OUT/pytest_combine.txt 2>&1 || { echo FAIL pytest; tail -30 $OUT/pytest_combine.txt; exit 1; }
-tail -2 $OUT/pytest_combine.txt
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests \
+    > $OUT/pytest_gpu.txt 2>&1 || { echo FAIL pytest; tail -30 $OUT/pytest_gpu.txt; exit 1; }
+tail -2 $OUT/pytest_gpu.txt
 summ() { python -c "import json;d=json.load(open('$1'));print('$2', round(d['value']/1e6,2), 'M ops/s', round(d['ms_per_step'],1), 'ms', d['config'].get('partition'), d['parity'][-48:])"; }
 timeout -k 10 400 python -u bench.py --config config5 --steps 3 --warmup 1 --no-cpu-baseline > $OUT/c5_auto.json 2> $OUT/c5_auto.err \
     || { echo FAIL c5; tail -20 $OUT/c5_auto.err; exit 1; }
