@@ -61,6 +61,17 @@ MT_HD void mt_gen_op(Eng& e, const MtOps& ops, uint32_t i, uint32_t k, uint32_t 
     wave_sync();
 }
 
+#if defined(MT_WTRACE) && !defined(__HIP_DEVICE_COMPILE__)
+// Host-emulation diagnostic (tools/write_sites.py): the HBM lines each message dirtied, by pool.
+void mt_wtrace_begin(uint32_t doc);
+void mt_wtrace_msg(uint32_t doc, int phase);
+#define MT_WT_BEGIN(doc) mt_wtrace_begin(doc)
+#define MT_WT_MSG(doc, ph) mt_wtrace_msg(doc, ph)
+#else
+#define MT_WT_BEGIN(doc) ((void)0)
+#define MT_WT_MSG(doc, ph) ((void)0)
+#endif
+
 // Applies ops [o0, op_off[run+1]) of the run.  With LDS pools (e.lds) it stops
 // before an op that could outgrow them and returns that op's index, so the HBM
 // kernel can resume there; otherwise it returns op_off[run+1].
@@ -186,6 +197,7 @@ MT_HD uint32_t mt_replay_run(Eng& e, const MtOps& ops, uint32_t run, uint32_t do
             if (e.curSeq > sq) { e.status |= MT_DS_ASSERT_SEQ; break; }
             e.curSeq = sq;
             e.setMinSeq(ms);
+            MT_WT_MSG(doc, 0);
 #if defined(MT_EVCOUNT3) && !defined(__HIP_DEVICE_COMPILE__)
             {   // host emulation: blocks a message added (op and zamboni) beyond 2 * height at its start
                 const int used = e.blkTop - e.blkFreeN;
@@ -219,6 +231,7 @@ MT_HD uint32_t mt_replay_doc(const MtState& S, const MtOps& ops, uint32_t run, M
     const uint32_t o0 = ops.start ? ops.start[run] : ops.op_off[run];
     uint32_t cur = o0, stop = o1;
     if (o0 < o1) {
+        MT_WT_BEGIN(doc);
         MtEngT<RES, FULL> e;
         e.bind(S, doc, sc);
         if constexpr (RES == MT_RES_HBM) { (void)l0; (void)l1; (void)l2; cur = mt_replay_run(e, ops, run, doc, nullptr, nullptr, o0); }
@@ -228,6 +241,7 @@ MT_HD uint32_t mt_replay_doc(const MtState& S, const MtOps& ops, uint32_t run, M
         }
         const bool stopped = e.dStop != 0;
         e.store(doc);
+        MT_WT_MSG(doc, 1);                                       // the write-back at the run's end
         if (stopped) { stop = cur; cur = o1; }                   // no hand-over: the host resumes it
         else if (RES != MT_RES_LDS && CONT && cur < o1) {
             // A document that outgrew LDS continues here with its pools in HBM (no second
@@ -237,6 +251,7 @@ MT_HD uint32_t mt_replay_doc(const MtState& S, const MtOps& ops, uint32_t run, M
             const uint32_t c2 = mt_replay_run(h, ops, run, doc, nullptr, nullptr, cur);
             if (h.dStop) stop = c2;
             h.store(doc);
+            MT_WT_MSG(doc, 1);
             cur |= MT_CUR_DONE;                              // finished here: no second launch
         }
     }

@@ -152,3 +152,80 @@ extern "C" int emu_test_heap(mt_ctx* c, uint32_t doc, const int32_t* ops, int n,
     }
     return np;
 }
+
+#if defined(MT_WTRACE)
+// Write tracing (diagnostic builds only, -DMT_WTRACE; tools/write_sites.py): after every message
+// of a replay the document's HBM pools are compared with a shadow copy, and every 64-byte line
+// that changed is counted against its pool (rows also per field).  Under LDS residency the blocks
+// and heap stay out of the pools until the run's write-back, which counts as phase 1.  A line
+// rewritten by several messages counts once per message (a GPU's L2 merges such writes only while
+// the line stays resident).
+namespace {
+mt_ctx* g_wt = nullptr;
+enum { WT_ROWS, WT_BLK, WT_HEAP, WT_WIN, WT_UID, WT_UDELTA, WT_UANC, WT_TEXT, WT_PSET, WT_HDR, WT_HOLD, WT_OVX, WT_MID,
+       WT_REG, WT_REGR, WT_N };
+struct WtRegion { uint8_t* base; size_t bytes; };
+std::vector<std::vector<uint8_t>> g_shadow(WT_N);
+unsigned long long g_lines[2][WT_N], g_rowField[12], g_msgs;
+WtRegion wt_region(uint32_t doc, int k) {
+    const MtState& S = g_wt->S; const MtDocLayout& y = g_wt->layout_h[doc];
+    switch (k) {
+    case WT_ROWS: return {(uint8_t*)(S.rows + y.row), sizeof(MtRow) * y.rowCap};
+    case WT_BLK: return {(uint8_t*)(S.blk + y.blk), sizeof(MtBlk) * y.blkCap};
+    case WT_HEAP: return {(uint8_t*)(S.heap + y.heap), sizeof(MtHeapE) * (y.heapCap + 1)};
+    case WT_WIN: return {(uint8_t*)(S.win + y.win), 4ull * y.winCap};
+    case WT_UID: return {(uint8_t*)(S.uid + y.win), 4ull * y.winCap};
+    case WT_UDELTA: return {(uint8_t*)(S.udelta + y.win), 4ull * y.winCap};
+    case WT_UANC: return {(uint8_t*)(S.uanc + y.anc), 4ull * y.winCap * MT_MAXH};
+    case WT_TEXT: return {(uint8_t*)(S.text + y.text), 4ull * y.textCap};
+    case WT_PSET: return {(uint8_t*)(S.pset + y.pset), sizeof(MtPSet) * y.psetCap};
+    case WT_HDR: return {(uint8_t*)(S.hdr + doc), sizeof(MtDocHdr)};
+    case WT_HOLD: return {(uint8_t*)(S.hold + (size_t)doc * MT_RFL), 4ull * MT_RFL};
+    case WT_OVX: return {(uint8_t*)(S.ovx + (size_t)doc * MT_OVX_CAP), sizeof(MtOvx) * MT_OVX_CAP};
+    case WT_MID: return {(uint8_t*)(S.mid + y.mid), 4ull * y.midCap};
+    case WT_REG: return {(uint8_t*)(S.reg + (size_t)doc * MT_REG_CAP), sizeof(MtReg) * MT_REG_CAP};
+    default: return {(uint8_t*)(S.regr + y.regr), 8ull * y.regCap};
+    }
+}
+}  // namespace
+void mt_wtrace_begin(uint32_t doc) {
+    if (!g_wt) return;
+    for (int k = 0; k < WT_N; k++) { const WtRegion r = wt_region(doc, k); g_shadow[k].assign(r.base, r.base + r.bytes); }
+}
+void mt_wtrace_msg(uint32_t doc, int phase) {
+    if (!g_wt) return;
+    if (phase == 0) g_msgs++;
+    for (int k = 0; k < WT_N; k++) {
+        const WtRegion r = wt_region(doc, k);
+        uint8_t* sh = g_shadow[k].data();
+        const uintptr_t a0 = (uintptr_t)r.base;
+        for (size_t pg = 0; pg < r.bytes; pg += 4096) {           // pages first, then 64-byte lines
+            const size_t pn = std::min<size_t>(4096, r.bytes - pg);
+            if (!memcmp(sh + pg, r.base + pg, pn)) continue;
+            for (size_t o = pg; o < pg + pn;) {
+                const size_t lineEnd = std::min(pg + pn, (size_t)(((a0 + o) / 64 + 1) * 64 - a0));
+                if (memcmp(sh + o, r.base + o, lineEnd - o)) {
+                    g_lines[phase][k]++;
+                    if (k == WT_ROWS)
+                        for (size_t b = o; b < lineEnd; b += 4)
+                            if (memcmp(sh + b, r.base + b, 4)) g_rowField[(b % sizeof(MtRow)) / 4]++;
+                    memcpy(sh + o, r.base + o, lineEnd - o);
+                }
+                o = lineEnd;
+            }
+        }
+    }
+}
+// on = 1: start tracing on c (counters reset); on = 0: stop and copy the counters out:
+// [2][WT_N] lines (per message / at run ends), 12 row-field dword counts, messages.
+extern "C" int emu_wtrace(mt_ctx* c, int on, unsigned long long* out) {
+    if (on) { g_wt = c; memset(g_lines, 0, sizeof g_lines); memset(g_rowField, 0, sizeof g_rowField); g_msgs = 0; return WT_N; }
+    g_wt = nullptr;
+    if (out) {
+        memcpy(out, g_lines, sizeof g_lines);
+        memcpy(out + 2 * WT_N, g_rowField, sizeof g_rowField);
+        out[2 * WT_N + 12] = g_msgs;
+    }
+    return WT_N;
+}
+#endif
