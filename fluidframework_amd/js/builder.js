@@ -187,11 +187,21 @@ const COLS = [["type", Uint8Array], ["flags", Uint8Array], ["client", Uint16Arra
     ["refSeq", Int32Array], ["msn", Int32Array], ["pos1", Int32Array], ["pos2", Int32Array],
     ["payloadOff", Uint32Array], ["payloadLen", Uint32Array], ["propId", Int32Array]];
 
-/** A growable typed-array column (amortized doubling; no per-element JS objects). */
+/** A growable typed-array column (amortized doubling; no per-element JS objects).  shared: its
+ * memory is a SharedArrayBuffer, so a worker that keeps one builder for many batches hands each
+ * batch's columns to the main thread without copying, and allocates nothing per batch (new
+ * ArrayBuffers count as external memory, and their growth makes V8 mark the whole heap: with
+ * the documents' parsed messages held in the worker, that is most of a window's packing time). */
 class Col {
-    constructor(T, cap = 1024) { this.T = T; this.a = new T(cap); this.n = 0; }
+    constructor(T, cap = 1024, shared = false) { this.T = T; this.shared = shared; this.a = this.alloc(cap); this.n = 0; }
+    alloc(cap) { return this.shared ? new this.T(new SharedArrayBuffer(cap * this.T.BYTES_PER_ELEMENT)) : new this.T(cap); }
+    grow(need) {
+        let cap = this.a.length * 2;
+        while (cap < need) cap *= 2;
+        const b = this.alloc(cap); b.set(this.a.subarray(0, this.n)); this.a = b;
+    }
     push(v) {
-        if (this.n === this.a.length) { const b = new this.T(this.a.length * 2); b.set(this.a); this.a = b; }
+        if (this.n === this.a.length) this.grow(this.n + 1);
         this.a[this.n++] = v;
     }
     view() { return this.a.subarray(0, this.n); }
@@ -200,10 +210,16 @@ class Col {
 /** Packs ISequencedDocumentMessages (protocol.ts:126-166) into mt_op_batch runs, straight
  * into typed-array columns. */
 class BatchBuilder {
-    constructor(props, names) {
+    constructor(props, names, shared = false) {
         this.props = props; this.names = names;
-        this.cols = {}; for (const [n, T] of COLS) this.cols[n] = new Col(T);
-        this.payload = new Col(Uint16Array, 4096); this.docIds = []; this.offsets = [0]; this.rel = [];
+        this.cols = {}; for (const [n, T] of COLS) this.cols[n] = new Col(T, 1024, shared);
+        this.payload = new Col(Uint16Array, 4096, shared); this.docIds = []; this.offsets = [0]; this.rel = [];
+    }
+    /** Empty again, keeping the columns' memory (a worker's builder, batch after batch). */
+    reset(props) {
+        this.props = props;
+        for (const k in this.cols) this.cols[k].n = 0;
+        this.payload.n = 0; this.docIds = []; this.offsets = [0]; this.rel = [];
     }
     get nOps() { return this.cols.type.n; }
     /** op.pos{k}, or op.relativePos{k} as an index into rel (getValidOpRange, client.ts:506-523). */
@@ -319,10 +335,7 @@ class BatchBuilder {
     reserve(n) {
         for (const k in this.cols) {
             const col = this.cols[k];
-            if (col.n + n <= col.a.length) continue;
-            let cap = col.a.length;
-            while (cap < col.n + n) cap *= 2;
-            const b = new col.T(cap); b.set(col.a.subarray(0, col.n)); col.a = b;
+            if (col.n + n > col.a.length) col.grow(col.n + n);
         }
     }
     /**
@@ -361,11 +374,7 @@ class BatchBuilder {
             }
             if (t === OP_INSERT) {
                 const seg = ct.seg, L = seg.length;
-                if (pay.n + L > pay.a.length) {
-                    let cap = pay.a.length * 2;
-                    while (cap < pay.n + L) cap *= 2;
-                    const b = new Uint16Array(cap); b.set(pay.a.subarray(0, pay.n)); pay.a = b;
-                }
+                if (pay.n + L > pay.a.length) pay.grow(pay.n + L);
                 const pa = pay.a, q = pay.n;
                 for (let j = 0; j < L; j++) pa[q + j] = seg.charCodeAt(j);
                 pay.n = q + L;

@@ -39,6 +39,7 @@ function binToJson(file, windows, objects = false) {
     return texts;
 }
 const held = new Map();            // doc id -> its stream's window JSON texts (ParallelPacker.prepare)
+let shared = null;                 // the worker's builder: shared-memory columns reused batch after batch
 const heldNames = new Map();       // doc id -> its ClientNames, kept across windows
 
 parentPort.on("message", ({ docs, prepare, windows, objects, resetNames }) => {
@@ -59,7 +60,9 @@ parentPort.on("message", ({ docs, prepare, windows, objects, resetNames }) => {
     }
     try {
         const props = new PropTable();
-        const bb = new BatchBuilder(props, null);
+        if (!shared) shared = new BatchBuilder(props, null, true);
+        const bb = shared;
+        bb.reset(props);
         const names = [];
         for (const d of docs) {
             let nm = d.held ? heldNames.get(d.id) : undefined;
@@ -73,16 +76,12 @@ parentPort.on("message", ({ docs, prepare, windows, objects, resetNames }) => {
             names.push(nm.names.slice());
         }
         const nPayload = bb.payload.n;
-        const b = bb.build();
-        const batch = {};
-        const transfer = [];
-        for (const k of Object.keys(b)) {
-            batch[k] = b[k].slice();                 // own, exactly sized buffers to transfer
-            transfer.push(batch[k].buffer);
-        }
+        // the columns are views of this worker's shared buffers: valid until its next batch (the
+        // main thread consumes a batch, mt_apply_batch_parts copies it, before asking for another)
+        const batch = bb.build();
         parentPort.postMessage({ batch, nPayload, names,
             props: { keys: props.keys, valueJson: props.valueJson, sets: props.sets, incrKeys: [...props.incrKeys],
-                nIncr: props.nIncr } }, transfer);
+                nIncr: props.nIncr } });
     } catch (e) {
         parentPort.postMessage({ error: String(e && e.stack || e) });
     }

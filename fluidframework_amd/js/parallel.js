@@ -21,7 +21,10 @@ const TYPES = { type: Uint8Array, flags: Uint8Array, client: Uint16Array, seq: I
 class ParallelPacker {
     constructor(nWorkers) {
         this.workers = [];
-        for (let i = 0; i < nWorkers; i++) this.workers.push(new Worker(path.join(__dirname, "pack_worker.js")));
+        // heaps sized for documents held as parsed message objects (hundreds of MB a worker): the
+        // default limits make V8 collect the old generation over and over while packing
+        const resourceLimits = { maxOldGenerationSizeMb: 16384, maxYoungGenerationSizeMb: 512 };
+        for (let i = 0; i < nWorkers; i++) this.workers.push(new Worker(path.join(__dirname, "pack_worker.js"), { resourceLimits }));
     }
     close() { return Promise.all(this.workers.map((w) => w.terminate())); }
     /**
