@@ -120,12 +120,7 @@
 #ifndef MT_G_ALLCH
 #define MT_G_ALLCH 0                   // 1: ... with every chunk's rows loaded in one round trip
 #endif
-enum { MT_MW_EXIT = 0, MT_MW_SCAN = 1, MT_MW_CHAIN = 2, MT_MW_PREFETCH = 3, MT_MW_HT = 4 };
-// htBuild's levels of more than this many distinct blocks are shared by the workgroup's waves
-// (MT_MW_HT: one slice of the level per wave, the table and slot list in LDS are shared)
-#ifndef MT_G_HTMW
-#define MT_G_HTMW 32
-#endif
+enum { MT_MW_EXIT = 0, MT_MW_SCAN = 1, MT_MW_CHAIN = 2, MT_MW_PREFETCH = 3 };
 // Jobs alternate between two LDS slots, so wave 0 can post an asynchronous job (PREFETCH: no
 // completion barrier) and write the next one while helpers still read the last.
 // Runtime switches of the long-document residency (mt_set_residency(ctx, 3, rows, flags, heap)):
@@ -443,7 +438,6 @@ struct __attribute__((aligned(16))) MtLdsBig {
         MtRow* R; int* win; MtBlk* blk; int* uanc; uint16_t* text;
     } mw[2];
     int posted;                       // jobs wave 0 has posted (the exit job goes to slot posted & 1)
-    int hlN;                          // hlist's length while an MT_MW_HT job appends to it (LDS atomics)
 };
 
 // per-wave scratch (LDS on the device)
@@ -1304,13 +1298,6 @@ template <int RES, bool FULL = true> struct MtEngT {
             } else if (op == MT_MW_CHAIN) {
                 const int nu = uni(J.n), H = uni(J.H);
                 for (int g0 = wv * 8 * MT_WAVE; g0 < nu; g0 += MT_G_NW * 8 * MT_WAVE) chainGroup(g0, nu, H);
-            } else if (op == MT_MW_HT) {
-                // one level of htBuild: this wave's slice of the level's slots [l0, l1)
-                const int rt = uni(J.r), l0 = uni(J.r0), l1 = uni(J.n);
-                bpOn = uni(J.c) != 0;
-                const int per = (l1 - l0 + MT_G_NW - 1) / MT_G_NW;
-                const int a = l0 + wv * per, b = (a + per) < l1 ? a + per : l1;
-                for (int base = a; base < b; base += MT_WAVE) htLevelChunk(base, (b - base) < MT_WAVE ? (b - base) : MT_WAVE, rt, true);
             } else if (op == MT_MW_PREFETCH && wv == 1) {
                 // zamboni's next pops come from the top of the heap: touch entries 1..7's rows,
                 // their leaf blocks, the blocks' rows and those rows' last text unit, so wave 0's
@@ -1413,12 +1400,12 @@ template <int RES, bool FULL = true> struct MtEngT {
         int sl = (int)htHash(key);
         won = false;
         for (;;) {
-            const int old = lds_cas_wg(&G.htk[sl], MT_BC_EMPTY, key);      // the workgroup's waves share the table
+            const int old = lds_cas(&G.htk[sl], MT_BC_EMPTY, key);
             if (old == MT_BC_EMPTY) { won = true; break; }
             if (old == key) break;
             sl = (sl + 1) & (MT_G_HT - 1);
         }
-        lds_add_wg(&G.htv[sl], val);
+        lds_add(&G.htv[sl], val);
         return sl;
     }
     MT_HD int htGet(int key) const {
@@ -1438,42 +1425,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         wave_for(m, [&](int k) MT_LAM { if (own(won, k)) mt_ldsg().hlist[h0 + own(rk, k)] = (uint16_t)own(sl, k); });
         hlistN += cnt;
     }
-    // hlist appends from several waves at once (an MT_MW_HT job): the slots this wave claimed go
-    // to a range it reserves with one LDS atomic on the shared length
-    MT_HD void htListShared(const LaneArr<int>& sl, const LaneArr<bool>& won, int m) {
-        const auto rk = wave_rank(won);
-        const int cnt = wave_count(won);
-        if (!cnt) return;
-        int h0 = 0;
-        wave_for(1, [&](int) MT_LAM { h0 = lds_fetch_add_wg(&mt_ldsg().hlN, cnt); });
-        h0 = lane0(h0);
-        wave_for(m, [&](int k) MT_LAM { if (own(won, k)) mt_ldsg().hlist[h0 + own(rk, k)] = (uint16_t)own(sl, k); });
-    }
-    // One chunk of an htBuild level: each slot of hlist[base, base + m) passes its sum to its
-    // block's parent (the root excluded: no descent asks for it).
-    MT_HD void htLevelChunk(int base, int m, int rt, bool shared) {
-        MtLdsBig& G = mt_ldsg();
-        const auto ch = wave_map(m, [&](int k) MT_LAM { return (int)G.hlist[base + k]; });
-#if defined(MT_PROFILE4)
-        MT_UC(6, m);
-        if (bpOn) MT_UC(7, wave_count(wave_map(m, [&](int k) MT_LAM {
-            const int b = G.htk[own(ch, k)];
-            return (G.bpc[b & (MT_G_BP - 1)] >> 20) != (uint32_t)(b >> MT_G_BPL);
-        })));
-#endif
-        const auto par = wave_map(m, [&](int k) MT_LAM { return bkParent(G.htk[own(ch, k)]); });
-        const auto val = wave_map(m, [&](int k) MT_LAM { return G.htv[own(ch, k)]; });
-        const auto a = wave_map(m, [&](int k) MT_LAM {
-            const int p = own(par, k);
-            bool w = false; int x = 0;
-            if ((p >= 0) & (p != rt)) x = htAdd(p, own(val, k), w);
-            return w ? x : ~x;
-        });
-        const auto sl = wave_map(m, [&](int k) MT_LAM { return own(a, k) >= 0 ? own(a, k) : ~own(a, k); });
-        const auto won = wave_map(m, [&](int k) MT_LAM { return own(a, k) >= 0; });
-        if (shared) htListShared(sl, won, m); else htList(sl, won, m);
-    }
-    // The corrections table for the current U set, bottom-up: leaf blocks get their U rows''
+    // The corrections table for the current U set, bottom-up: leaf blocks get their U rows'
     // deltas, then every distinct block of one height passes its sum to its parent (root
     // excluded: no descent asks for it).  False if it would outgrow MT_G_HTN (table left
     // empty, htOk false: the caller computes ancestor chains instead).
@@ -1507,14 +1459,26 @@ template <int RES, bool FULL = true> struct MtEngT {
                 wave_sync();
                 return false;
             }
-            if (MT_G_NW > 1 && l1 - l0 > MT_G_HTMW) {
-                // a wide level: every wave of the workgroup takes a slice (MT_MW_HT)
-                wave_for(1, [&](int) MT_LAM { G.hlN = hlistN; });
-                mwRun(MT_MW_HT, rt, bpOn ? 1 : 0, l0, l1);
-                hlistN = uni(G.hlN);
-            } else {
-                for (int base = l0; base < l1; base += MT_WAVE)
-                    htLevelChunk(base, (l1 - base) < MT_WAVE ? (l1 - base) : MT_WAVE, rt, false);
+            for (int base = l0; base < l1; base += MT_WAVE) {
+                const int m = (l1 - base) < MT_WAVE ? (l1 - base) : MT_WAVE;
+                const auto ch = wave_map(m, [&](int k) MT_LAM { return (int)G.hlist[base + k]; });
+#if defined(MT_PROFILE4)
+                MT_UC(6, m);
+                if (bpOn) MT_UC(7, wave_count(wave_map(m, [&](int k) MT_LAM {
+                    const int b = G.htk[own(ch, k)];
+                    return (G.bpc[b & (MT_G_BP - 1)] >> 20) != (uint32_t)(b >> MT_G_BPL);
+                })));
+#endif
+                const auto par = wave_map(m, [&](int k) MT_LAM { return bkParent(G.htk[own(ch, k)]); });
+                const auto val = wave_map(m, [&](int k) MT_LAM { return G.htv[own(ch, k)]; });
+                const auto a = wave_map(m, [&](int k) MT_LAM {
+                    const int p = own(par, k);
+                    bool w = false; int x = 0;
+                    if ((p >= 0) & (p != rt)) x = htAdd(p, own(val, k), w);
+                    return w ? x : ~x;
+                });
+                htList(wave_map(m, [&](int k) MT_LAM { return own(a, k) >= 0 ? own(a, k) : ~own(a, k); }),
+                       wave_map(m, [&](int k) MT_LAM { return own(a, k) >= 0; }), m);
             }
             wave_sync();
             l0 = l1; l1 = hlistN;

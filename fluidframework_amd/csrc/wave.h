@@ -130,15 +130,6 @@ __device__ __forceinline__ void mt_keep(int v) { __asm__ volatile("" ::"v"(v)); 
 // the same value, opaque to the compiler: lane-index arithmetic behind it is not hoisted to the
 // kernel's entry (where it would hold a VGPR, or a spill slot, across the whole replay loop)
 __device__ __forceinline__ int mt_opaque(int v) { __asm__ volatile("" : "+v"(v)); return v; }
-// the same on LDS another wave of the workgroup uses at the same time (workgroup scope)
-__device__ __forceinline__ void lds_add_wg(int* p, int v) { __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-__device__ __forceinline__ int lds_fetch_add_wg(int* p, int v) { return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-__device__ __forceinline__ int lds_cas_wg(int* p, int cmp, int v) {
-    __hip_atomic_compare_exchange_strong(p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return cmp;
-}
-// lane 0's value in every lane
-__device__ __forceinline__ int lane0(int x) { return __builtin_amdgcn_readlane(x, 0); }
 // per-lane compare-and-swap on LDS; returns the old value
 __device__ __forceinline__ int lds_cas(int* p, int cmp, int v) {
     __hip_atomic_compare_exchange_strong(p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -242,10 +233,6 @@ template <class F> inline LaneArr<int> wave_shfl(const LaneArr<int>& a, F src) {
 inline LaneArr<int> wave_set(LaneArr<int> a, int k, int v) { if (k >= 0 && k < MT_WAVE) a.v[k] = v; return a; }
 inline void lds_add(int* p, int v) { *p += v; }
 inline int lds_cas(int* p, int cmp, int v) { const int o = *p; if (o == cmp) *p = v; return o; }
-inline void lds_add_wg(int* p, int v) { *p += v; }
-inline int lds_fetch_add_wg(int* p, int v) { const int o = *p; *p += v; return o; }
-inline int lds_cas_wg(int* p, int cmp, int v) { return lds_cas(p, cmp, v); }
-inline int lane0(int x) { return x; }
 inline void mt_keep(int) {}
 inline int mt_opaque(int v) { return v; }
 inline unsigned long long wave_atomic_add(unsigned long long* p, unsigned long long d) { return __atomic_fetch_add(p, d, __ATOMIC_RELAXED); }
