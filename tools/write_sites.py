@@ -68,6 +68,15 @@ def run(cfg="config2", docs=16, res="blk"):
     eng.sync()
     out = np.zeros(2 * n + 13, np.uint64)
     wt(eng.h, 0, out.ctypes.data)
+    # the traced replay (free pools poisoned) must give the digests of a plain replay of the stream
+    neg = np.full(docs, -1, np.int32)
+    traced = eng.snapshot_digests(range(docs), neg, neg, threads=4)
+    eng.open_docs(0, docs)
+    eng.replay_resident()
+    eng.sync()
+    plain = eng.snapshot_digests(range(docs), neg, neg, threads=4)
+    if not np.array_equal(traced, plain) or eng.status(range(docs)).any():
+        raise SystemExit("traced replay differs from the plain one")
     msgs = float(out[2 * n + 12])
     per = out[:n].astype(float) * 64 / msgs
     end = out[n:2 * n].astype(float) * 64 / msgs
