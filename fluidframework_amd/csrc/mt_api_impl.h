@@ -291,6 +291,7 @@ int MT_FN(docs_open)(mt_ctx* c, uint32_t first, uint32_t n) {
     if (!c || (uint64_t)first + n > c->S.maxDocs) return MT_E_INVALID;
     if (n == 0) return MT_OK;
     for (uint32_t d = first; d < first + n && d < c->snap_chunk.size(); d++) c->snap_chunk[d] = 0;   // a new Client's options
+    for (uint32_t d = first; d < first + n && d < c->doc_wide.size(); d++) { c->doc_wide[d] = 0; c->doc_keys[d].clear(); }
     return mtb_launch_open(c, first, n);
 }
 int MT_FN(set_doc_snapshot_chunk)(mt_ctx* c, uint32_t n, const uint32_t* docs, const uint64_t* chunk) {
@@ -331,6 +332,13 @@ int MT_FN(set_props)(mt_ctx* c, const mt_prop_table* P) {
     c->S.p_val = (const int32_t*)c->b_pval.p; c->S.p_falsy = (const uint8_t*)c->b_pfalsy.p;
     c->S.p_class = (const uint32_t*)c->b_pclass.p; c->S.p_nsets = P->n_sets;
     c->S.p_vinfo = (P->value_kind || !P->n_values) ? (const int32_t*)c->b_pkind.p + 1 : nullptr;
+    c->h_set_off.assign(P->set_off, P->set_off + P->n_sets + 1);
+    c->h_set_key.assign(P->key, P->key + npairs);
+    {
+        std::vector<uint16_t> ks(c->h_set_key);
+        std::sort(ks.begin(), ks.end());
+        c->props_wide = (size_t)(std::unique(ks.begin(), ks.end()) - ks.begin()) > MT_WAVE;
+    }
     c->names.key_json.assign(P->key_json, P->key_json + P->n_keys);
     c->names.key_index.assign(P->key_index, P->key_index + P->n_keys);
     c->names.value_json.assign(P->value_json, P->value_json + P->n_values);
@@ -349,6 +357,46 @@ int MT_FN(set_doc_client_names)(mt_ctx* c, uint32_t doc, uint32_t n, const char*
     else c->doc_clients[doc].assign(cj, cj + n);
     return MT_OK;
 }
+
+// Notes property set `ps` on document `doc` (mt_ctx::doc_keys); true once the document's keys
+// pass a wave's lanes (its maps may then outgrow the non-FULL kernels).
+static bool mt_note_set(mt_ctx* c, uint32_t doc, int ps) {
+    if (ps < 0 || (size_t)ps + 1 >= c->h_set_off.size()) return false;
+    if (c->doc_wide.size() < c->S.maxDocs) { c->doc_wide.resize(c->S.maxDocs, 0); c->doc_keys.resize(c->S.maxDocs); }
+    if (c->doc_wide[doc]) return true;
+    std::vector<uint16_t>& ks = c->doc_keys[doc];
+    for (uint32_t q = c->h_set_off[ps]; q < c->h_set_off[ps + 1]; q++) {
+        const uint16_t k = c->h_set_key[q];
+        auto it = std::lower_bound(ks.begin(), ks.end(), k);
+        if (it == ks.end() || *it != k) ks.insert(it, k);
+    }
+    if (ks.size() > MT_WAVE) { c->doc_wide[doc] = 1; std::vector<uint16_t>().swap(ks); return true; }
+    return false;
+}
+// batch_wide for a batch of n_runs runs: run r's document doc(r) and its ops' property sets
+// pid(i) over [op0(r), op1(r)) (sets named twice in a run are noted once).
+extern "C++" {
+template <class DocOf, class Op0, class Op1, class Pid>
+static bool mt_scan_wide(mt_ctx* c, size_t n_runs, DocOf doc, Op0 op0, Op1 op1, Pid pid) {
+    bool wide = false;
+    if (c->h_set_off.size() < 2) return false;
+    std::vector<uint32_t> seen(c->h_set_off.size() - 1, 0);
+    for (size_t r = 0; r < n_runs; r++) {
+        const uint32_t d = doc(r);
+        if (d < c->doc_wide.size() && c->doc_wide[d]) { wide = true; continue; }
+        for (size_t i = op0(r); i < op1(r); i++) {
+            const int ps = pid(i);
+            if (ps < 0 || (size_t)ps >= seen.size() || seen[ps] == (uint32_t)r + 1) continue;
+            seen[ps] = (uint32_t)r + 1;
+            if (mt_note_set(c, d, ps)) { wide = true; break; }
+        }
+    }
+    return wide;
+}
+}
+// Device-built batches (the generators, the exchange: ops never seen on the host): wide when the
+// property sets together could make a document wide.
+static bool mt_dev_wide(const mt_ctx* c) { return c->props_wide; }
 
 // The batch's arrays in one device region, one pinned staging copy and one asynchronous H2D
 // (stream-ordered before the replay that follows; no host synchronization): doc ids, op
@@ -397,6 +445,8 @@ static int mt_upload_ops(mt_ctx* c, const mt_op_batch* B) {
     c->n_runs = B->n_runs;
     c->run_off.assign(B->op_offsets, B->op_offsets + R + 1); c->batch_gen++;
     c->batch_reg = reg;
+    c->batch_wide = mt_scan_wide(c, R, [&](size_t r) { return B->doc_ids[r]; }, [&](size_t r) { return B->op_offsets[r]; },
+                                 [&](size_t r) { return B->op_offsets[r + 1]; }, [&](size_t i) { return B->prop_id[i]; });
     return MT_OK;
 }
 
@@ -533,6 +583,8 @@ static int mt_upload_parts(mt_ctx* c, uint32_t P, const mt_op_batch* parts, cons
     c->n_runs = (uint32_t)R;
     c->run_off.swap(runOff); c->batch_gen++;
     c->batch_reg = reg;
+    c->batch_wide = mt_scan_wide(c, R, [&](size_t r) { return docs[r]; }, [&](size_t r) { return (size_t)c->run_off[r]; },
+                                 [&](size_t r) { return (size_t)c->run_off[r + 1]; }, [&](size_t i) { return (int)rec[i].prop_id; });
     return MT_OK;
 }
 int MT_FN(upload_batch_parts)(mt_ctx* c, uint32_t n_parts, const mt_op_batch* parts, const int32_t* const* prop_map,
@@ -691,6 +743,12 @@ int MT_FN(load_snapshot)(mt_ctx* c, const mt_load_batch* B) {
         mt_load_plan(B, i, plan);
     }
     plan_off[n] = (uint32_t)plan.size();
+    for (uint32_t i = 0; i < n; i++) {            // loaded maps count toward the documents' keys
+        const uint32_t d = B->doc_ids[i];
+        if (d < c->doc_wide.size()) { c->doc_wide[d] = 0; c->doc_keys[d].clear(); }
+        for (uint32_t k = B->seg_offsets[i]; k < B->seg_offsets[i + 1]; k++)
+            if (mt_note_set(c, d, B->segs[k].prop_id)) break;
+    }
     for (uint32_t i = 0; i < n; i++) {
         meta[i] = B->doc_ids[i]; meta[n + i] = B->seg_offsets[i];
         meta[2ull * n + 1 + i] = B->header_segments[i];
@@ -1323,6 +1381,7 @@ int MT_FN(generate_docs)(mt_ctx* c, const mt_gen_params* P, const uint32_t* ops_
     o.dtext = nullptr; o.dtcap = 0; o.resume = nullptr; o.start = nullptr;
     c->n_runs = P->n_docs;
     c->batch_reg = false;                     // generated streams hold no register ops
+    c->batch_wide = mt_dev_wide(c);
     c->gen_off.assign(off.begin(), off.end());
     c->run_off = c->gen_off; c->batch_gen++;
     if (!P->continue_docs) {
@@ -1399,6 +1458,7 @@ int MT_FN(upload_batch_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids,
     c->n_runs = n_runs;
     c->run_off.assign(op_offsets, op_offsets + n_runs + 1); c->batch_gen++;
     c->batch_reg = false;                     // device-built streams (shard.py) hold no register ops
+    c->batch_wide = mt_dev_wide(c);
     c->gen.enabled = 0;
     return mtb_sync(c);
 }
@@ -1458,6 +1518,7 @@ int MT_FN(upload_rows_dev)(mt_ctx* c, uint32_t n_runs, const uint32_t* doc_ids, 
     c->n_runs = n_runs;
     c->run_off.assign(op_offsets, op_offsets + n_runs + 1); c->batch_gen++;
     c->batch_reg = false;                     // exchanged generated streams hold no register ops
+    c->batch_wide = mt_dev_wide(c);
     c->gen.enabled = 0;
     if (n_runs && (rc = mtb_launch_rows(c, false, 0, n_runs, (uint32_t)L, nullptr, (uint64_t*)rows_dev,
                                         (uint64_t*)c->b_tmp1.p))) return rc;

@@ -2337,13 +2337,27 @@ template <int RES, bool FULL = true> struct MtEngT {
         if (a < 0 || b < 0) return false;
         const int na = uni(pset[a].n), nb = uni(pset[b].n);
         if (na != nb) return false;
-        for (int base = 0; base < na; base += MT_WAVE) {              // a's keys one per lane
-            const int cnt = (na - base) < MT_WAVE ? (na - base) : MT_WAVE;
+        if constexpr (FULL) {
+            if (__builtin_expect(na > MT_WAVE, 0)) return propsMatchWide(a, b, na);
+        } else if (na > MT_WAVE) { status |= MT_DS_PROPS_TOO_MANY; return false; }   // wide maps: FULL only
+        auto ok = wave_map(na, [&](int k) MT_LAM {               // a's keys one per lane
+            const int key = pkey(a, k);
+            const uint32_t ca = pclass(pval(a, k));
+            bool f = false;
+            for (int i = 0; i < nb; i++) f |= (int)(pkey(b, i) == key) & (int)(pclass(pval(b, i)) == ca);
+            return (f & (int)(ca != 0xFFFFFFFFu)) != 0;
+        });
+        return wave_count(ok) == na;
+    }
+    // ... for maps of more than 64 keys (equal counts n): a's keys in chunks of 64 lanes
+    MT_HD bool propsMatchWide(int a, int b, int n) {
+        for (int base = 0; base < n; base += MT_WAVE) {
+            const int cnt = (n - base) < MT_WAVE ? (n - base) : MT_WAVE;
             auto ok = wave_map(cnt, [&](int k) MT_LAM {
                 const int key = pkey(a, base + k);
                 const uint32_t ca = pclass(pval(a, base + k));
                 bool f = false;
-                for (int i = 0; i < nb; i++) f |= (int)(pkey(b, i) == key) & (int)(pclass(pval(b, i)) == ca);
+                for (int i = 0; i < n; i++) f |= (int)(pkey(b, i) == key) & (int)(pclass(pval(b, i)) == ca);
                 return (f & (int)(ca != 0xFFFFFFFFu)) != 0;
             });
             if (wave_count(ok) != cnt) return false;
@@ -2928,7 +2942,12 @@ template <int RES, bool FULL = true> struct MtEngT {
     MT_HD int applyPropSet(int old, int opset, int pm, int sq = 0) {
         if (opset < 0 || opset >= (int)S.p_nsets) { status |= MT_DS_UNSUPPORTED; return old; }
         int n = old >= 0 ? uni(pset[old].n) : 0;
-        if (n + (uni((int)S.p_off[opset + 1]) - uni((int)S.p_off[opset])) > MT_WAVE) return applyPropSetWide(old, opset, pm, sq);
+        // maps past a wave's lanes are built by the FULL kernels only: the host replays a batch in
+        // them once one of its documents has named more than MT_WAVE distinct keys (mt_ctx::batch_wide)
+        if constexpr (FULL) {
+            if (__builtin_expect(n + (uni((int)S.p_off[opset + 1]) - uni((int)S.p_off[opset])) > MT_WAVE, 0))
+                return applyPropSetWide(old, opset, pm, sq);
+        } else if (n > MT_WAVE) { status |= MT_DS_PROPS_TOO_MANY; return old; }
         auto kk = wave_map(n, [&](int i) MT_LAM { return pkey(old, i); });
         auto vv = wave_map(n, [&](int i) MT_LAM { return pval(old, i); });
         const int o0 = uni((int)S.p_off[opset]), o1 = uni((int)S.p_off[opset + 1]);
@@ -2963,7 +2982,9 @@ template <int RES, bool FULL = true> struct MtEngT {
             } else if (at >= 0) {
                 vv = wave_map(MT_WAVE, [&](int i) MT_LAM { return i == at ? nv : own(vv, i); });
             } else {
-                const int at2 = n;                   // n + (o1 - o0) <= MT_WAVE here
+                // FULL: n + (o1 - o0) <= MT_WAVE here; otherwise the document's keys number <= MT_WAVE
+                if constexpr (!FULL) if (n >= MT_WAVE) { status |= MT_DS_PROPS_TOO_MANY; return old; }
+                const int at2 = n;
                 kk = wave_map(MT_WAVE, [&](int i) MT_LAM { return i == at2 ? key : own(kk, i); });
                 vv = wave_map(MT_WAVE, [&](int i) MT_LAM { return i == at2 ? nv : own(vv, i); });
                 n++;

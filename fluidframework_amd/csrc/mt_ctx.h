@@ -74,6 +74,15 @@ struct mt_ctx {
     float last_ms = 0.f;
     // LDS residency of the replay (mt_set_residency): on/off and the pool caps
     bool batch_reg = false;            // the resident batch holds register ops (FULL kernels)
+    // Property maps past a wave's 64 lanes (applyPropSetWide) are built only by the FULL kernels:
+    // per document, the distinct keys of every property set its ops (and loaded segments) named
+    // since it was opened, until they pass MT_WAVE (doc_wide: sticky until reopened); a batch
+    // holding such a document replays in the FULL kernels (batch_wide).  Host copies of the
+    // property sets' keys (mt_set_props) for the scan.
+    bool batch_wide = false;
+    bool props_wide = false;           // the property sets name more than MT_WAVE distinct keys
+    std::vector<uint32_t> h_set_off; std::vector<uint16_t> h_set_key;
+    std::vector<std::vector<uint16_t>> doc_keys; std::vector<uint8_t> doc_wide;
     int use_lds = 2, lds_rows = MT_L_ROWS, lds_blks = MT_B_BLKS, lds_heap = MT_B_HEAP;
     void* stream = nullptr;
     void* ev0 = nullptr;

@@ -278,7 +278,7 @@ static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
     (void)hipGetLastError();
     (void)hipEventRecord((hipEvent_t)c->ev0, s);
     if (g.enabled) mtk_generate(s, n_runs, c->S, c->ops, g);
-    else launch_replay(c, s, n_runs, c->ops.drec || c->batch_reg);
+    else launch_replay(c, s, n_runs, c->ops.drec || c->batch_reg || c->batch_wide);
     (void)hipEventRecord((hipEvent_t)c->ev1, s);
     c->ev_pending = true;
     return mtb_check(c);

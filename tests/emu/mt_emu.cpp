@@ -73,7 +73,7 @@ static int mtb_launch_replay(mt_ctx* c, const MtGen& g, uint32_t n_runs) {
         }
         return MT_OK;
     }
-    if (c->ops.drec || c->batch_reg) replay_runs<true>(c, n_runs);
+    if (c->ops.drec || c->batch_reg || c->batch_wide) replay_runs<true>(c, n_runs);
     else replay_runs<false>(c, n_runs);
     return MT_OK;
 }

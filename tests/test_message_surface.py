@@ -5,6 +5,7 @@ batch.BatchBuilder) into the engine, and must match the oracle, which parses and
 the same messages itself (ora_apply_msg_json, MT/client.ts:790-850): observer text,
 segment structure, SnapshotV1 and SnapshotLegacy bytes and digests, perspective lengths.
 """
+import json
 import os
 
 import numpy as np
@@ -329,3 +330,65 @@ def test_batch_parts_node_host_on_gpu(surface):
     if NODE is None:
         pytest.skip("node is not installed")
     check_parts(os.path.join(ROOT, "fluidframework_amd", "js", "mtgpu.node"), surface)
+
+
+def check_wide_load_continue(factory, seed=13, n_docs=3, n_msgs=1200, cut=600):
+    """Maps past a wave's lanes come back from a snapshot: the library counts the loaded maps'
+    keys toward the document, so the stream continuing on it replays in the kernels that build
+    wide maps (mt_ctx::batch_wide; a narrow kernel would flag MT_DS_PROPS_TOO_MANY).  Documents
+    of the same batch that stay narrow ride along."""
+    from msg_gen import StreamGen
+    surf = ["very_wide_props", "mixed", "very_wide_props"]
+    streams = []
+    for d in range(n_docs):
+        sg = StreamGen(seed * 7 + d, **SURFACES[surf[d % 3]])
+        sg.run(cut)
+        sg.p_vwide = 0.0                 # the continuation names only a few keys (annotates of wide maps)
+        sg.run(n_msgs - cut)
+        streams.append((sg.msgs, sg.obs))
+    g1 = ClientGroup(factory(n_docs, **LIMITS))
+    first = [g1.new_client({"newMergeTreeSnapshotFormat": True}) for _ in range(n_docs)]
+    blobs = []
+    for c, (msgs, _) in zip(first, streams):
+        c.startOrUpdateCollaboration("observer")
+        for m in msgs[:cut]:
+            c.applyMsg(m)
+        blobs.append({e["path"]: e["value"]["contents"] for e in c.snapshot()["entries"]})
+    g1.flush()
+    g2 = ClientGroup(factory(n_docs, **LIMITS))
+    second = [g2.new_client({"newMergeTreeSnapshotFormat": True}) for _ in range(n_docs)]
+    for c, b, (msgs, _) in zip(second, blobs, streams):
+        c.load(b)
+        c.startOrUpdateCollaboration("observer")
+        for m in msgs:
+            if m["sequenceNumber"] > c.getCurrentSeq():
+                c.applyMsg(m)
+    g2.flush()
+    eng = g2.engine
+    assert (eng.status(range(n_docs)) == 0).all(), eng.status(range(n_docs))
+    texts = eng.get_text(range(n_docs))
+    from oracle_lib import OracleDoc
+    for d, (msgs, obs) in enumerate(streams):
+        assert texts[d] == obs.get_text(), f"doc {d}: text"
+        # the oracle loads the same blobs and takes the same rest of the stream
+        od = OracleDoc(False)
+        b = blobs[d]
+        assert od.load_snapshot([b["header"]] + [b[f"body_{i}"] for i in range(len(b) - 1)]) == 0
+        seq0 = json.loads(b["header"])["headerMetadata"]["sequenceNumber"]
+        for m in msgs:
+            if m["sequenceNumber"] > seq0:
+                assert od.apply_msg(m) == 0
+        assert od.get_text() == texts[d]
+        msn, seq = msgs[-1]["minimumSequenceNumber"], msgs[-1]["sequenceNumber"]
+        (eb, edig), = eng.snapshot([d], [msn], [seq])
+        ob, odig = od.snapshot(msn, seq)
+        assert eb == ob and edig == odig, f"doc {d}: snapshot"
+
+
+def test_wide_maps_load_and_continue_on_emulation():
+    check_wide_load_continue(emu_engine)
+
+
+@pytest.mark.gpu
+def test_wide_maps_load_and_continue_on_gpu():
+    check_wide_load_continue(lambda n, **kw: Engine(n, device=0, **kw), n_docs=6)
