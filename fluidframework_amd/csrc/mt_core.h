@@ -232,6 +232,9 @@ enum { MT_PH_U = 0, MT_PH_SPLIT, MT_PH_INSERT, MT_PH_RANGE, MT_PH_ZAMBONI, MT_PH
 #define MT_M_HREF1 0x01000000u        // heap-entry reference count, bits 24..31 (saturating)
 #define MT_M_HREF 0xFF000000u
 
+#ifndef MT_ROW64
+#define MT_ROW64 0
+#endif
 struct __attribute__((aligned(16))) MtRow {   // one 48-byte record per segment row
     int len;         // cachedLength (UTF-16 units; 1 for a marker)
     int seq;         // insertion seq
@@ -244,6 +247,9 @@ struct __attribute__((aligned(16))) MtRow {   // one 48-byte record per segment 
     unsigned long long ovl;  // removedClientOverlap: bit c for clients c < 63; bit 63 = more in the side list
     uint32_t rcl;            // removedClientId (16 bits)
     int mid;                 // marker: its markerId's per-document index + 1 (0: none)
+#if MT_ROW64
+    int pad[4];              // one row per 64-byte line (a row's update dirties one line)
+#endif
 };
 struct __attribute__((aligned(16))) MtBlk {   // one 64-byte record per B-tree block
     int c[8];        // children: segment rows (height 0) or blocks

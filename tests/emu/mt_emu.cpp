@@ -166,7 +166,7 @@ enum { WT_ROWS, WT_BLK, WT_HEAP, WT_WIN, WT_UID, WT_UDELTA, WT_UANC, WT_TEXT, WT
        WT_REG, WT_REGR, WT_N };
 struct WtRegion { uint8_t* base; size_t bytes; };
 std::vector<std::vector<uint8_t>> g_shadow(WT_N);
-unsigned long long g_lines[2][WT_N], g_rowField[12], g_msgs;
+unsigned long long g_lines[2][WT_N], g_rowField[16], g_msgs;
 WtRegion wt_region(uint32_t doc, int k) {
     const MtState& S = g_wt->S; const MtDocLayout& y = g_wt->layout_h[doc];
     switch (k) {

@@ -27,12 +27,13 @@ ROW_FIELDS = ["len", "seq", "removedSeq", "meta", "toff", "props", "parent", "tc
 
 
 def build():
-    lib = "/tmp/libmtemu_wtrace.so"
+    extra = os.environ.get("WT_FLAGS", "").split()
+    lib = "/tmp/libmtemu_wtrace%s.so" % "".join(f.replace("-D", "_").replace("=", "") for f in extra)
     src = os.path.join(ROOT, "tests", "emu", "mt_emu.cpp")
     deps = [src] + [os.path.join(ROOT, "fluidframework_amd", "csrc", f) for f in os.listdir(os.path.join(ROOT, "fluidframework_amd", "csrc"))]
     if not os.path.exists(lib) or any(os.path.getmtime(lib) < os.path.getmtime(d) for d in deps):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wno-unknown-pragmas",
-                               "-DMT_WTRACE", "-o", lib, src])
+                               "-DMT_WTRACE"] + extra + ["-o", lib, src])
     return lib
 
 
