@@ -337,7 +337,16 @@ int MT_FN(set_props)(mt_ctx* c, const mt_prop_table* P) {
     {
         std::vector<uint16_t> ks(c->h_set_key);
         std::sort(ks.begin(), ks.end());
-        c->props_wide = (size_t)(std::unique(ks.begin(), ks.end()) - ks.begin()) > MT_WAVE;
+        const bool wide = (size_t)(std::unique(ks.begin(), ks.end()) - ks.begin()) > MT_WAVE;
+        // Below MT_WAVE keys in all no document can outgrow the lanes, and batches are not
+        // scanned (mt_scan_wide); when the table first passes them, the documents open now
+        // have keys nobody counted: they replay in the FULL kernels until reopened.
+        if (wide && !c->props_wide) {
+            if (c->doc_wide.size() < c->S.maxDocs) { c->doc_wide.resize(c->S.maxDocs, 0); c->doc_keys.resize(c->S.maxDocs); }
+            std::fill(c->doc_wide.begin(), c->doc_wide.end(), (uint8_t)1);
+            for (auto& k : c->doc_keys) std::vector<uint16_t>().swap(k);
+        }
+        c->props_wide = wide;
     }
     c->names.key_json.assign(P->key_json, P->key_json + P->n_keys);
     c->names.key_index.assign(P->key_index, P->key_index + P->n_keys);
@@ -379,7 +388,7 @@ extern "C++" {
 template <class DocOf, class Op0, class Op1, class Pid>
 static bool mt_scan_wide(mt_ctx* c, size_t n_runs, DocOf doc, Op0 op0, Op1 op1, Pid pid) {
     bool wide = false;
-    if (c->h_set_off.size() < 2) return false;
+    if (!c->props_wide) return false;                 // no document can pass MT_WAVE keys
     std::vector<uint32_t> seen(c->h_set_off.size() - 1, 0);
     for (size_t r = 0; r < n_runs; r++) {
         const uint32_t d = doc(r);
