@@ -63,7 +63,9 @@
 #define MT_B_SLACK 13                 // block residency: free blocks kept beyond 2 * height before each message
 #endif
 #define MT_B_BT 128                   // corrections-table slots (block ids < MT_B_BLKS)
-#define MT_B_U 64                     // U-set entries kept in LDS (the rest, if any, in HBM)
+#ifndef MT_B_W
+#define MT_B_W 64                     // window entries kept in LDS (the rest, if any, in HBM)
+#endif
 #ifndef MT_B_HEAP
 #define MT_B_HEAP 94
 #endif
@@ -416,7 +418,9 @@ template <int NB, int NH, int NT> struct __attribute__((aligned(16))) MtLdsBlkT 
     static_assert(NB <= NT, "block ids index the corrections table");
     MtBlk blk[NB];
     MtHeapE heap[NH + 2];
-    int uid[MT_B_U], udelta[MT_B_U];
+    // the window's first MT_B_W entries (the rest in HBM): computeU reads them without an HBM
+    // round trip, and window appends and compaction write them here
+    int win[MT_B_W];
     // Per-block perspective corrections of the current U set (Σ delta of the U rows beneath
     // each block, indexed by block id): a descent level reads its children's lengths as
     // observer length + correction instead of scanning U (no ancestor chains kept).
@@ -667,32 +671,41 @@ template <int RES, bool FULL = true> struct MtEngT {
         if constexpr (LDS) return mt_lds().heap[k]; else if constexpr (BLKL) return LB().heap[k];
         else if constexpr (BIG) return mt_ldsg().heap[k]; else return heap[k];
     }
+    // Window entry k under block residency: the first MT_B_W in LDS.  Loads and stores are made
+    // in each branch (a reference to either home would be a generic pointer: flat_* accesses).
+    MT_HD int winGet(int k) const {
+        if constexpr (BLKR) { if (k < MT_B_W) return LB().win[k]; return win[k]; }
+        else return wn(k);
+    }
+    MT_HD void winSet(int k, int v) const {
+        if constexpr (BLKR) { if (k < MT_B_W) LB().win[k] = v; else win[k] = v; }
+        else wn(k) = v;
+    }
     MT_HD int& wn(int k) const {
+        static_assert(!BLKR, "block residency: winGet / winSet");
         if constexpr (LDS) return mt_lds().win[k];
         else if constexpr (BIG) { if (k < lRows) return mt_ldsg().win[k]; return win[k]; }   // beyond lRows: HBM home
         else return win[k];
     }
     MT_HD int& ui(int k) const { if constexpr (LDS) return mt_lds().uid[k]; else return uid[k]; }
     MT_HD int& ud(int k) const { if constexpr (LDS) return mt_lds().udelta[k]; else return udelta[k]; }
-    // MT_RES_BLK keeps the first MT_B_U U-set entries in LDS, MT_RES_BIG the first
-    // MT_G_U.  U loops run per 64-entry chunk (chunks never straddle the cap), so each
+    // MT_RES_BIG keeps the first MT_G_U U-set entries in LDS (block residency keeps no U
+    // entries: the corrections table holds their sums).  U loops run per 64-entry chunk (chunks never straddle the cap), so each
     // chunk picks its home at compile time: forU calls f(std::bool_constant<inLds>, base, m).
-    static constexpr bool UL = BLKR || RES == MT_RES_BIG;
+    static constexpr bool UL = RES == MT_RES_BIG;
     static constexpr bool BT = BLKR;   // per-block corrections table (MtLdsBlkT::bcorr)
-    static constexpr int UCAP = BLKR ? MT_B_U : (RES == MT_RES_BIG ? MT_G_U : 0);
+    static constexpr int UCAP = RES == MT_RES_BIG ? MT_G_U : 0;
     template <bool L> MT_HD int uiAt(int k) const {
-        if constexpr (UL && L) { if constexpr (BIG) return mt_ldsg().uid[k]; else return LB().uid[k]; }
+        if constexpr (UL && L) return mt_ldsg().uid[k];
         else return ui(k);
     }
     template <bool L> MT_HD int udAt(int k) const {
-        if constexpr (UL && L) { if constexpr (BIG) return mt_ldsg().udelta[k]; else return LB().udelta[k]; }
+        if constexpr (UL && L) return mt_ldsg().udelta[k];
         else return ud(k);
     }
     template <bool L> MT_HD void uPutAt(int k, int id, int delta) {
-        if constexpr (UL && L) {
-            if constexpr (BIG) { mt_ldsg().uid[k] = id; mt_ldsg().udelta[k] = delta; }
-            else { LB().uid[k] = id; LB().udelta[k] = delta; }
-        } else { ui(k) = id; ud(k) = delta; }
+        if constexpr (UL && L) { mt_ldsg().uid[k] = id; mt_ldsg().udelta[k] = delta; }
+        else { ui(k) = id; ud(k) = delta; }
     }
     template <bool L> MT_HD void ancPutAt(int u, int h, int a) {
         if constexpr (UL && L) {
@@ -959,6 +972,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             auto& B = LB();
             copyQ((MtQ16*)B.blk, (const MtQ16*)blk, blkTop * (int)(sizeof(MtBlk) / 16));
             copyI((int*)B.heap, (const int*)heap, 2 * (heapN + 1));
+            copyI(B.win, win, winN < MT_B_W ? winN : MT_B_W);
             wave_sync();
             gRowCap = S.rowCap; gBlkCap = blkCap; gHeapCap = S.heapCap; gWinCap = S.winCap;
             blkCap = gBlkCap < (uint32_t)lb ? gBlkCap : (uint32_t)lb;
@@ -1011,6 +1025,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             auto& B = LB();
             copyQ((MtQ16*)blk, (const MtQ16*)B.blk, blkTop * (int)(sizeof(MtBlk) / 16));
             copyI((int*)heap, (const int*)B.heap, 2 * (heapN + 1));
+            copyI(win, B.win, winN < MT_B_W ? winN : MT_B_W);
             wave_sync();
             blkCap = gBlkCap; S.heapCap = gHeapCap;
             nU = 0; uValid = false;
@@ -1058,7 +1073,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     MT_HD uint32_t winAddKnown(int s, uint32_t mt) {
         if (mt & MT_M_INWIN) return mt;
         if (winN >= (int)S.winCap) { status |= MT_DS_OOM_WINDOW; return mt; }
-        wn(winN++) = s;
+        winSet(winN++, s);
         if (winN > winHW) winHW = winN;
         row(s).meta = mt | MT_M_INWIN;
         return mt | MT_M_INWIN;
@@ -1067,7 +1082,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         const uint32_t mt = uni(row(s).meta);
         if (mt & MT_M_INWIN) return;
         if (winN >= (int)S.winCap) { status |= MT_DS_OOM_WINDOW; return; }
-        wn(winN++) = s;
+        winSet(winN++, s);
         if (winN > winHW) winHW = winN;
         row(s).meta = mt | MT_M_INWIN;
     }
@@ -1087,7 +1102,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         wave_for(n, [&](int j) MT_LAM {
             if (!own(add, j)) return;
             const int s = own(ids, j);
-            wn(w0 + own(rk, j)) = s;
+            winSet(w0 + own(rk, j), s);
             row(s).meta = row(s).meta | MT_M_INWIN;
         });
         winN += cnt;
@@ -1195,7 +1210,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             const int nw0 = newWin;
             wave_for(m, [&](int k) MT_LAM {
                 const WinI w = own(wi, k);
-                if (w.live) { if (nw0 + own(rk, k) != base + k) wn(nw0 + own(rk, k)) = w.id; }
+                if (w.live) { if (nw0 + own(rk, k) != base + k) winSet(nw0 + own(rk, k), w.id); }
                 else row(w.id).meta = row(w.id).meta & ~MT_M_INWIN;
                 if (w.recycle && f0 + own(rkr, k) < MT_RFL) sc->rfree[f0 + own(rkr, k)] = w.id;
             });
@@ -1287,8 +1302,8 @@ template <int RES, bool FULL = true> struct MtEngT {
                     const int q2 = q + MT_G_NW * MT_WAVE;
                     const int m = (n - q) < MT_WAVE ? (n - q) : MT_WAVE;
                     const int m2 = q2 < n ? ((n - q2) < MT_WAVE ? (n - q2) : MT_WAVE) : 0;
-                    const auto id1 = wave_map(m, [&](int k) MT_LAM { return wn(r0 + q + k); });
-                    const auto id2 = wave_map(m2, [&](int k) MT_LAM { return wn(r0 + q2 + k); });
+                    const auto id1 = wave_map(m, [&](int k) MT_LAM { return winGet(r0 + q + k); });
+                    const auto id2 = wave_map(m2, [&](int k) MT_LAM { return winGet(r0 + q2 + k); });
                     const auto w1 = wave_map(m, [&](int k) MT_LAM { return winEntry(own(id1, k), r, c); });
                     const auto w2 = wave_map(m2, [&](int k) MT_LAM { return winEntry(own(id2, k), r, c); });
                     auto put = [&](const LaneArr<WinI>& w, int qq, int mm) MT_LAM {
@@ -1356,7 +1371,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             for (int q = 0; q < NC; q++) {
                 const int base = q * MT_WAVE;
                 const int m = base >= wN0 ? 0 : ((wN0 - base) < MT_WAVE ? (wN0 - base) : MT_WAVE);
-                const auto ids = wave_map(m, [&](int k) MT_LAM { return wn(base + k); });
+                const auto ids = wave_map(m, [&](int k) MT_LAM { return winGet(base + k); });
                 wis[q] = wave_map(m, [&](int k) MT_LAM { return winEntry(own(ids, k), r, c); });
             }
 #pragma unroll
@@ -1368,7 +1383,7 @@ template <int RES, bool FULL = true> struct MtEngT {
 #else
             for (int base = 0; base < wN0; base += MT_WAVE) {
                 const int m = (wN0 - base) < MT_WAVE ? (wN0 - base) : MT_WAVE;
-                const auto ids = wave_map(m, [&](int k) MT_LAM { return wn(base + k); });
+                const auto ids = wave_map(m, [&](int k) MT_LAM { return winGet(base + k); });
                 const auto wi = wave_map(m, [&](int k) MT_LAM { return winEntry(own(ids, k), r, c); });
                 placeChunk(wi, base, m, prune, newWin);
             }
@@ -1519,7 +1534,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         // the chunk being read, so the early reads see what in-order reads would).
         auto winIds = [&](int base) MT_LAM {
             const int m = (winN - base) < MT_WAVE ? (winN - base) : MT_WAVE;
-            return wave_map(m, [&](int k) MT_LAM { return wn(base + k); });
+            return wave_map(m, [&](int k) MT_LAM { return winGet(base + k); });
         };
         auto winRows = [&](const LaneArr<int>& ids, int base) MT_LAM {
             const int m = (winN - base) < MT_WAVE ? (winN - base) : MT_WAVE;
@@ -1564,7 +1579,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                 wave_for(m, [&](int k) MT_LAM {
                     const WinI w = own(wi, k);
                     // compaction writes only entries that move (none until the first pruned one)
-                    if (w.live) { if (nw0 + own(rk, k) != base + k) wn(nw0 + own(rk, k)) = w.id; }
+                    if (w.live) { if (nw0 + own(rk, k) != base + k) winSet(nw0 + own(rk, k), w.id); }
                     else row(w.id).meta = row(w.id).meta & ~MT_M_INWIN;
                     if (w.recycle && f0 + own(rkr, k) < MT_RFL) sc->rfree[f0 + own(rkr, k)] = w.id;
                 });
@@ -1584,7 +1599,7 @@ template <int RES, bool FULL = true> struct MtEngT {
                 const int HH = BLKL ? H : 0;
                 int a = w.parent;
                 if constexpr (BT) {                       // the row's delta into every block above it
-                    if (pos < UCAP) uPutAt<true>(pos, w.id, w.delta); else uPutAt<false>(pos, w.id, w.delta);
+                    (void)pos;
                     for (int h = 0; (h <= HH) & (a >= 0); h++) { lds_add(&LB().bcorr[a], w.delta); a = bk(a).parent; }
                 } else if constexpr (UL) {
                     if (pos < UCAP) {
@@ -1632,6 +1647,7 @@ template <int RES, bool FULL = true> struct MtEngT {
     }
     MT_HD int perspectiveLength(int r, int c) {
         if (!(uValid && uRef == r && uCli == c)) computeU(r, c, false);
+        if constexpr (BT) return uni(bk(root).len) + uni(LB().bcorr[root]);   // the root's correction: Σ delta
         int s = 0;
         forU([&](auto inL, int base, int m) MT_LAM {
             constexpr bool L = decltype(inL)::value;
@@ -1646,7 +1662,7 @@ template <int RES, bool FULL = true> struct MtEngT {
         for (int base = 0; base < winN; base += MT_WAVE) {
             const int m = (winN - base) < MT_WAVE ? (winN - base) : MT_WAVE;
             s += wave_sum(wave_map(m, [&](int k) MT_LAM {
-                const int id = wn(base + k);
+                const int id = winGet(base + k);
                 const uint32_t mt = row(id).meta;
                 const bool removed = (mt & MT_M_REMOVED) != 0;
                 const int sq = row(id).seq, rs = row(id).rseq;
@@ -3247,7 +3263,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             auto rk = wave_rank(inw);
             const int w0 = winN;
             wave_for(m, [&](int k) MT_LAM {
-                if (own(inw, k)) { const int s = base + k; wn(w0 + own(rk, k)) = s; row(s).meta = row(s).meta | MT_M_INWIN; }
+                if (own(inw, k)) { const int s = base + k; winSet(w0 + own(rk, k), s); row(s).meta = row(s).meta | MT_M_INWIN; }
             });
             winN += cnt;
         }
