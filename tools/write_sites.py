@@ -90,12 +90,16 @@ def run(cfg="config2", docs=16, res="blk"):
            "row_dwords_changed_per_msg": {ROW_FIELDS[k]: round(fields[k], 2) for k in range(12)},
            "total_bytes_per_msg": round(per.sum() + end.sum(), 1),
            "algorithmic_bytes_per_msg_read_and_write": round(alg, 1)}
+    eng.close()
     return rep
 
 
 if __name__ == "__main__":
-    a = [x for x in sys.argv[1:] if not x.startswith("--")]
+    a = [x for i, x in enumerate(sys.argv[1:], 1) if not x.startswith("--") and sys.argv[i - 1] != "--json"]
     rep = run(a[0] if a else "config2", int(a[1]) if len(a) > 1 else 16, a[2] if len(a) > 2 else "blk")
     print(json.dumps(rep, indent=1))
     if "--json" in sys.argv:
-        json.dump(rep, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
+        with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
+            json.dump(rep, f, indent=1)
+    sys.stdout.flush()
+    os._exit(0)          # (the traced host-emulation build crashes in interpreter teardown; results are out)
