@@ -75,6 +75,9 @@
 #ifndef MT_BW_BLKS
 #define MT_BW_BLKS 248
 #endif
+#ifndef MT_BW_W
+#define MT_BW_W 256                   // window entries in LDS (long documents of many clients hold
+#endif                                // windows of ~75 entries at 16 clients)
 #ifndef MT_BW_HEAP
 #define MT_BW_HEAP 254
 #endif
@@ -414,20 +417,20 @@ struct __attribute__((aligned(16))) MtLdsPools {
 
 // LDS home of a document's blocks and heap while mt_replay_blk_kernel (NB = MT_B_BLKS) or
 // mt_replay_blkw_kernel (NB = MT_BW_BLKS) runs it.
-template <int NB, int NH, int NT> struct __attribute__((aligned(16))) MtLdsBlkT {
+template <int NB, int NH, int NT, int NW> struct __attribute__((aligned(16))) MtLdsBlkT {
     static_assert(NB <= NT, "block ids index the corrections table");
     MtBlk blk[NB];
     MtHeapE heap[NH + 2];
-    // the window's first MT_B_W entries (the rest in HBM): computeU reads them without an HBM
+    // the window's first NW entries (the rest in HBM): computeU reads them without an HBM
     // round trip, and window appends and compaction write them here
-    int win[MT_B_W];
+    int win[NW];
     // Per-block perspective corrections of the current U set (Σ delta of the U rows beneath
     // each block, indexed by block id): a descent level reads its children's lengths as
     // observer length + correction instead of scanning U (no ancestor chains kept).
     int bcorr[NT];
 };
-using MtLdsBlk = MtLdsBlkT<MT_B_BLKS, MT_B_HEAP, MT_B_BT>;
-using MtLdsBlkW = MtLdsBlkT<MT_BW_BLKS, MT_BW_HEAP, MT_BW_BT>;
+using MtLdsBlk = MtLdsBlkT<MT_B_BLKS, MT_B_HEAP, MT_B_BT, MT_B_W>;
+using MtLdsBlkW = MtLdsBlkT<MT_BW_BLKS, MT_BW_HEAP, MT_BW_BT, MT_BW_W>;
 
 // LDS home of a long document's heap, window and U set while mt_replay_big_kernel runs it.
 struct __attribute__((aligned(16))) MtLdsBig {
@@ -673,12 +676,13 @@ template <int RES, bool FULL = true> struct MtEngT {
     }
     // Window entry k under block residency: the first MT_B_W in LDS.  Loads and stores are made
     // in each branch (a reference to either home would be a generic pointer: flat_* accesses).
+    static constexpr int kW = BW ? MT_BW_W : MT_B_W;    // window entries in LDS (block residency)
     MT_HD int winGet(int k) const {
-        if constexpr (BLKR) { if (k < MT_B_W) return LB().win[k]; return win[k]; }
+        if constexpr (BLKR) { if (k < kW) return LB().win[k]; return win[k]; }
         else return wn(k);
     }
     MT_HD void winSet(int k, int v) const {
-        if constexpr (BLKR) { if (k < MT_B_W) LB().win[k] = v; else win[k] = v; }
+        if constexpr (BLKR) { if (k < kW) LB().win[k] = v; else win[k] = v; }
         else wn(k) = v;
     }
     MT_HD int& wn(int k) const {
@@ -972,7 +976,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             auto& B = LB();
             copyQ((MtQ16*)B.blk, (const MtQ16*)blk, blkTop * (int)(sizeof(MtBlk) / 16));
             copyI((int*)B.heap, (const int*)heap, 2 * (heapN + 1));
-            copyI(B.win, win, winN < MT_B_W ? winN : MT_B_W);
+            copyI(B.win, win, winN < kW ? winN : kW);
             wave_sync();
             gRowCap = S.rowCap; gBlkCap = blkCap; gHeapCap = S.heapCap; gWinCap = S.winCap;
             blkCap = gBlkCap < (uint32_t)lb ? gBlkCap : (uint32_t)lb;
@@ -1025,7 +1029,7 @@ template <int RES, bool FULL = true> struct MtEngT {
             auto& B = LB();
             copyQ((MtQ16*)blk, (const MtQ16*)B.blk, blkTop * (int)(sizeof(MtBlk) / 16));
             copyI((int*)heap, (const int*)B.heap, 2 * (heapN + 1));
-            copyI(win, B.win, winN < MT_B_W ? winN : MT_B_W);
+            copyI(win, B.win, winN < kW ? winN : kW);
             wave_sync();
             blkCap = gBlkCap; S.heapCap = gHeapCap;
             nU = 0; uValid = false;
